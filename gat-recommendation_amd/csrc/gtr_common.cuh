@@ -1,0 +1,141 @@
+// gtr_common.cuh — shared device helpers for the gfx950 GraphTransformer kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gtr.h"
+
+#define GTR_BLOCK 256
+#define GTR_WAVES (GTR_BLOCK / 64)
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+namespace gtr {
+
+void set_error(const char* fmt, ...);
+
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
+__device__ __forceinline__ float wave_max(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
+  return x;
+}
+
+// Sum inside aligned groups of `gl` lanes (gl a power of two <= 64).
+__device__ __forceinline__ float group_sum(float x, int gl) {
+  for (int o = 1; o < gl; o <<= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
+// Counter-based dropout stream: one 32-bit hash per (seed, stream, element).
+__device__ __forceinline__ uint32_t mix3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t h = a * 0x9E3779B1u;
+  h ^= b + 0x7F4A7C15u + (h << 6) + (h >> 2);
+  h *= 0x85EBCA77u;
+  h ^= c * 0xC2B2AE3Du;
+  h ^= h >> 16;
+  h *= 0x7FEB352Du;
+  h ^= h >> 15;
+  h *= 0x846CA68Bu;
+  h ^= h >> 16;
+  return h;
+}
+
+// kind 0: attention-probability dropout of layer l; kind 1: layer-output dropout.
+__device__ __forceinline__ uint32_t drop_stream(uint32_t kind, uint32_t layer, uint32_t ctr) {
+  return (kind << 28) ^ (layer << 20) ^ (ctr * 0x632BE5ABu);
+}
+
+struct Drop {
+  uint32_t seed, thresh;
+  float scale;
+  bool on;
+  __device__ __forceinline__ float mul(uint32_t stream, uint32_t idx) const {
+    if (!on) return 1.0f;
+    return mix3(seed, stream, idx) >= thresh ? scale : 0.0f;
+  }
+};
+
+__device__ __forceinline__ int lower_bound_i32(const int32_t* a, int n, int v) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// Rows [r0, r1) of row-group g: all sessions whose first node lies in [g*R, (g+1)*R).
+__device__ __forceinline__ void group_rows(const int32_t* node_ptr, int B, int R, int g, int& r0, int& r1) {
+  int s0 = lower_bound_i32(node_ptr, B, g * R);
+  int s1 = lower_bound_i32(node_ptr, B, (g + 1) * R);
+  r0 = node_ptr[s0];
+  r1 = node_ptr[s1];
+}
+
+// Last-arriver election across the workgroups of one launch (placement independent:
+// plain stores -> every wave drains -> barrier -> lane-0 agent release -> counter;
+// the last arriver does an agent acquire before reading the other groups' partials).
+__device__ __forceinline__ bool arrive_last(uint32_t* cnt, uint32_t total, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_flag = (prev == total - 1) ? 1 : 0;
+  }
+  __syncthreads();
+  if (*s_flag == 0) return false;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  return true;
+}
+
+__device__ __forceinline__ void reset_counter(uint32_t* cnt) {
+  __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// torch.optim.AdamW / Adam single-tensor arithmetic (fp32 element ops; bias
+// corrections computed in double like the Python scalars of torch/optim/adamw.py).
+struct AdamStep {
+  float lr, b1, b2, eps, wd, decay_mul, step_size, bc2_sqrt;
+  int decoupled;
+  __device__ __forceinline__ void init(const gtr_adam& o, int64_t t) {
+    lr = o.lr; b1 = o.beta1; b2 = o.beta2; eps = o.eps; wd = o.weight_decay;
+    decoupled = o.decoupled;
+    double bc1 = 1.0 - pow((double)o.beta1, (double)t);
+    double bc2 = 1.0 - pow((double)o.beta2, (double)t);
+    step_size = (float)((double)o.lr / bc1);
+    bc2_sqrt = (float)sqrt(bc2);
+    decay_mul = (float)(1.0 - (double)o.lr * (double)o.weight_decay);
+  }
+  __device__ __forceinline__ void apply(float& p, float& m, float& v, float g) const {
+    if (decoupled) p = p * decay_mul;
+    else g = g + wd * p;
+    m = m + (1.0f - b1) * (g - m);          // exp_avg.lerp_(grad, 1 - beta1)
+    v = v * b2 + (1.0f - b2) * g * g;       // exp_avg_sq.mul_(b2).addcmul_(g, g, 1 - b2)
+    float denom = sqrtf(v) / bc2_sqrt + eps;
+    p = p + (-step_size) * (m / denom);     // param.addcdiv_(exp_avg, denom, -step_size)
+  }
+};
+
+}  // namespace gtr
+
+#define GTR_HIP_CHECK_LAUNCH()                                              \
+  do {                                                                      \
+    hipError_t _e = hipGetLastError();                                      \
+    if (_e != hipSuccess) {                                                 \
+      gtr::set_error("%s: launch failed: %s", __func__, hipGetErrorString(_e)); \
+      return (int)_e;                                                       \
+    }                                                                       \
+  } while (0)

@@ -1,0 +1,603 @@
+// gtr_fwd.hip — forward kernels of the GraphTransformer hot path (gfx950).
+//
+// k_conv_fwd<D>: one TransformerConv layer + the previous layer's BatchNorm /
+//   residual / dropout, fused.  Reference: graph_transformer.py:140-152 (layer 0
+//   prologue: item_embedding + LapPE), :171-177 (conv -> bn -> +res -> dropout) and
+//   PyG TransformerConv.
+//   Work unit = a row group: every session whose first node falls in [g*R,(g+1)*R).
+//   Sessions are independent subgraphs (dataloader.py:157-202), so one workgroup
+//   owns every source of every destination it processes: projection, attention and
+//   gate need no inter-workgroup exchange.  Only BatchNorm couples sessions: each
+//   group writes (count, mean, M2) partials, the last arriving group combines them.
+//
+// k_readout<D>: last layer's BN/residual/dropout + mean readout (base.py:136-155)
+//   + scoring loss fwd/bwd (base.py:80-113, losses.py:8-164) + readout backward and
+//   the last BatchNorm's backward sums.
+
+#include "gtr_common.cuh"
+
+namespace {
+
+using namespace gtr;
+
+struct ConvFwdK {
+  gtr_batch bt;
+  int H, C, R, first, train, layer, pe_k, pad0;
+  float sqrt_c, bn_eps, bn_mom, scale;
+  uint32_t seed, thresh;
+  int drop_on, pad1;
+  const uint32_t* rng_ctr;
+  const float* table;
+  const float* pe_tab;
+  const float* wpe;
+  const float* bpe;
+  const float* p_out;
+  const float* p_xin;
+  const float* p_stats;
+  const float* p_gamma;
+  const float* p_beta;
+  const float* p_rmean;
+  const float* p_rvar;
+  const float* w_all;
+  const float* b_all;
+  const float* w_beta;
+  float* xin;
+  float* qkvs;
+  float* alpha;
+  float* agg;
+  float* gate;
+  float* out;
+  float* bn_part;
+  uint32_t* cnt;
+  float* bn_stats;
+  float* bn_rmean;
+  float* bn_rvar;
+  int64_t* bn_nbt;
+};
+
+template <int D>
+__global__ __launch_bounds__(GTR_BLOCK) void k_conv_fwd(ConvFwdK a) {
+  constexpr int XS = D + 4;                       // padded LDS row (16B aligned)
+  constexpr int VPL = D >= 64 ? D / 64 : 1;       // features per lane in row phases
+  __shared__ __attribute__((aligned(16))) float Xs[16 * XS];
+  __shared__ float s_bn[2 * D];
+  __shared__ int s_flag;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int N = a.bt.hdr[0], B = a.bt.hdr[1];
+  const int G = (N + a.R - 1) / a.R;
+  const int g = blockIdx.x;
+  if (g >= G) return;
+  int r0, r1;
+  group_rows(a.bt.node_ptr, B, a.R, g, r0, r1);
+  const uint32_t ctr = a.rng_ctr ? *a.rng_ctr : 0u;
+  const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
+
+  if (!a.first) {
+    for (int j = tid; j < D; j += GTR_BLOCK) {
+      float mean, rstd;
+      if (a.train) { mean = a.p_stats[j]; rstd = a.p_stats[D + j]; }
+      else { mean = a.p_rmean[j]; rstd = 1.0f / sqrtf(a.p_rvar[j] + a.bn_eps); }
+      s_bn[j] = mean;
+      s_bn[D + j] = rstd;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase P+M: layer input rows -> LDS -> QKVS projection on MFMA (f32 in, f32 acc)
+  const uint32_t st_prev = drop_stream(1, (uint32_t)(a.layer - 1), ctr);
+  const int lr = lane & 15, lg = lane >> 4;
+  constexpr int NCT = (4 * D) / 16;
+  for (int rt = r0; rt < r1; rt += 16) {
+    for (int idx = tid; idx < 16 * D; idx += GTR_BLOCK) {
+      const int i = idx / D, j = idx - i * D;
+      const int r = rt + i;
+      float val = 0.0f;
+      if (r < r1) {
+        const size_t o = (size_t)r * D + j;
+        if (a.first) {
+          const int item = a.bt.node_item[r];
+          val = a.table[(size_t)item * D + j];
+          if (a.pe_k > 0) {
+            const float* pr = a.bt.node_pe ? a.bt.node_pe + (size_t)r * a.pe_k
+                                           : a.pe_tab + (size_t)item * a.pe_k;
+            const float* wr = a.wpe + (size_t)j * a.pe_k;
+            float acc = 0.0f;
+            for (int k = 0; k < a.pe_k; ++k) acc += pr[k] * wr[k];
+            val = val + (acc + a.bpe[j]);
+          }
+        } else {
+          float y = (a.p_out[o] - s_bn[j]) * s_bn[D + j] * a.p_gamma[j] + a.p_beta[j];
+          y = y + a.p_xin[o];
+          val = y * dr.mul(st_prev, (uint32_t)o);
+        }
+        a.xin[o] = val;
+      }
+      Xs[i * XS + j] = val;
+    }
+    __syncthreads();
+    for (int ct = wave; ct < NCT; ct += GTR_WAVES) {
+      f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+      const float* wrow = a.w_all + (size_t)(ct * 16 + lr) * D + lg * 4;
+      const float* xrow = Xs + lr * XS + lg * 4;
+#pragma unroll
+      for (int kb = 0; kb < D / 16; ++kb) {
+        const float4 av = *reinterpret_cast<const float4*>(xrow + kb * 16);
+        const float4 bv = *reinterpret_cast<const float4*>(wrow + kb * 16);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc, 0, 0, 0);
+      }
+      const int col = ct * 16 + lr;
+      const float bias = a.b_all[col];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = rt + lg * 4 + i;
+        if (row < r1) a.qkvs[(size_t)row * (4 * D) + col] = acc[i] + bias;
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- phase A: attention over in-edges (CSR by destination) + beta gate; wave per row
+  const int d0 = lane * VPL;
+  const bool act = d0 < D;
+  const int C = a.C, H = a.H;
+  const int GL = C / VPL;
+  const int head = act ? d0 / C : 0;
+  const bool leader = act && ((lane & (GL - 1)) == 0);
+  const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
+  for (int t = r0 + wave; t < r1; t += GTR_WAVES) {
+    const float* qt = a.qkvs + (size_t)t * (4 * D);
+    float q[VPL], s[VPL], ag[VPL];
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      q[v] = act ? qt[d0 + v] : 0.0f;
+      s[v] = act ? qt[3 * D + d0 + v] : 0.0f;
+      ag[v] = 0.0f;
+    }
+    const int e0 = a.bt.in_ptr[t], e1 = a.bt.in_ptr[t + 1];
+    float m = -INFINITY, z = 0.0f;
+    for (int e = e0; e < e1; ++e) {
+      const float* kt = a.qkvs + (size_t)a.bt.in_src[e] * (4 * D) + D;
+      float dt = 0.0f;
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) dt += act ? q[v] * kt[d0 + v] : 0.0f;
+      dt = group_sum(dt, GL);
+      const float l = dt / a.sqrt_c;
+      const float mn = fmaxf(m, l);
+      z = z * expf(m - mn) + expf(l - mn);
+      m = mn;
+    }
+    const float zd = z + 1e-16f;
+    for (int e = e0; e < e1; ++e) {
+      const float* kv = a.qkvs + (size_t)a.bt.in_src[e] * (4 * D);
+      float dt = 0.0f;
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) dt += act ? q[v] * kv[D + d0 + v] : 0.0f;
+      dt = group_sum(dt, GL);
+      const float l = dt / a.sqrt_c;
+      const float al = expf(l - m) / zd;
+      if (leader) a.alpha[(size_t)e * H + head] = al;
+      const float ad = al * dr.mul(st_attn, (uint32_t)(e * H + head));
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) ag[v] += act ? ad * kv[2 * D + d0 + v] : 0.0f;
+    }
+    float u = 0.0f;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      if (act) {
+        const int j = d0 + v;
+        u += a.w_beta[j] * ag[v] + a.w_beta[D + j] * s[v] + a.w_beta[2 * D + j] * (ag[v] - s[v]);
+      }
+    }
+    u = wave_sum(u);
+    const float beta = 1.0f / (1.0f + expf(-u));
+    if (act) {
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) {
+        const size_t o = (size_t)t * D + d0 + v;
+        a.agg[o] = ag[v];
+        a.out[o] = beta * s[v] + (1.0f - beta) * ag[v];
+      }
+    }
+    if (lane == 0) a.gate[t] = beta;
+  }
+
+  if (!a.train) return;
+
+  // ---- phase S: BatchNorm batch statistics (two-pass per group, Chan combine by the last arriver)
+  __syncthreads();
+  float* part = a.bn_part + (size_t)g * (1 + 2 * D);
+  for (int j = tid; j < D; j += GTR_BLOCK) {
+    float sum = 0.0f;
+    for (int r = r0; r < r1; ++r) sum += a.out[(size_t)r * D + j];
+    const int n = r1 - r0;
+    const float mean = n > 0 ? sum / (float)n : 0.0f;
+    float m2 = 0.0f;
+    for (int r = r0; r < r1; ++r) {
+      const float d = a.out[(size_t)r * D + j] - mean;
+      m2 += d * d;
+    }
+    part[1 + j] = mean;
+    part[1 + D + j] = m2;
+  }
+  if (tid == 0) part[0] = (float)(r1 - r0);
+  if (!arrive_last(a.cnt, (uint32_t)G, &s_flag)) return;
+  for (int j = tid; j < D; j += GTR_BLOCK) {
+    double n = 0.0, sum = 0.0;
+    for (int q = 0; q < G; ++q) {
+      const float* pp = a.bn_part + (size_t)q * (1 + 2 * D);
+      n += (double)pp[0];
+      sum += (double)pp[0] * (double)pp[1 + j];
+    }
+    const double mean = sum / n;
+    double m2 = 0.0;
+    for (int q = 0; q < G; ++q) {
+      const float* pp = a.bn_part + (size_t)q * (1 + 2 * D);
+      const double d = (double)pp[1 + j] - mean;
+      m2 += (double)pp[1 + D + j] + (double)pp[0] * d * d;
+    }
+    const float var = (float)(m2 / n);
+    const float meanf = (float)mean;
+    a.bn_stats[j] = meanf;
+    a.bn_stats[D + j] = 1.0f / sqrtf(var + a.bn_eps);
+    const float uvar = n > 1.0 ? (float)(m2 / (n - 1.0)) : var;
+    a.bn_rmean[j] = (1.0f - a.bn_mom) * a.bn_rmean[j] + a.bn_mom * meanf;
+    a.bn_rvar[j] = (1.0f - a.bn_mom) * a.bn_rvar[j] + a.bn_mom * uvar;
+  }
+  if (tid == 0) {
+    reset_counter(a.cnt);
+    if (a.bn_nbt) *a.bn_nbt += 1;
+  }
+}
+
+struct ReadoutK {
+  gtr_batch bt;
+  int L1, train, flags, loss_kind;
+  float temperature, dual_alpha, bn_eps, scale;
+  uint32_t seed, thresh;
+  int drop_on, pad0;
+  const uint32_t* rng_ctr;
+  const float* table;
+  const float* out;
+  const float* xin;
+  const float* stats;
+  const float* gamma;
+  const float* beta;
+  const float* rmean;
+  const float* rvar;
+  float* se;
+  const float* dse_in;
+  float* dse_out;
+  float* coef_tgt;
+  float* coef_neg;
+  float* loss_part;
+  float* loss_out;
+  uint32_t* cnt;
+  float* dy;
+  float* gpart;
+  float* gsum;
+};
+
+template <int D>
+__device__ __forceinline__ float row_dot(const float* row, const float (&x)[D >= 64 ? D / 64 : 1], int d0, bool act) {
+  constexpr int VPL = D >= 64 ? D / 64 : 1;
+  float s = 0.0f;
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) s += act ? x[v] * row[d0 + v] : 0.0f;
+  return wave_sum(s);
+}
+
+template <int D>
+__global__ __launch_bounds__(GTR_BLOCK) void k_readout(ReadoutK a) {
+  constexpr int VPL = D >= 64 ? D / 64 : 1;
+  __shared__ float s_bn[2 * D];
+  __shared__ float s_red[GTR_WAVES][2 * D];
+  __shared__ float s_loss[GTR_WAVES][2];
+  __shared__ int s_flag;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int B = a.bt.hdr[1];
+  const int n = a.bt.n_neg;
+  const int d0 = lane * VPL;
+  const bool act = d0 < D;
+  const uint32_t ctr = a.rng_ctr ? *a.rng_ctr : 0u;
+  const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
+  const uint32_t st = drop_stream(1, (uint32_t)a.L1, ctr);
+  const bool do_fwd = a.flags & GTR_RO_FWD, do_loss = a.flags & GTR_RO_LOSS, do_bwd = a.flags & GTR_RO_BWD;
+  const bool use_lw = a.loss_kind == GTR_LOSS_LISTWISE || a.loss_kind == GTR_LOSS_DUAL;
+  const bool use_bpr = a.loss_kind == GTR_LOSS_BPR || a.loss_kind == GTR_LOSS_DUAL;
+  const float w_lw = a.loss_kind == GTR_LOSS_DUAL ? a.dual_alpha : 1.0f;
+  const float w_bpr = a.loss_kind == GTR_LOSS_DUAL ? 1.0f - a.dual_alpha : 1.0f;
+  const float inv_bn = 1.0f / ((float)B * (float)n);  // BPR mean over B*n
+  const float inv_b = 1.0f / (float)B;                // listwise mean over B
+  const float inv_t = 1.0f / a.temperature;
+
+  if (do_fwd || do_bwd) {
+    for (int j = tid; j < D; j += GTR_BLOCK) {
+      float mean, rstd;
+      if (a.train) { mean = a.stats[j]; rstd = a.stats[D + j]; }
+      else { mean = a.rmean[j]; rstd = 1.0f / sqrtf(a.rvar[j] + a.bn_eps); }
+      s_bn[j] = mean;
+      s_bn[D + j] = rstd;
+    }
+  }
+  __syncthreads();
+
+  float gs[VPL], gx[VPL];
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) { gs[v] = 0.0f; gx[v] = 0.0f; }
+  float lw_sum = 0.0f, bpr_sum = 0.0f;
+
+  for (int b = blockIdx.x * GTR_WAVES + wave; b < B; b += gridDim.x * GTR_WAVES) {
+    const int n0 = a.bt.node_ptr[b], n1 = a.bt.node_ptr[b + 1];
+    const float cnt = (float)(n1 - n0);
+    float se[VPL], dse[VPL];
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) dse[v] = 0.0f;
+    if (do_fwd) {
+      float acc[VPL];
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) acc[v] = 0.0f;
+      for (int i = n0; i < n1; ++i) {
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) {
+          if (act) {
+            const int j = d0 + v;
+            const size_t o = (size_t)i * D + j;
+            float y = (a.out[o] - s_bn[j]) * s_bn[D + j] * a.gamma[j] + a.beta[j];
+            y = y + a.xin[o];
+            acc[v] += y * dr.mul(st, (uint32_t)o);
+          }
+        }
+      }
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) {
+        se[v] = acc[v] / cnt;
+        if (act) a.se[(size_t)b * D + d0 + v] = se[v];
+      }
+    } else {
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) se[v] = act ? a.se[(size_t)b * D + d0 + v] : 0.0f;
+    }
+
+    if (do_loss) {
+      const float* trow = a.table + (size_t)a.bt.target[b] * D;
+      const int* negs = a.bt.negatives + (size_t)b * n;
+      const float pos = row_dot<D>(trow, se, d0, act);
+      float dpos = 0.0f;
+      // pass 1: BPR terms (independent per negative) + online log-sum-exp for listwise
+      float m = pos * inv_t, z = 1.0f;
+      for (int k = 0; k < n; ++k) {
+        const float* nrow = a.table + (size_t)negs[k] * D;
+        const float sk = row_dot<D>(nrow, se, d0, act);
+        float cb = 0.0f;
+        if (use_bpr) {
+          const float sg = 1.0f / (1.0f + expf(-(pos - sk)));
+          bpr_sum += -logf(sg + 1e-8f);
+          const float dz = -(sg * (1.0f - sg)) / (sg + 1e-8f) * inv_bn * w_bpr;
+          dpos += dz;
+          cb = -dz;
+        }
+        if (use_lw) {
+          const float l = sk * inv_t;
+          const float mn = fmaxf(m, l);
+          z = z * expf(m - mn) + expf(l - mn);
+          m = mn;
+        }
+        if (!use_lw) {
+          if (lane == 0) a.coef_neg[(size_t)b * n + k] = cb;
+#pragma unroll
+          for (int v = 0; v < VPL; ++v) dse[v] += act ? cb * nrow[d0 + v] : 0.0f;
+        }
+      }
+      if (use_lw) {
+        const float lse = m + logf(z);
+        lw_sum += lse - pos * inv_t;
+        dpos += (expf(pos * inv_t - lse) - 1.0f) * inv_b * inv_t * w_lw;
+        // pass 2: softmax coefficients (+ BPR coefficients recomputed for dual)
+        for (int k = 0; k < n; ++k) {
+          const float* nrow = a.table + (size_t)negs[k] * D;
+          const float sk = row_dot<D>(nrow, se, d0, act);
+          float cb = expf(sk * inv_t - lse) * inv_b * inv_t * w_lw;
+          if (use_bpr) {
+            const float sg = 1.0f / (1.0f + expf(-(pos - sk)));
+            cb += (sg * (1.0f - sg)) / (sg + 1e-8f) * inv_bn * w_bpr;
+          }
+          if (lane == 0) a.coef_neg[(size_t)b * n + k] = cb;
+#pragma unroll
+          for (int v = 0; v < VPL; ++v) dse[v] += act ? cb * nrow[d0 + v] : 0.0f;
+        }
+      }
+      if (lane == 0) a.coef_tgt[b] = dpos;
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) dse[v] += act ? dpos * trow[d0 + v] : 0.0f;
+      if (a.dse_out && act) {
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) a.dse_out[(size_t)b * D + d0 + v] = dse[v];
+      }
+    } else if (do_bwd) {
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) dse[v] = act ? a.dse_in[(size_t)b * D + d0 + v] : 0.0f;
+    }
+
+    if (do_bwd) {
+      const float inv_cnt = 1.0f / cnt;
+      for (int i = n0; i < n1; ++i) {
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) {
+          if (act) {
+            const int j = d0 + v;
+            const size_t o = (size_t)i * D + j;
+            const float dyv = dse[v] * inv_cnt * dr.mul(st, (uint32_t)o);
+            a.dy[o] = dyv;
+            const float xh = (a.out[o] - s_bn[j]) * s_bn[D + j];
+            gs[v] += dyv;
+            gx[v] += dyv * xh;
+          }
+        }
+      }
+    }
+  }
+
+  if (!(do_loss || do_bwd)) return;
+  // ---- block partials -> last arriver (fixed order => deterministic)
+  if (lane == 0) { s_loss[wave][0] = lw_sum; s_loss[wave][1] = bpr_sum; }
+  if (do_bwd && act) {
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) { s_red[wave][d0 + v] = gs[v]; s_red[wave][D + d0 + v] = gx[v]; }
+  }
+  __syncthreads();
+  if (do_loss && tid < 2) {
+    float acc = 0.0f;
+    for (int w = 0; w < GTR_WAVES; ++w) acc += s_loss[w][tid];
+    a.loss_part[(size_t)blockIdx.x * 2 + tid] = acc;
+  }
+  if (do_bwd) {
+    for (int j = tid; j < 2 * D; j += GTR_BLOCK) {
+      float acc = 0.0f;
+      for (int w = 0; w < GTR_WAVES; ++w) acc += s_red[w][j];
+      a.gpart[(size_t)blockIdx.x * 2 * D + j] = acc;
+    }
+  }
+  if (!arrive_last(a.cnt, gridDim.x, &s_flag)) return;
+  if (do_loss && tid == 0) {
+    float lw = 0.0f, bp = 0.0f;
+    for (int q = 0; q < (int)gridDim.x; ++q) { lw += a.loss_part[(size_t)q * 2]; bp += a.loss_part[(size_t)q * 2 + 1]; }
+    float loss = 0.0f;
+    if (use_lw) loss += w_lw * (lw * inv_b);
+    if (use_bpr) loss += w_bpr * (bp * inv_bn);
+    a.loss_out[0] = loss;
+  }
+  if (do_bwd) {
+    for (int j = tid; j < 2 * D; j += GTR_BLOCK) {
+      float acc = 0.0f;
+      for (int q = 0; q < (int)gridDim.x; ++q) acc += a.gpart[(size_t)q * 2 * D + j];
+      a.gsum[j] = acc;
+    }
+  }
+  if (tid == 0) reset_counter(a.cnt);
+}
+
+bool check_dims(const gtr_config* c, const char* fn) {
+  const int D = c->dim, H = c->heads;
+  if (!(D == 32 || D == 64 || D == 128 || D == 256)) {
+    set_error("%s: dim %d unsupported (32/64/128/256)", fn, D);
+    return false;
+  }
+  if (H <= 0 || D % H != 0) { set_error("%s: heads %d must divide dim %d", fn, H, D); return false; }
+  const int C = D / H, vpl = D >= 64 ? D / 64 : 1;
+  if (C < vpl || (C & (C - 1)) != 0) { set_error("%s: head dim %d unsupported", fn, C); return false; }
+  if (c->row_group <= 0) { set_error("%s: row_group must be > 0", fn); return false; }
+  if (c->pe_k < 0 || c->pe_k > 256) { set_error("%s: pe_k %d out of range", fn, c->pe_k); return false; }
+  return true;
+}
+
+void drop_params(const gtr_config* c, uint32_t& thresh, float& scale, int& on) {
+  on = (c->training && c->dropout > 0.0f) ? 1 : 0;
+  double p = c->dropout;
+  if (p >= 1.0) p = 0.999999;
+  thresh = (uint32_t)(p * 4294967296.0);
+  scale = on ? (float)(1.0 / (1.0 - p)) : 1.0f;
+}
+
+}  // namespace
+
+extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_embed* emb,
+                            const gtr_layer* layers, int l, gtr_stream_t stream) {
+  if (!cfg || !bt || !layers || l < 0 || l >= cfg->num_layers) {
+    set_error("gtr_conv_fwd: bad arguments");
+    return GTR_E_ARG;
+  }
+  if (!check_dims(cfg, "gtr_conv_fwd")) return GTR_E_ARG;
+  if (l == 0 && (!emb || !emb->table)) { set_error("gtr_conv_fwd: layer 0 needs the table"); return GTR_E_ARG; }
+  if (l == 0 && cfg->pe_k > 0 && (!emb->wpe || !emb->bpe || (!emb->pe_tab && !bt->node_pe))) {
+    set_error("gtr_conv_fwd: Laplacian PE not precomputed");
+    return GTR_E_ARG;
+  }
+  const gtr_layer& L = layers[l];
+  ConvFwdK k{};
+  k.bt = *bt;
+  k.H = cfg->heads;
+  k.C = cfg->dim / cfg->heads;
+  k.R = cfg->row_group;
+  k.first = l == 0;
+  k.train = cfg->training;
+  k.layer = l;
+  k.pe_k = cfg->pe_k;
+  k.sqrt_c = (float)sqrt((double)k.C);
+  k.bn_eps = cfg->bn_eps;
+  k.bn_mom = cfg->bn_momentum;
+  drop_params(cfg, k.thresh, k.scale, k.drop_on);
+  k.seed = cfg->seed;
+  k.rng_ctr = cfg->rng_ctr;
+  if (l == 0) {
+    k.table = emb->table; k.pe_tab = emb->pe_tab; k.wpe = emb->wpe; k.bpe = emb->bpe;
+  } else {
+    const gtr_layer& P = layers[l - 1];
+    k.p_out = P.out; k.p_xin = P.xin; k.p_stats = P.bn_stats; k.p_gamma = P.bn_gamma;
+    k.p_beta = P.bn_beta; k.p_rmean = P.bn_rmean; k.p_rvar = P.bn_rvar;
+  }
+  k.w_all = L.w_all; k.b_all = L.b_all; k.w_beta = L.w_beta;
+  k.xin = L.xin; k.qkvs = L.qkvs; k.alpha = L.alpha; k.agg = L.agg; k.gate = L.gate; k.out = L.out;
+  k.bn_part = L.bn_part; k.cnt = L.cnt; k.bn_stats = L.bn_stats; k.bn_rmean = L.bn_rmean;
+  k.bn_rvar = L.bn_rvar; k.bn_nbt = L.bn_nbt;
+  const int grid = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;
+  if (grid <= 0) return GTR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  switch (cfg->dim) {
+    case 32: hipLaunchKernelGGL(k_conv_fwd<32>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    case 64: hipLaunchKernelGGL(k_conv_fwd<64>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    case 128: hipLaunchKernelGGL(k_conv_fwd<128>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    default: hipLaunchKernelGGL(k_conv_fwd<256>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+  }
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+extern "C" int gtr_readout_loss(const gtr_config* cfg, const gtr_batch* bt, const float* table,
+                                const gtr_layer* layers, const gtr_head* head, gtr_stream_t stream) {
+  if (!cfg || !bt || !layers || !head) { set_error("gtr_readout_loss: bad arguments"); return GTR_E_ARG; }
+  if (!check_dims(cfg, "gtr_readout_loss")) return GTR_E_ARG;
+  if ((head->flags & GTR_RO_LOSS) && (head->loss_kind < GTR_LOSS_BPR || head->loss_kind > GTR_LOSS_DUAL || bt->n_neg <= 0 || !table)) {
+    set_error("gtr_readout_loss: bad loss configuration");
+    return GTR_E_ARG;
+  }
+  if ((head->flags & GTR_RO_BWD) && !cfg->training) {
+    set_error("gtr_readout_loss: backward requires training mode (batch statistics)");
+    return GTR_E_ARG;
+  }
+  const int L1 = cfg->num_layers - 1;
+  const gtr_layer& L = layers[L1];
+  ReadoutK k{};
+  k.bt = *bt;
+  k.L1 = L1;
+  k.train = cfg->training;
+  k.flags = head->flags;
+  k.loss_kind = head->loss_kind;
+  k.temperature = head->temperature;
+  k.dual_alpha = head->dual_alpha;
+  k.bn_eps = cfg->bn_eps;
+  drop_params(cfg, k.thresh, k.scale, k.drop_on);
+  k.seed = cfg->seed;
+  k.rng_ctr = cfg->rng_ctr;
+  k.table = table;
+  k.out = L.out; k.xin = L.xin; k.stats = L.bn_stats; k.gamma = L.bn_gamma; k.beta = L.bn_beta;
+  k.rmean = L.bn_rmean; k.rvar = L.bn_rvar;
+  k.se = head->se; k.dse_in = head->dse_in; k.dse_out = head->dse_out; k.coef_tgt = head->coef_tgt; k.coef_neg = head->coef_neg;
+  k.loss_part = head->loss_part; k.loss_out = head->loss_out; k.cnt = head->cnt;
+  k.dy = L.dy; k.gpart = L.bn_gpart; k.gsum = L.bn_gsum;
+  int grid = (bt->b_cap + GTR_WAVES - 1) / GTR_WAVES;
+  if (grid > 256) grid = 256;
+  if (grid <= 0) return GTR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  switch (cfg->dim) {
+    case 32: hipLaunchKernelGGL(k_readout<32>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    case 64: hipLaunchKernelGGL(k_readout<64>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    case 128: hipLaunchKernelGGL(k_readout<128>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    default: hipLaunchKernelGGL(k_readout<256>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+  }
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}

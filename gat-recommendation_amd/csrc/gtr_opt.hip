@@ -1,0 +1,386 @@
+// gtr_opt.hip — item-table gradient bookkeeping and the fused AdamW/Adam kernels.
+//
+// The reference materialises a dense [T, D] embedding gradient every step
+// (nn.Embedding(sparse=False), base.py:36) and runs torch.optim.AdamW over all
+// T*D elements (train_baseline.py:252-256).  Here the table gradient is kept as a
+// contribution list (node rows dx0, target/negative rows coef*se) sorted by row
+// (stable radix sort => deterministic segmented sums), and the optimizer is split:
+//   * gtr_adamw_sweep: rows NOT touched this step — AdamW with g = 0 (identical
+//     arithmetic to the dense update), 24 B/element, independent of the backward,
+//     so it can run concurrently with the forward/backward chain;
+//   * gtr_adamw_rows:  touched rows — segmented sum + AdamW;
+//   * gtr_adamw_small: every other parameter (flat buffer, partial slabs summed).
+
+#include <hipcub/hipcub.hpp>
+
+#include <cstdarg>
+#include <cstdio>
+
+#include "gtr_common.cuh"
+
+namespace gtr {
+
+static thread_local char g_err[512] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+}  // namespace gtr
+
+namespace {
+
+using namespace gtr;
+
+struct SmallK {
+  float* param;
+  float* m;
+  float* v;
+  float* grad_out;
+  int64_t total;
+  int nseg, pad0;
+  gtr_adam opt;
+  gtr_segment segs[GTR_SMALL_MAX_SEG];
+};
+
+__global__ __launch_bounds__(GTR_BLOCK) void k_adamw_small(SmallK a) {
+  __shared__ AdamStep s_st;
+  const int64_t e = (int64_t)blockIdx.x * GTR_BLOCK + threadIdx.x;
+  if (a.grad_out == nullptr && threadIdx.x == 0) s_st.init(a.opt, *a.opt.step_dev + 1);
+  __syncthreads();
+  int s = -1;
+  for (int i = 0; i < a.nseg; ++i)
+    if (e >= a.segs[i].begin && e < a.segs[i].begin + a.segs[i].len) s = i;
+  if (s < 0) return;
+  const gtr_segment& sg = a.segs[s];
+  const int64_t off = e - sg.begin;
+  float g = 0.0f;
+  for (int p = 0; p < sg.nparts; ++p) g += sg.src[(int64_t)p * sg.pstride + off];
+  if (a.grad_out) {
+    a.grad_out[e] = g;
+    return;
+  }
+  const AdamStep st = s_st;
+  float pv = a.param[e], mv = a.m[e], vv = a.v[e];
+  st.apply(pv, mv, vv, g);
+  a.param[e] = pv;
+  a.m[e] = mv;
+  a.v[e] = vv;
+}
+
+__global__ __launch_bounds__(GTR_BLOCK) void k_contrib_prep(gtr_batch bt, int T, int32_t* keys, int32_t* vals,
+                                                            int32_t* stamp, const int64_t* step_dev) {
+  const int j = blockIdx.x * GTR_BLOCK + threadIdx.x;
+  const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
+  if (j >= m_cap) return;
+  const int N = bt.hdr[0], B = bt.hdr[1];
+  int key = T;
+  if (j < bt.n_cap) {
+    if (j < N) key = bt.node_item[j];
+  } else if (j < bt.n_cap + bt.b_cap) {
+    const int b = j - bt.n_cap;
+    if (b < B) key = bt.target[b];
+  } else {
+    const int q = j - bt.n_cap - bt.b_cap;
+    if (q / bt.n_neg < B) key = bt.negatives[q];
+  }
+  if (key < 0 || key > T) key = T;
+  keys[j] = key;
+  vals[j] = j;
+  if (stamp && key > 0 && key < T) stamp[key] = (int32_t)(*step_dev + 1);
+}
+
+template <int D>
+__global__ __launch_bounds__(GTR_BLOCK) void k_adamw_rows(gtr_batch bt, int T, const int32_t* skeys,
+                                                          const int32_t* svals, const float* dx0,
+                                                          const float* se, const float* coef_tgt,
+                                                          const float* coef_neg, float* table, float* m,
+                                                          float* v, float* grad_dense, gtr_adam opt) {
+  constexpr int VPL = D >= 64 ? D / 64 : 1;
+  constexpr int CHUNK = 16;
+  __shared__ AdamStep s_st;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (grad_dense == nullptr && threadIdx.x == 0) s_st.init(opt, *opt.step_dev + 1);
+  __syncthreads();
+  const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
+  const int d0 = lane * VPL;
+  const bool act = d0 < D;
+  const int c0 = (blockIdx.x * GTR_WAVES + wave) * CHUNK;
+  if (c0 >= m_cap) return;
+  const int c1 = min(m_cap, c0 + CHUNK);
+  for (int i = c0; i < c1; ++i) {
+    const int key = skeys[i];
+    if (key <= 0 || key >= T) continue;
+    if (i > 0 && skeys[i - 1] == key) continue;  // not a segment start
+    float g[VPL];
+#pragma unroll
+    for (int q = 0; q < VPL; ++q) g[q] = 0.0f;
+    for (int k = i; k < m_cap && skeys[k] == key; ++k) {
+      const int j = svals[k];
+      const float* src;
+      float c;
+      if (j < bt.n_cap) {
+        src = dx0 + (size_t)j * D;
+        c = 1.0f;
+      } else if (j < bt.n_cap + bt.b_cap) {
+        const int b = j - bt.n_cap;
+        src = se + (size_t)b * D;
+        c = coef_tgt[b];
+      } else {
+        const int qn = j - bt.n_cap - bt.b_cap;
+        src = se + (size_t)(qn / bt.n_neg) * D;
+        c = coef_neg[qn];
+      }
+#pragma unroll
+      for (int q = 0; q < VPL; ++q) g[q] += act ? c * src[d0 + q] : 0.0f;
+    }
+    if (!act) continue;
+    const size_t base = (size_t)key * D + d0;
+    if (grad_dense) {
+#pragma unroll
+      for (int q = 0; q < VPL; ++q) grad_dense[base + q] = g[q];
+    } else {
+      const AdamStep st = s_st;
+#pragma unroll
+      for (int q = 0; q < VPL; ++q) {
+        float pv = table[base + q], mv = m[base + q], vv = v[base + q];
+        st.apply(pv, mv, vv, g[q]);
+        table[base + q] = pv;
+        m[base + q] = mv;
+        v[base + q] = vv;
+      }
+    }
+  }
+}
+
+// Untouched rows: 16 B per thread per tensor, grid-stride; rows with stamp == step+1 skipped.
+__global__ __launch_bounds__(GTR_BLOCK) void k_adamw_sweep(int64_t nvec, int vpr_log2, const int32_t* stamp,
+                                                           float4* table, float4* m, float4* v, gtr_adam opt) {
+  __shared__ AdamStep s_st;
+  __shared__ int32_t s_t;
+  if (threadIdx.x == 0) {
+    const int64_t t = *opt.step_dev + 1;
+    s_st.init(opt, t);
+    s_t = (int32_t)t;
+  }
+  __syncthreads();
+  const AdamStep st = s_st;
+  const int32_t t = s_t;
+  const int64_t stride = (int64_t)gridDim.x * GTR_BLOCK;
+  for (int64_t i = (int64_t)blockIdx.x * GTR_BLOCK + threadIdx.x; i < nvec; i += stride) {
+    const int64_t row = i >> vpr_log2;
+    if (stamp[row] == t) continue;
+    float4 p = table[i], mm = m[i], vv = v[i];
+    st.apply(p.x, mm.x, vv.x, 0.0f);
+    st.apply(p.y, mm.y, vv.y, 0.0f);
+    st.apply(p.z, mm.z, vv.z, 0.0f);
+    st.apply(p.w, mm.w, vv.w, 0.0f);
+    table[i] = p;
+    m[i] = mm;
+    v[i] = vv;
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(GTR_BLOCK) void k_scatter_rows(gtr_batch bt, int mode, const float* src,
+                                                            const float* coef_tgt, const float* coef_neg,
+                                                            float* dense) {
+  constexpr int VPL = D >= 64 ? D / 64 : 1;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = blockIdx.x * GTR_WAVES + wave;
+  const int d0 = lane * VPL;
+  if (d0 >= D) return;
+  const int N = bt.hdr[0], B = bt.hdr[1];
+  int key;
+  const float* s;
+  float c;
+  if (mode == 0) {
+    if (r >= N) return;
+    key = bt.node_item[r];
+    s = src + (size_t)r * D;
+    c = 1.0f;
+  } else {
+    if (r >= B * (1 + bt.n_neg)) return;
+    if (r < B) {
+      key = bt.target[r];
+      s = src + (size_t)r * D;
+      c = coef_tgt[r];
+    } else {
+      const int q = r - B;
+      key = bt.negatives[q];
+      s = src + (size_t)(q / bt.n_neg) * D;
+      c = coef_neg[q];
+    }
+  }
+  if (key <= 0) return;  // padding_idx = 0
+#pragma unroll
+  for (int q = 0; q < VPL; ++q) atomicAdd(dense + (size_t)key * D + d0 + q, c * s[d0 + q]);
+}
+
+__global__ void k_step_end(int64_t* step_dev, uint32_t* rng_ctr) {
+  if (step_dev) *step_dev += 1;
+  if (rng_ctr) *rng_ctr += 1;
+}
+
+int key_bits(int T) {
+  int b = 1;
+  while ((1LL << b) <= (long long)T) ++b;
+  return b;
+}
+
+bool dim_ok(int D) { return D == 32 || D == 64 || D == 128 || D == 256; }
+
+}  // namespace
+
+extern "C" {
+
+int gtr_version(void) { return 100; }
+int gtr_abi_version(void) { return GTR_ABI_VERSION; }
+const char* gtr_last_error(void) { return gtr::g_err; }
+
+int gtr_device_check(int device) {
+  hipDeviceProp_t prop;
+  hipError_t e = hipGetDeviceProperties(&prop, device);
+  if (e != hipSuccess) {
+    set_error("gtr_device_check: %s", hipGetErrorString(e));
+    return (int)e;
+  }
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    set_error("gtr_device_check: device %d is %s, this library is built for gfx950", device, prop.gcnArchName);
+    return GTR_E_DEVICE;
+  }
+  return GTR_OK;
+}
+
+int gtr_adamw_small(float* param, float* m, float* v, float* grad_out, int64_t total, const gtr_segment* segs,
+                    int nseg, const gtr_adam* opt, gtr_stream_t stream) {
+  if (!segs || nseg <= 0 || nseg > GTR_SMALL_MAX_SEG || total <= 0) {
+    set_error("gtr_adamw_small: bad segment table (nseg=%d)", nseg);
+    return GTR_E_ARG;
+  }
+  if (!grad_out && (!param || !m || !v || !opt || !opt->step_dev)) {
+    set_error("gtr_adamw_small: missing optimizer state");
+    return GTR_E_ARG;
+  }
+  SmallK k{};
+  k.param = param; k.m = m; k.v = v; k.grad_out = grad_out; k.total = total; k.nseg = nseg;
+  if (opt) k.opt = *opt;
+  for (int i = 0; i < nseg; ++i) k.segs[i] = segs[i];
+  const int64_t blocks = (total + GTR_BLOCK - 1) / GTR_BLOCK;
+  hipLaunchKernelGGL(k_adamw_small, dim3((unsigned)blocks), dim3(GTR_BLOCK), 0, (hipStream_t)stream, k);
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+int gtr_contrib_prep(const gtr_batch* bt, int num_items, int32_t* keys, int32_t* vals, int32_t* stamp,
+                     const int64_t* step_dev, gtr_stream_t stream) {
+  if (!bt || !keys || !vals || (stamp && !step_dev) || bt->n_neg <= 0) {
+    set_error("gtr_contrib_prep: bad arguments");
+    return GTR_E_ARG;
+  }
+  const int m_cap = bt->n_cap + bt->b_cap * (1 + bt->n_neg);
+  const int blocks = (m_cap + GTR_BLOCK - 1) / GTR_BLOCK;
+  hipLaunchKernelGGL(k_contrib_prep, dim3(blocks), dim3(GTR_BLOCK), 0, (hipStream_t)stream, *bt, num_items,
+                     keys, vals, stamp, step_dev);
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+int gtr_contrib_sort_bytes(int m_cap, int num_items, size_t* bytes) {
+  if (!bytes || m_cap <= 0) { set_error("gtr_contrib_sort_bytes: bad arguments"); return GTR_E_ARG; }
+  size_t b = 0;
+  hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                                     (const int32_t*)nullptr, (int32_t*)nullptr, m_cap, 0,
+                                                     key_bits(num_items));
+  if (e != hipSuccess) { set_error("gtr_contrib_sort_bytes: %s", hipGetErrorString(e)); return (int)e; }
+  *bytes = b;
+  return GTR_OK;
+}
+
+int gtr_contrib_sort(const int32_t* keys, const int32_t* vals, int32_t* skeys, int32_t* svals, int m_cap,
+                     int num_items, void* tmp, size_t tmp_bytes, gtr_stream_t stream) {
+  size_t b = tmp_bytes;
+  hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, b, keys, skeys, vals, svals, m_cap, 0, key_bits(num_items),
+                                                     (hipStream_t)stream);
+  if (e != hipSuccess) { set_error("gtr_contrib_sort: %s", hipGetErrorString(e)); return (int)e; }
+  return GTR_OK;
+}
+
+int gtr_adamw_rows(const gtr_batch* bt, int num_items, int dim, const int32_t* skeys, const int32_t* svals,
+                   const float* dx0, const float* se, const float* coef_tgt, const float* coef_neg, float* table,
+                   float* m, float* v, float* grad_dense, const gtr_adam* opt, gtr_stream_t stream) {
+  if (!bt || !dim_ok(dim) || !skeys || !svals || !dx0 || !se || !coef_tgt || !coef_neg) {
+    set_error("gtr_adamw_rows: bad arguments");
+    return GTR_E_ARG;
+  }
+  if (!grad_dense && (!table || !m || !v || !opt || !opt->step_dev)) {
+    set_error("gtr_adamw_rows: missing optimizer state");
+    return GTR_E_ARG;
+  }
+  gtr_adam o{};
+  if (opt) o = *opt;
+  const int m_cap = bt->n_cap + bt->b_cap * (1 + bt->n_neg);
+  const int waves = (m_cap + 15) / 16;
+  const int blocks = (waves + GTR_WAVES - 1) / GTR_WAVES;
+  hipStream_t s = (hipStream_t)stream;
+#define GTR_ROWS(DD)                                                                                         \
+  hipLaunchKernelGGL(k_adamw_rows<DD>, dim3(blocks), dim3(GTR_BLOCK), 0, s, *bt, num_items, skeys, svals, dx0, \
+                     se, coef_tgt, coef_neg, table, m, v, grad_dense, o)
+  switch (dim) {
+    case 32: GTR_ROWS(32); break;
+    case 64: GTR_ROWS(64); break;
+    case 128: GTR_ROWS(128); break;
+    default: GTR_ROWS(256); break;
+  }
+#undef GTR_ROWS
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+int gtr_adamw_sweep(int num_items, int dim, const int32_t* stamp, float* table, float* m, float* v,
+                    const gtr_adam* opt, gtr_stream_t stream) {
+  if (!dim_ok(dim) || !stamp || !table || !m || !v || !opt || !opt->step_dev || num_items <= 0) {
+    set_error("gtr_adamw_sweep: bad arguments");
+    return GTR_E_ARG;
+  }
+  const int64_t nvec = (int64_t)num_items * dim / 4;
+  int vpr_log2 = 0;
+  while ((1 << vpr_log2) < dim / 4) ++vpr_log2;
+  int64_t blocks = (nvec + GTR_BLOCK - 1) / GTR_BLOCK;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(k_adamw_sweep, dim3((unsigned)blocks), dim3(GTR_BLOCK), 0, (hipStream_t)stream, nvec, vpr_log2,
+                     stamp, (float4*)table, (float4*)m, (float4*)v, *opt);
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+int gtr_scatter_rows(const gtr_batch* bt, int dim, int mode, const float* src, const float* coef_tgt,
+                     const float* coef_neg, float* dense, gtr_stream_t stream) {
+  if (!bt || !dim_ok(dim) || !src || !dense || (mode == 1 && (!coef_tgt || !coef_neg))) {
+    set_error("gtr_scatter_rows: bad arguments");
+    return GTR_E_ARG;
+  }
+  const int rows = mode == 0 ? bt->n_cap : bt->b_cap * (1 + bt->n_neg);
+  const int blocks = (rows + GTR_WAVES - 1) / GTR_WAVES;
+  if (blocks <= 0) return GTR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  switch (dim) {
+    case 32: hipLaunchKernelGGL(k_scatter_rows<32>, dim3(blocks), dim3(GTR_BLOCK), 0, s, *bt, mode, src, coef_tgt, coef_neg, dense); break;
+    case 64: hipLaunchKernelGGL(k_scatter_rows<64>, dim3(blocks), dim3(GTR_BLOCK), 0, s, *bt, mode, src, coef_tgt, coef_neg, dense); break;
+    case 128: hipLaunchKernelGGL(k_scatter_rows<128>, dim3(blocks), dim3(GTR_BLOCK), 0, s, *bt, mode, src, coef_tgt, coef_neg, dense); break;
+    default: hipLaunchKernelGGL(k_scatter_rows<256>, dim3(blocks), dim3(GTR_BLOCK), 0, s, *bt, mode, src, coef_tgt, coef_neg, dense); break;
+  }
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+int gtr_step_end(int64_t* step_dev, uint32_t* rng_ctr, gtr_stream_t stream) {
+  hipLaunchKernelGGL(k_step_end, dim3(1), dim3(1), 0, (hipStream_t)stream, step_dev, rng_ctr);
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,139 @@
+"""ctypes binding of libgtr_hip.so (the C ABI declared in include/gtr.h).
+
+This is the FFI a maintainer of the reference would add: plain
+pointers, int sizes and a hipStream_t; non-zero status -> RuntimeError with the
+library's message.  The library is built in-tree (``gat-recommendation_amd/build``)
+by ``__graft_entry__.build()`` / ``make -C gat-recommendation_amd/csrc``.  There is
+no fallback: if the library is missing, every compute call raises.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(os.path.dirname(_HERE))  # gat-recommendation_amd/
+LIB_PATH = os.environ.get("GTR_LIB", os.path.join(PKG_ROOT, "build", "libgtr_hip.so"))
+
+P = C.c_void_p
+i32 = C.c_int32
+i64 = C.c_int64
+f32 = C.c_float
+u32 = C.c_uint32
+
+
+class GtrBatch(C.Structure):
+    _fields_ = [
+        ("hdr", P), ("node_item", P), ("node_ptr", P), ("in_ptr", P), ("in_src", P),
+        ("out_ptr", P), ("out_edge", P), ("out_dst", P), ("target", P), ("negatives", P),
+        ("node_pe", P), ("n_cap", i32), ("b_cap", i32), ("e_cap", i32), ("n_neg", i32),
+    ]
+
+
+class GtrConfig(C.Structure):
+    _fields_ = [
+        ("num_items", i32), ("dim", i32), ("heads", i32), ("pe_k", i32), ("num_layers", i32),
+        ("row_group", i32), ("training", i32), ("dropout", f32), ("bn_eps", f32),
+        ("bn_momentum", f32), ("seed", u32), ("rng_ctr", P),
+    ]
+
+
+class GtrLayer(C.Structure):
+    _fields_ = [
+        ("w_all", P), ("b_all", P), ("w_beta", P), ("bn_gamma", P), ("bn_beta", P),
+        ("bn_rmean", P), ("bn_rvar", P), ("bn_nbt", P),
+        ("xin", P), ("qkvs", P), ("alpha", P), ("agg", P), ("gate", P), ("out", P),
+        ("bn_stats", P), ("bn_part", P), ("bn_gsum", P), ("bn_gpart", P), ("cnt", P),
+        ("dy", P), ("dqkvs", P), ("du", P), ("dlogit", P), ("dagg", P),
+    ]
+
+
+class GtrEmbed(C.Structure):
+    _fields_ = [("table", P), ("pe_tab", P), ("wpe", P), ("bpe", P)]
+
+
+class GtrHead(C.Structure):
+    _fields_ = [
+        ("flags", i32), ("loss_kind", i32), ("temperature", f32), ("dual_alpha", f32),
+        ("se", P), ("dse_in", P), ("dse_out", P), ("coef_tgt", P), ("coef_neg", P),
+        ("loss_part", P), ("loss_out", P), ("cnt", P),
+    ]
+
+
+class GtrSegment(C.Structure):
+    _fields_ = [
+        ("begin", i64), ("len", i64), ("src", P), ("pstride", i64), ("nparts", i32), ("pad", i32),
+    ]
+
+
+class GtrAdam(C.Structure):
+    _fields_ = [
+        ("lr", f32), ("beta1", f32), ("beta2", f32), ("eps", f32), ("weight_decay", f32),
+        ("decoupled", i32), ("step_dev", P),
+    ]
+
+
+GTR_LOSS = {"none": 0, "bpr": 1, "listwise": 2, "sampled_softmax": 2, "dual": 3}
+RO_FWD, RO_LOSS, RO_BWD = 1, 2, 4
+SMALL_MAX_SEG = 48
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "gtr_version": (C.c_int, []),
+    "gtr_abi_version": (C.c_int, []),
+    "gtr_last_error": (C.c_char_p, []),
+    "gtr_device_check": (C.c_int, [C.c_int]),
+    "gtr_conv_fwd": (C.c_int, [P, P, P, P, C.c_int, P]),
+    "gtr_readout_loss": (C.c_int, [P, P, P, P, P, P]),
+    "gtr_conv_bwd": (C.c_int, [P, P, P, C.c_int, P, P]),
+    "gtr_wgrad": (C.c_int, [P, P, P, P, P, P, P, C.c_int, i64, P]),
+    "gtr_adamw_small": (C.c_int, [P, P, P, P, i64, P, C.c_int, P, P]),
+    "gtr_contrib_prep": (C.c_int, [P, C.c_int, P, P, P, P, P]),
+    "gtr_contrib_sort_bytes": (C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_size_t)]),
+    "gtr_contrib_sort": (C.c_int, [P, P, P, P, C.c_int, C.c_int, P, C.c_size_t, P]),
+    "gtr_adamw_rows": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P, P, P, P, P, P, P]),
+    "gtr_adamw_sweep": (C.c_int, [C.c_int, C.c_int, P, P, P, P, P, P]),
+    "gtr_scatter_rows": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P]),
+    "gtr_step_end": (C.c_int, [P, P, P]),
+}
+
+EXPORTS = tuple(_SIGS)
+
+_lib = None
+
+
+class GtrLibraryMissing(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libgtr_hip.so once; raise loudly if it is absent (no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise GtrLibraryMissing(
+                f"libgtr_hip.so not found at {LIB_PATH}; build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` or "
+                "`make -C gat-recommendation_amd/csrc` (hipcc --offload-arch=gfx950)"
+            )
+        h = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(h, name)
+            fn.restype = res
+            fn.argtypes = args
+        if h.gtr_abi_version() != 1:
+            raise RuntimeError("libgtr_hip.so ABI version mismatch")
+        _lib = h
+    return _lib
+
+
+def check(status: int, what: str = "") -> None:
+    if status != 0:
+        msg = lib().gtr_last_error().decode(errors="replace")
+        raise RuntimeError(f"libgtr_hip {what} failed (status {status}): {msg}")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a torch tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,380 @@
+"""Device-side engine of the GraphTransformer hot path.
+
+Owns (per model):
+  * the flat dense-parameter buffer: every parameter except the item table is a
+    view into one fp32 buffer laid out in 256-aligned segments
+    [w_all (query,key,value,skip) | b_all | w_beta | bn_gamma | bn_beta] per layer
+    and [wpe | bpe] for the LapPE projection, so one kernel updates them all;
+  * per-capacity workspaces (saved activations, gradient slabs, arrival counters);
+  * the ctypes argument structs, built once per workspace so a launch costs one
+    foreign call.
+
+Kernel order of one training step:
+  conv_fwd(0..L-1) -> readout_loss(FWD|LOSS|BWD) -> conv_bwd(L-1..0) -> wgrad
+  -> adamw_rows + adamw_small (-> step_end); contrib_prep -> adamw_sweep and
+  contrib_sort run on side streams, overlapped with the chain.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass
+
+import torch
+
+from etpgt.backend import _lib as L
+from etpgt.data.batch import Caps, SessionBatch, blob_layout
+
+ALIGN = 256
+
+
+def _al(n: int) -> int:
+    return (n + ALIGN - 1) // ALIGN * ALIGN
+
+
+@dataclass
+class Seg:
+    name: str
+    begin: int
+    numel: int
+    shape: tuple
+
+
+class ParamLayout:
+    """Flat layout of the dense (non-table) parameters of a GraphTransformer."""
+
+    def __init__(self, D: int, L_: int, pe_k: int):
+        self.D, self.L, self.K = D, L_, pe_k
+        self.segs: dict[str, Seg] = {}
+        off = 0
+
+        def add(name, shape):
+            nonlocal off
+            n = int(math.prod(shape))
+            self.segs[name] = Seg(name, off, n, tuple(shape))
+            off += _al(n)
+
+        for l in range(L_):
+            add(f"{l}.w_all", (4 * D, D))
+            add(f"{l}.b_all", (4 * D,))
+            add(f"{l}.w_beta", (1, 3 * D))
+            add(f"{l}.gamma", (D,))
+            add(f"{l}.beta", (D,))
+        if pe_k > 0:
+            add("pe.w", (D, pe_k))
+            add("pe.b", (D,))
+        self.total = off
+        self.layer_block = 4 * D * D + 4 * D + 3 * D   # slab layout of one layer
+        self.pe_block = D * pe_k + D if pe_k > 0 else 0
+        self.slab_stride = _al(max(self.layer_block, self.pe_block))
+
+    def seg(self, name: str) -> Seg:
+        return self.segs[name]
+
+
+def model_param_map(model) -> list[tuple[str, torch.nn.Parameter, int]]:
+    """(flat segment, parameter, row offset) for every dense parameter of the model."""
+    D = model.hidden_dim
+    out = []
+    for l, (conv, bn) in enumerate(zip(model.convs, model.batch_norms)):
+        out += [
+            (f"{l}.w_all", conv.lin_query.weight, 0), (f"{l}.w_all", conv.lin_key.weight, D),
+            (f"{l}.w_all", conv.lin_value.weight, 2 * D), (f"{l}.w_all", conv.lin_skip.weight, 3 * D),
+            (f"{l}.b_all", conv.lin_query.bias, 0), (f"{l}.b_all", conv.lin_key.bias, D),
+            (f"{l}.b_all", conv.lin_value.bias, 2 * D), (f"{l}.b_all", conv.lin_skip.bias, 3 * D),
+            (f"{l}.w_beta", conv.lin_beta.weight, 0),
+            (f"{l}.gamma", bn.weight, 0), (f"{l}.beta", bn.bias, 0),
+        ]
+    if model.use_laplacian_pe:
+        out += [("pe.w", model.laplacian_pe.projection.weight, 0), ("pe.b", model.laplacian_pe.projection.bias, 0)]
+    return out
+
+
+class FlatParams:
+    """Re-points the model's dense parameters at views of one flat device buffer."""
+
+    def __init__(self, model, device):
+        self.model = model
+        self.layout = ParamLayout(model.hidden_dim, model.num_layers, model.laplacian_k if model.use_laplacian_pe else 0)
+        self.device = device
+        self.flat = torch.zeros(self.layout.total, dtype=torch.float32, device=device)
+        self.map = model_param_map(model)
+        D = model.hidden_dim
+        with torch.no_grad():
+            for name, p, row in self.map:
+                view = self._view(name, p, row, D)
+                view.copy_(p.data.to(device=device, dtype=torch.float32))
+                p.data = view
+        self._ptrs = self._snapshot()
+
+    def _view(self, name, p, row, D):
+        s = self.layout.seg(name)
+        n = p.numel()
+        start = s.begin + row * (D if name.endswith("w_all") else 1)
+        return self.flat[start : start + n].view(p.shape)
+
+    def _snapshot(self):
+        return tuple(p.data_ptr() for _, p, _ in self.map)
+
+    def intact(self) -> bool:
+        return self._snapshot() == self._ptrs
+
+    def params(self) -> list[torch.nn.Parameter]:
+        return [p for _, p, _ in self.map]
+
+    def grad_views(self, flat_grad: torch.Tensor) -> list[torch.Tensor]:
+        D = self.model.hidden_dim
+        out = []
+        for name, p, row in self.map:
+            s = self.layout.seg(name)
+            start = s.begin + row * (D if name.endswith("w_all") else 1)
+            out.append(flat_grad[start : start + p.numel()].view(p.shape))
+        return out
+
+    def seg_ptr(self, name: str) -> int:
+        return self.flat.data_ptr() + 4 * self.layout.seg(name).begin
+
+
+def _i32(n, device):
+    return torch.zeros(max(int(n), 1), dtype=torch.int32, device=device)
+
+
+def _f32(*shape, device):
+    return torch.zeros(*[max(int(s), 1) for s in shape], dtype=torch.float32, device=device)
+
+
+class Workspace:
+    """Capacity-sized activations + gradient buffers for one in-flight batch."""
+
+    def __init__(self, eng: "Engine", caps: Caps, R: int, P: int):
+        dev = eng.device
+        D, H, Lc = eng.D, eng.H, eng.L
+        self.caps, self.R, self.P = caps, R, P
+        n, b, e, k = caps.n_cap, caps.b_cap, caps.e_cap, max(caps.n_neg, 1)
+        g = (n + R - 1) // R
+        self.g_cap = g
+        self.layers = []
+        self.structs = (L.GtrLayer * Lc)()
+        for l in range(Lc):
+            t = dict(
+                xin=_f32(n, D, device=dev), qkvs=_f32(n, 4 * D, device=dev), alpha=_f32(e, H, device=dev),
+                agg=_f32(n, D, device=dev), gate=_f32(n, device=dev), out=_f32(n, D, device=dev),
+                bn_stats=_f32(2 * D, device=dev), bn_part=_f32(g, 1 + 2 * D, device=dev),
+                bn_gsum=_f32(2 * D, device=dev), bn_gpart=_f32(max(g, 256), 2 * D, device=dev),
+                cnt=_i32(4, dev), dy=_f32(n, D, device=dev), dqkvs=_f32(n, 4 * D, device=dev),
+                du=_f32(n, device=dev), dlogit=_f32(e, H, device=dev), dagg=_f32(n, D, device=dev),
+            )
+            self.layers.append(t)
+        self.dx0 = _f32(n, D, device=dev)
+        self.se = _f32(b, D, device=dev)
+        self.dse_in = _f32(b, D, device=dev)
+        self.dse_out = _f32(b, D, device=dev)
+        self.coef_tgt = _f32(b, device=dev)
+        self.coef_neg = _f32(b * k, device=dev)
+        self.loss_part = _f32(512, device=dev)
+        self.loss_out = _f32(1, device=dev)
+        self.head_cnt = _i32(4, dev)
+        lay = eng.flat.layout
+        self.slabs = _f32(Lc, P, lay.slab_stride, device=dev)
+        self.pe_slab = _f32(P, lay.slab_stride, device=dev) if eng.K > 0 else None
+        self.slab_ptrs = (C.c_void_p * Lc)(*[self.slabs[l].data_ptr() for l in range(Lc)])
+        self.head = L.GtrHead()
+        self._fill_layer_structs(eng)
+
+    def _fill_layer_structs(self, eng):
+        for l, t in enumerate(self.layers):
+            s = self.structs[l]
+            for f in ("xin", "qkvs", "alpha", "agg", "gate", "out", "bn_stats", "bn_part", "bn_gsum",
+                      "bn_gpart", "cnt", "dy", "dqkvs", "du", "dlogit", "dagg"):
+                setattr(s, f, t[f].data_ptr())
+        self.refresh_params(eng)
+
+    def refresh_params(self, eng):
+        for l in range(eng.L):
+            s = self.structs[l]
+            bn = eng.model.batch_norms[l]
+            s.w_all = eng.flat.seg_ptr(f"{l}.w_all")
+            s.b_all = eng.flat.seg_ptr(f"{l}.b_all")
+            s.w_beta = eng.flat.seg_ptr(f"{l}.w_beta")
+            s.bn_gamma = eng.flat.seg_ptr(f"{l}.gamma")
+            s.bn_beta = eng.flat.seg_ptr(f"{l}.beta")
+            s.bn_rmean = bn.running_mean.data_ptr()
+            s.bn_rvar = bn.running_var.data_ptr()
+            s.bn_nbt = bn.num_batches_tracked.data_ptr()
+
+
+class Engine:
+    """Binds a GraphTransformer (reference layout) to libgtr_hip on one device."""
+
+    def __init__(self, model, device: torch.device):
+        if device.type != "cuda":
+            raise RuntimeError("the GraphTransformer hot path runs on an MI355X (gfx950) GPU only")
+        lib = L.lib()
+        L.check(lib.gtr_device_check(device.index if device.index is not None else torch.cuda.current_device()),
+                "device check")
+        self.model = model
+        self.device = device
+        self.D = model.hidden_dim
+        self.H = model.num_heads
+        self.L = model.num_layers
+        self.K = model.laplacian_k if model.use_laplacian_pe else 0
+        self.T = model.num_items
+        self.flat = FlatParams(model, device)
+        self.rng_ctr = torch.zeros(1, dtype=torch.int32, device=device)
+        self.seed = int(torch.randint(0, 2**31 - 1, (1,), generator=torch.Generator().manual_seed(0x5EED)).item())
+        self.embed = L.GtrEmbed()
+        self._ws_cache: dict[Caps, Workspace] = {}
+
+    # ------------------------------------------------------------------ helpers
+    def check_intact(self):
+        if not self.flat.intact():
+            raise RuntimeError("model parameters were re-allocated after binding the HIP engine "
+                               "(e.g. model.to()); re-create the engine")
+
+    def choose_R(self, caps: Caps) -> int:
+        return 16 if caps.n_cap <= 8192 else (32 if caps.n_cap <= 65536 else 64)
+
+    def choose_P(self, caps: Caps) -> int:
+        return max(1, min(32, (caps.n_cap + 511) // 512))
+
+    def workspace(self, caps: Caps, fresh: bool = False) -> Workspace:
+        if fresh:
+            return Workspace(self, caps, self.choose_R(caps), self.choose_P(caps))
+        ws = self._ws_cache.pop(caps, None)
+        if ws is None:
+            ws = Workspace(self, caps, self.choose_R(caps), self.choose_P(caps))
+        self._ws_cache[caps] = ws  # most recently used last
+        while len(self._ws_cache) > 8:
+            self._ws_cache.pop(next(iter(self._ws_cache)))
+        return ws
+
+    def config(self, ws: Workspace, training: bool) -> L.GtrConfig:
+        m = self.model
+        cfg = L.GtrConfig()
+        cfg.num_items = self.T
+        cfg.dim = self.D
+        cfg.heads = self.H
+        cfg.pe_k = self.K
+        cfg.num_layers = self.L
+        cfg.row_group = ws.R
+        cfg.training = 1 if training else 0
+        cfg.dropout = float(m.dropout)
+        bn = m.batch_norms[0]
+        cfg.bn_eps = float(bn.eps)
+        cfg.bn_momentum = float(bn.momentum if bn.momentum is not None else 0.1)
+        cfg.seed = self.seed
+        cfg.rng_ctr = self.rng_ctr.data_ptr()
+        return cfg
+
+    def fill_embed(self):
+        m = self.model
+        e = self.embed
+        e.table = m.item_embedding.weight.data_ptr()
+        if self.K > 0:
+            pe = m.laplacian_pe._cached_pe
+            e.pe_tab = None if pe is None else pe.data_ptr()
+            e.wpe = self.flat.seg_ptr("pe.w")
+            e.bpe = self.flat.seg_ptr("pe.b")
+        else:
+            e.pe_tab = e.wpe = e.bpe = None
+        return e
+
+    @staticmethod
+    def batch_struct(caps: Caps, blob: torch.Tensor, node_pe: torch.Tensor | None = None) -> L.GtrBatch:
+        lay = blob_layout(caps)
+        base = blob.data_ptr()
+        bs = L.GtrBatch()
+        for name in ("hdr", "node_item", "node_ptr", "in_ptr", "in_src", "out_ptr", "out_edge", "out_dst",
+                     "target", "negatives"):
+            setattr(bs, name, base + 4 * lay[name][0])
+        bs.node_pe = None if node_pe is None else node_pe.data_ptr()
+        bs.n_cap, bs.b_cap, bs.e_cap, bs.n_neg = caps.n_cap, caps.b_cap, caps.e_cap, caps.n_neg
+        return bs
+
+    def stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    # ------------------------------------------------------------------ launches
+    def run_forward(self, ws: Workspace, cfg: L.GtrConfig, bs: L.GtrBatch, flags: int,
+                    loss_kind: int = 0, temperature: float = 1.0, alpha: float = 0.7):
+        lib = L.lib()
+        st = self.stream()
+        emb = self.fill_embed()
+        for l in range(self.L):
+            L.check(lib.gtr_conv_fwd(C.byref(cfg), C.byref(bs), C.byref(emb), ws.structs, l, st), "conv_fwd")
+        self.run_head(ws, cfg, bs, flags, loss_kind, temperature, alpha)
+
+    def run_head(self, ws, cfg, bs, flags, loss_kind=0, temperature=1.0, alpha=0.7, dse_out=False):
+        h = ws.head
+        h.flags = flags
+        h.loss_kind = loss_kind
+        h.temperature = float(temperature)
+        h.dual_alpha = float(alpha)
+        h.se = ws.se.data_ptr()
+        h.dse_in = ws.dse_in.data_ptr()
+        h.dse_out = ws.dse_out.data_ptr() if dse_out else None
+        h.coef_tgt = ws.coef_tgt.data_ptr()
+        h.coef_neg = ws.coef_neg.data_ptr()
+        h.loss_part = ws.loss_part.data_ptr()
+        h.loss_out = ws.loss_out.data_ptr()
+        h.cnt = ws.head_cnt.data_ptr()
+        L.check(L.lib().gtr_readout_loss(C.byref(cfg), C.byref(bs), self.model.item_embedding.weight.data_ptr(),
+                                         ws.structs, C.byref(h), self.stream()), "readout_loss")
+
+    def run_backward(self, ws: Workspace, cfg: L.GtrConfig, bs: L.GtrBatch):
+        """conv_bwd(L-1..0) + weight-gradient slabs; expects layers[L-1].dy / bn_gsum."""
+        lib = L.lib()
+        st = self.stream()
+        for l in range(self.L - 1, -1, -1):
+            L.check(lib.gtr_conv_bwd(C.byref(cfg), C.byref(bs), ws.structs, l, ws.dx0.data_ptr(), st), "conv_bwd")
+        pe_tab = None
+        if self.K > 0 and self.model.laplacian_pe._cached_pe is not None:
+            pe_tab = self.model.laplacian_pe._cached_pe.data_ptr()
+        L.check(lib.gtr_wgrad(C.byref(cfg), C.byref(bs), ws.structs, ws.dx0.data_ptr(), pe_tab, ws.slab_ptrs,
+                              None if ws.pe_slab is None else ws.pe_slab.data_ptr(), ws.P,
+                              self.flat.layout.slab_stride, st), "wgrad")
+
+    def segments(self, ws: Workspace):
+        """Segment table mapping each flat parameter segment to its gradient source."""
+        lay = self.flat.layout
+        segs = []
+        D, K = self.D, self.K
+        stride = lay.slab_stride
+        for l in range(self.L):
+            base = ws.slabs[l].data_ptr()
+            g = ws.layers[l]["bn_gsum"].data_ptr()
+            for name, src, n in ((f"{l}.w_all", base, ws.P), (f"{l}.b_all", base + 4 * (4 * D * D), ws.P),
+                                 (f"{l}.w_beta", base + 4 * (4 * D * D + 4 * D), ws.P),
+                                 (f"{l}.gamma", g + 4 * D, 1), (f"{l}.beta", g, 1)):
+                s = lay.seg(name)
+                segs.append((s.begin, s.numel, src, stride, n))
+        if K > 0:
+            base = ws.pe_slab.data_ptr()
+            for name, src in (("pe.w", base), ("pe.b", base + 4 * D * K)):
+                s = lay.seg(name)
+                segs.append((s.begin, s.numel, src, stride, ws.P))
+        arr = (L.GtrSegment * len(segs))()
+        for i, (b, n, src, ps, npart) in enumerate(segs):
+            arr[i].begin, arr[i].len, arr[i].src, arr[i].pstride, arr[i].nparts = b, n, src, ps, npart
+        return arr, len(segs)
+
+    def reduce_small_grads(self, ws: Workspace, flat_grad: torch.Tensor):
+        segs, n = self.segments(ws)
+        L.check(L.lib().gtr_adamw_small(None, None, None, flat_grad.data_ptr(), self.flat.layout.total, segs, n,
+                                        None, self.stream()), "adamw_small(reduce)")
+
+    # ------------------------------------------------------------------ batches
+    def prepare(self, batch) -> tuple[Caps, torch.Tensor, torch.Tensor | None]:
+        if not isinstance(batch, SessionBatch):
+            batch = SessionBatch(batch.x, batch.edge_index, getattr(batch, "batch", None),
+                                 getattr(batch, "target_item", None), getattr(batch, "negative_items", None),
+                                 getattr(batch, "laplacian_pe", None), getattr(batch, "ptr", None))
+        batch.check_ids(self.T)
+        caps, blob = batch.device_blob(self.device)
+        pe = batch.laplacian_pe
+        node_pe = None
+        if self.K > 0 and pe is not None:
+            node_pe = torch.zeros(caps.n_cap, self.K, dtype=torch.float32, device=self.device)
+            node_pe[: pe.shape[0]].copy_(pe.to(self.device, torch.float32))
+        return caps, blob, node_pe

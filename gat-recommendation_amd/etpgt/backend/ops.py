@@ -1,0 +1,139 @@
+"""Autograd entry points over libgtr_hip (the eager / torch.autograd path).
+
+* ``score_loss``: BPR / listwise / dual sampled scoring loss (base.py:80-113,
+  losses.py:8-201) — forward and backward in one kernel launch, the backward
+  applied with the saved coefficients (dense table gradient by ``gtr_scatter_rows``).
+* ``GraphTransformerFn``: the whole GraphTransformer forward (all layers + mean
+  readout) as one autograd node; its backward runs readout-bwd, conv_bwd per
+  layer, the weight-gradient kernel and the slab reduction.
+
+The fused training step (etpgt.train.fused) drives the same kernels without
+autograd and with the optimizer fused in.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from etpgt.backend import _lib as L
+
+
+def _dev_i32(t: torch.Tensor, device) -> torch.Tensor:
+    return t.to(device=device, dtype=torch.int32).contiguous()
+
+
+class _ScoreLossFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, se, table, target, negatives, kind, temperature, alpha):
+        lib = L.lib()
+        dev = se.device
+        B, D = se.shape
+        n = negatives.numel() // max(B, 1)
+        if D not in (32, 64, 128, 256):
+            raise ValueError(f"embedding dim {D} unsupported by the HIP scoring kernel")
+        if table.shape[1] != D:
+            raise ValueError("session embedding and item table dims differ")
+        se_c = se.detach().float().contiguous()
+        tgt = _dev_i32(target.reshape(-1), dev)
+        neg = _dev_i32(negatives.reshape(-1), dev)
+        hdr = torch.tensor([0, B, 0, n, 0, 0, 0, 0], dtype=torch.int32, device=dev)
+        node_ptr = torch.zeros(B + 1, dtype=torch.int32, device=dev)
+        bs = L.GtrBatch()
+        bs.hdr, bs.node_ptr, bs.target, bs.negatives = hdr.data_ptr(), node_ptr.data_ptr(), tgt.data_ptr(), neg.data_ptr()
+        bs.n_cap, bs.b_cap, bs.e_cap, bs.n_neg = 1, B, 1, n
+        cfg = L.GtrConfig()
+        cfg.num_items, cfg.dim, cfg.heads, cfg.num_layers, cfg.row_group = table.shape[0], D, 1, 1, 16
+        cfg.training, cfg.bn_eps, cfg.bn_momentum = 0, 1e-5, 0.1
+        layer = (L.GtrLayer * 1)()
+        dse = torch.empty(B, D, dtype=torch.float32, device=dev)
+        coef_t = torch.empty(B, dtype=torch.float32, device=dev)
+        coef_n = torch.empty(max(B * n, 1), dtype=torch.float32, device=dev)
+        part = torch.empty(512, dtype=torch.float32, device=dev)
+        loss = torch.empty(1, dtype=torch.float32, device=dev)
+        cnt = torch.zeros(4, dtype=torch.int32, device=dev)
+        h = L.GtrHead()
+        h.flags, h.loss_kind, h.temperature, h.dual_alpha = L.RO_LOSS, L.GTR_LOSS[kind], float(temperature), float(alpha)
+        h.se, h.dse_out, h.coef_tgt, h.coef_neg = se_c.data_ptr(), dse.data_ptr(), coef_t.data_ptr(), coef_n.data_ptr()
+        h.loss_part, h.loss_out, h.cnt = part.data_ptr(), loss.data_ptr(), cnt.data_ptr()
+        tab = table.detach().contiguous()
+        st = torch.cuda.current_stream(dev).cuda_stream
+        L.check(lib.gtr_readout_loss(C.byref(cfg), C.byref(bs), tab.data_ptr(), layer, C.byref(h), st), "score_loss")
+        ctx.save_for_backward(se_c, dse, coef_t, coef_n, tgt, neg, hdr, node_ptr)
+        ctx.meta = (table.shape, D, n)
+        return loss.reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        se_c, dse, coef_t, coef_n, tgt, neg, hdr, node_ptr = ctx.saved_tensors
+        (T, D), _, n = ctx.meta
+        dse_g = dse * g if ctx.needs_input_grad[0] else None
+        dtab = None
+        if ctx.needs_input_grad[1]:
+            dtab = torch.zeros(T, D, dtype=torch.float32, device=se_c.device)
+            bs = L.GtrBatch()
+            bs.hdr, bs.node_ptr, bs.target, bs.negatives = hdr.data_ptr(), node_ptr.data_ptr(), tgt.data_ptr(), neg.data_ptr()
+            bs.n_cap, bs.b_cap, bs.e_cap, bs.n_neg = 1, se_c.shape[0], 1, n
+            st = torch.cuda.current_stream(se_c.device).cuda_stream
+            L.check(L.lib().gtr_scatter_rows(C.byref(bs), D, 1, se_c.data_ptr(), coef_t.data_ptr(), coef_n.data_ptr(),
+                                             dtab.data_ptr(), st), "scatter_rows")
+            dtab = dtab * g
+        return dse_g, dtab, None, None, None, None, None
+
+
+def score_loss(se, target, negatives, table, kind="bpr", temperature=1.0, alpha=0.7):
+    """Sampled scoring loss on the HIP kernel.  ``table`` is the item-table weight
+    (or an nn.Embedding)."""
+    if isinstance(table, torch.nn.Embedding):
+        table = table.weight
+    if se.device.type != "cuda":
+        raise RuntimeError("score_loss runs on the MI355X HIP path only (tensors are on CPU)")
+    if kind not in L.GTR_LOSS or kind == "none":
+        raise ValueError(f"Unknown loss type: {kind}")
+    B = se.shape[0]
+    if negatives.dim() == 1:
+        negatives = negatives.view(B, -1)
+    return _ScoreLossFn.apply(se, table, target, negatives, kind, temperature, alpha)
+
+
+class GraphTransformerFn(torch.autograd.Function):
+    """Whole-model forward as one autograd node (inputs: table + dense params)."""
+
+    @staticmethod
+    def forward(ctx, eng, caps, blob, node_pe, B, training, need_grad, table, *params):
+        eng.check_intact()
+        need_grad = bool(need_grad) and training
+        ws = eng.workspace(caps, fresh=need_grad)
+        rng = torch.empty(1, dtype=torch.int32, device=eng.device)
+        rng.copy_(eng.rng_ctr)
+        if training:
+            eng.rng_ctr.add_(1)
+        cfg = eng.config(ws, training)
+        cfg.rng_ctr = rng.data_ptr()
+        bs = eng.batch_struct(caps, blob, node_pe)
+        eng.run_forward(ws, cfg, bs, L.RO_FWD)
+        se = ws.se[:B].clone()
+        ctx.eng = None
+        if need_grad:
+            ctx.eng, ctx.ws, ctx.cfg, ctx.bs, ctx.B = eng, ws, cfg, bs, B
+            ctx.keep = (blob, node_pe, rng)
+        return se
+
+    @staticmethod
+    def backward(ctx, dse):
+        if ctx.eng is None:
+            raise RuntimeError("backward through the GraphTransformer requires train() mode "
+                               "(BatchNorm batch statistics) and grad mode at forward time")
+        eng, ws, cfg, bs, B = ctx.eng, ctx.ws, ctx.cfg, ctx.bs, ctx.B
+        ws.dse_in[:B].copy_(dse)
+        eng.run_head(ws, cfg, bs, L.RO_BWD)
+        eng.run_backward(ws, cfg, bs)
+        flat_grad = torch.empty(eng.flat.layout.total, dtype=torch.float32, device=eng.device)
+        eng.reduce_small_grads(ws, flat_grad)
+        table = eng.model.item_embedding.weight
+        dtab = torch.zeros_like(table)
+        L.check(L.lib().gtr_scatter_rows(C.byref(bs), eng.D, 0, ws.dx0.data_ptr(), None, None, dtab.data_ptr(),
+                                         eng.stream()), "scatter_rows")
+        grads = eng.flat.grad_views(flat_grad)
+        return (None, None, None, None, None, None, None, dtab, *grads)

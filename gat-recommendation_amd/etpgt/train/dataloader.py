@@ -1,0 +1,123 @@
+"""Session dataset / collate — API of etpgt/train/dataloader.py (reference).
+
+Same constructor, item semantics and batch layout as the reference
+(dataloader.py:22-241): sessions sorted by timestamp, truncated to the last
+``max_session_length`` events, target = last event, context = the rest,
+negatives drawn with ``torch.randint(1, num_items)`` rejecting session items,
+induced subgraph = graph edges with both endpoints in the context in the stored
+``(item_i, item_j)`` direction.  Differences are in HOW, not WHAT: the induced
+subgraph is found by binary search over sorted edge keys instead of a pandas
+``isin`` over all 737k edges per session (≈24 ms -> tens of µs), and
+``collate_fn`` returns an ``etpgt.data.SessionBatch`` (PyG ``Batch`` duck type
+with the packed CSR image the HIP kernels consume).
+"""
+
+from __future__ import annotations
+
+from pathlib import Path
+
+import numpy as np
+import pandas as pd
+import torch
+from torch.utils.data import Dataset
+
+from etpgt.data.batch import SessionBatch
+
+
+class SessionDataset(Dataset):
+    def __init__(self, sessions_path: Path | str, graph_edges_path: Path | str, num_negatives: int = 5,
+                 max_session_length: int = 50):
+        self.sessions_path = Path(sessions_path)
+        self.graph_edges_path = Path(graph_edges_path)
+        self.num_negatives = num_negatives
+        self.max_session_length = max_session_length
+        self.sessions_df = pd.read_csv(sessions_path)
+        df = self.sessions_df.sort_values(["session_id", "timestamp"], kind="stable")
+        sid = df["session_id"].to_numpy()
+        self._items = df["itemid"].to_numpy().astype(np.int64)
+        bounds = np.nonzero(np.r_[True, sid[1:] != sid[:-1], True])[0]
+        self._ptr = bounds
+        self.session_ids = list(sid[bounds[:-1]])
+        g = pd.read_csv(graph_edges_path, usecols=["item_i", "item_j"])
+        ii = g["item_i"].to_numpy().astype(np.int64)
+        jj = g["item_j"].to_numpy().astype(np.int64)
+        self.edge_index = torch.from_numpy(np.stack([ii, jj]))
+        self.num_items = int(max(self._items.max(initial=0), ii.max(initial=0), jj.max(initial=0)) + 1)
+        self._T = self.num_items
+        keys = ii * self._T + jj
+        order = np.argsort(keys, kind="stable")
+        self._ekeys = keys[order]
+        self._eorder = order
+
+    def __len__(self) -> int:
+        return len(self.session_ids)
+
+    def __getitem__(self, idx: int) -> dict:
+        items = self._items[self._ptr[idx] : self._ptr[idx + 1]]
+        if len(items) > self.max_session_length:
+            items = items[-self.max_session_length :]
+        target = items[-1]
+        context = items[:-1]
+        return {
+            "session_items": torch.tensor(context, dtype=torch.long),
+            "target_item": torch.tensor(target, dtype=torch.long),
+            "negative_items": torch.tensor(self._sample_negatives(items), dtype=torch.long),
+            "edge_index": self._build_session_subgraph(context),
+        }
+
+    def _sample_negatives(self, session_items: np.ndarray) -> list:
+        s = set(int(v) for v in session_items)
+        out = []
+        while len(out) < self.num_negatives:
+            v = torch.randint(1, self.num_items, (1,)).item()
+            if v not in s:
+                out.append(v)
+        return out
+
+    def _build_session_subgraph(self, context_items: np.ndarray) -> torch.Tensor:
+        u = np.unique(context_items)
+        if u.size == 0:
+            return torch.zeros((2, 0), dtype=torch.long)
+        a, b = np.meshgrid(u, u, indexing="ij")
+        k = (a * self._T + b).reshape(-1)
+        lo = np.searchsorted(self._ekeys, k, side="left")
+        hi = np.searchsorted(self._ekeys, k, side="right")
+        sel = np.concatenate([self._eorder[l:h] for l, h in zip(lo, hi) if h > l]) if np.any(hi > lo) else np.zeros(0, np.int64)
+        if sel.size == 0:
+            return torch.zeros((2, 0), dtype=torch.long)
+        sel.sort()  # reference keeps graph-file order
+        return self.edge_index[:, torch.from_numpy(sel)]
+
+
+def collate_fn(batch: list[dict]) -> SessionBatch:
+    """Global -> local remap per session + PyG-style concatenation (dataloader.py:157-202)."""
+    xs, eis, bv, tg, ng = [], [], [], [], []
+    off = 0
+    for b, item in enumerate(batch):
+        uniq = torch.unique(item["session_items"])
+        ei = item["edge_index"]
+        if ei.numel() > 0:
+            u = uniq.numpy()
+            src = np.searchsorted(u, ei[0].numpy())
+            dst = np.searchsorted(u, ei[1].numpy())
+            ok = (src < u.size) & (dst < u.size)
+            ok &= (u[np.minimum(src, u.size - 1)] == ei[0].numpy()) & (u[np.minimum(dst, u.size - 1)] == ei[1].numpy())
+            local = torch.from_numpy(np.stack([src[ok], dst[ok]]).astype(np.int64))
+        else:
+            local = torch.zeros((2, 0), dtype=torch.long)
+        xs.append(uniq)
+        eis.append(local + off)
+        bv.append(torch.full((uniq.numel(),), b, dtype=torch.long))
+        off += uniq.numel()
+        tg.append(item["target_item"].reshape(()))
+        ng.append(item["negative_items"].reshape(-1))
+    return SessionBatch(torch.cat(xs), torch.cat(eis, dim=1), torch.cat(bv), torch.stack(tg), torch.cat(ng),
+                        num_graphs=len(batch))
+
+
+def create_dataloader(sessions_path: Path | str, graph_edges_path: Path | str, batch_size: int = 32,
+                      num_negatives: int = 5, max_session_length: int = 50, shuffle: bool = True,
+                      num_workers: int = 0) -> torch.utils.data.DataLoader:
+    ds = SessionDataset(sessions_path, graph_edges_path, num_negatives, max_session_length)
+    return torch.utils.data.DataLoader(ds, batch_size=batch_size, shuffle=shuffle, num_workers=num_workers,
+                                       collate_fn=collate_fn)

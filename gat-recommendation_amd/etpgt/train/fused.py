@@ -1,0 +1,214 @@
+"""Fused training step: forward + loss + backward + (Adam|AdamW) in HIP kernels,
+optionally captured once into a hipGraph and replayed per batch.
+
+One step of ``Trainer.train_epoch`` (trainer.py:80-133) with
+``torch.optim.AdamW(lr, weight_decay)`` (train_baseline.py:252-256):
+
+  main stream:  conv_fwd(0..L-1) -> readout_loss(FWD|LOSS|BWD) -> conv_bwd(L-1..0)
+                -> wgrad -> [join] -> adamw_rows -> adamw_small -> [join] -> step_end
+  side stream 1: contrib_prep (keys + touched-row stamps) -> adamw_sweep (untouched rows)
+  side stream 2: contrib_sort (stable radix sort of the table-gradient contributions)
+
+The item table never gets a dense gradient: untouched rows take the g = 0 AdamW
+update (same arithmetic as the dense reference update, 24 B/element instead of
+32) concurrently with the forward/backward chain; touched rows are updated from
+their segment sums once the backward is done.  Optimizer state (exp_avg,
+exp_avg_sq, step) lives in this object; ``export_optimizer_state`` writes it back
+into a ``torch.optim.AdamW`` state_dict layout.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from etpgt.backend import _lib as L
+from etpgt.backend.engine import Engine
+from etpgt.data.batch import Caps, SessionBatch
+
+
+class FusedTrainStep:
+    def __init__(self, model, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 1e-5, decoupled: bool = True, loss: str = "bpr",
+                 temperature: float = 1.0, alpha: float = 0.7, caps: Caps | None = None,
+                 use_graph: bool = True):
+        if loss not in ("bpr", "listwise", "dual", "sampled_softmax"):
+            raise ValueError(f"Unknown loss type: {loss}")
+        self.model = model
+        self.eng: Engine = model.hip_engine()
+        self.dev = self.eng.device
+        self.loss_kind = L.GTR_LOSS[loss]
+        self.temperature = float(temperature)
+        self.alpha = float(alpha)
+        self.use_graph = use_graph
+        eng = self.eng
+        T, D = eng.T, eng.D
+        self.adam = L.GtrAdam()
+        self.adam.lr, self.adam.beta1, self.adam.beta2 = float(lr), float(betas[0]), float(betas[1])
+        self.adam.eps, self.adam.weight_decay, self.adam.decoupled = float(eps), float(weight_decay), int(decoupled)
+        self.step_dev = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        self.adam.step_dev = self.step_dev.data_ptr()
+        self.m_tab = torch.zeros(T, D, dtype=torch.float32, device=self.dev)
+        self.v_tab = torch.zeros(T, D, dtype=torch.float32, device=self.dev)
+        self.m_flat = torch.zeros_like(eng.flat.flat)
+        self.v_flat = torch.zeros_like(eng.flat.flat)
+        self.stamp = torch.zeros(T, dtype=torch.int32, device=self.dev)
+        self.caps = None
+        self.graph = None
+        if caps is not None:
+            self._bind(caps)
+
+    # ------------------------------------------------------------------ buffers
+    def _bind(self, caps: Caps):
+        eng = self.eng
+        self.caps = caps
+        self.ws = eng.workspace(caps)
+        from etpgt.data.batch import blob_layout
+
+        self.blob = torch.zeros(blob_layout(caps)["_total"], dtype=torch.int32, device=self.dev)
+        self.node_pe = None
+        if eng.K > 0:
+            self.node_pe_buf = torch.zeros(caps.n_cap, eng.K, dtype=torch.float32, device=self.dev)
+        self.bs = eng.batch_struct(caps, self.blob, None)
+        self.bs_pe = eng.batch_struct(caps, self.blob, self.node_pe_buf) if eng.K > 0 else None
+        m_cap = caps.n_cap + caps.b_cap * (1 + caps.n_neg)
+        self.m_cap = m_cap
+        self.keys = torch.zeros(m_cap, dtype=torch.int32, device=self.dev)
+        self.vals = torch.zeros(m_cap, dtype=torch.int32, device=self.dev)
+        self.skeys = torch.zeros(m_cap, dtype=torch.int32, device=self.dev)
+        self.svals = torch.zeros(m_cap, dtype=torch.int32, device=self.dev)
+        nb = C.c_size_t(0)
+        L.check(L.lib().gtr_contrib_sort_bytes(m_cap, eng.T, C.byref(nb)), "sort_bytes")
+        self.sort_tmp = torch.zeros(max(int(nb.value), 16), dtype=torch.uint8, device=self.dev)
+        self.segs, self.nseg = eng.segments(self.ws)
+        self.cfg = eng.config(self.ws, True)
+        self.side1 = torch.cuda.Stream(self.dev)
+        self.side2 = torch.cuda.Stream(self.dev)
+        self.graph = None
+        self.graph_pe = None
+
+    def ensure_caps(self, batch: SessionBatch):
+        N, B, E, n = batch.sizes()
+        if self.caps is None:
+            self._bind(Caps.bucket(2 * N, B, 2 * E, n))
+        elif not self.caps.fits(N, B, E, n):
+            if n != self.caps.n_neg:
+                raise ValueError("the number of negatives per session must stay fixed")
+            self._bind(self.caps.grow(N, B, E, n))
+
+    def load(self, batch: SessionBatch) -> bool:
+        """Copy a batch into the fixed device blob (one H2D/D2D copy). Returns
+        whether the batch carries precomputed PE rows."""
+        self.ensure_caps(batch)
+        batch.check_ids(self.eng.T)
+        _, host = batch.packed(self.caps)
+        src = torch.from_numpy(host)
+        self.blob.copy_(src.to(self.dev, non_blocking=True) if self.blob.device != src.device else src)
+        if self.eng.K > 0 and batch.laplacian_pe is not None:
+            pe = batch.laplacian_pe
+            self.node_pe_buf[: pe.shape[0]].copy_(pe.to(self.dev, torch.float32))
+            return True
+        return False
+
+    def load_blob(self, blob: torch.Tensor):
+        """D2D copy of a pre-staged packed blob of the same capacities."""
+        self.blob.copy_(blob, non_blocking=True)
+
+    # ------------------------------------------------------------------ launches
+    def _launch(self, with_pe: bool):
+        eng = self.eng
+        lib = L.lib()
+        ws, cfg = self.ws, self.cfg
+        bs = self.bs_pe if with_pe else self.bs
+        main = torch.cuda.current_stream(self.dev)
+        ev0 = torch.cuda.Event()
+        ev0.record(main)
+        # side 1: keys/stamps -> sweep of untouched rows
+        self.side1.wait_event(ev0)
+        with torch.cuda.stream(self.side1):
+            s1 = self.side1.cuda_stream
+            L.check(lib.gtr_contrib_prep(C.byref(bs), eng.T, self.keys.data_ptr(), self.vals.data_ptr(),
+                                         self.stamp.data_ptr(), self.step_dev.data_ptr(), s1), "contrib_prep")
+            ev_prep = torch.cuda.Event()
+            ev_prep.record(self.side1)
+            L.check(lib.gtr_adamw_sweep(eng.T, eng.D, self.stamp.data_ptr(), eng.model.item_embedding.weight.data_ptr(),
+                                        self.m_tab.data_ptr(), self.v_tab.data_ptr(), C.byref(self.adam), s1), "sweep")
+        # side 2: sort contributions by row
+        self.side2.wait_event(ev_prep)
+        with torch.cuda.stream(self.side2):
+            L.check(lib.gtr_contrib_sort(self.keys.data_ptr(), self.vals.data_ptr(), self.skeys.data_ptr(),
+                                         self.svals.data_ptr(), self.m_cap, eng.T, self.sort_tmp.data_ptr(),
+                                         self.sort_tmp.numel(), self.side2.cuda_stream), "contrib_sort")
+        # main: forward, loss, backward, weight gradients
+        eng.run_forward(ws, cfg, bs, L.RO_FWD | L.RO_LOSS | L.RO_BWD, self.loss_kind, self.temperature, self.alpha)
+        eng.run_backward(ws, cfg, bs)
+        main.wait_stream(self.side2)
+        st = main.cuda_stream
+        L.check(lib.gtr_adamw_rows(C.byref(bs), eng.T, eng.D, self.skeys.data_ptr(), self.svals.data_ptr(),
+                                   ws.dx0.data_ptr(), ws.se.data_ptr(), ws.coef_tgt.data_ptr(), ws.coef_neg.data_ptr(),
+                                   eng.model.item_embedding.weight.data_ptr(), self.m_tab.data_ptr(),
+                                   self.v_tab.data_ptr(), None, C.byref(self.adam), st), "adamw_rows")
+        L.check(lib.gtr_adamw_small(eng.flat.flat.data_ptr(), self.m_flat.data_ptr(), self.v_flat.data_ptr(), None,
+                                    eng.flat.layout.total, self.segs, self.nseg, C.byref(self.adam), st), "adamw_small")
+        main.wait_stream(self.side1)
+        L.check(lib.gtr_step_end(self.step_dev.data_ptr(), eng.rng_ctr.data_ptr(), st), "step_end")
+
+    def capture(self, with_pe: bool = False):
+        """Capture one step into a hipGraph (after one eager warm-up step)."""
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(self.dev)
+        s.wait_stream(torch.cuda.current_stream(self.dev))
+        with torch.cuda.graph(g, stream=s):
+            self._launch(with_pe)
+        torch.cuda.current_stream(self.dev).wait_stream(s)
+        if with_pe:
+            self.graph_pe = g
+        else:
+            self.graph = g
+        return g
+
+    def run(self, with_pe: bool = False):
+        """One training step over the batch currently in the device blob."""
+        self.eng.check_intact()
+        if not self.model.training:
+            raise RuntimeError("FusedTrainStep requires model.train()")
+        if self.use_graph:
+            g = self.graph_pe if with_pe else self.graph
+            if g is None:
+                self._launch(with_pe)  # eager warm-up (first touch of every code path)
+                torch.cuda.synchronize(self.dev)
+                self.capture(with_pe)
+                return self.ws.loss_out[0]
+            g.replay()
+        else:
+            self._launch(with_pe)
+        return self.ws.loss_out[0]
+
+    def __call__(self, batch: SessionBatch):
+        if self.eng.K > 0 and batch.laplacian_pe is None and self.model.laplacian_pe._cached_pe is None:
+            raise RuntimeError("Laplacian PE not precomputed. Call precompute() first.")
+        N = batch.sizes()[0]
+        if N <= 1:
+            raise ValueError("Expected more than 1 value per channel when training (BatchNorm1d)")
+        with_pe = self.load(batch)
+        return self.run(with_pe)
+
+    # ------------------------------------------------------------------ state
+    @property
+    def steps(self) -> int:
+        return int(self.step_dev.item())
+
+    def export_optimizer_state(self, optimizer: torch.optim.Optimizer):
+        """Write exp_avg / exp_avg_sq / step into a torch Adam(W) optimizer's state."""
+        t = torch.tensor(float(self.steps))
+        tab = self.model.item_embedding.weight
+        views_m = self.eng.flat.grad_views(self.m_flat)
+        views_v = self.eng.flat.grad_views(self.v_flat)
+        pm = {id(p): (m, v) for p, m, v in zip(self.eng.flat.params(), views_m, views_v)}
+        pm[id(tab)] = (self.m_tab, self.v_tab)
+        for group in optimizer.param_groups:
+            for p in group["params"]:
+                if id(p) in pm:
+                    m, v = pm[id(p)]
+                    optimizer.state[p] = {"step": t.clone(), "exp_avg": m.clone(), "exp_avg_sq": v.clone()}

@@ -1,0 +1,234 @@
+/*
+ * gtr.h — C ABI of libgtr_hip.so, the MI355X (gfx950) training hot path of the
+ * GraphTransformer session recommender (Axionis47/GAT-Recommendation).
+ *
+ * The reference has NO native boundary: its hot path is a Python module API
+ * (etpgt.model / etpgt.train).  These entry points are what a
+ * maintainer's FFI for that path binds (the ctypes stub in INTEGRATION.md).
+ * Each one replaces a span of reference Python (file:line in /root/reference):
+ *
+ *   gtr_conv_fwd      graph_transformer.py:140-152 (embedding + LapPE add, layer 0)
+ *                     + graph_transformer.py:171-177 (TransformerConv -> BatchNorm
+ *                     -> residual -> dropout) for one layer, fused; PyG
+ *                     TransformerConv semantics per SURVEY.md Appendix A.
+ *   gtr_readout_loss  base.py:136-155 (mean SessionReadout) + base.py:80-113 /
+ *                     losses.py:8-228 (BPR / listwise / dual scoring loss), forward
+ *                     and backward, fused; trainer.py:86-122 loss dispatch.
+ *   gtr_conv_bwd      autograd of graph_transformer.py:171-177 for one layer.
+ *   gtr_wgrad         weight/bias gradients of lin_{query,key,value,skip},
+ *                     lin_beta and laplacian_pe.projection (laplacian_pe.py:194-197).
+ *   gtr_contrib_prep  embedding-row gradient bookkeeping (nn.Embedding(padding_idx=0)
+ *     gtr_contrib_sort  backward, base.py:35-37) as a sorted-segment reduction.
+ *   gtr_adamw_rows / gtr_adamw_sweep / gtr_adamw_small
+ *                     torch.optim.AdamW(lr, wd) step of train_baseline.py:252-256
+ *                     (trainer.py:125-127) over the item table and the dense params.
+ *   gtr_scatter_rows  eager (autograd) path: dense table gradient.
+ *   gtr_step_end      step / dropout-stream counters.
+ *
+ * Conventions: plain pointers + sizes, no torch types; every
+ * pointer is a device pointer unless marked (host); stream is a hipStream_t;
+ * every function returns 0 on success or a non-zero code (hipError_t value,
+ * or GTR_E_* below) and never throws; gtr_last_error() returns a message.
+ * Functions never allocate: workspace is caller-provided.  Indices are int32
+ * on device.  Live batch sizes (N, B, E) are read from device memory (hdr) so
+ * that a captured hipGraph can be replayed over batches of varying shape
+ * within fixed capacities.
+ */
+#ifndef GTR_H
+#define GTR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GTR_ABI_VERSION 1
+
+#define GTR_OK 0
+#define GTR_E_ARG 1001      /* bad argument / unsupported shape */
+#define GTR_E_DEVICE 1002   /* not a gfx950 device */
+
+typedef void* gtr_stream_t; /* hipStream_t */
+
+/* Batch in HBM: fixed-capacity arrays, live sizes in hdr[] on device.
+ * hdr[0] = N (nodes), hdr[1] = B (sessions), hdr[2] = E (edges).            */
+typedef struct gtr_batch {
+  const int32_t* hdr;
+  const int32_t* node_item; /* [n_cap]   global item id of each node          */
+  const int32_t* node_ptr;  /* [b_cap+1] first node of each session (PyG ptr)  */
+  const int32_t* in_ptr;    /* [n_cap+1] CSR by destination                    */
+  const int32_t* in_src;    /* [e_cap]   source node of dst-ordered edge        */
+  const int32_t* out_ptr;   /* [n_cap+1] CSR by source                         */
+  const int32_t* out_edge;  /* [e_cap]   dst-order position of src-ordered edge */
+  const int32_t* out_dst;   /* [e_cap]   destination node of src-ordered edge   */
+  const int32_t* target;    /* [b_cap]                                          */
+  const int32_t* negatives; /* [b_cap * n_neg]                                  */
+  const float* node_pe;     /* optional [n_cap, pe_k] batch.laplacian_pe, or NULL */
+  int32_t n_cap, b_cap, e_cap, n_neg;
+} gtr_batch;
+
+typedef struct gtr_config {
+  int32_t num_items;  /* T: table rows                          */
+  int32_t dim;        /* D = embedding_dim = hidden_dim          */
+  int32_t heads;      /* H (C = D / H)                           */
+  int32_t pe_k;       /* LapPE k, 0 = no LapPE                   */
+  int32_t num_layers; /* L                                       */
+  int32_t row_group;  /* R: sessions are grouped by first node / R */
+  int32_t training;   /* 1 = train mode (batch BN stats, dropout) */
+  float dropout;      /* p                                       */
+  float bn_eps;       /* 1e-5                                    */
+  float bn_momentum;  /* 0.1                                     */
+  uint32_t seed;      /* dropout stream seed                     */
+  const uint32_t* rng_ctr; /* device counter mixed into dropout masks */
+} gtr_config;
+
+/* Parameters + saved activations of one TransformerConv/BatchNorm layer.
+ * w_all = [lin_query; lin_key; lin_value; lin_skip].weight stacked [4D, D],
+ * b_all the matching biases [4D]; w_beta = lin_beta.weight [3D].             */
+typedef struct gtr_layer {
+  const float* w_all;
+  const float* b_all;
+  const float* w_beta;
+  const float* bn_gamma;
+  const float* bn_beta;
+  float* bn_rmean;
+  float* bn_rvar;
+  int64_t* bn_nbt;
+  float* xin;      /* [n_cap, D]  layer input (x_{l-1})            */
+  float* qkvs;     /* [n_cap, 4D] query | key | value | skip        */
+  float* alpha;    /* [e_cap, H]  attention probabilities            */
+  float* agg;      /* [n_cap, D]  attention aggregate               */
+  float* gate;     /* [n_cap]     beta gate                         */
+  float* out;      /* [n_cap, D]  conv output (pre BatchNorm)        */
+  float* bn_stats; /* [2D] batch mean, rstd                         */
+  float* bn_part;  /* [g_cap, 1+2D] forward partials                 */
+  float* bn_gsum;  /* [2D] sum(dy), sum(dy*xhat)                     */
+  float* bn_gpart; /* [max(g_cap, 256), 2D] backward partials         */
+  uint32_t* cnt;   /* [4] arrival counters (zero-initialised once)     */
+  float* dy;       /* [n_cap, D]  grad wrt BN(out)+x_{l-1} (pre dropout) */
+  float* dqkvs;    /* [n_cap, 4D]                                    */
+  float* du;       /* [n_cap]     grad wrt gate logit                 */
+  float* dlogit;   /* [e_cap, H]                                     */
+  float* dagg;     /* [n_cap, D]                                     */
+} gtr_layer;
+
+/* Embedding + LapPE inputs of layer 0. */
+typedef struct gtr_embed {
+  const float* table;  /* [T, D] item_embedding.weight              */
+  const float* pe_tab; /* [T, pe_k] laplacian_pe._cached_pe or NULL  */
+  const float* wpe;    /* [D, pe_k] laplacian_pe.projection.weight    */
+  const float* bpe;    /* [D]                                        */
+} gtr_embed;
+
+/* Loss head. */
+#define GTR_LOSS_NONE 0
+#define GTR_LOSS_BPR 1
+#define GTR_LOSS_LISTWISE 2
+#define GTR_LOSS_DUAL 3
+#define GTR_RO_FWD 1
+#define GTR_RO_LOSS 2
+#define GTR_RO_BWD 4
+
+typedef struct gtr_head {
+  int32_t flags;       /* GTR_RO_* */
+  int32_t loss_kind;   /* GTR_LOSS_* */
+  float temperature;
+  float dual_alpha;
+  float* se;           /* [b_cap, D] session embeddings (out if FWD, in otherwise) */
+  const float* dse_in; /* [b_cap, D] upstream grad (BWD without LOSS)  */
+  float* dse_out;      /* [b_cap, D] d loss / d se (LOSS; optional)    */
+  float* coef_tgt;     /* [b_cap]     d loss / d pos score              */
+  float* coef_neg;     /* [b_cap*n]   d loss / d neg score              */
+  float* loss_part;    /* [512] per-workgroup (listwise, bpr) partial sums */
+  float* loss_out;     /* [1]                                           */
+  uint32_t* cnt;       /* [4]                                           */
+} gtr_head;
+
+int gtr_version(void);
+int gtr_abi_version(void);
+const char* gtr_last_error(void);
+/* 0 if `device` is a gfx950 (MI355X) device. */
+int gtr_device_check(int device);
+
+/* Forward of layer `l`; l == 0 gathers table rows (+LapPE), l > 0 applies the
+ * previous layer's BatchNorm + residual + dropout in its prologue.  In training
+ * mode the last arriving workgroup finalises this layer's BatchNorm statistics
+ * and updates running_mean / running_var / num_batches_tracked.               */
+int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_embed* emb,
+                 const gtr_layer* layers, int l, gtr_stream_t stream);
+
+/* Mean readout of the last layer (+ scoring loss forward/backward, + readout
+ * backward into layers[L-1].dy and the last BatchNorm's backward sums).         */
+int gtr_readout_loss(const gtr_config* cfg, const gtr_batch* bt, const float* table,
+                     const gtr_layer* layers, const gtr_head* head, gtr_stream_t stream);
+
+/* Backward of layer `l` given layers[l].dy and layers[l].bn_gsum.  Writes
+ * layers[l].dqkvs/du and either layers[l-1].dy (+ its BN sums) or dx0.        */
+int gtr_conv_bwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l,
+                 float* dx0, gtr_stream_t stream);
+
+/* Weight-gradient partial slabs for every layer (+ LapPE projection).
+ * Slab layout matches the flat parameter layout of each layer block:
+ *   [w_all 4D*D | b_all 4D | w_beta 3D] and PE [wpe D*k | bpe D].
+ * slabs[p * slab_stride + offset]; n_chunks partials over the node range.     */
+int gtr_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers,
+              const float* dx0, const float* pe_tab, float* const* layer_slab, float* pe_slab,
+              int n_chunks, int64_t slab_stride, gtr_stream_t stream);
+
+/* One segment of the flat dense-parameter buffer for gtr_adamw_small. */
+typedef struct gtr_segment {
+  int64_t begin;      /* element offset in the flat buffer (multiple of 256) */
+  int64_t len;
+  const float* src;   /* gradient partials                                  */
+  int64_t pstride;    /* distance between partials                           */
+  int32_t nparts;
+  int32_t pad;
+} gtr_segment;
+
+typedef struct gtr_adam {
+  float lr, beta1, beta2, eps, weight_decay;
+  int32_t decoupled;          /* 1 = AdamW, 0 = Adam (L2 into the gradient) */
+  const int64_t* step_dev;    /* completed optimizer steps (device)          */
+} gtr_adam;
+
+#define GTR_SMALL_MAX_SEG 48
+/* Sum each segment's gradient partials and apply (Adam|AdamW) — or, when
+ * grad_out != NULL, only write the summed gradient there (eager path).        */
+int gtr_adamw_small(float* param, float* m, float* v, float* grad_out, int64_t total,
+                    const gtr_segment* segs, int nseg, const gtr_adam* opt, gtr_stream_t stream);
+
+/* Contribution list of the item-table gradient: j < n_cap node rows (dx0),
+ * then b_cap target rows, then b_cap*n negative rows (coef * se[b]).
+ * Writes keys/vals (sentinel key = T for unused slots) and marks touched rows
+ * stamp[row] = step+1.  m_cap = n_cap + b_cap*(1+n).                          */
+int gtr_contrib_prep(const gtr_batch* bt, int num_items, int32_t* keys, int32_t* vals,
+                     int32_t* stamp, const int64_t* step_dev, gtr_stream_t stream);
+int gtr_contrib_sort_bytes(int m_cap, int num_items, size_t* bytes);
+int gtr_contrib_sort(const int32_t* keys, const int32_t* vals, int32_t* skeys, int32_t* svals,
+                     int m_cap, int num_items, void* tmp, size_t tmp_bytes, gtr_stream_t stream);
+
+/* Touched rows: segmented sum of contributions in sorted (stable) order, then
+ * AdamW on the row.  grad_dense != NULL: write the row gradient instead.      */
+int gtr_adamw_rows(const gtr_batch* bt, int num_items, int dim, const int32_t* skeys,
+                   const int32_t* svals, const float* dx0, const float* se, const float* coef_tgt,
+                   const float* coef_neg, float* table, float* m, float* v, float* grad_dense,
+                   const gtr_adam* opt, gtr_stream_t stream);
+
+/* Untouched rows (stamp[row] != step+1): AdamW with zero gradient.            */
+int gtr_adamw_sweep(int num_items, int dim, const int32_t* stamp, float* table, float* m, float* v,
+                    const gtr_adam* opt, gtr_stream_t stream);
+
+/* Eager path: dense[key_j] += coef_j * src_j over a contribution range.
+ * mode 0: node rows (src = dx0, coef 1); mode 1: score rows (src = se).       */
+int gtr_scatter_rows(const gtr_batch* bt, int dim, int mode, const float* src, const float* coef_tgt,
+                     const float* coef_neg, float* dense, gtr_stream_t stream);
+
+/* step_dev += 1 (if non-NULL); rng_ctr += 1 (if non-NULL).                    */
+int gtr_step_end(int64_t* step_dev, uint32_t* rng_ctr, gtr_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GTR_H */

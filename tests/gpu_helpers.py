@@ -1,0 +1,97 @@
+"""Shared helpers for the GPU parity tests (HIP path vs the CPU oracle)."""
+
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+import etpgt_ref as R
+from etpgt.data.batch import SessionBatch, collate_sessions
+from etpgt.data.synthetic import make_batches, make_sessions_and_graph
+from etpgt.model import create_graph_transformer_optimized
+
+
+def small_data(num_items=300, num_sessions=3000, num_edges=4000, seed=3):
+    return make_sessions_and_graph(num_items=num_items, num_sessions=num_sessions, num_edges=num_edges, seed=seed)
+
+
+def edge_case_batch(n_neg=5, T=300) -> SessionBatch:
+    """Reference conftest dummy_batch (tests/conftest.py:25-50) sessions plus
+    edge cases: a node with no in-edges, a single-node session with a self loop,
+    a session without edges, a dense session with self loops."""
+    items = [
+        {"x": [1, 2, 3], "edge_index": [[0, 1, 1, 2], [1, 0, 2, 1]]},
+        {"x": [4, 5, 6, 7], "edge_index": [[0, 1, 1, 2, 2, 3], [1, 0, 2, 1, 3, 2]]},
+        {"x": [10, 11, 12], "edge_index": [[0, 0], [1, 2]]},          # node 0 has no in-edge
+        {"x": [20], "edge_index": [[0], [0]]},                         # single node, self loop
+        {"x": [30, 31], "edge_index": [[], []]},                       # no edges at all
+        {"x": list(range(40, 52)), "edge_index": [[a for a in range(12) for b in range(a, 12)],
+                                                   [b for a in range(12) for b in range(a, 12)]]},
+    ]
+    rng = np.random.default_rng(0)
+    out = []
+    for it in items:
+        x = np.array(it["x"], np.int64)
+        seen = set(x.tolist())
+        negs = [v for v in rng.integers(1, T, size=4 * n_neg) if int(v) not in seen][:n_neg]
+        out.append({"x": x, "edge_index": np.array(it["edge_index"], np.int64).reshape(2, -1),
+                    "target_item": int(rng.integers(1, T)), "negative_items": np.array(negs, np.int64)})
+    return collate_sessions(out)
+
+
+def make_pair(T, D, H, L=2, K=0, dropout=0.0, seed=0, pe_table=None):
+    """HIP model (cuda) + oracle model (cpu) with identical parameters."""
+    torch.manual_seed(seed)
+    m = create_graph_transformer_optimized(T, embedding_dim=D, hidden_dim=D, num_layers=L, num_heads=H,
+                                           dropout=dropout, use_laplacian_pe=K > 0, laplacian_k=max(K, 1))
+    if K > 0:
+        m.laplacian_pe._cached_pe = pe_table if pe_table is not None else torch.rand(T, K)
+    # non-trivial BN affine params so their gradients are exercised
+    with torch.no_grad():
+        for bn in m.batch_norms:
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.2, 0.2)
+    ref = R.ref_create_graph_transformer_optimized(T, embedding_dim=D, hidden_dim=D, num_layers=L, num_heads=H,
+                                                   dropout=dropout, use_laplacian_pe=K > 0, laplacian_k=max(K, 1))
+    if K > 0:
+        ref.laplacian_pe._cached_pe = torch.zeros(T, K)
+    ref.load_state_dict({k: v.detach().clone() for k, v in m.state_dict().items()})
+    return m.cuda(), ref
+
+
+def ref_batch(sb: SessionBatch):
+    return R.ref_batch_from(sb)
+
+
+def assert_close(a, b, rtol=1e-3, name="", floor=0.0):
+    """|a - b| <= rtol * (|b| + scale*1e-2) elementwise, scale = max|b|: 1e-3 relative
+    with an absolute floor at 1e-5 of the tensor's scale for near-zero entries; ``floor``
+    adds an absolute term for tensors that are mathematically zero (e.g. the key-bias
+    gradient, to which the per-destination softmax is invariant)."""
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    assert a.shape == b.shape, f"{name}: shape {a.shape} vs {b.shape}"
+    scale = float(b.abs().max()) if b.numel() else 0.0
+    tol = rtol * (b.abs() + 1e-2 * scale) + floor + 1e-12
+    err = (a - b).abs()
+    bad = err > tol
+    if bool(bad.any()):
+        i = int(torch.argmax((err - tol).reshape(-1)))
+        raise AssertionError(f"{name}: {int(bad.sum())}/{b.numel()} mismatches; worst idx {i}: "
+                             f"{a.reshape(-1)[i].item():.7g} vs {b.reshape(-1)[i].item():.7g} (scale {scale:.3g})")
+
+
+def batches(data, B, n, count, seed=0):
+    return make_batches(data, B, count, n, seed=seed)
+
+
+def assert_close_norm(a, b, rtol=1e-3, name=""):
+    """Tensor-level relative error ||a - b|| / ||b|| <= rtol (parameter trajectories:
+    Adam normalises near-zero, rounding-dominated gradient entries to +-lr steps, so a
+    few entries legitimately differ while the tensor as a whole must agree)."""
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    assert a.shape == b.shape, f"{name}: shape {a.shape} vs {b.shape}"
+    den = float(b.norm())
+    err = float((a - b).norm()) / den if den > 0 else float((a - b).norm())
+    assert err <= rtol, f"{name}: relative error {err:.3g} > {rtol}"

@@ -1,0 +1,204 @@
+"""GPU parity: the HIP path (libgtr_hip via etpgt) against the CPU oracle.
+
+Tolerance (BASELINE.json north star): 1e-3 relative, fp32 — see gpu_helpers.assert_close.
+Dropout is 0 in every value-level comparison (the HIP dropout stream cannot
+reproduce the CPU generator); dropout > 0 is covered by determinism/finiteness.
+"""
+
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover - collected only on the GPU box
+    pytest.skip("no GPU", allow_module_level=True)
+
+import etpgt_ref as R  # noqa: E402
+from gpu_helpers import assert_close, assert_close_norm, batches, edge_case_batch, make_pair, ref_batch, small_data  # noqa: E402
+
+from etpgt.train.fused import FusedTrainStep  # noqa: E402
+from etpgt.train.losses import create_loss_function  # noqa: E402
+
+DATA = None
+
+
+def data():
+    global DATA
+    if DATA is None:
+        DATA = small_data()
+    return DATA
+
+
+CONFIGS = [
+    # (D, H, K)
+    (32, 2, 0),
+    (64, 1, 0),
+    (64, 2, 8),
+    (128, 4, 16),
+    (256, 2, 0),
+]
+
+
+def test_device_is_gfx950():
+    from etpgt.backend import _lib as L
+
+    L.check(L.lib().gtr_device_check(0), "device check")
+
+
+@pytest.mark.parametrize("D,H,K", CONFIGS)
+def test_forward_eval(D, H, K):
+    T = data().table_rows
+    m, ref = make_pair(T, D, H, K=K, seed=1)
+    m.eval(); ref.eval()
+    for sb in batches(data(), 32, 5, 2, seed=D) + [edge_case_batch(5, T)]:
+        with torch.no_grad():
+            se = m(sb.to("cuda"))
+            se_ref = ref(ref_batch(sb))
+        assert_close(se, se_ref, name=f"se D={D} H={H}")
+
+
+@pytest.mark.parametrize("D,H,K", CONFIGS)
+@pytest.mark.parametrize("loss", ["model_bpr", "listwise", "dual"])
+def test_train_grads(D, H, K, loss):
+    """Train mode (batch BN stats), dropout 0: loss, session embeddings and every
+    parameter gradient (dense table gradient included) against oracle autograd."""
+    T = data().table_rows
+    n = 5 if loss != "listwise" else 20
+    m, ref = make_pair(T, D, H, K=K, seed=2)
+    m.train(); ref.train()
+    sb = batches(data(), 32, n, 1, seed=7 + D)[0]
+    if loss == "model_bpr":
+        sb2 = sb
+    else:
+        sb2 = sb
+    dsb = sb2.to("cuda")
+    se = m(dsb)
+    B = sb.num_graphs
+    neg = dsb.negative_items.view(B, n)
+    if loss == "model_bpr":
+        L_hip = m.compute_loss(se, dsb.target_item, neg)
+    else:
+        fn = create_loss_function(loss, alpha=0.7, temperature=0.5)
+        out = fn(se, dsb.target_item, neg, m.item_embedding)
+        L_hip = out[0] if isinstance(out, tuple) else out
+    m.zero_grad()
+    L_hip.backward()
+    rb = ref_batch(sb)
+    se_ref = ref(rb)
+    kind = "bpr" if loss == "model_bpr" else loss
+    L_ref = R.ref_loss(kind, se_ref, rb.target_item, rb.negative_items.view(B, n), ref.item_embedding, 0.7, 0.5)
+    ref.zero_grad()
+    L_ref.backward()
+    assert_close(se, se_ref, name="se")
+    assert_close(L_hip.reshape(1), L_ref.reshape(1), name="loss")
+    hp = dict(m.named_parameters())
+    gscale = max(float(p.grad.abs().max()) for p in ref.parameters())
+    for name, p in ref.named_parameters():
+        assert hp[name].grad is not None, name
+        assert_close(hp[name].grad, p.grad, rtol=2e-3, name=f"grad {name}", floor=1e-6 * gscale)
+    for name, b in ref.named_buffers():
+        if "running" in name:
+            assert_close(dict(m.named_buffers())[name], b, name=name)
+
+
+def test_edge_cases_train():
+    T = data().table_rows
+    m, ref = make_pair(T, 64, 2, K=0, seed=3)
+    m.train(); ref.train()
+    sb = edge_case_batch(5, T)
+    dsb = sb.to("cuda")
+    se = m(dsb)
+    L_hip = m.compute_loss(se, dsb.target_item, dsb.negative_items.view(sb.num_graphs, 5))
+    L_hip.backward()
+    rb = ref_batch(sb)
+    se_ref = ref(rb)
+    L_ref = ref.compute_loss(se_ref, rb.target_item, rb.negative_items.view(sb.num_graphs, 5))
+    L_ref.backward()
+    assert_close(L_hip.reshape(1), L_ref.reshape(1), name="loss")
+    hp = dict(m.named_parameters())
+    gscale = max(float(p.grad.abs().max()) for p in ref.parameters())
+    for name, p in ref.named_parameters():
+        assert_close(hp[name].grad, p.grad, rtol=2e-3, name=f"grad {name}", floor=1e-6 * gscale)
+
+
+@pytest.mark.parametrize("D,H,K,loss,opt", [
+    (64, 1, 0, "bpr", "adamw"),        # config C2 shape
+    (128, 4, 16, "listwise", "adamw"),  # config C3 shape
+    (64, 2, 0, "dual", "adam"),
+])
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_fused_steps(D, H, K, loss, opt, use_graph):
+    """k fused steps (forward+loss+backward+optimizer, hipGraph replay) == k
+    reference trainer steps (trainer.py:80-133) with torch.optim.AdamW/Adam."""
+    T = data().table_rows
+    n = 5 if loss != "listwise" else 100
+    m, ref = make_pair(T, D, H, K=K, seed=4)
+    m.train(); ref.train()
+    lr, wd = 1e-3, 1e-2
+    fused = FusedTrainStep(m, lr=lr, weight_decay=wd if opt == "adamw" else 0.0, decoupled=opt == "adamw",
+                           loss=loss, temperature=1.0, alpha=0.7, use_graph=use_graph)
+    if opt == "adamw":
+        ropt = torch.optim.AdamW(ref.parameters(), lr=lr, weight_decay=wd)
+    else:
+        ropt = torch.optim.Adam(ref.parameters(), lr=lr)
+    bl = batches(data(), 32, n, 4, seed=11)
+    losses, rlosses = [], []
+    for sb in bl:
+        losses.append(float(fused(sb.to("cuda"))))
+        rlosses.append(float(R.ref_train_step(ref, ref_batch(sb), ropt, loss)))
+    np.testing.assert_allclose(losses, rlosses, rtol=2e-3)
+    hp = dict(m.named_parameters())
+    for name, p in ref.named_parameters():
+        if name.endswith("lin_key.bias"):
+            # d loss / d key-bias is exactly 0 (softmax over a destination's in-edges is
+            # invariant to a shift shared by all its logits); both sides see rounding
+            # noise (~1e-10) that Adam normalises to +-lr steps, so the trajectory is
+            # noise-driven on either implementation: bound it instead of matching it.
+            assert float((hp[name].detach().cpu() - p.detach()).abs().max()) <= 2 * lr * len(bl) + 1e-6
+            continue
+        assert_close_norm(hp[name], p, rtol=1e-3, name=f"param {name}")
+    for name, b in ref.named_buffers():
+        if "running" in name:
+            assert_close_norm(dict(m.named_buffers())[name], b, rtol=1e-3, name=name)
+    assert int(dict(m.named_buffers())["batch_norms.0.num_batches_tracked"]) == len(bl)
+
+
+def test_fused_dropout_deterministic_and_finite():
+    T = data().table_rows
+    m, _ = make_pair(T, 64, 2, K=0, dropout=0.1, seed=5)
+    m2 = copy.deepcopy(m)
+    m.train(); m2.train()
+    bl = batches(data(), 32, 5, 3, seed=12)
+    f1 = FusedTrainStep(m, loss="bpr")
+    f2 = FusedTrainStep(m2, loss="bpr", use_graph=False)
+    l1 = [float(f1(sb.to("cuda"))) for sb in bl]
+    l2 = [float(f2(sb.to("cuda"))) for sb in bl]
+    assert all(np.isfinite(l1))
+    # graph replay and eager launches draw the same dropout masks
+    np.testing.assert_allclose(l1, l2, rtol=1e-5)
+    assert torch.equal(m.item_embedding.weight, m2.item_embedding.weight) or torch.allclose(
+        m.item_embedding.weight, m2.item_embedding.weight, rtol=1e-5, atol=1e-7)
+
+
+def test_table_untouched_rows_follow_dense_adamw():
+    """Rows not in the batch still decay / move with their moments (dense AdamW)."""
+    T = data().table_rows
+    m, ref = make_pair(T, 64, 1, K=0, seed=6)
+    m.train(); ref.train()
+    fused = FusedTrainStep(m, lr=1e-2, weight_decay=1e-1, loss="bpr")
+    ropt = torch.optim.AdamW(ref.parameters(), lr=1e-2, weight_decay=1e-1)
+    bl = batches(data(), 16, 5, 3, seed=13)
+    for sb in bl:
+        fused(sb.to("cuda"))
+        R.ref_train_step(ref, ref_batch(sb), ropt, "bpr")
+    assert_close_norm(m.item_embedding.weight, ref.item_embedding.weight, rtol=1e-3, name="table")
+    untouched = torch.ones(T, dtype=torch.bool)
+    for sb in bl:
+        for t in (sb.x, sb.target_item, sb.negative_items):
+            untouched[t] = False
+    # rows never in a batch: pure decay + zero-gradient moment updates, elementwise
+    assert_close(m.item_embedding.weight[untouched.cuda()], ref.item_embedding.weight[untouched], rtol=1e-5,
+                 name="untouched rows")
