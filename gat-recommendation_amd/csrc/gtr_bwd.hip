@@ -9,7 +9,7 @@
 // k_wgrad: lin_{query,key,value,skip} weight/bias, lin_beta and LapPE projection
 //   gradients as deterministic per-chunk partial slabs (summed by the optimizer).
 
-#include "gtr_common.cuh"
+#include "gtr_layer.cuh"
 
 namespace {
 
@@ -46,153 +46,235 @@ struct ConvBwdK {
   float* dx0;
 };
 
+// Destination-row backward: BatchNorm backward, beta gate, softmax backward, dQ, dS.
+// KB/VB (stride KST), AL/DL (edge-indexed, H per edge) are LDS on the fast path.
 template <int D>
-__global__ __launch_bounds__(GTR_BLOCK) void k_conv_bwd(ConvBwdK a) {
-  constexpr int VPL = D >= 64 ? D / 64 : 1;
-  constexpr int AS = 4 * D + 4;
-  extern __shared__ __attribute__((aligned(16))) float As[];  // [16][AS] + flag word
-  int& s_flag = *reinterpret_cast<int*>(As + 16 * AS);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int N = a.bt.hdr[0], B = a.bt.hdr[1];
-  const int G = (N + a.R - 1) / a.R;
-  const int g = blockIdx.x;
-  if (g >= G) return;
-  int r0, r1;
-  group_rows(a.bt.node_ptr, B, a.R, g, r0, r1);
-  const uint32_t ctr = a.rng_ctr ? *a.rng_ctr : 0u;
-  const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
+__device__ __forceinline__ void bwd_dst_row(const ConvBwdK& a, int t, int tl, const float* KB, const float* VB,
+                                            int KST, const int* EP, const int* ES, const float* AL, float* DL,
+                                            int eoff, int lane, const Drop& dr, uint32_t st_attn,
+                                            const float (&k_g)[LayerGeom<D>::VPL],
+                                            const float (&k_mean)[LayerGeom<D>::VPL],
+                                            const float (&k_rstd)[LayerGeom<D>::VPL],
+                                            const float (&k_s1)[LayerGeom<D>::VPL],
+                                            const float (&k_s2)[LayerGeom<D>::VPL]) {
+  constexpr int VPL = LayerGeom<D>::VPL;
   const int d0 = lane * VPL;
   const bool act = d0 < D;
   const int C = a.C, H = a.H;
   const int GL = C / VPL;
   const int head = act ? d0 / C : 0;
   const bool leader = act && ((lane & (GL - 1)) == 0);
+  const size_t ro = (size_t)t * D + d0;
+  float dyv[VPL], ov[VPL], ag[VPL], sv[VPL];
+  load_vec<VPL>(dyv, a.dy + ro, act);
+  load_vec<VPL>(ov, a.out + ro, act);
+  load_vec<VPL>(ag, a.agg + ro, act);
+  load_vec<VPL>(sv, a.qkvs + (size_t)t * (4 * D) + 3 * D + d0, act);
+  const float beta = a.gate[t];
+  float gv[VPL];
+  float dbeta = 0.0f;
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) {
+    const float xh = (ov[v] - k_mean[v]) * k_rstd[v];
+    gv[v] = act ? (dyv[v] - k_s1[v] - xh * k_s2[v]) * k_rstd[v] * k_g[v] : 0.0f;
+    dbeta += gv[v] * (sv[v] - ag[v]);
+  }
+  dbeta = wave_sum(dbeta);
+  const float du = dbeta * beta * (1.0f - beta);
+  if (lane == 0) a.du[t] = du;
+  float dag[VPL], ds[VPL], dq[VPL];
+  {
+    float w1[VPL], w2[VPL], w3[VPL];
+    load_vec<VPL>(w1, a.w_beta + d0, act);
+    load_vec<VPL>(w2, a.w_beta + D + d0, act);
+    load_vec<VPL>(w3, a.w_beta + 2 * D + d0, act);
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      dag[v] = gv[v] * (1.0f - beta) + du * (w1[v] + w3[v]);
+      ds[v] = gv[v] * beta + du * (w2[v] - w3[v]);
+      dq[v] = 0.0f;
+    }
+  }
+  store_vec<VPL>(a.dqkvs + (size_t)t * (4 * D) + 3 * D + d0, ds, act);
+  store_vec<VPL>(a.dagg + ro, dag, act);
+  const int e0 = EP[tl], e1 = EP[tl + 1];
+  float sdot = 0.0f;
+  for (int e = e0; e < e1; ++e) {
+    float vv[VPL];
+    load_vec<VPL>(vv, VB + (size_t)ES[e] * KST + d0, act);
+    float d = 0.0f;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) d += dag[v] * vv[v];
+    d = group_sum(d, GL);
+    const float al = AL[(size_t)e * H + head];
+    sdot += al * (d * dr.mul(st_attn, (uint32_t)((e + eoff) * H + head)));
+  }
+  for (int e = e0; e < e1; ++e) {
+    const int src = ES[e];
+    float vv[VPL], kv[VPL];
+    load_vec<VPL>(vv, VB + (size_t)src * KST + d0, act);
+    load_vec<VPL>(kv, KB + (size_t)src * KST + d0, act);
+    float d = 0.0f;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) d += dag[v] * vv[v];
+    d = group_sum(d, GL);
+    const float al = AL[(size_t)e * H + head];
+    const float da = d * dr.mul(st_attn, (uint32_t)((e + eoff) * H + head));
+    const float dl = al * (da - sdot);
+    if (leader) DL[(size_t)e * H + head] = dl;
+    const float c = dl / a.sqrt_c;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) dq[v] += c * kv[v];
+  }
+  store_vec<VPL>(a.dqkvs + (size_t)t * (4 * D) + d0, dq, act);
+}
+
+// Source-row backward: dK, dV gathered over out-edges (no atomics).
+template <int D>
+__device__ __forceinline__ void bwd_src_row(const ConvBwdK& a, int s, int sl, const float* QB, int QST,
+                                            const float* GB, int GST, const int* OP, const int* OE, const int* OD,
+                                            const float* AL, const float* DL, int eoff, int lane, const Drop& dr,
+                                            uint32_t st_attn) {
+  constexpr int VPL = LayerGeom<D>::VPL;
+  const int d0 = lane * VPL;
+  const bool act = d0 < D;
+  const int C = a.C, H = a.H;
+  const int head = act ? d0 / C : 0;
+  float dk[VPL], dv[VPL];
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) { dk[v] = 0.0f; dv[v] = 0.0f; }
+  const int i0 = OP[sl], i1 = OP[sl + 1];
+  for (int i = i0; i < i1; ++i) {
+    const int p = OE[i];
+    const int t = OD[i];
+    const float dl = DL[(size_t)p * H + head] / a.sqrt_c;
+    const float ad = AL[(size_t)p * H + head] * dr.mul(st_attn, (uint32_t)((p + eoff) * H + head));
+    float qv[VPL], gv[VPL];
+    load_vec<VPL>(qv, QB + (size_t)t * QST + d0, act);
+    load_vec<VPL>(gv, GB + (size_t)t * GST + d0, act);
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      dk[v] += dl * qv[v];
+      dv[v] += ad * gv[v];
+    }
+  }
+  store_vec<VPL>(a.dqkvs + (size_t)s * (4 * D) + D + d0, dk, act);
+  store_vec<VPL>(a.dqkvs + (size_t)s * (4 * D) + 2 * D + d0, dv, act);
+}
+
+template <int D>
+__global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
+  using G = LayerGeom<D>;
+  constexpr int VPL = G::VPL, RMAX = G::RMAX, AS = G::AS;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* R1 = sm + G::B_R1;
+  float* ALs = sm + G::B_ALPHA;
+  float* DLs = sm + G::B_DLOG;
+  int* iptr = reinterpret_cast<int*>(sm + G::B_IPTR);
+  int* isrc = reinterpret_cast<int*>(sm + G::B_ISRC);
+  int* optr = reinterpret_cast<int*>(sm + G::B_OPTR);
+  int* oedge = reinterpret_cast<int*>(sm + G::B_OEDGE);
+  int* odst = reinterpret_cast<int*>(sm + G::B_ODST);
+  int* s_flag = reinterpret_cast<int*>(sm + G::B_FLAG);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int N = a.bt.hdr[0], B = a.bt.hdr[1];
+  const int Gn = (N + a.R - 1) / a.R;
+  const int g = blockIdx.x;
+  if (g >= Gn) return;
+  int r0, r1;
+  group_rows(a.bt.node_ptr, B, a.R, g, r0, r1);
+  const int nrow = r1 - r0;
+  const int H = a.H;
+  const int e_lo = a.bt.in_ptr[r0], e_hi = a.bt.in_ptr[r1];
+  const int o_lo = a.bt.out_ptr[r0];
+  const int ne = e_hi - e_lo;
+  const bool fast = G::KV && nrow <= RMAX && ne <= G::EMAX && H <= 8;
+  const uint32_t ctr = a.rng_ctr ? *a.rng_ctr : 0u;
+  const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
+  const int d0 = lane * VPL;
+  const bool act = d0 < D;
   const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
   const float invN = 1.0f / (float)N;
 
-  // per-lane BatchNorm backward constants
   float k_g[VPL], k_mean[VPL], k_rstd[VPL], k_s1[VPL], k_s2[VPL];
+  {
+    const int j = act ? d0 : 0;
+    load_vec<VPL>(k_g, a.gamma + j, true);
+    load_vec<VPL>(k_mean, a.stats + j, true);
+    load_vec<VPL>(k_rstd, a.stats + D + j, true);
+    load_vec<VPL>(k_s1, a.gsum + j, true);
+    load_vec<VPL>(k_s2, a.gsum + D + j, true);
 #pragma unroll
-  for (int v = 0; v < VPL; ++v) {
-    const int j = act ? d0 + v : 0;
-    k_g[v] = a.gamma[j];
-    k_mean[v] = a.stats[j];
-    k_rstd[v] = a.stats[D + j];
-    k_s1[v] = a.gsum[j] * invN;
-    k_s2[v] = a.gsum[D + j] * invN;
+    for (int v = 0; v < VPL; ++v) { k_s1[v] *= invN; k_s2[v] *= invN; }
   }
 
-  // ---- phase 1: per destination row: BN backward, gate backward, softmax backward, dQ, dS
-  for (int t = r0 + wave; t < r1; t += GTR_WAVES) {
-    const float* qt = a.qkvs + (size_t)t * (4 * D);
-    float gv[VPL], ag[VPL], sv[VPL];
-    const float beta = a.gate[t];
-    float dbeta = 0.0f;
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) {
-      if (act) {
-        const size_t o = (size_t)t * D + d0 + v;
-        const float xh = (a.out[o] - k_mean[v]) * k_rstd[v];
-        gv[v] = (a.dy[o] - k_s1[v] - xh * k_s2[v]) * k_rstd[v] * k_g[v];
-        ag[v] = a.agg[o];
-        sv[v] = qt[3 * D + d0 + v];
-        dbeta += gv[v] * (sv[v] - ag[v]);
-      } else {
-        gv[v] = ag[v] = sv[v] = 0.0f;
-      }
+  // ---- stage (fast): CSR slices, alpha slice, K|V rows of the group
+  if (fast) {
+    for (int i = tid; i <= nrow; i += CONV_BLOCK) {
+      iptr[i] = a.bt.in_ptr[r0 + i] - e_lo;
+      optr[i] = a.bt.out_ptr[r0 + i] - o_lo;
     }
-    dbeta = wave_sum(dbeta);
-    const float du = dbeta * beta * (1.0f - beta);
-    if (lane == 0) a.du[t] = du;
-    float dag[VPL], dq[VPL];
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) {
-      dq[v] = 0.0f;
-      dag[v] = 0.0f;
-      if (act) {
-        const int j = d0 + v;
-        const float w1 = a.w_beta[j], w2 = a.w_beta[D + j], w3 = a.w_beta[2 * D + j];
-        dag[v] = gv[v] * (1.0f - beta) + du * (w1 + w3);
-        const float ds = gv[v] * beta + du * (w2 - w3);
-        a.dqkvs[(size_t)t * (4 * D) + 3 * D + j] = ds;
-        a.dagg[(size_t)t * D + j] = dag[v];
-      }
+    for (int k = tid; k < ne; k += CONV_BLOCK) {
+      isrc[k] = a.bt.in_src[e_lo + k] - r0;
+      oedge[k] = a.bt.out_edge[o_lo + k] - e_lo;
+      odst[k] = a.bt.out_dst[o_lo + k] - r0;
     }
-    const int e0 = a.bt.in_ptr[t], e1 = a.bt.in_ptr[t + 1];
-    float sdot = 0.0f;
-    for (int e = e0; e < e1; ++e) {
-      const float* vt = a.qkvs + (size_t)a.bt.in_src[e] * (4 * D) + 2 * D;
-      float d = 0.0f;
-#pragma unroll
-      for (int v = 0; v < VPL; ++v) d += act ? dag[v] * vt[d0 + v] : 0.0f;
-      d = group_sum(d, GL);
-      const float al = a.alpha[(size_t)e * H + head];
-      const float da = d * dr.mul(st_attn, (uint32_t)(e * H + head));
-      sdot += al * da;
-    }
-    for (int e = e0; e < e1; ++e) {
-      const float* kv = a.qkvs + (size_t)a.bt.in_src[e] * (4 * D);
-      float d = 0.0f;
-#pragma unroll
-      for (int v = 0; v < VPL; ++v) d += act ? dag[v] * kv[2 * D + d0 + v] : 0.0f;
-      d = group_sum(d, GL);
-      const float al = a.alpha[(size_t)e * H + head];
-      const float da = d * dr.mul(st_attn, (uint32_t)(e * H + head));
-      const float dl = al * (da - sdot);
-      if (leader) a.dlogit[(size_t)e * H + head] = dl;
-      const float c = dl / a.sqrt_c;
-#pragma unroll
-      for (int v = 0; v < VPL; ++v) dq[v] += act ? c * kv[D + d0 + v] : 0.0f;
-    }
-    if (act) {
-#pragma unroll
-      for (int v = 0; v < VPL; ++v) a.dqkvs[(size_t)t * (4 * D) + d0 + v] = dq[v];
-    }
-  }
-  __syncthreads();
-
-  // ---- phase 2: per source row: dK, dV over out-edges (CSR by source)
-  for (int s = r0 + wave; s < r1; s += GTR_WAVES) {
-    float dk[VPL], dv[VPL];
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) { dk[v] = 0.0f; dv[v] = 0.0f; }
-    const int i0 = a.bt.out_ptr[s], i1 = a.bt.out_ptr[s + 1];
-    for (int i = i0; i < i1; ++i) {
-      const int p = a.bt.out_edge[i];
-      const int t = a.bt.out_dst[i];
-      const float dl = a.dlogit[(size_t)p * H + head] / a.sqrt_c;
-      const float ad = a.alpha[(size_t)p * H + head] * dr.mul(st_attn, (uint32_t)(p * H + head));
-      const float* qt = a.qkvs + (size_t)t * (4 * D);
-      const float* dgt = a.dagg + (size_t)t * D;
-#pragma unroll
-      for (int v = 0; v < VPL; ++v) {
-        if (act) {
-          dk[v] += dl * qt[d0 + v];
-          dv[v] += ad * dgt[d0 + v];
-        }
-      }
-    }
-    if (act) {
-#pragma unroll
-      for (int v = 0; v < VPL; ++v) {
-        a.dqkvs[(size_t)s * (4 * D) + D + d0 + v] = dk[v];
-        a.dqkvs[(size_t)s * (4 * D) + 2 * D + d0 + v] = dv[v];
-      }
-    }
-  }
-  __syncthreads();
-
-  // ---- phase 3: dX = dQKVS . W_all (MFMA f32), + residual; prev-layer dropout mask
-  const int lr = lane & 15, lg = lane >> 4;
-  const uint32_t st_prev = drop_stream(1, (uint32_t)(a.layer - 1), ctr);
-  for (int rt = r0; rt < r1; rt += 16) {
-    for (int idx = tid; idx < 16 * 4 * D; idx += GTR_BLOCK) {
-      const int i = idx / (4 * D), j = idx - i * (4 * D);
-      const int r = rt + i;
-      As[i * AS + j] = r < r1 ? a.dqkvs[(size_t)r * (4 * D) + j] : 0.0f;
+    for (int k = tid; k < ne * H; k += CONV_BLOCK) ALs[k] = a.alpha[(size_t)e_lo * H + k];
+    for (int idx = tid; idx < nrow * (D / 4); idx += CONV_BLOCK) {
+      const int i = idx / (D / 4), c = (idx - i * (D / 4)) * 4;
+      const float* src = a.qkvs + (size_t)(r0 + i) * (4 * D);
+      *reinterpret_cast<float4*>(R1 + i * D + c) = *reinterpret_cast<const float4*>(src + D + c);
+      *reinterpret_cast<float4*>(R1 + RMAX * D + i * D + c) = *reinterpret_cast<const float4*>(src + 2 * D + c);
     }
     __syncthreads();
-    for (int ct = wave; ct < D / 16; ct += GTR_WAVES) {
+  }
+
+  // ---- phase 1: destination rows
+  if (fast) {
+    for (int t = r0 + wave; t < r1; t += CONV_WAVES)
+      bwd_dst_row<D>(a, t, t - r0, R1, R1 + RMAX * D, D, iptr, isrc, ALs, DLs, e_lo, lane, dr, st_attn,
+                     k_g, k_mean, k_rstd, k_s1, k_s2);
+  } else {
+    for (int t = r0 + wave; t < r1; t += CONV_WAVES)
+      bwd_dst_row<D>(a, t, t, a.qkvs + D, a.qkvs + 2 * D, 4 * D, a.bt.in_ptr, a.bt.in_src, a.alpha, a.dlogit, 0,
+                     lane, dr, st_attn, k_g, k_mean, k_rstd, k_s1, k_s2);
+  }
+  __syncthreads();
+
+  // ---- phase 2: source rows (fast: Q and dA rows re-staged into R1)
+  if (fast) {
+    for (int idx = tid; idx < nrow * (D / 4); idx += CONV_BLOCK) {
+      const int i = idx / (D / 4), c = (idx - i * (D / 4)) * 4;
+      *reinterpret_cast<float4*>(R1 + i * D + c) =
+          *reinterpret_cast<const float4*>(a.qkvs + (size_t)(r0 + i) * (4 * D) + c);
+      *reinterpret_cast<float4*>(R1 + RMAX * D + i * D + c) =
+          *reinterpret_cast<const float4*>(a.dagg + (size_t)(r0 + i) * D + c);
+    }
+    __syncthreads();
+    for (int s = r0 + wave; s < r1; s += CONV_WAVES)
+      bwd_src_row<D>(a, s, s - r0, R1, D, R1 + RMAX * D, D, optr, oedge, odst, ALs, DLs, e_lo, lane, dr, st_attn);
+  } else {
+    for (int s = r0 + wave; s < r1; s += CONV_WAVES)
+      bwd_src_row<D>(a, s, s, a.qkvs, 4 * D, a.dagg, D, a.bt.out_ptr, a.bt.out_edge, a.bt.out_dst, a.alpha,
+                     a.dlogit, 0, lane, dr, st_attn);
+  }
+  __syncthreads();
+
+  // ---- phase 3: dX = dQKVS . W_all (MFMA f32), + residual; previous layer's dropout mask
+  const int lr = lane & 15, lg = lane >> 4;
+  const uint32_t st_prev = drop_stream(1, (uint32_t)(a.layer - 1), ctr);
+  float* As = R1;
+  for (int rt = r0; rt < r1; rt += 16) {
+    for (int idx = tid; idx < 16 * D; idx += CONV_BLOCK) {  // float4 granules
+      const int i = idx / D, c = (idx - i * D) * 4;
+      const int r = rt + i;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < r1) v = *reinterpret_cast<const float4*>(a.dqkvs + (size_t)r * (4 * D) + c);
+      *reinterpret_cast<float4*>(As + i * AS + c) = v;
+    }
+    __syncthreads();
+    for (int ct = wave; ct < D / 16; ct += CONV_WAVES) {
       f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
       const float* arow = As + lr * AS + lg * 4;
       const float* bcol = a.w_all + (size_t)(lg * 4) * D + ct * 16 + lr;
@@ -200,10 +282,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_conv_bwd(ConvBwdK a) {
       for (int kb = 0; kb < D / 4; ++kb) {
         const float4 av = *reinterpret_cast<const float4*>(arow + kb * 16);
         const float* bp = bcol + (size_t)(kb * 16) * D;
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bp[0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bp[D], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bp[2 * D], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bp[3 * D], acc, 0, 0, 0);
+        acc = mfma4(av, make_float4(bp[0], bp[D], bp[2 * D], bp[3 * D]), acc);
       }
       const int col = ct * 16 + lr;
 #pragma unroll
@@ -223,9 +302,10 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_conv_bwd(ConvBwdK a) {
   if (!a.has_prev) return;
   // ---- phase 4: previous layer's BatchNorm backward sums: sum(dy), sum(dy * xhat)
   float* part = a.p_gpart + (size_t)g * 2 * D;
-  for (int j = tid; j < D; j += GTR_BLOCK) {
+  for (int j = tid; j < D; j += CONV_BLOCK) {
     const float mean = a.p_stats[j], rstd = a.p_stats[D + j];
     float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll 4
     for (int r = r0; r < r1; ++r) {
       const size_t o = (size_t)r * D + j;
       const float d = a.p_dy[o];
@@ -235,10 +315,11 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_conv_bwd(ConvBwdK a) {
     part[j] = s1;
     part[D + j] = s2;
   }
-  if (!arrive_last(a.p_cnt, (uint32_t)G, &s_flag)) return;
-  for (int j = tid; j < 2 * D; j += GTR_BLOCK) {
+  if (!arrive_last(a.p_cnt, (uint32_t)Gn, s_flag)) return;
+  for (int j = tid; j < 2 * D; j += CONV_BLOCK) {
     float acc = 0.0f;
-    for (int q = 0; q < G; ++q) acc += a.p_gpart[(size_t)q * 2 * D + j];
+#pragma unroll 4
+    for (int q = 0; q < Gn; ++q) acc += a.p_gpart[(size_t)q * 2 * D + j];
     a.p_gsum[j] = acc;
   }
   if (tid == 0) reset_counter(a.p_cnt);
@@ -271,8 +352,9 @@ struct WgradK {
 };
 
 __global__ __launch_bounds__(GTR_BLOCK) void k_wgrad(WgradK a) {
-  __shared__ __attribute__((aligned(16))) float As[16][64];
-  __shared__ __attribute__((aligned(16))) float Bs[16][64];
+  constexpr int TK = 32;  // node rows staged per round
+  __shared__ __attribute__((aligned(16))) float As[TK][64];
+  __shared__ __attribute__((aligned(16))) float Bs[TK][64];
   const int tid = threadIdx.x;
   const int blk = blockIdx.x;
   int jid = 0;
@@ -291,6 +373,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_wgrad(WgradK a) {
     const int j = tile * GTR_BLOCK + tid;
     if (j >= 3 * D) return;
     float acc = 0.0f;
+#pragma unroll 4
     for (int t = t0; t < t1; ++t) {
       const float u = J.A[t];
       float f;
@@ -311,35 +394,43 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_wgrad(WgradK a) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int k = 0; k < 4; ++k) acc[i][k] = 0.0f;
-  for (int tb = t0; tb < t1; tb += 16) {
-    for (int idx = tid; idx < 16 * 64; idx += GTR_BLOCK) {
+  for (int tb = t0; tb < t1; tb += TK) {
+    float av[TK * 64 / GTR_BLOCK], bv[TK * 64 / GTR_BLOCK];
+#pragma unroll
+    for (int q = 0; q < TK * 64 / GTR_BLOCK; ++q) {
+      const int idx = tid + q * GTR_BLOCK;
       const int i = idx >> 6, c = idx & 63;
       const int t = tb + i;
-      float av = 0.0f, bv = 0.0f;
+      av[q] = 0.0f;
+      bv[q] = 0.0f;
       if (t < t1) {
-        if (m0 + c < J.M1) av = J.A[(size_t)t * J.lda + m0 + c];
+        if (m0 + c < J.M1) av[q] = J.A[(size_t)t * J.lda + m0 + c];
         const int col = n0 + c;
         if (col < J.M2) {
           const float* brow = J.bidx ? J.B + (size_t)J.bidx[t] * J.ldb : J.B + (size_t)t * J.ldb;
-          bv = brow[col];
+          bv[q] = brow[col];
         } else if (col == J.M2) {
-          bv = 1.0f;
+          bv[q] = 1.0f;
         }
       }
-      As[i][c] = av;
-      Bs[i][c] = bv;
+    }
+#pragma unroll
+    for (int q = 0; q < TK * 64 / GTR_BLOCK; ++q) {
+      const int idx = tid + q * GTR_BLOCK;
+      As[idx >> 6][idx & 63] = av[q];
+      Bs[idx >> 6][idx & 63] = bv[q];
     }
     __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
+#pragma unroll 8
+    for (int k = 0; k < TK; ++k) {
       const float4 a4 = *reinterpret_cast<const float4*>(&As[k][ty * 4]);
       const float4 b4 = *reinterpret_cast<const float4*>(&Bs[k][tx * 4]);
-      const float av[4] = {a4.x, a4.y, a4.z, a4.w};
-      const float bv[4] = {b4.x, b4.y, b4.z, b4.w};
+      const float ar[4] = {a4.x, a4.y, a4.z, a4.w};
+      const float br[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[i][q] += av[i] * bv[q];
+        for (int q = 0; q < 4; ++q) acc[i][q] += ar[i] * br[q];
     }
     __syncthreads();
   }
@@ -397,21 +488,24 @@ extern "C" int gtr_conv_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   k.dx0 = dx0;
   const int grid = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;
   if (grid <= 0) return GTR_OK;
-  const size_t lds = (size_t)16 * (4 * D + 4) * sizeof(float) + 16;
   hipStream_t s = (hipStream_t)stream;
+#define GTR_BWD(DD) set_lds_limit<DD>(k_conv_bwd<DD>, (size_t)LayerGeom<DD>::B_WORDS * 4); \
+  hipLaunchKernelGGL(k_conv_bwd<DD>, dim3(grid), dim3(CONV_BLOCK), \
+                                       (size_t)LayerGeom<DD>::B_WORDS * 4, s, k)
   switch (D) {
-    case 32: hipLaunchKernelGGL(k_conv_bwd<32>, dim3(grid), dim3(GTR_BLOCK), lds, s, k); break;
-    case 64: hipLaunchKernelGGL(k_conv_bwd<64>, dim3(grid), dim3(GTR_BLOCK), lds, s, k); break;
-    case 128: hipLaunchKernelGGL(k_conv_bwd<128>, dim3(grid), dim3(GTR_BLOCK), lds, s, k); break;
-    default: hipLaunchKernelGGL(k_conv_bwd<256>, dim3(grid), dim3(GTR_BLOCK), lds, s, k); break;
+    case 32: GTR_BWD(32); break;
+    case 64: GTR_BWD(64); break;
+    case 128: GTR_BWD(128); break;
+    default: GTR_BWD(256); break;
   }
+#undef GTR_BWD
   GTR_HIP_CHECK_LAUNCH();
   return GTR_OK;
 }
 
 extern "C" int gtr_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers,
                          const float* dx0, const float* pe_tab, float* const* layer_slab, float* pe_slab,
-                         int n_chunks, int64_t slab_stride, gtr_stream_t stream) {
+                         int n_chunks, int64_t slab_stride, int l_begin, int l_end, gtr_stream_t stream) {
   if (!cfg || !bt || !layers || !layer_slab || n_chunks <= 0) {
     set_error("gtr_wgrad: bad arguments");
     return GTR_E_ARG;
@@ -423,8 +517,9 @@ extern "C" int gtr_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_l
   k.P = n_chunks;
   k.D = D;
   k.stride = slab_stride;
+  if (l_begin < 0 || l_end > Lc || l_begin > l_end) { set_error("gtr_wgrad: bad layer range"); return GTR_E_ARG; }
   int nj = 0, blocks = 0;
-  for (int l = 0; l < Lc; ++l) {
+  for (int l = l_begin; l < l_end; ++l) {
     const gtr_layer& L = layers[l];
     float* base = layer_slab[l];
     WJob& w = k.jobs[nj++];
@@ -439,7 +534,7 @@ extern "C" int gtr_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_l
     q.outW = base + (size_t)4 * D * D + 4 * D;
     blocks += q.nt * n_chunks;
   }
-  if (cfg->pe_k > 0 && pe_slab) {
+  if (cfg->pe_k > 0 && pe_slab && l_begin == 0) {
     if (!dx0 || (!pe_tab && !bt->node_pe)) { set_error("gtr_wgrad: PE gradient needs dx0 and PE rows"); return GTR_E_ARG; }
     const int K = cfg->pe_k;
     WJob& w = k.jobs[nj++];
@@ -452,6 +547,7 @@ extern "C" int gtr_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_l
     blocks += w.nt * n_chunks;
   }
   k.njobs = nj;
+  if (nj == 0 || blocks == 0) return GTR_OK;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_wgrad, dim3(blocks), dim3(GTR_BLOCK), 0, s, k);
   GTR_HIP_CHECK_LAUNCH();

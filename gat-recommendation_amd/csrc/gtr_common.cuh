@@ -71,10 +71,31 @@ __device__ __forceinline__ int lower_bound_i32(const int32_t* a, int n, int v) {
   return lo;
 }
 
+// First s in [0, B) with a[s] >= v (B if none), a non-decreasing; wave-cooperative
+// 64-ary search: one round of 64 parallel loads per 64x narrowing (1 round for B <= 64).
+__device__ __forceinline__ int wave_lower_bound(const int32_t* a, int B, int v) {
+  const int lane = threadIdx.x & 63;
+  int lo = 0, hi = B;
+  while (hi - lo > 64) {
+    const int step = (hi - lo + 63) >> 6;
+    const int idx = lo + lane * step;
+    const int val = idx < hi ? a[idx] : 0x7FFFFFFF;
+    const int c = __popcll(__ballot(val < v));
+    const int nlo = c > 0 ? lo + (c - 1) * step + 1 : lo;
+    const int nhi = min(hi, lo + c * step);
+    lo = nlo;
+    hi = nhi;
+  }
+  const int idx = lo + lane;
+  const int val = idx < hi ? a[idx] : 0x7FFFFFFF;
+  return lo + __popcll(__ballot(val < v));
+}
+
 // Rows [r0, r1) of row-group g: all sessions whose first node lies in [g*R, (g+1)*R).
+// Must be called by every lane of a wave (ballot); every wave gets the same answer.
 __device__ __forceinline__ void group_rows(const int32_t* node_ptr, int B, int R, int g, int& r0, int& r1) {
-  int s0 = lower_bound_i32(node_ptr, B, g * R);
-  int s1 = lower_bound_i32(node_ptr, B, (g + 1) * R);
+  const int s0 = wave_lower_bound(node_ptr, B, g * R);
+  const int s1 = wave_lower_bound(node_ptr, B, (g + 1) * R);
   r0 = node_ptr[s0];
   r1 = node_ptr[s1];
 }

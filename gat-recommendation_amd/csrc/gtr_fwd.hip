@@ -14,7 +14,7 @@
 //   + scoring loss fwd/bwd (base.py:80-113, losses.py:8-164) + readout backward and
 //   the last BatchNorm's backward sums.
 
-#include "gtr_common.cuh"
+#include "gtr_layer.cuh"
 
 namespace {
 
@@ -55,26 +55,107 @@ struct ConvFwdK {
   int64_t* bn_nbt;
 };
 
+// Attention + gate of one destination row (wave per row).  KB/VB: K/V row bases with
+// row stride KST (LDS on the fast path, global qkvs otherwise); EP/ES: CSR of the rows
+// (local indices on the fast path); eoff: offset of EP's edge indices in alpha.
+template <int D, typename EI>
+__device__ __forceinline__ void attn_row(const ConvFwdK& a, int t, int tl, const float* KB, const float* VB, int KST,
+                                         const EI* EP, const EI* ES, int eoff, int lane, const Drop& dr,
+                                         uint32_t st_attn, float* xo_row) {
+  constexpr int VPL = LayerGeom<D>::VPL;
+  const int d0 = lane * VPL;
+  const bool act = d0 < D;
+  const int C = a.C, H = a.H;
+  const int GL = C / VPL;
+  const int head = act ? d0 / C : 0;
+  const bool leader = act && ((lane & (GL - 1)) == 0);
+  const float* qt = a.qkvs + (size_t)t * (4 * D);
+  float q[VPL], s[VPL], ag[VPL];
+  load_vec<VPL>(q, qt + d0, act);
+  load_vec<VPL>(s, qt + 3 * D + d0, act);
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) ag[v] = 0.0f;
+  const int e0 = EP[tl], e1 = EP[tl + 1];
+  float m = -INFINITY, z = 0.0f;
+  for (int e = e0; e < e1; ++e) {
+    float kv[VPL];
+    load_vec<VPL>(kv, KB + (size_t)ES[e] * KST + d0, act);
+    float dt = 0.0f;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) dt += q[v] * kv[v];
+    const float l = group_sum(dt, GL) / a.sqrt_c;
+    const float mn = fmaxf(m, l);
+    z = z * expf(m - mn) + expf(l - mn);
+    m = mn;
+  }
+  const float zd = z + 1e-16f;
+  for (int e = e0; e < e1; ++e) {
+    const int src = ES[e];
+    float kv[VPL], vv[VPL];
+    load_vec<VPL>(kv, KB + (size_t)src * KST + d0, act);
+    load_vec<VPL>(vv, VB + (size_t)src * KST + d0, act);
+    float dt = 0.0f;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) dt += q[v] * kv[v];
+    const float l = group_sum(dt, GL) / a.sqrt_c;
+    const float al = expf(l - m) / zd;
+    const int eg = e + eoff;
+    if (leader) a.alpha[(size_t)eg * H + head] = al;
+    const float ad = al * dr.mul(st_attn, (uint32_t)(eg * H + head));
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) ag[v] += ad * vv[v];
+  }
+  float u = 0.0f;
+  if (act) {
+    float w1[VPL], w2[VPL], w3[VPL];
+    load_vec<VPL>(w1, a.w_beta + d0, true);
+    load_vec<VPL>(w2, a.w_beta + D + d0, true);
+    load_vec<VPL>(w3, a.w_beta + 2 * D + d0, true);
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) u += w1[v] * ag[v] + w2[v] * s[v] + w3[v] * (ag[v] - s[v]);
+  }
+  u = wave_sum(u);
+  const float beta = 1.0f / (1.0f + expf(-u));
+  float o[VPL];
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) o[v] = beta * s[v] + (1.0f - beta) * ag[v];
+  store_vec<VPL>(a.agg + (size_t)t * D + d0, ag, act);
+  store_vec<VPL>(a.out + (size_t)t * D + d0, o, act);
+  if (xo_row) store_vec<VPL>(xo_row + d0, o, act);
+  if (lane == 0) a.gate[t] = beta;
+}
+
 template <int D>
-__global__ __launch_bounds__(GTR_BLOCK) void k_conv_fwd(ConvFwdK a) {
-  constexpr int XS = D + 4;                       // padded LDS row (16B aligned)
-  constexpr int VPL = D >= 64 ? D / 64 : 1;       // features per lane in row phases
-  __shared__ __attribute__((aligned(16))) float Xs[16 * XS];
-  __shared__ float s_bn[2 * D];
-  __shared__ int s_flag;
+__global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
+  using G = LayerGeom<D>;
+  constexpr int RMAX = G::RMAX, XS = G::XS, KPE = G::KPE;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* XO = sm + G::F_XO;
+  float* KVs = sm + G::F_KV;
+  float* PEs = sm + G::F_PE;
+  float* s_bn = sm + G::F_BN;
+  int* items = reinterpret_cast<int*>(sm + G::F_ITEMS);
+  int* iptr = reinterpret_cast<int*>(sm + G::F_IPTR);
+  int* isrc = reinterpret_cast<int*>(sm + G::F_ISRC);
+  int* s_flag = reinterpret_cast<int*>(sm + G::F_FLAG);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int N = a.bt.hdr[0], B = a.bt.hdr[1];
-  const int G = (N + a.R - 1) / a.R;
+  const int Gn = (N + a.R - 1) / a.R;
   const int g = blockIdx.x;
-  if (g >= G) return;
+  if (g >= Gn) return;
   int r0, r1;
   group_rows(a.bt.node_ptr, B, a.R, g, r0, r1);
+  const int nrow = r1 - r0;
+  const int e_lo = a.bt.in_ptr[r0], e_hi = a.bt.in_ptr[r1];
+  const bool fast = G::KV && nrow <= RMAX && (e_hi - e_lo) <= G::EMAX;
   const uint32_t ctr = a.rng_ctr ? *a.rng_ctr : 0u;
   const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
+  const bool pe_lds = a.first && a.pe_k > 0 && a.pe_k <= KPE;
 
+  // ---- stage: previous BN params, CSR slice, LapPE projection weight
   if (!a.first) {
-    for (int j = tid; j < D; j += GTR_BLOCK) {
+    for (int j = tid; j < D; j += CONV_BLOCK) {
       float mean, rstd;
       if (a.train) { mean = a.p_stats[j]; rstd = a.p_stats[D + j]; }
       else { mean = a.p_rmean[j]; rstd = 1.0f / sqrtf(a.p_rvar[j] + a.bn_eps); }
@@ -82,159 +163,155 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_conv_fwd(ConvFwdK a) {
       s_bn[D + j] = rstd;
     }
   }
-  __syncthreads();
+  if (fast) {
+    for (int i = tid; i <= nrow; i += CONV_BLOCK) iptr[i] = a.bt.in_ptr[r0 + i] - e_lo;
+    for (int k = tid; k < e_hi - e_lo; k += CONV_BLOCK) isrc[k] = a.bt.in_src[e_lo + k] - r0;
+  }
+  if (pe_lds) {
+    for (int idx = tid; idx < D * a.pe_k; idx += CONV_BLOCK) {
+      const int j = idx / a.pe_k, k = idx - j * a.pe_k;
+      PEs[j * KPE + k] = a.wpe[idx];
+    }
+  }
 
-  // ---- phase P+M: layer input rows -> LDS -> QKVS projection on MFMA (f32 in, f32 acc)
+  // ---- phase P+M: layer input rows -> LDS -> QKVS projection (MFMA f32), chunks of RMAX rows
   const uint32_t st_prev = drop_stream(1, (uint32_t)(a.layer - 1), ctr);
   const int lr = lane & 15, lg = lane >> 4;
   constexpr int NCT = (4 * D) / 16;
-  for (int rt = r0; rt < r1; rt += 16) {
-    for (int idx = tid; idx < 16 * D; idx += GTR_BLOCK) {
-      const int i = idx / D, j = idx - i * D;
-      const int r = rt + i;
-      float val = 0.0f;
-      if (r < r1) {
-        const size_t o = (size_t)r * D + j;
-        if (a.first) {
-          const int item = a.bt.node_item[r];
-          val = a.table[(size_t)item * D + j];
-          if (a.pe_k > 0) {
-            const float* pr = a.bt.node_pe ? a.bt.node_pe + (size_t)r * a.pe_k
-                                           : a.pe_tab + (size_t)item * a.pe_k;
-            const float* wr = a.wpe + (size_t)j * a.pe_k;
-            float acc = 0.0f;
-            for (int k = 0; k < a.pe_k; ++k) acc += pr[k] * wr[k];
-            val = val + (acc + a.bpe[j]);
-          }
-        } else {
-          float y = (a.p_out[o] - s_bn[j]) * s_bn[D + j] * a.p_gamma[j] + a.p_beta[j];
-          y = y + a.p_xin[o];
-          val = y * dr.mul(st_prev, (uint32_t)o);
+  // W fragments of this wave's first column tiles, loaded before the prologue so the
+  // weight fetch overlaps the row gather (column tile ct = wave + i*CONV_WAVES).
+  constexpr int PRE = D <= 64 ? (NCT / CONV_WAVES) : 1;
+  float4 wpre[PRE][D / 16];
+#pragma unroll
+  for (int pi = 0; pi < PRE; ++pi) {
+    const float* wrow = a.w_all + (size_t)((wave + pi * CONV_WAVES) * 16 + lr) * D + lg * 4;
+#pragma unroll
+    for (int kb = 0; kb < D / 16; ++kb) wpre[pi][kb] = *reinterpret_cast<const float4*>(wrow + kb * 16);
+  }
+  for (int rc = r0; rc < r1; rc += RMAX) {
+    const int m = min(RMAX, r1 - rc);
+    if (a.first) {
+      for (int i = tid; i < m; i += CONV_BLOCK) items[i] = a.bt.node_item[rc + i];
+      __syncthreads();
+      if (pe_lds) {
+        for (int idx = tid; idx < m * a.pe_k; idx += CONV_BLOCK) {
+          const int i = idx / a.pe_k, k = idx - i * a.pe_k;
+          const float* pr = a.bt.node_pe ? a.bt.node_pe + (size_t)(rc + i) * a.pe_k
+                                         : a.pe_tab + (size_t)items[i] * a.pe_k;
+          PEs[D * KPE + i * KPE + k] = pr[k];
         }
-        a.xin[o] = val;
       }
-      Xs[i * XS + j] = val;
     }
     __syncthreads();
-    for (int ct = wave; ct < NCT; ct += GTR_WAVES) {
-      f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-      const float* wrow = a.w_all + (size_t)(ct * 16 + lr) * D + lg * 4;
-      const float* xrow = Xs + lr * XS + lg * 4;
+    for (int idx = tid; idx < m * D; idx += CONV_BLOCK) {
+      const int i = idx / D, j = idx - i * D;
+      const int r = rc + i;
+      const size_t o = (size_t)r * D + j;
+      float val;
+      if (a.first) {
+        val = a.table[(size_t)items[i] * D + j];
+        if (a.pe_k > 0) {
+          float acc = 0.0f;
+          if (pe_lds) {
+            const float* pr = PEs + D * KPE + i * KPE;
+            const float* wr = PEs + j * KPE;
+            for (int k = 0; k < a.pe_k; ++k) acc += pr[k] * wr[k];
+          } else {
+            const float* pr = a.bt.node_pe ? a.bt.node_pe + (size_t)r * a.pe_k : a.pe_tab + (size_t)items[i] * a.pe_k;
+            const float* wr = a.wpe + (size_t)j * a.pe_k;
+            for (int k = 0; k < a.pe_k; ++k) acc += pr[k] * wr[k];
+          }
+          val = val + (acc + a.bpe[j]);
+        }
+      } else {
+        float y = (a.p_out[o] - s_bn[j]) * s_bn[D + j] * a.p_gamma[j] + a.p_beta[j];
+        y = y + a.p_xin[o];
+        val = y * dr.mul(st_prev, (uint32_t)o);
+      }
+      a.xin[o] = val;
+      XO[i * XS + j] = val;
+    }
+    __syncthreads();
 #pragma unroll
-      for (int kb = 0; kb < D / 16; ++kb) {
-        const float4 av = *reinterpret_cast<const float4*>(xrow + kb * 16);
-        const float4 bv = *reinterpret_cast<const float4*>(wrow + kb * 16);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, bv.x, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, bv.y, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.z, bv.z, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(av.w, bv.w, acc, 0, 0, 0);
+    for (int ti = 0; ti < NCT / CONV_WAVES; ++ti) {
+      const int ct = wave + ti * CONV_WAVES;
+      float4 wf[D / 16];
+      if (ti < PRE) {
+#pragma unroll
+        for (int kb = 0; kb < D / 16; ++kb) wf[kb] = wpre[ti < PRE ? ti : 0][kb];
+      } else {
+        const float* wrow = a.w_all + (size_t)(ct * 16 + lr) * D + lg * 4;
+#pragma unroll
+        for (int kb = 0; kb < D / 16; ++kb) wf[kb] = *reinterpret_cast<const float4*>(wrow + kb * 16);
       }
       const int col = ct * 16 + lr;
       const float bias = a.b_all[col];
+      const int which = col / D, cc = col - which * D;
+      float* kvdst = (fast && (which == 1 || which == 2)) ? KVs + (which - 1) * RMAX * D + cc : nullptr;
+      for (int rt = 0; rt * 16 < m; ++rt) {
+        f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+        const float* xrow = XO + (rt * 16 + lr) * XS + lg * 4;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = rt + lg * 4 + i;
-        if (row < r1) a.qkvs[(size_t)row * (4 * D) + col] = acc[i] + bias;
+        for (int kb = 0; kb < D / 16; ++kb)
+          acc = mfma4(*reinterpret_cast<const float4*>(xrow + kb * 16), wf[kb], acc);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = rt * 16 + lg * 4 + i;
+          if (row < m) {
+            const float v = acc[i] + bias;
+            a.qkvs[(size_t)(rc + row) * (4 * D) + col] = v;
+            if (kvdst) kvdst[row * D] = v;
+          }
+        }
       }
     }
     __syncthreads();
   }
 
-  // ---- phase A: attention over in-edges (CSR by destination) + beta gate; wave per row
-  const int d0 = lane * VPL;
-  const bool act = d0 < D;
-  const int C = a.C, H = a.H;
-  const int GL = C / VPL;
-  const int head = act ? d0 / C : 0;
-  const bool leader = act && ((lane & (GL - 1)) == 0);
+  // ---- phase A: attention over in-edges + beta gate (wave per destination row)
   const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
-  for (int t = r0 + wave; t < r1; t += GTR_WAVES) {
-    const float* qt = a.qkvs + (size_t)t * (4 * D);
-    float q[VPL], s[VPL], ag[VPL];
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) {
-      q[v] = act ? qt[d0 + v] : 0.0f;
-      s[v] = act ? qt[3 * D + d0 + v] : 0.0f;
-      ag[v] = 0.0f;
-    }
-    const int e0 = a.bt.in_ptr[t], e1 = a.bt.in_ptr[t + 1];
-    float m = -INFINITY, z = 0.0f;
-    for (int e = e0; e < e1; ++e) {
-      const float* kt = a.qkvs + (size_t)a.bt.in_src[e] * (4 * D) + D;
-      float dt = 0.0f;
-#pragma unroll
-      for (int v = 0; v < VPL; ++v) dt += act ? q[v] * kt[d0 + v] : 0.0f;
-      dt = group_sum(dt, GL);
-      const float l = dt / a.sqrt_c;
-      const float mn = fmaxf(m, l);
-      z = z * expf(m - mn) + expf(l - mn);
-      m = mn;
-    }
-    const float zd = z + 1e-16f;
-    for (int e = e0; e < e1; ++e) {
-      const float* kv = a.qkvs + (size_t)a.bt.in_src[e] * (4 * D);
-      float dt = 0.0f;
-#pragma unroll
-      for (int v = 0; v < VPL; ++v) dt += act ? q[v] * kv[D + d0 + v] : 0.0f;
-      dt = group_sum(dt, GL);
-      const float l = dt / a.sqrt_c;
-      const float al = expf(l - m) / zd;
-      if (leader) a.alpha[(size_t)e * H + head] = al;
-      const float ad = al * dr.mul(st_attn, (uint32_t)(e * H + head));
-#pragma unroll
-      for (int v = 0; v < VPL; ++v) ag[v] += act ? ad * kv[2 * D + d0 + v] : 0.0f;
-    }
-    float u = 0.0f;
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) {
-      if (act) {
-        const int j = d0 + v;
-        u += a.w_beta[j] * ag[v] + a.w_beta[D + j] * s[v] + a.w_beta[2 * D + j] * (ag[v] - s[v]);
-      }
-    }
-    u = wave_sum(u);
-    const float beta = 1.0f / (1.0f + expf(-u));
-    if (act) {
-#pragma unroll
-      for (int v = 0; v < VPL; ++v) {
-        const size_t o = (size_t)t * D + d0 + v;
-        a.agg[o] = ag[v];
-        a.out[o] = beta * s[v] + (1.0f - beta) * ag[v];
-      }
-    }
-    if (lane == 0) a.gate[t] = beta;
+  if (fast) {
+    for (int t = r0 + wave; t < r1; t += CONV_WAVES)
+      attn_row<D, int>(a, t, t - r0, KVs, KVs + RMAX * D, D, iptr, isrc, e_lo, lane, dr, st_attn,
+                       XO + (t - r0) * XS);
+  } else {
+    for (int t = r0 + wave; t < r1; t += CONV_WAVES)
+      attn_row<D, int32_t>(a, t, t, a.qkvs + D, a.qkvs + 2 * D, 4 * D, a.bt.in_ptr, a.bt.in_src, 0, lane, dr,
+                           st_attn, nullptr);
   }
-
   if (!a.train) return;
 
   // ---- phase S: BatchNorm batch statistics (two-pass per group, Chan combine by the last arriver)
   __syncthreads();
   float* part = a.bn_part + (size_t)g * (1 + 2 * D);
-  for (int j = tid; j < D; j += GTR_BLOCK) {
+  for (int j = tid; j < D; j += CONV_BLOCK) {
     float sum = 0.0f;
-    for (int r = r0; r < r1; ++r) sum += a.out[(size_t)r * D + j];
-    const int n = r1 - r0;
-    const float mean = n > 0 ? sum / (float)n : 0.0f;
+    if (fast) for (int i = 0; i < nrow; ++i) sum += XO[i * XS + j];
+    else for (int r = r0; r < r1; ++r) sum += a.out[(size_t)r * D + j];
+    const float mean = nrow > 0 ? sum / (float)nrow : 0.0f;
     float m2 = 0.0f;
-    for (int r = r0; r < r1; ++r) {
-      const float d = a.out[(size_t)r * D + j] - mean;
-      m2 += d * d;
+    if (fast) {
+      for (int i = 0; i < nrow; ++i) { const float d = XO[i * XS + j] - mean; m2 += d * d; }
+    } else {
+      for (int r = r0; r < r1; ++r) { const float d = a.out[(size_t)r * D + j] - mean; m2 += d * d; }
     }
     part[1 + j] = mean;
     part[1 + D + j] = m2;
   }
-  if (tid == 0) part[0] = (float)(r1 - r0);
-  if (!arrive_last(a.cnt, (uint32_t)G, &s_flag)) return;
-  for (int j = tid; j < D; j += GTR_BLOCK) {
+  if (tid == 0) part[0] = (float)nrow;
+  if (!arrive_last(a.cnt, (uint32_t)Gn, s_flag)) return;
+  for (int j = tid; j < D; j += CONV_BLOCK) {
     double n = 0.0, sum = 0.0;
-    for (int q = 0; q < G; ++q) {
+#pragma unroll 4
+    for (int q = 0; q < Gn; ++q) {
       const float* pp = a.bn_part + (size_t)q * (1 + 2 * D);
       n += (double)pp[0];
       sum += (double)pp[0] * (double)pp[1 + j];
     }
     const double mean = sum / n;
     double m2 = 0.0;
-    for (int q = 0; q < G; ++q) {
+#pragma unroll 4
+    for (int q = 0; q < Gn; ++q) {
       const float* pp = a.bn_part + (size_t)q * (1 + 2 * D);
       const double d = (double)pp[1 + j] - mean;
       m2 += (double)pp[1 + D + j] + (double)pp[0] * d * d;
@@ -282,17 +359,10 @@ struct ReadoutK {
 };
 
 template <int D>
-__device__ __forceinline__ float row_dot(const float* row, const float (&x)[D >= 64 ? D / 64 : 1], int d0, bool act) {
-  constexpr int VPL = D >= 64 ? D / 64 : 1;
-  float s = 0.0f;
-#pragma unroll
-  for (int v = 0; v < VPL; ++v) s += act ? x[v] * row[d0 + v] : 0.0f;
-  return wave_sum(s);
-}
-
-template <int D>
 __global__ __launch_bounds__(GTR_BLOCK) void k_readout(ReadoutK a) {
   constexpr int VPL = D >= 64 ? D / 64 : 1;
+  constexpr int NB = 8;   // node rows in flight per wave
+  constexpr int NK = 8;   // negative rows in flight per wave
   __shared__ float s_bn[2 * D];
   __shared__ float s_red[GTR_WAVES][2 * D];
   __shared__ float s_loss[GTR_WAVES][2];
@@ -324,6 +394,14 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_readout(ReadoutK a) {
     }
   }
   __syncthreads();
+  float bm[VPL], br[VPL], bg[VPL], bb[VPL];
+  if (do_fwd || do_bwd) {
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const int j = act ? d0 + v : 0;
+      bm[v] = s_bn[j]; br[v] = s_bn[D + j]; bg[v] = a.gamma[j]; bb[v] = a.beta[j];
+    }
+  }
 
   float gs[VPL], gx[VPL];
 #pragma unroll
@@ -340,101 +418,142 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_readout(ReadoutK a) {
       float acc[VPL];
 #pragma unroll
       for (int v = 0; v < VPL; ++v) acc[v] = 0.0f;
-      for (int i = n0; i < n1; ++i) {
+      for (int i0 = n0; i0 < n1; i0 += NB) {
+        float ov[NB][VPL], xv[NB][VPL];
 #pragma unroll
-        for (int v = 0; v < VPL; ++v) {
-          if (act) {
-            const int j = d0 + v;
-            const size_t o = (size_t)i * D + j;
-            float y = (a.out[o] - s_bn[j]) * s_bn[D + j] * a.gamma[j] + a.beta[j];
-            y = y + a.xin[o];
-            acc[v] += y * dr.mul(st, (uint32_t)o);
+        for (int q = 0; q < NB; ++q) {
+          const bool ok = act && (i0 + q < n1);
+          load_vec<VPL>(ov[q], a.out + (size_t)(i0 + q) * D + d0, ok);
+          load_vec<VPL>(xv[q], a.xin + (size_t)(i0 + q) * D + d0, ok);
+        }
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          if (i0 + q < n1) {
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) {
+              const size_t o = (size_t)(i0 + q) * D + d0 + v;
+              float y = (ov[q][v] - bm[v]) * br[v] * bg[v] + bb[v];
+              y = y + xv[q][v];
+              acc[v] += y * dr.mul(st, (uint32_t)o);
+            }
           }
         }
       }
 #pragma unroll
-      for (int v = 0; v < VPL; ++v) {
-        se[v] = acc[v] / cnt;
-        if (act) a.se[(size_t)b * D + d0 + v] = se[v];
-      }
+      for (int v = 0; v < VPL; ++v) se[v] = acc[v] / cnt;
+      store_vec<VPL>(a.se + (size_t)b * D + d0, se, act);
     } else {
-#pragma unroll
-      for (int v = 0; v < VPL; ++v) se[v] = act ? a.se[(size_t)b * D + d0 + v] : 0.0f;
+      load_vec<VPL>(se, a.se + (size_t)b * D + d0, act);
     }
 
     if (do_loss) {
       const float* trow = a.table + (size_t)a.bt.target[b] * D;
       const int* negs = a.bt.negatives + (size_t)b * n;
-      const float pos = row_dot<D>(trow, se, d0, act);
-      float dpos = 0.0f;
-      // pass 1: BPR terms (independent per negative) + online log-sum-exp for listwise
-      float m = pos * inv_t, z = 1.0f;
-      for (int k = 0; k < n; ++k) {
-        const float* nrow = a.table + (size_t)negs[k] * D;
-        const float sk = row_dot<D>(nrow, se, d0, act);
-        float cb = 0.0f;
-        if (use_bpr) {
-          const float sg = 1.0f / (1.0f + expf(-(pos - sk)));
-          bpr_sum += -logf(sg + 1e-8f);
-          const float dz = -(sg * (1.0f - sg)) / (sg + 1e-8f) * inv_bn * w_bpr;
-          dpos += dz;
-          cb = -dz;
-        }
-        if (use_lw) {
-          const float l = sk * inv_t;
-          const float mn = fmaxf(m, l);
-          z = z * expf(m - mn) + expf(l - mn);
-          m = mn;
-        }
-        if (!use_lw) {
-          if (lane == 0) a.coef_neg[(size_t)b * n + k] = cb;
+      float tv[VPL];
+      load_vec<VPL>(tv, trow + d0, act);
+      float pos = 0.0f;
 #pragma unroll
-          for (int v = 0; v < VPL; ++v) dse[v] += act ? cb * nrow[d0 + v] : 0.0f;
+      for (int v = 0; v < VPL; ++v) pos += se[v] * tv[v];
+      pos = wave_sum(pos);
+      float dpos = 0.0f;
+      float m = pos * inv_t, z = 1.0f;
+      int nid = 0;
+      // pass 1: BPR terms (+ coefficients when BPR only) and online log-sum-exp for listwise
+      for (int k0 = 0; k0 < n; k0 += NK) {
+        if ((k0 & 63) == 0) nid = (k0 + lane < n) ? negs[k0 + lane] : 0;
+        float rv[NK][VPL];
+#pragma unroll
+        for (int q = 0; q < NK; ++q) {
+          const int id = __shfl(nid, (k0 + q) & 63);
+          load_vec<VPL>(rv[q], a.table + (size_t)id * D + d0, act && (k0 + q < n));
+        }
+#pragma unroll
+        for (int q = 0; q < NK; ++q) {
+          const int k = k0 + q;
+          if (k >= n) break;
+          float sk = 0.0f;
+#pragma unroll
+          for (int v = 0; v < VPL; ++v) sk += se[v] * rv[q][v];
+          sk = wave_sum(sk);
+          float cb = 0.0f;
+          if (use_bpr) {
+            const float sg = 1.0f / (1.0f + expf(-(pos - sk)));
+            bpr_sum += -logf(sg + 1e-8f);
+            const float dz = -(sg * (1.0f - sg)) / (sg + 1e-8f) * inv_bn * w_bpr;
+            dpos += dz;
+            cb = -dz;
+          }
+          if (use_lw) {
+            const float l = sk * inv_t;
+            const float mn = fmaxf(m, l);
+            z = z * expf(m - mn) + expf(l - mn);
+            m = mn;
+          } else {
+            if (lane == 0) a.coef_neg[(size_t)b * n + k] = cb;
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) dse[v] += cb * rv[q][v];
+          }
         }
       }
       if (use_lw) {
         const float lse = m + logf(z);
         lw_sum += lse - pos * inv_t;
         dpos += (expf(pos * inv_t - lse) - 1.0f) * inv_b * inv_t * w_lw;
-        // pass 2: softmax coefficients (+ BPR coefficients recomputed for dual)
-        for (int k = 0; k < n; ++k) {
-          const float* nrow = a.table + (size_t)negs[k] * D;
-          const float sk = row_dot<D>(nrow, se, d0, act);
-          float cb = expf(sk * inv_t - lse) * inv_b * inv_t * w_lw;
-          if (use_bpr) {
-            const float sg = 1.0f / (1.0f + expf(-(pos - sk)));
-            cb += (sg * (1.0f - sg)) / (sg + 1e-8f) * inv_bn * w_bpr;
-          }
-          if (lane == 0) a.coef_neg[(size_t)b * n + k] = cb;
+        // pass 2: softmax coefficients (+ BPR coefficients for dual)
+        for (int k0 = 0; k0 < n; k0 += NK) {
+          if ((k0 & 63) == 0) nid = (k0 + lane < n) ? negs[k0 + lane] : 0;
+          float rv[NK][VPL];
 #pragma unroll
-          for (int v = 0; v < VPL; ++v) dse[v] += act ? cb * nrow[d0 + v] : 0.0f;
+          for (int q = 0; q < NK; ++q) {
+            const int id = __shfl(nid, (k0 + q) & 63);
+            load_vec<VPL>(rv[q], a.table + (size_t)id * D + d0, act && (k0 + q < n));
+          }
+#pragma unroll
+          for (int q = 0; q < NK; ++q) {
+            const int k = k0 + q;
+            if (k >= n) break;
+            float sk = 0.0f;
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) sk += se[v] * rv[q][v];
+            sk = wave_sum(sk);
+            float cb = expf(sk * inv_t - lse) * inv_b * inv_t * w_lw;
+            if (use_bpr) {
+              const float sg = 1.0f / (1.0f + expf(-(pos - sk)));
+              cb += (sg * (1.0f - sg)) / (sg + 1e-8f) * inv_bn * w_bpr;
+            }
+            if (lane == 0) a.coef_neg[(size_t)b * n + k] = cb;
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) dse[v] += cb * rv[q][v];
+          }
         }
       }
       if (lane == 0) a.coef_tgt[b] = dpos;
 #pragma unroll
-      for (int v = 0; v < VPL; ++v) dse[v] += act ? dpos * trow[d0 + v] : 0.0f;
-      if (a.dse_out && act) {
-#pragma unroll
-        for (int v = 0; v < VPL; ++v) a.dse_out[(size_t)b * D + d0 + v] = dse[v];
-      }
+      for (int v = 0; v < VPL; ++v) dse[v] += dpos * tv[v];
+      if (a.dse_out) store_vec<VPL>(a.dse_out + (size_t)b * D + d0, dse, act);
     } else if (do_bwd) {
-#pragma unroll
-      for (int v = 0; v < VPL; ++v) dse[v] = act ? a.dse_in[(size_t)b * D + d0 + v] : 0.0f;
+      load_vec<VPL>(dse, a.dse_in + (size_t)b * D + d0, act);
     }
 
     if (do_bwd) {
       const float inv_cnt = 1.0f / cnt;
-      for (int i = n0; i < n1; ++i) {
+      for (int i0 = n0; i0 < n1; i0 += NB) {
+        float ov[NB][VPL];
 #pragma unroll
-        for (int v = 0; v < VPL; ++v) {
-          if (act) {
-            const int j = d0 + v;
-            const size_t o = (size_t)i * D + j;
-            const float dyv = dse[v] * inv_cnt * dr.mul(st, (uint32_t)o);
-            a.dy[o] = dyv;
-            const float xh = (a.out[o] - s_bn[j]) * s_bn[D + j];
-            gs[v] += dyv;
-            gx[v] += dyv * xh;
+        for (int q = 0; q < NB; ++q) load_vec<VPL>(ov[q], a.out + (size_t)(i0 + q) * D + d0, act && (i0 + q < n1));
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+          if (i0 + q < n1) {
+            float dyv[VPL];
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) {
+              const size_t o = (size_t)(i0 + q) * D + d0 + v;
+              dyv[v] = dse[v] * inv_cnt * dr.mul(st, (uint32_t)o);
+              const float xh = (ov[q][v] - bm[v]) * br[v];
+              gs[v] += dyv[v];
+              gx[v] += dyv[v] * xh;
+            }
+            store_vec<VPL>(a.dy + (size_t)(i0 + q) * D + d0, dyv, act);
           }
         }
       }
@@ -473,6 +592,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_readout(ReadoutK a) {
   if (do_bwd) {
     for (int j = tid; j < 2 * D; j += GTR_BLOCK) {
       float acc = 0.0f;
+#pragma unroll 4
       for (int q = 0; q < (int)gridDim.x; ++q) acc += a.gpart[(size_t)q * 2 * D + j];
       a.gsum[j] = acc;
     }
@@ -546,12 +666,16 @@ extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   const int grid = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;
   if (grid <= 0) return GTR_OK;
   hipStream_t s = (hipStream_t)stream;
+#define GTR_FWD(DD) set_lds_limit<DD>(k_conv_fwd<DD>, (size_t)LayerGeom<DD>::F_WORDS * 4); \
+  hipLaunchKernelGGL(k_conv_fwd<DD>, dim3(grid), dim3(CONV_BLOCK), \
+                                       (size_t)LayerGeom<DD>::F_WORDS * 4, s, k)
   switch (cfg->dim) {
-    case 32: hipLaunchKernelGGL(k_conv_fwd<32>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
-    case 64: hipLaunchKernelGGL(k_conv_fwd<64>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
-    case 128: hipLaunchKernelGGL(k_conv_fwd<128>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
-    default: hipLaunchKernelGGL(k_conv_fwd<256>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    case 32: GTR_FWD(32); break;
+    case 64: GTR_FWD(64); break;
+    case 128: GTR_FWD(128); break;
+    default: GTR_FWD(256); break;
   }
+#undef GTR_FWD
   GTR_HIP_CHECK_LAUNCH();
   return GTR_OK;
 }

@@ -1,0 +1,95 @@
+// gtr_layer.cuh — geometry shared by the layer kernels (forward and backward).
+//
+// A layer kernel's workgroup owns one row group: every session whose first node lies
+// in [g*R, (g+1)*R).  On the fast path (group rows <= RMAX, group edges <= EMAX) the
+// group's CSR slices and K/V (forward) or K/V, Q, dA (backward) rows are staged in LDS
+// so that the per-edge work of the attention never waits on HBM/L2; otherwise the
+// same code runs against global memory (any session size, any dim).
+#pragma once
+
+#include "gtr_common.cuh"
+
+#define CONV_BLOCK 512
+#define CONV_WAVES (CONV_BLOCK / 64)
+
+namespace gtr {
+
+template <int D>
+struct LayerGeom {
+  static constexpr int VPL = D >= 64 ? D / 64 : 1;    // features per lane in row loops
+  static constexpr int RMAX = D <= 64 ? 64 : (D == 128 ? 32 : 16);
+  static constexpr bool KV = D <= 128;                 // K/V rows staged in LDS
+  static constexpr int XS = D + 4;                     // padded LDS row (16B aligned)
+  static constexpr int EMAX = 1024;                    // edges of a group staged in LDS
+  static constexpr int KPE = 16;                       // LapPE width staged in LDS
+  // ---- forward LDS carve (4-byte words)
+  static constexpr int F_XO = 0;                              // [RMAX][XS]   X rows, then OUT rows
+  static constexpr int F_KV = F_XO + RMAX * XS;               // [2][RMAX][D] K rows | V rows
+  static constexpr int F_PE = F_KV + (KV ? 2 * RMAX * D : 0); // [D][KPE] Wpe | [RMAX][KPE] P rows
+  static constexpr int F_BN = F_PE + (D + RMAX) * KPE;        // [2D] previous BN mean | rstd
+  static constexpr int F_ITEMS = F_BN + 2 * D;                // [RMAX] node items
+  static constexpr int F_IPTR = F_ITEMS + RMAX;               // [RMAX+1] local in_ptr
+  static constexpr int F_ISRC = F_IPTR + RMAX + 4;            // [EMAX] local in_src
+  static constexpr int F_FLAG = F_ISRC + EMAX;
+  static constexpr int F_WORDS = F_FLAG + 4;
+  // ---- backward LDS carve (4-byte words)
+  static constexpr int AS = 4 * D + 4;                        // dQKVS staging row for dX
+  static constexpr int B_R1N = (2 * RMAX * D > 16 * AS) ? 2 * RMAX * D : 16 * AS;
+  static constexpr int B_R1 = 0;                              // K|V rows, then Q|dA rows, then dQKVS tile
+  static constexpr int B_ALPHA = B_R1 + B_R1N;                // [EMAX*8] alpha of group edges
+  static constexpr int B_DLOG = B_ALPHA + EMAX * 8;           // [EMAX*8] dlogit of group edges
+  static constexpr int B_IPTR = B_DLOG + EMAX * 8;            // [RMAX+1]
+  static constexpr int B_ISRC = B_IPTR + RMAX + 4;            // [EMAX]
+  static constexpr int B_OPTR = B_ISRC + EMAX;                // [RMAX+1]
+  static constexpr int B_OEDGE = B_OPTR + RMAX + 4;           // [EMAX] local dst-order position
+  static constexpr int B_ODST = B_OEDGE + EMAX;               // [EMAX] local dst row
+  static constexpr int B_FLAG = B_ODST + EMAX;
+  static constexpr int B_WORDS = B_FLAG + 4;
+};
+
+// One 16x16 f32 MFMA tile-step over 4 k values held as float4 by each lane.
+__device__ __forceinline__ f32x4 mfma4(const float4 a, const float4 b, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc, 0, 0, 0);
+  return acc;
+}
+
+template <int VPL>
+__device__ __forceinline__ void load_vec(float (&x)[VPL], const float* p, bool act) {
+  if constexpr (VPL == 4) {
+    float4 t = act ? *reinterpret_cast<const float4*>(p) : make_float4(0.f, 0.f, 0.f, 0.f);
+    x[0] = t.x; x[1] = t.y; x[2] = t.z; x[3] = t.w;
+  } else if constexpr (VPL == 2) {
+    float2 t = act ? *reinterpret_cast<const float2*>(p) : make_float2(0.f, 0.f);
+    x[0] = t.x; x[1] = t.y;
+  } else {
+    x[0] = act ? p[0] : 0.0f;
+  }
+}
+
+template <int VPL>
+__device__ __forceinline__ void store_vec(float* p, const float (&x)[VPL], bool act) {
+  if (!act) return;
+  if constexpr (VPL == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(x[0], x[1], x[2], x[3]);
+  } else if constexpr (VPL == 2) {
+    *reinterpret_cast<float2*>(p) = make_float2(x[0], x[1]);
+  } else {
+    p[0] = x[0];
+  }
+}
+
+// Dynamic LDS above 64 KiB needs the per-kernel limit raised once (gfx950: 160 KiB per CU).
+template <int D, typename K>
+inline void set_lds_limit(K kernel, size_t bytes) {
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)bytes);
+    done = true;
+  }
+}
+
+}  // namespace gtr

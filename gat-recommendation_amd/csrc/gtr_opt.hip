@@ -93,67 +93,67 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_contrib_prep(gtr_batch bt, int T,
   if (stamp && key > 0 && key < T) stamp[key] = (int32_t)(*step_dev + 1);
 }
 
+// Touched rows: one thread per (segment start, float4 column).  p/m/v of the row are
+// fetched up front (they depend only on the key), the segment's contributions are
+// summed in sorted (stable) order, then AdamW — or the dense gradient is written.
 template <int D>
 __global__ __launch_bounds__(GTR_BLOCK) void k_adamw_rows(gtr_batch bt, int T, const int32_t* skeys,
                                                           const int32_t* svals, const float* dx0,
                                                           const float* se, const float* coef_tgt,
                                                           const float* coef_neg, float* table, float* m,
                                                           float* v, float* grad_dense, gtr_adam opt) {
-  constexpr int VPL = D >= 64 ? D / 64 : 1;
-  constexpr int CHUNK = 16;
+  constexpr int C4 = D / 4;
   __shared__ AdamStep s_st;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (grad_dense == nullptr && threadIdx.x == 0) s_st.init(opt, *opt.step_dev + 1);
   __syncthreads();
   const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
-  const int d0 = lane * VPL;
-  const bool act = d0 < D;
-  const int c0 = (blockIdx.x * GTR_WAVES + wave) * CHUNK;
-  if (c0 >= m_cap) return;
-  const int c1 = min(m_cap, c0 + CHUNK);
-  for (int i = c0; i < c1; ++i) {
-    const int key = skeys[i];
-    if (key <= 0 || key >= T) continue;
-    if (i > 0 && skeys[i - 1] == key) continue;  // not a segment start
-    float g[VPL];
-#pragma unroll
-    for (int q = 0; q < VPL; ++q) g[q] = 0.0f;
-    for (int k = i; k < m_cap && skeys[k] == key; ++k) {
-      const int j = svals[k];
-      const float* src;
-      float c;
-      if (j < bt.n_cap) {
-        src = dx0 + (size_t)j * D;
-        c = 1.0f;
-      } else if (j < bt.n_cap + bt.b_cap) {
-        const int b = j - bt.n_cap;
-        src = se + (size_t)b * D;
-        c = coef_tgt[b];
-      } else {
-        const int qn = j - bt.n_cap - bt.b_cap;
-        src = se + (size_t)(qn / bt.n_neg) * D;
-        c = coef_neg[qn];
-      }
-#pragma unroll
-      for (int q = 0; q < VPL; ++q) g[q] += act ? c * src[d0 + q] : 0.0f;
-    }
-    if (!act) continue;
-    const size_t base = (size_t)key * D + d0;
-    if (grad_dense) {
-#pragma unroll
-      for (int q = 0; q < VPL; ++q) grad_dense[base + q] = g[q];
-    } else {
-      const AdamStep st = s_st;
-#pragma unroll
-      for (int q = 0; q < VPL; ++q) {
-        float pv = table[base + q], mv = m[base + q], vv = v[base + q];
-        st.apply(pv, mv, vv, g[q]);
-        table[base + q] = pv;
-        m[base + q] = mv;
-        v[base + q] = vv;
-      }
-    }
+  const int gid = blockIdx.x * GTR_BLOCK + threadIdx.x;
+  const int i = gid / C4, c = gid - (gid / C4) * C4;
+  if (i >= m_cap) return;
+  const int key = skeys[i];
+  const int prev = i > 0 ? skeys[i - 1] : -1;
+  if (key <= 0 || key >= T || prev == key) return;
+  const size_t base = (size_t)key * C4 + c;
+  float4 pv = make_float4(0.f, 0.f, 0.f, 0.f), mv = pv, vv = pv;
+  if (!grad_dense) {
+    pv = reinterpret_cast<const float4*>(table)[base];
+    mv = reinterpret_cast<const float4*>(m)[base];
+    vv = reinterpret_cast<const float4*>(v)[base];
   }
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  int k = i;
+  do {
+    const int j = svals[k];
+    const float* src;
+    float cf;
+    if (j < bt.n_cap) {
+      src = dx0 + (size_t)j * D;
+      cf = 1.0f;
+    } else if (j < bt.n_cap + bt.b_cap) {
+      const int b = j - bt.n_cap;
+      src = se + (size_t)b * D;
+      cf = coef_tgt[b];
+    } else {
+      const int qn = j - bt.n_cap - bt.b_cap;
+      src = se + (size_t)(qn / bt.n_neg) * D;
+      cf = coef_neg[qn];
+    }
+    const float4 sv = reinterpret_cast<const float4*>(src)[c];
+    g.x += cf * sv.x; g.y += cf * sv.y; g.z += cf * sv.z; g.w += cf * sv.w;
+    ++k;
+  } while (k < m_cap && skeys[k] == key);
+  if (grad_dense) {
+    reinterpret_cast<float4*>(grad_dense)[base] = g;
+    return;
+  }
+  const AdamStep st = s_st;
+  st.apply(pv.x, mv.x, vv.x, g.x);
+  st.apply(pv.y, mv.y, vv.y, g.y);
+  st.apply(pv.z, mv.z, vv.z, g.z);
+  st.apply(pv.w, mv.w, vv.w, g.w);
+  reinterpret_cast<float4*>(table)[base] = pv;
+  reinterpret_cast<float4*>(m)[base] = mv;
+  reinterpret_cast<float4*>(v)[base] = vv;
 }
 
 // Untouched rows: 16 B per thread per tensor, grid-stride; rows with stamp == step+1 skipped.
@@ -323,8 +323,8 @@ int gtr_adamw_rows(const gtr_batch* bt, int num_items, int dim, const int32_t* s
   gtr_adam o{};
   if (opt) o = *opt;
   const int m_cap = bt->n_cap + bt->b_cap * (1 + bt->n_neg);
-  const int waves = (m_cap + 15) / 16;
-  const int blocks = (waves + GTR_WAVES - 1) / GTR_WAVES;
+  const int64_t threads = (int64_t)m_cap * (dim / 4);
+  const int blocks = (int)((threads + GTR_BLOCK - 1) / GTR_BLOCK);
   hipStream_t s = (hipStream_t)stream;
 #define GTR_ROWS(DD)                                                                                         \
   hipLaunchKernelGGL(k_adamw_rows<DD>, dim3(blocks), dim3(GTR_BLOCK), 0, s, *bt, num_items, skeys, svals, dx0, \

@@ -236,7 +236,8 @@ class Engine:
         return 16 if caps.n_cap <= 8192 else (32 if caps.n_cap <= 65536 else 64)
 
     def choose_P(self, caps: Caps) -> int:
-        return max(1, min(32, (caps.n_cap + 511) // 512))
+        # split-K of the weight gradients: <= 32 node rows per workgroup, <= 64 slabs
+        return max(1, min(64, (caps.n_cap + 31) // 32))
 
     def workspace(self, caps: Caps, fresh: bool = False) -> Workspace:
         if fresh:
@@ -322,18 +323,30 @@ class Engine:
         L.check(L.lib().gtr_readout_loss(C.byref(cfg), C.byref(bs), self.model.item_embedding.weight.data_ptr(),
                                          ws.structs, C.byref(h), self.stream()), "readout_loss")
 
-    def run_backward(self, ws: Workspace, cfg: L.GtrConfig, bs: L.GtrBatch):
-        """conv_bwd(L-1..0) + weight-gradient slabs; expects layers[L-1].dy / bn_gsum."""
-        lib = L.lib()
-        st = self.stream()
-        for l in range(self.L - 1, -1, -1):
-            L.check(lib.gtr_conv_bwd(C.byref(cfg), C.byref(bs), ws.structs, l, ws.dx0.data_ptr(), st), "conv_bwd")
+    def _wgrad(self, ws, cfg, bs, l0, l1, st):
         pe_tab = None
         if self.K > 0 and self.model.laplacian_pe._cached_pe is not None:
             pe_tab = self.model.laplacian_pe._cached_pe.data_ptr()
-        L.check(lib.gtr_wgrad(C.byref(cfg), C.byref(bs), ws.structs, ws.dx0.data_ptr(), pe_tab, ws.slab_ptrs,
-                              None if ws.pe_slab is None else ws.pe_slab.data_ptr(), ws.P,
-                              self.flat.layout.slab_stride, st), "wgrad")
+        L.check(L.lib().gtr_wgrad(C.byref(cfg), C.byref(bs), ws.structs, ws.dx0.data_ptr(), pe_tab, ws.slab_ptrs,
+                                  None if ws.pe_slab is None else ws.pe_slab.data_ptr(), ws.P,
+                                  self.flat.layout.slab_stride, l0, l1, st), "wgrad")
+
+    def run_backward(self, ws: Workspace, cfg: L.GtrConfig, bs: L.GtrBatch, side: torch.cuda.Stream | None = None):
+        """conv_bwd(L-1..0) + weight-gradient slabs; expects layers[L-1].dy / bn_gsum.
+        With ``side``, layer l >= 1 weight gradients run on that stream concurrently
+        with conv_bwd(l-1..0); the caller must join ``side`` before reading slabs."""
+        lib = L.lib()
+        main = torch.cuda.current_stream(self.device)
+        st = main.cuda_stream
+        for l in range(self.L - 1, -1, -1):
+            L.check(lib.gtr_conv_bwd(C.byref(cfg), C.byref(bs), ws.structs, l, ws.dx0.data_ptr(), st), "conv_bwd")
+            if side is not None and l >= 1:
+                side.wait_stream(main)
+                self._wgrad(ws, cfg, bs, l, l + 1, side.cuda_stream)
+        if side is not None:
+            self._wgrad(ws, cfg, bs, 0, 1, st)
+        else:
+            self._wgrad(ws, cfg, bs, 0, self.L, st)
 
     def segments(self, ws: Workspace):
         """Segment table mapping each flat parameter segment to its gradient source."""

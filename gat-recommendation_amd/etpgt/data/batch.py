@@ -206,6 +206,10 @@ def pack_batch(sb: SessionBatch, caps: Caps) -> np.ndarray:
         raise ValueError(f"batch (N={N}, B={B}, E={E}, n={n_neg}) exceeds capacity {caps}")
     x = _np(sb.x).astype(np.int64)
     ei = _np(sb.edge_index).astype(np.int64).reshape(2, -1)
+    if sb.batch is not None and N:
+        bv = _np(sb.batch).astype(np.int64)
+        if bv.shape[0] != N or np.any(np.diff(bv) < 0) or bv[0] < 0:
+            raise ValueError("batch vector must be sorted with contiguous sessions (PyG layout)")
     ptr = _np(sb.ptr).astype(np.int64)
     if ptr.shape[0] != B + 1 or ptr[0] != 0 or ptr[-1] != N or np.any(np.diff(ptr) < 0):
         raise ValueError("batch vector must be sorted with contiguous sessions (PyG layout)")

@@ -20,6 +20,7 @@ into a ``torch.optim.AdamW`` state_dict layout.
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 
@@ -42,6 +43,8 @@ class FusedTrainStep:
         self.temperature = float(temperature)
         self.alpha = float(alpha)
         self.use_graph = use_graph
+        # experiment knob: run the untouched-row sweep after the chain instead of beside it
+        self.serial_sweep = os.environ.get("GTR_SERIAL_SWEEP", "0") == "1"
         eng = self.eng
         T, D = eng.T, eng.D
         self.adam = L.GtrAdam()
@@ -85,6 +88,7 @@ class FusedTrainStep:
         self.cfg = eng.config(self.ws, True)
         self.side1 = torch.cuda.Stream(self.dev)
         self.side2 = torch.cuda.Stream(self.dev)
+        self.side3 = torch.cuda.Stream(self.dev)
         self.graph = None
         self.graph_pe = None
 
@@ -132,8 +136,8 @@ class FusedTrainStep:
                                          self.stamp.data_ptr(), self.step_dev.data_ptr(), s1), "contrib_prep")
             ev_prep = torch.cuda.Event()
             ev_prep.record(self.side1)
-            L.check(lib.gtr_adamw_sweep(eng.T, eng.D, self.stamp.data_ptr(), eng.model.item_embedding.weight.data_ptr(),
-                                        self.m_tab.data_ptr(), self.v_tab.data_ptr(), C.byref(self.adam), s1), "sweep")
+            if not self.serial_sweep:
+                self._sweep(s1)
         # side 2: sort contributions by row
         self.side2.wait_event(ev_prep)
         with torch.cuda.stream(self.side2):
@@ -142,7 +146,8 @@ class FusedTrainStep:
                                          self.sort_tmp.numel(), self.side2.cuda_stream), "contrib_sort")
         # main: forward, loss, backward, weight gradients
         eng.run_forward(ws, cfg, bs, L.RO_FWD | L.RO_LOSS | L.RO_BWD, self.loss_kind, self.temperature, self.alpha)
-        eng.run_backward(ws, cfg, bs)
+        eng.run_backward(ws, cfg, bs, side=self.side3)
+        main.wait_stream(self.side3)
         main.wait_stream(self.side2)
         st = main.cuda_stream
         L.check(lib.gtr_adamw_rows(C.byref(bs), eng.T, eng.D, self.skeys.data_ptr(), self.svals.data_ptr(),
@@ -152,7 +157,15 @@ class FusedTrainStep:
         L.check(lib.gtr_adamw_small(eng.flat.flat.data_ptr(), self.m_flat.data_ptr(), self.v_flat.data_ptr(), None,
                                     eng.flat.layout.total, self.segs, self.nseg, C.byref(self.adam), st), "adamw_small")
         main.wait_stream(self.side1)
+        if self.serial_sweep:
+            self._sweep(st)
         L.check(lib.gtr_step_end(self.step_dev.data_ptr(), eng.rng_ctr.data_ptr(), st), "step_end")
+
+    def _sweep(self, stream_handle):
+        eng = self.eng
+        L.check(L.lib().gtr_adamw_sweep(eng.T, eng.D, self.stamp.data_ptr(), eng.model.item_embedding.weight.data_ptr(),
+                                        self.m_tab.data_ptr(), self.v_tab.data_ptr(), C.byref(self.adam),
+                                        stream_handle), "sweep")
 
     def capture(self, with_pe: bool = False):
         """Capture one step into a hipGraph (after one eager warm-up step)."""

@@ -169,13 +169,14 @@ int gtr_readout_loss(const gtr_config* cfg, const gtr_batch* bt, const float* ta
 int gtr_conv_bwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l,
                  float* dx0, gtr_stream_t stream);
 
-/* Weight-gradient partial slabs for every layer (+ LapPE projection).
+/* Weight-gradient partial slabs for layers [l_begin, l_end) (+ LapPE projection
+ * when l_begin == 0).
  * Slab layout matches the flat parameter layout of each layer block:
  *   [w_all 4D*D | b_all 4D | w_beta 3D] and PE [wpe D*k | bpe D].
  * slabs[p * slab_stride + offset]; n_chunks partials over the node range.     */
 int gtr_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers,
               const float* dx0, const float* pe_tab, float* const* layer_slab, float* pe_slab,
-              int n_chunks, int64_t slab_stride, gtr_stream_t stream);
+              int n_chunks, int64_t slab_stride, int l_begin, int l_end, gtr_stream_t stream);
 
 /* One segment of the flat dense-parameter buffer for gtr_adamw_small. */
 typedef struct gtr_segment {

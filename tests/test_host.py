@@ -1,0 +1,243 @@
+"""Host-side logic of the product package (no GPU): batch layout / CSR packing,
+capacity bucketing, id validation, synthetic workload shape, the CSV dataset and
+collate, the flat parameter layout, API surface and error conventions."""
+
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+import etpgt_ref as R
+from etpgt.data.batch import Caps, SessionBatch, blob_layout, build_csr, collate_sessions
+from etpgt.data.synthetic import batch_stats, make_batches, make_sessions_and_graph
+from etpgt.model import SessionReadout, create_graph_transformer, create_graph_transformer_optimized
+
+
+def _unpack(sb):
+    caps, blob = sb.packed()
+    lay = blob_layout(caps)
+    return caps, {k: blob[v[0] : v[0] + v[1]] for k, v in lay.items() if k != "_total"}
+
+
+def test_csr_roundtrip_random():
+    rng = np.random.default_rng(0)
+    n = 50
+    src = rng.integers(0, n, 300)
+    dst = rng.integers(0, n, 300)
+    in_ptr, in_src, out_ptr, out_edge, out_dst, order = build_csr(src, dst, n)
+    d_of = np.repeat(np.arange(n), np.diff(in_ptr))
+    assert sorted(zip(in_src.tolist(), d_of.tolist())) == sorted(zip(src.tolist(), dst.tolist()))
+    # stable: inside a destination row, original edge order is kept
+    for t in range(n):
+        seg = order[in_ptr[t] : in_ptr[t + 1]]
+        assert np.all(np.diff(seg) > 0)
+    for s in range(n):
+        for i in range(out_ptr[s], out_ptr[s + 1]):
+            assert in_src[out_edge[i]] == s and d_of[out_edge[i]] == out_dst[i]
+
+
+def test_pack_batch_layout_and_padding():
+    items = [{"x": [3, 7], "edge_index": [[0, 0, 1], [0, 1, 1]], "target_item": 9, "negative_items": [1, 2]},
+             {"x": [4, 5, 6], "edge_index": [[0, 1], [2, 2]], "target_item": 8, "negative_items": [3, 10]}]
+    sb = collate_sessions(items)
+    caps, f = _unpack(sb)
+    assert caps.n_cap >= 5 and caps.e_cap >= 5 and caps.n_neg == 2
+    assert list(f["hdr"][:4]) == [5, 2, 5, 2]
+    assert list(f["node_item"][:5]) == [3, 7, 4, 5, 6]
+    assert list(f["node_ptr"][:3]) == [0, 2, 5]
+    assert all(v == 5 for v in f["node_ptr"][3:])          # padded with N
+    assert list(f["target"][:2]) == [9, 8]
+    assert list(f["negatives"][:4]) == [1, 2, 3, 10]
+    assert f["in_ptr"][5] == 5 and all(v == 5 for v in f["in_ptr"][6:])
+
+
+def test_pack_rejects_cross_session_edges_and_bad_ids():
+    sb = SessionBatch(torch.tensor([1, 2, 3]), torch.tensor([[0], [2]]), torch.tensor([0, 0, 1]),
+                      torch.tensor([5, 6]), torch.tensor([7, 8]))
+    with pytest.raises(ValueError, match="inside one session"):
+        sb.packed()
+    sb2 = SessionBatch(torch.tensor([1, 2, 300]), torch.zeros(2, 0, dtype=torch.long), torch.tensor([0, 0, 1]),
+                       torch.tensor([5, 6]), torch.tensor([7, 8]))
+    with pytest.raises(IndexError):
+        sb2.check_ids(100)
+    sb3 = SessionBatch(torch.tensor([1, 2, 3]), torch.zeros(2, 0, dtype=torch.long), torch.tensor([1, 0, 1]))
+    with pytest.raises(ValueError, match="sorted"):
+        sb3.packed()
+
+
+def test_caps_bucketing_is_monotone_and_coarse():
+    vals = [Caps.bucket(x, 32, x, 5).n_cap for x in range(1, 2000)]
+    assert all(v >= x for v, x in zip(vals, range(1, 2000)))
+    assert len(set(vals)) < 40
+    c = Caps(100, 32, 300, 5)
+    assert c.fits(100, 32, 300, 5) and not c.fits(101, 32, 300, 5) and not c.fits(10, 32, 10, 6)
+
+
+def test_synthetic_workload_shape():
+    d = make_sessions_and_graph(num_items=2000, num_sessions=4000, num_edges=20000, seed=1)
+    assert d.edge_keys.size == 20000
+    T = d.table_rows
+    a, b = d.edge_keys // T, d.edge_keys % T
+    assert np.all(a <= b) and a.min() >= 1
+    bl = make_batches(d, 32, 4, 5)
+    st = batch_stats(bl)
+    assert 2.5 < st["nodes_per_session"] < 6 and st["edges_per_session"] > 3
+    for sb in bl:
+        ei = sb.edge_index.numpy()
+        x = sb.x.numpy()
+        # edges directed smaller -> larger item id (plus self loops), dataloader.py:45-48,149-152
+        assert np.all(x[ei[0]] <= x[ei[1]])
+        negs = sb.negative_items.view(32, 5).numpy()
+        assert negs.min() >= 1
+
+
+def test_session_dataset_and_collate(tmp_path):
+    sessions = pd.DataFrame({
+        "timestamp": [1, 2, 3, 4, 10, 11, 12],
+        "visitorid": ["a"] * 4 + ["b"] * 3,
+        "event": ["view"] * 7,
+        "itemid": [5, 3, 5, 9, 2, 4, 6],
+        "transactionid": [None] * 7,
+        "session_id": [0, 0, 0, 0, 1, 1, 1],
+    })
+    edges = pd.DataFrame({"item_i": [3, 3, 5, 2, 4, 1], "item_j": [5, 3, 9, 4, 6, 2], "count": [1] * 6})
+    sp, gp = tmp_path / "s.csv", tmp_path / "g.csv"
+    sessions.to_csv(sp, index=False)
+    edges.to_csv(gp, index=False)
+    from etpgt.train.dataloader import SessionDataset, collate_fn, create_dataloader
+
+    torch.manual_seed(0)
+    ds = SessionDataset(sp, gp, num_negatives=3)
+    assert ds.num_items == 10 and len(ds) == 2
+    it = ds[0]
+    assert it["target_item"].item() == 9
+    assert sorted(it["session_items"].tolist()) == [3, 5, 5]
+    # induced edges among context {3, 5}: (3,5), (3,3); (5,9) excluded (9 is the target)
+    assert sorted(map(tuple, it["edge_index"].t().tolist())) == [(3, 3), (3, 5)]
+    assert not set(it["negative_items"].tolist()) & {3, 5, 9}
+    b = collate_fn([ds[0], ds[1]])
+    assert b.x.tolist() == [3, 5, 2, 4]
+    assert sorted(map(tuple, b.edge_index.t().tolist())) == [(0, 0), (0, 1), (2, 3)]
+    assert b.batch.tolist() == [0, 0, 1, 1] and b.num_graphs == 2
+    dl = create_dataloader(sp, gp, batch_size=2, num_negatives=3, shuffle=False)
+    assert next(iter(dl)).num_graphs == 2
+
+
+def test_product_model_structure_matches_reference():
+    m = create_graph_transformer_optimized(36, embedding_dim=64, hidden_dim=64, laplacian_k=8)
+    assert sum(p.numel() for p in m.parameters()) == 36800
+    ref = R.ref_create_graph_transformer_optimized(36, embedding_dim=64, hidden_dim=64, laplacian_k=8)
+    assert list(m.state_dict().keys()) == list(ref.state_dict().keys())
+    assert [n for n, _ in m.named_parameters()] == [n for n, _ in ref.named_parameters()]
+    assert m.use_ffn is False and m.num_layers == 2 and m.num_heads == 2
+    m2 = create_graph_transformer(188, embedding_dim=64, hidden_dim=64, num_layers=2, num_heads=2,
+                                  use_laplacian_pe=False, use_ffn=True, ffn_expansion=4)
+    assert sum(p.numel() for p in m2.parameters()) == 112128
+    W = m.item_embedding.weight.detach()
+    assert float(W[0].abs().max()) == 0.0
+
+
+def test_flat_layout_covers_every_dense_param():
+    from etpgt.backend.engine import FlatParams
+
+    m = create_graph_transformer_optimized(50, embedding_dim=32, hidden_dim=32, num_heads=2, laplacian_k=4)
+    before = {n: p.detach().clone() for n, p in m.named_parameters()}
+    fp = FlatParams(m, torch.device("cpu"))
+    after = dict(m.named_parameters())
+    for n, p in after.items():
+        assert torch.equal(p.detach(), before[n]), n
+        if n != "item_embedding.weight":
+            assert p.data_ptr() >= fp.flat.data_ptr() and p.data_ptr() < fp.flat.data_ptr() + 4 * fp.flat.numel()
+    lay = fp.layout
+    assert all(s.begin % 256 == 0 for s in lay.segs.values())
+    # w_all rows: query | key | value | skip
+    w = fp.flat[lay.seg("0.w_all").begin : lay.seg("0.w_all").begin + 4 * 32 * 32].view(128, 32)
+    assert torch.equal(w[:32], m.convs[0].lin_query.weight.detach())
+    assert torch.equal(w[96:], m.convs[0].lin_skip.weight.detach())
+
+
+def test_cpu_model_fails_loudly():
+    m = create_graph_transformer_optimized(50, embedding_dim=32, hidden_dim=32, use_laplacian_pe=False)
+    sb = collate_sessions([{"x": [1, 2], "edge_index": [[0], [1]], "target_item": 3, "negative_items": [4]}])
+    with pytest.raises(RuntimeError, match="HIP path only"):
+        m(sb)
+    from etpgt.backend.ops import score_loss
+
+    with pytest.raises(RuntimeError, match="HIP path only"):
+        score_loss(torch.randn(2, 32), torch.tensor([1, 2]), torch.tensor([[3], [4]]), m.item_embedding)
+
+
+def test_unsupported_variants_are_rejected():
+    m = create_graph_transformer_optimized(50, embedding_dim=32, hidden_dim=32, use_laplacian_pe=False,
+                                           readout_type="max")
+    with pytest.raises(NotImplementedError):
+        m._check_supported()
+    m2 = create_graph_transformer(50, embedding_dim=32, hidden_dim=32, use_laplacian_pe=False)
+    with pytest.raises(NotImplementedError):
+        m2._check_supported()
+
+
+def test_loss_factory_and_errors():
+    from etpgt.train.losses import BPRLoss, DualLoss, ListwiseLoss, SampledSoftmaxLoss, create_loss_function
+
+    assert isinstance(create_loss_function("bpr"), BPRLoss)
+    assert isinstance(create_loss_function("listwise", temperature=0.5), ListwiseLoss)
+    assert isinstance(create_loss_function("dual", alpha=0.3), DualLoss)
+    assert isinstance(create_loss_function("sampled_softmax"), SampledSoftmaxLoss)
+    with pytest.raises(ValueError, match="Unknown loss type"):
+        create_loss_function("nope")
+    # reference Trainer dispatch inspects forward's co_varnames (trainer.py:96)
+    assert len(DualLoss().forward.__code__.co_varnames) > 4
+
+
+@pytest.mark.parametrize("mode", ["mean", "max", "last", "attention"])
+def test_standalone_readout_matches_golden(golden_dir, mode):
+    g = np.load(os.path.join(golden_dir, "readout.npz"))
+    ro = SessionReadout(hidden_dim=8, readout_type=mode)
+    if mode == "attention":
+        with torch.no_grad():
+            ro.attention.weight.copy_(torch.from_numpy(g["attention_w"]))
+            ro.attention.bias.copy_(torch.from_numpy(g["attention_b"]))
+    x = torch.from_numpy(g["x"]).requires_grad_(True)
+    se = ro(x, torch.from_numpy(g["batch"]))
+    w = torch.linspace(-1, 1, se.numel()).view_as(se)
+    (se * w).sum().backward()
+    np.testing.assert_allclose(se.detach().numpy(), g[f"{mode}_se"], rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(x.grad.numpy(), g[f"{mode}_dx"], rtol=1e-5, atol=1e-6)
+    with pytest.raises(ValueError, match="Unknown readout type"):
+        SessionReadout(8, "bogus")
+
+
+def test_lappe_precompute_matches_oracle_and_errors():
+    from etpgt.encodings import LaplacianPECached, compute_laplacian_pe
+
+    ei = torch.tensor([[0, 1, 1, 2, 2, 3], [1, 0, 2, 1, 3, 2]])
+    pe = compute_laplacian_pe(ei, num_nodes=4, k=2)
+    assert pe.shape == (4, 2) and pe.dtype == torch.float32 and bool((pe >= 0).all())
+    np.testing.assert_allclose(np.sort(np.abs(pe.numpy()), axis=None),
+                               np.sort(np.abs(R.ref_compute_laplacian_pe(ei, 4, 2).numpy()), axis=None), atol=1e-5)
+    mod = LaplacianPECached(k=2, embedding_dim=16)
+    with pytest.raises(RuntimeError, match="not precomputed"):
+        mod(torch.tensor([0, 1]))
+
+    class D:
+        edge_index = ei
+        num_nodes = 4
+
+    mod.precompute(D())
+    assert mod(torch.tensor([0, 2, 3])).shape == (3, 16)
+    assert mod.project(torch.randn(4, 2)).shape == (4, 16)
+
+
+def test_metrics_and_seed():
+    from etpgt.utils import compute_ndcg_at_k, compute_recall_at_k, set_seed
+
+    set_seed(42)
+    a = torch.rand(10)
+    set_seed(42)
+    assert torch.equal(a, torch.rand(10))
+    p = torch.tensor([[1, 2, 3, 4, 5], [6, 7, 8, 9, 10], [11, 12, 13, 14, 15]])
+    assert compute_recall_at_k(p, torch.tensor([2, 9, 20]), 5) == pytest.approx(2 / 3)
+    assert compute_ndcg_at_k(p, torch.tensor([1, 9, 20]), 5) == pytest.approx(0.4769, abs=1e-4)
