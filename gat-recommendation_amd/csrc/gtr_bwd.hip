@@ -17,7 +17,7 @@ using namespace gtr;
 
 struct ConvBwdK {
   gtr_batch bt;
-  int H, C, R, layer, has_prev, pad0;
+  int H, C, layer, has_prev, cred, gpart_n;  // gpart_n: partials feeding gsum (-1: hdr G)
   float sqrt_c, scale;
   uint32_t seed, thresh;
   int drop_on, pad1;
@@ -25,7 +25,8 @@ struct ConvBwdK {
   const float* dy;
   const float* out;
   const float* stats;
-  const float* gsum;
+  float* gsum;
+  const float* gpart;
   const float* gamma;
   const float* qkvs;
   const float* alpha;
@@ -166,6 +167,8 @@ template <int D>
 __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
   using G = LayerGeom<D>;
   constexpr int VPL = G::VPL, RMAX = G::RMAX, AS = G::AS;
+  constexpr int NCT = D / 16;                                   // dX column tiles
+  constexpr int CPW = NCT > CONV_WAVES ? NCT / CONV_WAVES : 1;  // column tiles per wave
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* R1 = sm + G::B_R1;
   float* ALs = sm + G::B_ALPHA;
@@ -175,19 +178,21 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
   int* optr = reinterpret_cast<int*>(sm + G::B_OPTR);
   int* oedge = reinterpret_cast<int*>(sm + G::B_OEDGE);
   int* odst = reinterpret_cast<int*>(sm + G::B_ODST);
+  float* s_gs = sm + G::B_GS;
   int* s_flag = reinterpret_cast<int*>(sm + G::B_FLAG);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int N = a.bt.hdr[0], B = a.bt.hdr[1];
-  const int Gn = (N + a.R - 1) / a.R;
+  const int N = a.bt.hdr[0];
+  const int Gn = a.bt.hdr[4];
   const int g = blockIdx.x;
   if (g >= Gn) return;
-  int r0, r1;
-  group_rows(a.bt.node_ptr, B, a.R, g, r0, r1);
+  const int r0 = a.bt.grp_row[g], r1 = a.bt.grp_row[g + 1];
+  // groups hold whole sessions, so the group's out-edges (CSR by source) start at the
+  // same offset as its in-edges: edges with src < r0 are exactly those with dst < r0
+  const int e_lo = a.bt.grp_edge[g], e_hi = a.bt.grp_edge[g + 1];
+  const int o_lo = e_lo;
   const int nrow = r1 - r0;
   const int H = a.H;
-  const int e_lo = a.bt.in_ptr[r0], e_hi = a.bt.in_ptr[r1];
-  const int o_lo = a.bt.out_ptr[r0];
   const int ne = e_hi - e_lo;
   const bool fast = G::KV && nrow <= RMAX && ne <= G::EMAX && H <= 8;
   const uint32_t ctr = a.rng_ctr ? *a.rng_ctr : 0u;
@@ -197,16 +202,16 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
   const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
   const float invN = 1.0f / (float)N;
 
-  float k_g[VPL], k_mean[VPL], k_rstd[VPL], k_s1[VPL], k_s2[VPL];
-  {
-    const int j = act ? d0 : 0;
-    load_vec<VPL>(k_g, a.gamma + j, true);
-    load_vec<VPL>(k_mean, a.stats + j, true);
-    load_vec<VPL>(k_rstd, a.stats + D + j, true);
-    load_vec<VPL>(k_s1, a.gsum + j, true);
-    load_vec<VPL>(k_s2, a.gsum + D + j, true);
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) { k_s1[v] *= invN; k_s2[v] *= invN; }
+  // ---- this layer's BatchNorm backward sums: reduce the producer's partials (cred)
+  if (a.cred) {
+    const int np = a.gpart_n >= 0 ? a.gpart_n : Gn;
+    for (int j = tid; j < 2 * D; j += CONV_BLOCK) {
+      float acc = 0.0f;
+#pragma unroll 8
+      for (int q = 0; q < np; ++q) acc += a.gpart[(size_t)q * 2 * D + j];
+      s_gs[j] = acc;
+      if (g == 0) a.gsum[j] = acc;
+    }
   }
 
   // ---- stage (fast): CSR slices, alpha slice, K|V rows of the group
@@ -227,7 +232,20 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
       *reinterpret_cast<float4*>(R1 + i * D + c) = *reinterpret_cast<const float4*>(src + D + c);
       *reinterpret_cast<float4*>(R1 + RMAX * D + i * D + c) = *reinterpret_cast<const float4*>(src + 2 * D + c);
     }
-    __syncthreads();
+  }
+  __syncthreads();
+
+  float k_g[VPL], k_mean[VPL], k_rstd[VPL], k_s1[VPL], k_s2[VPL];
+  {
+    const int j = act ? d0 : 0;
+    load_vec<VPL>(k_g, a.gamma + j, true);
+    load_vec<VPL>(k_mean, a.stats + j, true);
+    load_vec<VPL>(k_rstd, a.stats + D + j, true);
+    const float* gs = a.cred ? s_gs : a.gsum;
+    load_vec<VPL>(k_s1, gs + j, true);
+    load_vec<VPL>(k_s2, gs + D + j, true);
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) { k_s1[v] *= invN; k_s2[v] *= invN; }
   }
 
   // ---- phase 1: destination rows
@@ -261,10 +279,18 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
   }
   __syncthreads();
 
-  // ---- phase 3: dX = dQKVS . W_all (MFMA f32), + residual; previous layer's dropout mask
+  // ---- phase 3: dX = dQKVS . W_all (MFMA f32), + residual; previous layer's dropout mask;
+  //      the previous BatchNorm's backward sums (sum dy, sum dy*xhat) accumulate in the epilogue
   const int lr = lane & 15, lg = lane >> 4;
   const uint32_t st_prev = drop_stream(1, (uint32_t)(a.layer - 1), ctr);
   float* As = R1;
+  float s1[CPW], s2[CPW], pm[CPW], pr[CPW];
+#pragma unroll
+  for (int c = 0; c < CPW; ++c) {
+    s1[c] = 0.0f; s2[c] = 0.0f; pm[c] = 0.0f; pr[c] = 0.0f;
+    const int ct = wave + c * CONV_WAVES;
+    if (a.has_prev && ct < NCT) { pm[c] = a.p_stats[ct * 16 + lr]; pr[c] = a.p_stats[D + ct * 16 + lr]; }
+  }
   for (int rt = r0; rt < r1; rt += 16) {
     for (int idx = tid; idx < 16 * D; idx += CONV_BLOCK) {  // float4 granules
       const int i = idx / D, c = (idx - i * D) * 4;
@@ -274,7 +300,10 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
       *reinterpret_cast<float4*>(As + i * AS + c) = v;
     }
     __syncthreads();
-    for (int ct = wave; ct < D / 16; ct += CONV_WAVES) {
+#pragma unroll
+    for (int c = 0; c < CPW; ++c) {
+      const int ct = wave + c * CONV_WAVES;
+      if (ct >= NCT) continue;
       f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
       const float* arow = As + lr * AS + lg * 4;
       const float* bcol = a.w_all + (size_t)(lg * 4) * D + ct * 16 + lr;
@@ -291,8 +320,14 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
         if (row < r1) {
           const size_t o = (size_t)row * D + col;
           const float dx = a.dy[o] + acc[i];
-          if (a.has_prev) a.p_dy[o] = dx * dr.mul(st_prev, (uint32_t)o);
-          else a.dx0[o] = dx;
+          if (a.has_prev) {
+            const float d = dx * dr.mul(st_prev, (uint32_t)o);
+            a.p_dy[o] = d;
+            s1[c] += d;
+            s2[c] += d * ((a.p_out[o] - pm[c]) * pr[c]);
+          } else {
+            a.dx0[o] = dx;
+          }
         }
       }
     }
@@ -300,21 +335,20 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
   }
 
   if (!a.has_prev) return;
-  // ---- phase 4: previous layer's BatchNorm backward sums: sum(dy), sum(dy * xhat)
+  // ---- previous layer's BatchNorm backward partials: reduce the 4 row quads of each column
   float* part = a.p_gpart + (size_t)g * 2 * D;
-  for (int j = tid; j < D; j += CONV_BLOCK) {
-    const float mean = a.p_stats[j], rstd = a.p_stats[D + j];
-    float s1 = 0.0f, s2 = 0.0f;
-#pragma unroll 4
-    for (int r = r0; r < r1; ++r) {
-      const size_t o = (size_t)r * D + j;
-      const float d = a.p_dy[o];
-      s1 += d;
-      s2 += d * ((a.p_out[o] - mean) * rstd);
+#pragma unroll
+  for (int c = 0; c < CPW; ++c) {
+    const int ct = wave + c * CONV_WAVES;
+    float x1 = s1[c], x2 = s2[c];
+    x1 += __shfl_xor(x1, 16); x1 += __shfl_xor(x1, 32);
+    x2 += __shfl_xor(x2, 16); x2 += __shfl_xor(x2, 32);
+    if (ct < NCT && lg == 0) {
+      part[ct * 16 + lr] = x1;
+      part[D + ct * 16 + lr] = x2;
     }
-    part[j] = s1;
-    part[D + j] = s2;
   }
+  if (a.cred) return;  // the next conv_bwd reduces the partials
   if (!arrive_last(a.p_cnt, (uint32_t)Gn, s_flag)) return;
   for (int j = tid; j < 2 * D; j += CONV_BLOCK) {
     float acc = 0.0f;
@@ -462,13 +496,20 @@ extern "C" int gtr_conv_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   }
   if (!cfg->training) { set_error("gtr_conv_bwd: backward requires training mode"); return GTR_E_ARG; }
   if (l == 0 && !dx0) { set_error("gtr_conv_bwd: layer 0 needs dx0"); return GTR_E_ARG; }
+  if (!bt->grp_row || !bt->grp_edge) { set_error("gtr_conv_bwd: batch lacks row-group ranges"); return GTR_E_ARG; }
   const gtr_layer& L = layers[l];
   ConvBwdK k{};
   k.bt = *bt;
   k.H = cfg->heads;
   k.C = D / cfg->heads;
-  k.R = cfg->row_group;
   k.layer = l;
+  k.cred = cfg->consumer_reduce;
+  // partials feeding this layer's sums: the readout grid for the last layer, else the conv groups
+  k.gpart_n = -1;
+  if (l == cfg->num_layers - 1) {
+    int rg = (bt->b_cap + GTR_WAVES - 1) / GTR_WAVES;
+    k.gpart_n = rg > 256 ? 256 : rg;
+  }
   k.has_prev = l > 0;
   k.sqrt_c = (float)sqrt((double)k.C);
   k.drop_on = (cfg->dropout > 0.0f) ? 1 : 0;
@@ -477,7 +518,7 @@ extern "C" int gtr_conv_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   k.scale = k.drop_on ? (float)(1.0 / (1.0 - p)) : 1.0f;
   k.seed = cfg->seed;
   k.rng_ctr = cfg->rng_ctr;
-  k.dy = L.dy; k.out = L.out; k.stats = L.bn_stats; k.gsum = L.bn_gsum; k.gamma = L.bn_gamma;
+  k.dy = L.dy; k.out = L.out; k.stats = L.bn_stats; k.gsum = L.bn_gsum; k.gpart = L.bn_gpart; k.gamma = L.bn_gamma;
   k.qkvs = L.qkvs; k.alpha = L.alpha; k.agg = L.agg; k.gate = L.gate; k.w_all = L.w_all; k.w_beta = L.w_beta;
   k.dqkvs = L.dqkvs; k.du = L.du; k.dlogit = L.dlogit; k.dagg = L.dagg;
   if (l > 0) {

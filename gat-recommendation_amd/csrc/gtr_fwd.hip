@@ -4,15 +4,17 @@
 //   residual / dropout, fused.  Reference: graph_transformer.py:140-152 (layer 0
 //   prologue: item_embedding + LapPE), :171-177 (conv -> bn -> +res -> dropout) and
 //   PyG TransformerConv.
-//   Work unit = a row group: every session whose first node falls in [g*R,(g+1)*R).
-//   Sessions are independent subgraphs (dataloader.py:157-202), so one workgroup
-//   owns every source of every destination it processes: projection, attention and
-//   gate need no inter-workgroup exchange.  Only BatchNorm couples sessions: each
-//   group writes (count, mean, M2) partials, the last arriving group combines them.
+//   Work unit = a row group: every session whose first node falls in [g*R,(g+1)*R)
+//   (ranges precomputed in the batch image).  Sessions are independent subgraphs
+//   (dataloader.py:157-202), so one workgroup owns every source of every destination
+//   it processes: projection, attention and gate need no inter-workgroup exchange.
+//   Only BatchNorm couples sessions: each group writes (count, mean, M2) partials which
+//   the CONSUMING kernel reduces in its prologue (consumer_reduce) or the last arriving
+//   group combines (large grids).
 //
 // k_readout<D>: last layer's BN/residual/dropout + mean readout (base.py:136-155)
 //   + scoring loss fwd/bwd (base.py:80-113, losses.py:8-164) + readout backward and
-//   the last BatchNorm's backward sums.
+//   the last BatchNorm's backward partial sums.
 
 #include "gtr_layer.cuh"
 
@@ -22,7 +24,7 @@ using namespace gtr;
 
 struct ConvFwdK {
   gtr_batch bt;
-  int H, C, R, first, train, layer, pe_k, pad0;
+  int H, C, first, train, layer, pe_k, cred, pad0;
   float sqrt_c, bn_eps, bn_mom, scale;
   uint32_t seed, thresh;
   int drop_on, pad1;
@@ -33,11 +35,13 @@ struct ConvFwdK {
   const float* bpe;
   const float* p_out;
   const float* p_xin;
-  const float* p_stats;
+  float* p_stats;        // previous layer's finalized stats (read, or written by block 0 when cred)
+  const float* p_part;   // previous layer's forward partials (cred)
   const float* p_gamma;
   const float* p_beta;
-  const float* p_rmean;
-  const float* p_rvar;
+  float* p_rmean;
+  float* p_rvar;
+  int64_t* p_nbt;
   const float* w_all;
   const float* b_all;
   const float* w_beta;
@@ -55,13 +59,48 @@ struct ConvFwdK {
   int64_t* bn_nbt;
 };
 
-// Attention + gate of one destination row (wave per row).  KB/VB: K/V row bases with
-// row stride KST (LDS on the fast path, global qkvs otherwise); EP/ES: CSR of the rows
+// Block prologue shared by k_conv_fwd (previous layer) and k_readout (last layer):
+// BatchNorm mean/rstd of the layer feeding this kernel into s_mean/s_rstd.
+//   eval: running stats; train + cred: reduce the producer's partials (block 0 also
+//   publishes the stats and updates running_mean/var/num_batches_tracked);
+//   train, producer-finalised: read the stats.
+template <int D, int BLK>
+__device__ __forceinline__ void prev_bn_stats(int train, int cred, int G, const float* part, float* stats,
+                                              float* rmean, float* rvar, int64_t* nbt, float eps, float mom,
+                                              float* s_mean, float* s_rstd, float* s_uvar) {
+  if (!train) {
+    for (int j = threadIdx.x; j < D; j += BLK) {
+      s_mean[j] = rmean[j];
+      s_rstd[j] = 1.0f / sqrtf(rvar[j] + eps);
+    }
+  } else if (cred) {
+    bn_stats_from_parts<D, BLK>(part, G, eps, s_mean, s_rstd, s_uvar);
+    if (blockIdx.x == 0) {
+      for (int j = threadIdx.x; j < D; j += BLK) {
+        stats[j] = s_mean[j];
+        stats[D + j] = s_rstd[j];
+        rmean[j] = (1.0f - mom) * rmean[j] + mom * s_mean[j];
+        rvar[j] = (1.0f - mom) * rvar[j] + mom * s_uvar[j];
+      }
+      if (threadIdx.x == 0 && nbt) *nbt += 1;
+    }
+  } else {
+    for (int j = threadIdx.x; j < D; j += BLK) {
+      s_mean[j] = stats[j];
+      s_rstd[j] = stats[D + j];
+    }
+  }
+}
+
+// Attention + gate of one destination row (wave per row).  QB/SB/KB/VB: row bases
+// with stride ST (LDS on the fast path, global qkvs otherwise); EP/ES: CSR of the rows
 // (local indices on the fast path); eoff: offset of EP's edge indices in alpha.
-template <int D, typename EI>
-__device__ __forceinline__ void attn_row(const ConvFwdK& a, int t, int tl, const float* KB, const float* VB, int KST,
-                                         const EI* EP, const EI* ES, int eoff, int lane, const Drop& dr,
-                                         uint32_t st_attn, float* xo_row) {
+template <int D>
+__device__ __forceinline__ void attn_row(const ConvFwdK& a, int t, int tl, const float* QB, const float* SB,
+                                         const float* KB, const float* VB, int ST, const int* EP, const int* ES,
+                                         int eoff, int lane, const Drop& dr, uint32_t st_attn,
+                                         const float (&w1)[LayerGeom<D>::VPL], const float (&w2)[LayerGeom<D>::VPL],
+                                         const float (&w3)[LayerGeom<D>::VPL], float* xo_row) {
   constexpr int VPL = LayerGeom<D>::VPL;
   const int d0 = lane * VPL;
   const bool act = d0 < D;
@@ -69,17 +108,16 @@ __device__ __forceinline__ void attn_row(const ConvFwdK& a, int t, int tl, const
   const int GL = C / VPL;
   const int head = act ? d0 / C : 0;
   const bool leader = act && ((lane & (GL - 1)) == 0);
-  const float* qt = a.qkvs + (size_t)t * (4 * D);
   float q[VPL], s[VPL], ag[VPL];
-  load_vec<VPL>(q, qt + d0, act);
-  load_vec<VPL>(s, qt + 3 * D + d0, act);
+  load_vec<VPL>(q, QB + (size_t)tl * ST + d0, act);
+  load_vec<VPL>(s, SB + (size_t)tl * ST + d0, act);
 #pragma unroll
   for (int v = 0; v < VPL; ++v) ag[v] = 0.0f;
   const int e0 = EP[tl], e1 = EP[tl + 1];
   float m = -INFINITY, z = 0.0f;
   for (int e = e0; e < e1; ++e) {
     float kv[VPL];
-    load_vec<VPL>(kv, KB + (size_t)ES[e] * KST + d0, act);
+    load_vec<VPL>(kv, KB + (size_t)ES[e] * ST + d0, act);
     float dt = 0.0f;
 #pragma unroll
     for (int v = 0; v < VPL; ++v) dt += q[v] * kv[v];
@@ -92,8 +130,8 @@ __device__ __forceinline__ void attn_row(const ConvFwdK& a, int t, int tl, const
   for (int e = e0; e < e1; ++e) {
     const int src = ES[e];
     float kv[VPL], vv[VPL];
-    load_vec<VPL>(kv, KB + (size_t)src * KST + d0, act);
-    load_vec<VPL>(vv, VB + (size_t)src * KST + d0, act);
+    load_vec<VPL>(kv, KB + (size_t)src * ST + d0, act);
+    load_vec<VPL>(vv, VB + (size_t)src * ST + d0, act);
     float dt = 0.0f;
 #pragma unroll
     for (int v = 0; v < VPL; ++v) dt += q[v] * kv[v];
@@ -106,14 +144,8 @@ __device__ __forceinline__ void attn_row(const ConvFwdK& a, int t, int tl, const
     for (int v = 0; v < VPL; ++v) ag[v] += ad * vv[v];
   }
   float u = 0.0f;
-  if (act) {
-    float w1[VPL], w2[VPL], w3[VPL];
-    load_vec<VPL>(w1, a.w_beta + d0, true);
-    load_vec<VPL>(w2, a.w_beta + D + d0, true);
-    load_vec<VPL>(w3, a.w_beta + 2 * D + d0, true);
 #pragma unroll
-    for (int v = 0; v < VPL; ++v) u += w1[v] * ag[v] + w2[v] * s[v] + w3[v] * (ag[v] - s[v]);
-  }
+  for (int v = 0; v < VPL; ++v) u += w1[v] * ag[v] + w2[v] * s[v] + w3[v] * (ag[v] - s[v]);
   u = wave_sum(u);
   const float beta = 1.0f / (1.0f + expf(-u));
   float o[VPL];
@@ -128,10 +160,11 @@ __device__ __forceinline__ void attn_row(const ConvFwdK& a, int t, int tl, const
 template <int D>
 __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
   using G = LayerGeom<D>;
-  constexpr int RMAX = G::RMAX, XS = G::XS, KPE = G::KPE;
+  constexpr int VPL = G::VPL, RMAX = G::RMAX, XS = G::XS, KPE = G::KPE;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* XO = sm + G::F_XO;
   float* KVs = sm + G::F_KV;
+  float* QSs = sm + G::F_QS;
   float* PEs = sm + G::F_PE;
   float* s_bn = sm + G::F_BN;
   int* items = reinterpret_cast<int*>(sm + G::F_ITEMS);
@@ -140,28 +173,40 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
   int* s_flag = reinterpret_cast<int*>(sm + G::F_FLAG);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int N = a.bt.hdr[0], B = a.bt.hdr[1];
-  const int Gn = (N + a.R - 1) / a.R;
+  const int Gn = a.bt.hdr[4];
   const int g = blockIdx.x;
   if (g >= Gn) return;
-  int r0, r1;
-  group_rows(a.bt.node_ptr, B, a.R, g, r0, r1);
+  const int r0 = a.bt.grp_row[g], r1 = a.bt.grp_row[g + 1];
+  const int e_lo = a.bt.grp_edge[g], e_hi = a.bt.grp_edge[g + 1];
   const int nrow = r1 - r0;
-  const int e_lo = a.bt.in_ptr[r0], e_hi = a.bt.in_ptr[r1];
   const bool fast = G::KV && nrow <= RMAX && (e_hi - e_lo) <= G::EMAX;
   const uint32_t ctr = a.rng_ctr ? *a.rng_ctr : 0u;
   const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
   const bool pe_lds = a.first && a.pe_k > 0 && a.pe_k <= KPE;
+  const int lr = lane & 15, lg = lane >> 4;
+  constexpr int NCT = (4 * D) / 16;
+  const int d0 = lane * VPL;
+  const bool act = d0 < D;
 
-  // ---- stage: previous BN params, CSR slice, LapPE projection weight
+  // ---- W fragments of this wave's first column tiles and the gate weights, issued
+  //      before anything else so the weight fetch overlaps the staging round trip
+  constexpr int PRE = D <= 64 ? (NCT / CONV_WAVES) : 1;
+  float4 wpre[PRE][D / 16];
+#pragma unroll
+  for (int pi = 0; pi < PRE; ++pi) {
+    const float* wrow = a.w_all + (size_t)((wave + pi * CONV_WAVES) * 16 + lr) * D + lg * 4;
+#pragma unroll
+    for (int kb = 0; kb < D / 16; ++kb) wpre[pi][kb] = *reinterpret_cast<const float4*>(wrow + kb * 16);
+  }
+  float w1[VPL], w2[VPL], w3[VPL];
+  load_vec<VPL>(w1, a.w_beta + d0, act);
+  load_vec<VPL>(w2, a.w_beta + D + d0, act);
+  load_vec<VPL>(w3, a.w_beta + 2 * D + d0, act);
+
+  // ---- stage: previous BN stats, CSR slice, node items, LapPE projection weight
   if (!a.first) {
-    for (int j = tid; j < D; j += CONV_BLOCK) {
-      float mean, rstd;
-      if (a.train) { mean = a.p_stats[j]; rstd = a.p_stats[D + j]; }
-      else { mean = a.p_rmean[j]; rstd = 1.0f / sqrtf(a.p_rvar[j] + a.bn_eps); }
-      s_bn[j] = mean;
-      s_bn[D + j] = rstd;
-    }
+    prev_bn_stats<D, CONV_BLOCK>(a.train, a.cred, Gn, a.p_part, a.p_stats, a.p_rmean, a.p_rvar, a.p_nbt, a.bn_eps,
+                                 a.bn_mom, s_bn, s_bn + D, XO);
   }
   if (fast) {
     for (int i = tid; i <= nrow; i += CONV_BLOCK) iptr[i] = a.bt.in_ptr[r0 + i] - e_lo;
@@ -173,36 +218,28 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
       PEs[j * KPE + k] = a.wpe[idx];
     }
   }
+  if (a.first) {
+    for (int i = tid; i < min(RMAX, nrow); i += CONV_BLOCK) items[i] = a.bt.node_item[r0 + i];
+  }
+  __syncthreads();
 
   // ---- phase P+M: layer input rows -> LDS -> QKVS projection (MFMA f32), chunks of RMAX rows
   const uint32_t st_prev = drop_stream(1, (uint32_t)(a.layer - 1), ctr);
-  const int lr = lane & 15, lg = lane >> 4;
-  constexpr int NCT = (4 * D) / 16;
-  // W fragments of this wave's first column tiles, loaded before the prologue so the
-  // weight fetch overlaps the row gather (column tile ct = wave + i*CONV_WAVES).
-  constexpr int PRE = D <= 64 ? (NCT / CONV_WAVES) : 1;
-  float4 wpre[PRE][D / 16];
-#pragma unroll
-  for (int pi = 0; pi < PRE; ++pi) {
-    const float* wrow = a.w_all + (size_t)((wave + pi * CONV_WAVES) * 16 + lr) * D + lg * 4;
-#pragma unroll
-    for (int kb = 0; kb < D / 16; ++kb) wpre[pi][kb] = *reinterpret_cast<const float4*>(wrow + kb * 16);
-  }
   for (int rc = r0; rc < r1; rc += RMAX) {
     const int m = min(RMAX, r1 - rc);
-    if (a.first) {
+    if (a.first && rc != r0) {
       for (int i = tid; i < m; i += CONV_BLOCK) items[i] = a.bt.node_item[rc + i];
       __syncthreads();
-      if (pe_lds) {
-        for (int idx = tid; idx < m * a.pe_k; idx += CONV_BLOCK) {
-          const int i = idx / a.pe_k, k = idx - i * a.pe_k;
-          const float* pr = a.bt.node_pe ? a.bt.node_pe + (size_t)(rc + i) * a.pe_k
-                                         : a.pe_tab + (size_t)items[i] * a.pe_k;
-          PEs[D * KPE + i * KPE + k] = pr[k];
-        }
-      }
     }
-    __syncthreads();
+    if (pe_lds) {
+      for (int idx = tid; idx < m * a.pe_k; idx += CONV_BLOCK) {
+        const int i = idx / a.pe_k, k = idx - i * a.pe_k;
+        const float* pr = a.bt.node_pe ? a.bt.node_pe + (size_t)(rc + i) * a.pe_k
+                                       : a.pe_tab + (size_t)items[i] * a.pe_k;
+        PEs[D * KPE + i * KPE + k] = pr[k];
+      }
+      __syncthreads();
+    }
     for (int idx = tid; idx < m * D; idx += CONV_BLOCK) {
       const int i = idx / D, j = idx - i * D;
       const int r = rc + i;
@@ -247,7 +284,9 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
       const int col = ct * 16 + lr;
       const float bias = a.b_all[col];
       const int which = col / D, cc = col - which * D;
-      float* kvdst = (fast && (which == 1 || which == 2)) ? KVs + (which - 1) * RMAX * D + cc : nullptr;
+      // LDS copies on the fast path: 0 = query -> QS[0], 1 = key -> KV[0], 2 = value -> KV[1], 3 = skip -> QS[1]
+      float* ldst = nullptr;
+      if (fast) ldst = (which == 0 ? QSs : which == 1 ? KVs : which == 2 ? KVs + RMAX * D : QSs + RMAX * D) + cc;
       for (int rt = 0; rt * 16 < m; ++rt) {
         f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
         const float* xrow = XO + (rt * 16 + lr) * XS + lg * 4;
@@ -260,7 +299,7 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
           if (row < m) {
             const float v = acc[i] + bias;
             a.qkvs[(size_t)(rc + row) * (4 * D) + col] = v;
-            if (kvdst) kvdst[row * D] = v;
+            if (ldst) ldst[row * D] = v;
           }
         }
       }
@@ -272,57 +311,64 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
   const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
   if (fast) {
     for (int t = r0 + wave; t < r1; t += CONV_WAVES)
-      attn_row<D, int>(a, t, t - r0, KVs, KVs + RMAX * D, D, iptr, isrc, e_lo, lane, dr, st_attn,
-                       XO + (t - r0) * XS);
+      attn_row<D>(a, t, t - r0, QSs, QSs + RMAX * D, KVs, KVs + RMAX * D, D, iptr, isrc, e_lo, lane, dr, st_attn,
+                  w1, w2, w3, XO + (t - r0) * XS);
   } else {
     for (int t = r0 + wave; t < r1; t += CONV_WAVES)
-      attn_row<D, int32_t>(a, t, t, a.qkvs + D, a.qkvs + 2 * D, 4 * D, a.bt.in_ptr, a.bt.in_src, 0, lane, dr,
-                           st_attn, nullptr);
+      attn_row<D>(a, t, t, a.qkvs, a.qkvs + 3 * D, a.qkvs + D, a.qkvs + 2 * D, 4 * D, a.bt.in_ptr, a.bt.in_src, 0,
+                  lane, dr, st_attn, w1, w2, w3, nullptr);
   }
   if (!a.train) return;
 
-  // ---- phase S: BatchNorm batch statistics (two-pass per group, Chan combine by the last arriver)
+  // ---- phase S: this group's BatchNorm partial (count, mean, M2); slices of rows per thread
   __syncthreads();
+  constexpr int NS = CONV_BLOCK / D >= 1 ? CONV_BLOCK / D : 1;
+  float* red = XO + RMAX * XS - (NS + 1) * D;  // scratch: tail of XO is past the group's rows
+  if (!fast || nrow * XS > RMAX * XS - (NS + 1) * D) red = sm + G::F_PE;  // PE region is free after the prologue
   float* part = a.bn_part + (size_t)g * (1 + 2 * D);
-  for (int j = tid; j < D; j += CONV_BLOCK) {
+  {
+    const int j = tid % D, sl = tid / D;
     float sum = 0.0f;
-    if (fast) for (int i = 0; i < nrow; ++i) sum += XO[i * XS + j];
-    else for (int r = r0; r < r1; ++r) sum += a.out[(size_t)r * D + j];
-    const float mean = nrow > 0 ? sum / (float)nrow : 0.0f;
+    if (sl < NS) {
+      if (fast) for (int i = sl; i < nrow; i += NS) sum += XO[i * XS + j];
+      else for (int i = sl; i < nrow; i += NS) sum += a.out[(size_t)(r0 + i) * D + j];
+    }
+    __syncthreads();
+    if (sl < NS) red[sl * D + j] = sum;
+    __syncthreads();
+    if (tid < D) {
+      float tot = 0.0f;
+      for (int q = 0; q < NS; ++q) tot += red[q * D + tid];
+      const float mean = nrow > 0 ? tot / (float)nrow : 0.0f;
+      red[NS * D + tid] = mean;
+      part[1 + tid] = mean;
+    }
+    __syncthreads();
     float m2 = 0.0f;
-    if (fast) {
-      for (int i = 0; i < nrow; ++i) { const float d = XO[i * XS + j] - mean; m2 += d * d; }
-    } else {
-      for (int r = r0; r < r1; ++r) { const float d = a.out[(size_t)r * D + j] - mean; m2 += d * d; }
+    if (sl < NS) {
+      const float mean = red[NS * D + j];
+      if (fast) for (int i = sl; i < nrow; i += NS) { const float d = XO[i * XS + j] - mean; m2 += d * d; }
+      else for (int i = sl; i < nrow; i += NS) { const float d = a.out[(size_t)(r0 + i) * D + j] - mean; m2 += d * d; }
     }
-    part[1 + j] = mean;
-    part[1 + D + j] = m2;
+    __syncthreads();
+    if (sl < NS) red[sl * D + j] = m2;
+    __syncthreads();
+    if (tid < D) {
+      float tot = 0.0f;
+      for (int q = 0; q < NS; ++q) tot += red[q * D + tid];
+      part[1 + D + tid] = tot;
+    }
+    if (tid == 0) part[0] = (float)nrow;
   }
-  if (tid == 0) part[0] = (float)nrow;
+  if (a.cred) return;  // the consuming kernel reduces the partials
   if (!arrive_last(a.cnt, (uint32_t)Gn, s_flag)) return;
+  bn_stats_from_parts<D, CONV_BLOCK>(a.bn_part, Gn, a.bn_eps, s_bn, s_bn + D, red);
+  __syncthreads();
   for (int j = tid; j < D; j += CONV_BLOCK) {
-    double n = 0.0, sum = 0.0;
-#pragma unroll 4
-    for (int q = 0; q < Gn; ++q) {
-      const float* pp = a.bn_part + (size_t)q * (1 + 2 * D);
-      n += (double)pp[0];
-      sum += (double)pp[0] * (double)pp[1 + j];
-    }
-    const double mean = sum / n;
-    double m2 = 0.0;
-#pragma unroll 4
-    for (int q = 0; q < Gn; ++q) {
-      const float* pp = a.bn_part + (size_t)q * (1 + 2 * D);
-      const double d = (double)pp[1 + j] - mean;
-      m2 += (double)pp[1 + D + j] + (double)pp[0] * d * d;
-    }
-    const float var = (float)(m2 / n);
-    const float meanf = (float)mean;
-    a.bn_stats[j] = meanf;
-    a.bn_stats[D + j] = 1.0f / sqrtf(var + a.bn_eps);
-    const float uvar = n > 1.0 ? (float)(m2 / (n - 1.0)) : var;
-    a.bn_rmean[j] = (1.0f - a.bn_mom) * a.bn_rmean[j] + a.bn_mom * meanf;
-    a.bn_rvar[j] = (1.0f - a.bn_mom) * a.bn_rvar[j] + a.bn_mom * uvar;
+    a.bn_stats[j] = s_bn[j];
+    a.bn_stats[D + j] = s_bn[D + j];
+    a.bn_rmean[j] = (1.0f - a.bn_mom) * a.bn_rmean[j] + a.bn_mom * s_bn[j];
+    a.bn_rvar[j] = (1.0f - a.bn_mom) * a.bn_rvar[j] + a.bn_mom * red[j];
   }
   if (tid == 0) {
     reset_counter(a.cnt);
@@ -332,19 +378,21 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
 
 struct ReadoutK {
   gtr_batch bt;
-  int L1, train, flags, loss_kind;
-  float temperature, dual_alpha, bn_eps, scale;
+  int L1, train, flags, loss_kind, cred, fin, pad0, pad1;
+  float temperature, dual_alpha, bn_eps, bn_mom, scale;
   uint32_t seed, thresh;
-  int drop_on, pad0;
+  int drop_on;
   const uint32_t* rng_ctr;
   const float* table;
   const float* out;
   const float* xin;
-  const float* stats;
+  float* stats;
+  const float* part;
   const float* gamma;
   const float* beta;
-  const float* rmean;
-  const float* rvar;
+  float* rmean;
+  float* rvar;
+  int64_t* nbt;
   float* se;
   const float* dse_in;
   float* dse_out;
@@ -363,7 +411,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_readout(ReadoutK a) {
   constexpr int VPL = D >= 64 ? D / 64 : 1;
   constexpr int NB = 8;   // node rows in flight per wave
   constexpr int NK = 8;   // negative rows in flight per wave
-  __shared__ float s_bn[2 * D];
+  __shared__ float s_bn[3 * D];
   __shared__ float s_red[GTR_WAVES][2 * D];
   __shared__ float s_loss[GTR_WAVES][2];
   __shared__ int s_flag;
@@ -384,14 +432,11 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_readout(ReadoutK a) {
   const float inv_b = 1.0f / (float)B;                // listwise mean over B
   const float inv_t = 1.0f / a.temperature;
 
-  if (do_fwd || do_bwd) {
-    for (int j = tid; j < D; j += GTR_BLOCK) {
-      float mean, rstd;
-      if (a.train) { mean = a.stats[j]; rstd = a.stats[D + j]; }
-      else { mean = a.rmean[j]; rstd = 1.0f / sqrtf(a.rvar[j] + a.bn_eps); }
-      s_bn[j] = mean;
-      s_bn[D + j] = rstd;
-    }
+  if (do_fwd) {
+    prev_bn_stats<D, GTR_BLOCK>(a.train, a.cred, a.bt.hdr[4], a.part, a.stats, a.rmean, a.rvar, a.nbt, a.bn_eps,
+                                a.bn_mom, s_bn, s_bn + D, s_bn + 2 * D);
+  } else if (do_bwd) {
+    for (int j = tid; j < D; j += GTR_BLOCK) { s_bn[j] = a.stats[j]; s_bn[D + j] = a.stats[D + j]; }
   }
   __syncthreads();
   float bm[VPL], br[VPL], bg[VPL], bb[VPL];
@@ -561,8 +606,8 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_readout(ReadoutK a) {
   }
 
   if (!(do_loss || do_bwd)) return;
-  // ---- block partials -> last arriver (fixed order => deterministic)
-  if (lane == 0) { s_loss[wave][0] = lw_sum; s_loss[wave][1] = bpr_sum; }
+  // ---- block partials (loss partials pre-scaled by the mean normalisers) in fixed order
+  if (lane == 0) { s_loss[wave][0] = lw_sum * (w_lw * inv_b); s_loss[wave][1] = bpr_sum * (w_bpr * inv_bn); }
   if (do_bwd && act) {
 #pragma unroll
     for (int v = 0; v < VPL; ++v) { s_red[wave][d0 + v] = gs[v]; s_red[wave][D + d0 + v] = gx[v]; }
@@ -580,13 +625,11 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_readout(ReadoutK a) {
       a.gpart[(size_t)blockIdx.x * 2 * D + j] = acc;
     }
   }
+  if (!a.fin) return;  // loss summed by gtr_step_end, BN sums reduced by the consuming conv_bwd
   if (!arrive_last(a.cnt, gridDim.x, &s_flag)) return;
   if (do_loss && tid == 0) {
-    float lw = 0.0f, bp = 0.0f;
-    for (int q = 0; q < (int)gridDim.x; ++q) { lw += a.loss_part[(size_t)q * 2]; bp += a.loss_part[(size_t)q * 2 + 1]; }
     float loss = 0.0f;
-    if (use_lw) loss += w_lw * (lw * inv_b);
-    if (use_bpr) loss += w_bpr * (bp * inv_bn);
+    for (int q = 0; q < (int)gridDim.x; ++q) loss += a.loss_part[(size_t)q * 2] + a.loss_part[(size_t)q * 2 + 1];
     a.loss_out[0] = loss;
   }
   if (do_bwd) {
@@ -631,6 +674,7 @@ extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     return GTR_E_ARG;
   }
   if (!check_dims(cfg, "gtr_conv_fwd")) return GTR_E_ARG;
+  if (!bt->grp_row || !bt->grp_edge) { set_error("gtr_conv_fwd: batch lacks row-group ranges"); return GTR_E_ARG; }
   if (l == 0 && (!emb || !emb->table)) { set_error("gtr_conv_fwd: layer 0 needs the table"); return GTR_E_ARG; }
   if (l == 0 && cfg->pe_k > 0 && (!emb->wpe || !emb->bpe || (!emb->pe_tab && !bt->node_pe))) {
     set_error("gtr_conv_fwd: Laplacian PE not precomputed");
@@ -641,11 +685,11 @@ extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   k.bt = *bt;
   k.H = cfg->heads;
   k.C = cfg->dim / cfg->heads;
-  k.R = cfg->row_group;
   k.first = l == 0;
   k.train = cfg->training;
   k.layer = l;
   k.pe_k = cfg->pe_k;
+  k.cred = cfg->consumer_reduce;
   k.sqrt_c = (float)sqrt((double)k.C);
   k.bn_eps = cfg->bn_eps;
   k.bn_mom = cfg->bn_momentum;
@@ -656,8 +700,8 @@ extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     k.table = emb->table; k.pe_tab = emb->pe_tab; k.wpe = emb->wpe; k.bpe = emb->bpe;
   } else {
     const gtr_layer& P = layers[l - 1];
-    k.p_out = P.out; k.p_xin = P.xin; k.p_stats = P.bn_stats; k.p_gamma = P.bn_gamma;
-    k.p_beta = P.bn_beta; k.p_rmean = P.bn_rmean; k.p_rvar = P.bn_rvar;
+    k.p_out = P.out; k.p_xin = P.xin; k.p_stats = P.bn_stats; k.p_part = P.bn_part; k.p_gamma = P.bn_gamma;
+    k.p_beta = P.bn_beta; k.p_rmean = P.bn_rmean; k.p_rvar = P.bn_rvar; k.p_nbt = P.bn_nbt;
   }
   k.w_all = L.w_all; k.b_all = L.b_all; k.w_beta = L.w_beta;
   k.xin = L.xin; k.qkvs = L.qkvs; k.alpha = L.alpha; k.agg = L.agg; k.gate = L.gate; k.out = L.out;
@@ -667,8 +711,7 @@ extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   if (grid <= 0) return GTR_OK;
   hipStream_t s = (hipStream_t)stream;
 #define GTR_FWD(DD) set_lds_limit<DD>(k_conv_fwd<DD>, (size_t)LayerGeom<DD>::F_WORDS * 4); \
-  hipLaunchKernelGGL(k_conv_fwd<DD>, dim3(grid), dim3(CONV_BLOCK), \
-                                       (size_t)LayerGeom<DD>::F_WORDS * 4, s, k)
+  hipLaunchKernelGGL(k_conv_fwd<DD>, dim3(grid), dim3(CONV_BLOCK), (size_t)LayerGeom<DD>::F_WORDS * 4, s, k)
   switch (cfg->dim) {
     case 32: GTR_FWD(32); break;
     case 64: GTR_FWD(64); break;
@@ -700,16 +743,22 @@ extern "C" int gtr_readout_loss(const gtr_config* cfg, const gtr_batch* bt, cons
   k.train = cfg->training;
   k.flags = head->flags;
   k.loss_kind = head->loss_kind;
+  k.cred = cfg->consumer_reduce;
+  // finalise in-kernel unless a consumer takes over: the BN sums go to conv_bwd and the
+  // loss to gtr_step_end in the fused step; a loss-only call always finalises itself.
+  k.fin = (!cfg->consumer_reduce || !(head->flags & GTR_RO_BWD)) ? 1 : 0;
   k.temperature = head->temperature;
   k.dual_alpha = head->dual_alpha;
   k.bn_eps = cfg->bn_eps;
+  k.bn_mom = cfg->bn_momentum;
   drop_params(cfg, k.thresh, k.scale, k.drop_on);
   k.seed = cfg->seed;
   k.rng_ctr = cfg->rng_ctr;
   k.table = table;
-  k.out = L.out; k.xin = L.xin; k.stats = L.bn_stats; k.gamma = L.bn_gamma; k.beta = L.bn_beta;
-  k.rmean = L.bn_rmean; k.rvar = L.bn_rvar;
-  k.se = head->se; k.dse_in = head->dse_in; k.dse_out = head->dse_out; k.coef_tgt = head->coef_tgt; k.coef_neg = head->coef_neg;
+  k.out = L.out; k.xin = L.xin; k.stats = L.bn_stats; k.part = L.bn_part; k.gamma = L.bn_gamma; k.beta = L.bn_beta;
+  k.rmean = L.bn_rmean; k.rvar = L.bn_rvar; k.nbt = L.bn_nbt;
+  k.se = head->se; k.dse_in = head->dse_in; k.dse_out = head->dse_out; k.coef_tgt = head->coef_tgt;
+  k.coef_neg = head->coef_neg;
   k.loss_part = head->loss_part; k.loss_out = head->loss_out; k.cnt = head->cnt;
   k.dy = L.dy; k.gpart = L.bn_gpart; k.gsum = L.bn_gsum;
   int grid = (bt->b_cap + GTR_WAVES - 1) / GTR_WAVES;

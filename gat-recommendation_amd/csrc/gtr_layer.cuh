@@ -25,7 +25,8 @@ struct LayerGeom {
   // ---- forward LDS carve (4-byte words)
   static constexpr int F_XO = 0;                              // [RMAX][XS]   X rows, then OUT rows
   static constexpr int F_KV = F_XO + RMAX * XS;               // [2][RMAX][D] K rows | V rows
-  static constexpr int F_PE = F_KV + (KV ? 2 * RMAX * D : 0); // [D][KPE] Wpe | [RMAX][KPE] P rows
+  static constexpr int F_QS = F_KV + (KV ? 2 * RMAX * D : 0); // [2][RMAX][D] Q rows | S rows
+  static constexpr int F_PE = F_QS + (KV ? 2 * RMAX * D : 0); // [D][KPE] Wpe | [RMAX][KPE] P rows
   static constexpr int F_BN = F_PE + (D + RMAX) * KPE;        // [2D] previous BN mean | rstd
   static constexpr int F_ITEMS = F_BN + 2 * D;                // [RMAX] node items
   static constexpr int F_IPTR = F_ITEMS + RMAX;               // [RMAX+1] local in_ptr
@@ -43,7 +44,8 @@ struct LayerGeom {
   static constexpr int B_OPTR = B_ISRC + EMAX;                // [RMAX+1]
   static constexpr int B_OEDGE = B_OPTR + RMAX + 4;           // [EMAX] local dst-order position
   static constexpr int B_ODST = B_OEDGE + EMAX;               // [EMAX] local dst row
-  static constexpr int B_FLAG = B_ODST + EMAX;
+  static constexpr int B_GS = B_ODST + EMAX;                  // [2D] reduced BN backward sums
+  static constexpr int B_FLAG = B_GS + 2 * D;
   static constexpr int B_WORDS = B_FLAG + 4;
 };
 
@@ -78,6 +80,34 @@ __device__ __forceinline__ void store_vec(float* p, const float (&x)[VPL], bool 
     *reinterpret_cast<float2*>(p) = make_float2(x[0], x[1]);
   } else {
     p[0] = x[0];
+  }
+}
+
+// Consumer-side BatchNorm statistics: combine G per-group (count, mean, M2) partials
+// (layout [G][1+2D]) into mean / rstd; thread per feature, fixed order (deterministic).
+template <int D, int BLK>
+__device__ __forceinline__ void bn_stats_from_parts(const float* part, int G, float eps, float* s_mean,
+                                                    float* s_rstd, float* s_uvar) {
+  for (int j = threadIdx.x; j < D; j += BLK) {
+    double n = 0.0, sum = 0.0;
+#pragma unroll 8
+    for (int q = 0; q < G; ++q) {
+      const float* pp = part + (size_t)q * (1 + 2 * D);
+      n += (double)pp[0];
+      sum += (double)pp[0] * (double)pp[1 + j];
+    }
+    const double mean = sum / n;
+    double m2 = 0.0;
+#pragma unroll 8
+    for (int q = 0; q < G; ++q) {
+      const float* pp = part + (size_t)q * (1 + 2 * D);
+      const double d = (double)pp[1 + j] - mean;
+      m2 += (double)pp[1 + D + j] + (double)pp[0] * d * d;
+    }
+    const float var = (float)(m2 / n);
+    s_mean[j] = (float)mean;
+    s_rstd[j] = 1.0f / sqrtf(var + eps);
+    s_uvar[j] = n > 1.0 ? (float)(m2 / (n - 1.0)) : var;
   }
 }
 

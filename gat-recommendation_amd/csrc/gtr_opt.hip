@@ -220,9 +220,26 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_scatter_rows(gtr_batch bt, int mo
   for (int q = 0; q < VPL; ++q) atomicAdd(dense + (size_t)key * D + d0 + q, c * s[d0 + q]);
 }
 
-__global__ void k_step_end(int64_t* step_dev, uint32_t* rng_ctr) {
-  if (step_dev) *step_dev += 1;
-  if (rng_ctr) *rng_ctr += 1;
+// Step epilogue: advance the step / dropout-stream counters and (optionally) sum the
+// readout's pre-scaled loss partials [nparts][2] in fixed order.
+__global__ void k_step_end(int64_t* step_dev, uint32_t* rng_ctr, const float* loss_part, int nparts,
+                           float* loss_out) {
+  __shared__ float s_acc[64];
+  const int tid = threadIdx.x;
+  float acc = 0.0f;
+  if (loss_part)
+    for (int q = tid; q < nparts; q += 64) acc += loss_part[(size_t)q * 2] + loss_part[(size_t)q * 2 + 1];
+  s_acc[tid] = acc;
+  __syncthreads();
+  if (tid == 0) {
+    if (loss_part && loss_out) {
+      float t = 0.0f;
+      for (int q = 0; q < 64; ++q) t += s_acc[q];
+      loss_out[0] = t;
+    }
+    if (step_dev) *step_dev += 1;
+    if (rng_ctr) *rng_ctr += 1;
+  }
 }
 
 int key_bits(int T) {
@@ -377,8 +394,11 @@ int gtr_scatter_rows(const gtr_batch* bt, int dim, int mode, const float* src, c
   return GTR_OK;
 }
 
-int gtr_step_end(int64_t* step_dev, uint32_t* rng_ctr, gtr_stream_t stream) {
-  hipLaunchKernelGGL(k_step_end, dim3(1), dim3(1), 0, (hipStream_t)stream, step_dev, rng_ctr);
+int gtr_step_end(int64_t* step_dev, uint32_t* rng_ctr, const float* loss_part, int nparts, float* loss_out,
+                 gtr_stream_t stream) {
+  if (loss_part && (nparts < 0 || !loss_out)) { set_error("gtr_step_end: bad loss partials"); return GTR_E_ARG; }
+  hipLaunchKernelGGL(k_step_end, dim3(1), dim3(64), 0, (hipStream_t)stream, step_dev, rng_ctr, loss_part, nparts,
+                     loss_out);
   GTR_HIP_CHECK_LAUNCH();
   return GTR_OK;
 }

@@ -27,7 +27,8 @@ class GtrBatch(C.Structure):
     _fields_ = [
         ("hdr", P), ("node_item", P), ("node_ptr", P), ("in_ptr", P), ("in_src", P),
         ("out_ptr", P), ("out_edge", P), ("out_dst", P), ("target", P), ("negatives", P),
-        ("node_pe", P), ("n_cap", i32), ("b_cap", i32), ("e_cap", i32), ("n_neg", i32),
+        ("node_pe", P), ("grp_row", P), ("grp_edge", P),
+        ("n_cap", i32), ("b_cap", i32), ("e_cap", i32), ("n_neg", i32),
     ]
 
 
@@ -35,7 +36,7 @@ class GtrConfig(C.Structure):
     _fields_ = [
         ("num_items", i32), ("dim", i32), ("heads", i32), ("pe_k", i32), ("num_layers", i32),
         ("row_group", i32), ("training", i32), ("dropout", f32), ("bn_eps", f32),
-        ("bn_momentum", f32), ("seed", u32), ("rng_ctr", P),
+        ("bn_momentum", f32), ("seed", u32), ("rng_ctr", P), ("consumer_reduce", i32), ("pad0", i32),
     ]
 
 
@@ -95,7 +96,7 @@ _SIGS = {
     "gtr_adamw_rows": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P, P, P, P, P, P, P]),
     "gtr_adamw_sweep": (C.c_int, [C.c_int, C.c_int, P, P, P, P, P, P]),
     "gtr_scatter_rows": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P]),
-    "gtr_step_end": (C.c_int, [P, P, P]),
+    "gtr_step_end": (C.c_int, [P, P, P, C.c_int, P, P]),
 }
 
 EXPORTS = tuple(_SIGS)

@@ -18,6 +18,7 @@ Kernel order of one training step:
 from __future__ import annotations
 
 import ctypes as C
+import os
 import math
 from dataclasses import dataclass
 
@@ -144,6 +145,11 @@ def _f32(*shape, device):
     return torch.zeros(*[max(int(s), 1) for s in shape], dtype=torch.float32, device=device)
 
 
+def readout_grid(b_cap: int) -> int:
+    """Workgroups of gtr_readout_loss (= its loss / BN-sum partial count)."""
+    return max(1, min((b_cap + 3) // 4, 256))
+
+
 class Workspace:
     """Capacity-sized activations + gradient buffers for one in-flight batch."""
 
@@ -233,7 +239,7 @@ class Engine:
                                "(e.g. model.to()); re-create the engine")
 
     def choose_R(self, caps: Caps) -> int:
-        return 16 if caps.n_cap <= 8192 else (32 if caps.n_cap <= 65536 else 64)
+        return caps.R
 
     def choose_P(self, caps: Caps) -> int:
         # split-K of the weight gradients: <= 32 node rows per workgroup, <= 64 slabs
@@ -266,6 +272,10 @@ class Engine:
         cfg.bn_momentum = float(bn.momentum if bn.momentum is not None else 0.1)
         cfg.seed = self.seed
         cfg.rng_ctr = self.rng_ctr.data_ptr()
+        # consumer-side reduction of BatchNorm partials pays while a consumer block can
+        # fold every group's partial in its prologue; large grids use the last arriver
+        cred = os.environ.get("GTR_CONSUMER_REDUCE")
+        cfg.consumer_reduce = int(cred) if cred is not None else (1 if ws.g_cap <= 64 else 0)
         return cfg
 
     def fill_embed(self):
@@ -287,7 +297,7 @@ class Engine:
         base = blob.data_ptr()
         bs = L.GtrBatch()
         for name in ("hdr", "node_item", "node_ptr", "in_ptr", "in_src", "out_ptr", "out_edge", "out_dst",
-                     "target", "negatives"):
+                     "target", "negatives", "grp_row", "grp_edge"):
             setattr(bs, name, base + 4 * lay[name][0])
         bs.node_pe = None if node_pe is None else node_pe.data_ptr()
         bs.n_cap, bs.b_cap, bs.e_cap, bs.n_neg = caps.n_cap, caps.b_cap, caps.e_cap, caps.n_neg

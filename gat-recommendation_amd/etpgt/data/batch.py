@@ -37,6 +37,16 @@ class Caps:
     e_cap: int
     n_neg: int
 
+    @property
+    def R(self) -> int:
+        """Row-group width of the layer kernels: a workgroup owns every session whose
+        first node lies in [g*R, (g+1)*R)."""
+        return 16 if self.n_cap <= 8192 else (32 if self.n_cap <= 65536 else 64)
+
+    @property
+    def g_cap(self) -> int:
+        return (self.n_cap + self.R - 1) // self.R
+
     def fits(self, n: int, b: int, e: int, n_neg: int) -> bool:
         return n <= self.n_cap and b <= self.b_cap and e <= self.e_cap and n_neg == self.n_neg
 
@@ -68,9 +78,11 @@ def _align4(x: int) -> int:
 def blob_layout(caps: Caps) -> dict:
     """int32 offsets of each array inside the packed blob (16-byte aligned regions)."""
     n, b, e, k = caps.n_cap, caps.b_cap, caps.e_cap, max(caps.n_neg, 1)
+    g = caps.g_cap
     sizes = [
         ("hdr", 8), ("node_item", n), ("node_ptr", b + 1), ("in_ptr", n + 1), ("in_src", e),
         ("out_ptr", n + 1), ("out_edge", e), ("out_dst", e), ("target", b), ("negatives", b * k),
+        ("grp_row", g + 1), ("grp_edge", g + 1),
     ]
     off, lay = 0, {}
     for name, sz in sizes:
@@ -233,7 +245,17 @@ def pack_batch(sb: SessionBatch, caps: Caps) -> np.ndarray:
         if fill is not None and a.shape[0] < sz:
             blob[o + a.shape[0] : o + sz] = fill
 
-    put("hdr", [N, B, E, n_neg, 0, 0, 0, 0])
+    # row groups: group g = sessions whose first node lies in [g*R, (g+1)*R)
+    R = caps.R
+    G = (N + R - 1) // R
+    starts = ptr[:-1]
+    sess_of_group = np.searchsorted(starts, np.arange(G + 1) * R, side="left")
+    grp_row = np.append(ptr, N)[np.minimum(sess_of_group, B)]
+    grp_row[-1] = N
+    grp_edge = in_ptr[grp_row]
+    put("hdr", [N, B, E, n_neg, G, R, 0, 0])
+    put("grp_row", grp_row, fill=N)
+    put("grp_edge", grp_edge, fill=E)
     put("node_item", x)
     put("node_ptr", ptr, fill=N)
     put("in_ptr", in_ptr, fill=E)

@@ -25,7 +25,7 @@ import os
 import torch
 
 from etpgt.backend import _lib as L
-from etpgt.backend.engine import Engine
+from etpgt.backend.engine import Engine, readout_grid
 from etpgt.data.batch import Caps, SessionBatch
 
 
@@ -44,7 +44,7 @@ class FusedTrainStep:
         self.alpha = float(alpha)
         self.use_graph = use_graph
         # experiment knob: run the untouched-row sweep after the chain instead of beside it
-        self.serial_sweep = os.environ.get("GTR_SERIAL_SWEEP", "0") == "1"
+        self.serial_sweep = os.environ.get("GTR_SERIAL_SWEEP", "1") == "1"
         eng = self.eng
         T, D = eng.T, eng.D
         self.adam = L.GtrAdam()
@@ -159,7 +159,10 @@ class FusedTrainStep:
         main.wait_stream(self.side1)
         if self.serial_sweep:
             self._sweep(st)
-        L.check(lib.gtr_step_end(self.step_dev.data_ptr(), eng.rng_ctr.data_ptr(), st), "step_end")
+        # with consumer-side reduction the readout leaves its loss partials to step_end
+        lp = ws.loss_part.data_ptr() if cfg.consumer_reduce else None
+        L.check(lib.gtr_step_end(self.step_dev.data_ptr(), eng.rng_ctr.data_ptr(), lp,
+                                 readout_grid(self.caps.b_cap), ws.loss_out.data_ptr(), st), "step_end")
 
     def _sweep(self, stream_handle):
         eng = self.eng

@@ -53,7 +53,10 @@ extern "C" {
 typedef void* gtr_stream_t; /* hipStream_t */
 
 /* Batch in HBM: fixed-capacity arrays, live sizes in hdr[] on device.
- * hdr[0] = N (nodes), hdr[1] = B (sessions), hdr[2] = E (edges).            */
+ * hdr[0] = N (nodes), hdr[1] = B (sessions), hdr[2] = E (edges),
+ * hdr[4] = G (row groups), hdr[5] = R (row-group width, == gtr_config.row_group).
+ * Row group g owns every session whose first node lies in [g*R, (g+1)*R):
+ * rows [grp_row[g], grp_row[g+1]) and dst-ordered edges [grp_edge[g], grp_edge[g+1]).  */
 typedef struct gtr_batch {
   const int32_t* hdr;
   const int32_t* node_item; /* [n_cap]   global item id of each node          */
@@ -66,6 +69,8 @@ typedef struct gtr_batch {
   const int32_t* target;    /* [b_cap]                                          */
   const int32_t* negatives; /* [b_cap * n_neg]                                  */
   const float* node_pe;     /* optional [n_cap, pe_k] batch.laplacian_pe, or NULL */
+  const int32_t* grp_row;   /* [g_cap+1] first row of each row group             */
+  const int32_t* grp_edge;  /* [g_cap+1] first dst-ordered edge of each row group */
   int32_t n_cap, b_cap, e_cap, n_neg;
 } gtr_batch;
 
@@ -82,6 +87,11 @@ typedef struct gtr_config {
   float bn_momentum;  /* 0.1                                     */
   uint32_t seed;      /* dropout stream seed                     */
   const uint32_t* rng_ctr; /* device counter mixed into dropout masks */
+  int32_t consumer_reduce; /* 1: a BatchNorm's batch statistics (fwd) and backward sums are
+                              reduced from the producer's per-group partials by the CONSUMING
+                              kernel (no inter-workgroup fences; for <= 64 row groups);
+                              0: the producer's last-arriving workgroup finalises them */
+  int32_t pad0;
 } gtr_config;
 
 /* Parameters + saved activations of one TransformerConv/BatchNorm layer.
@@ -226,8 +236,10 @@ int gtr_adamw_sweep(int num_items, int dim, const int32_t* stamp, float* table, 
 int gtr_scatter_rows(const gtr_batch* bt, int dim, int mode, const float* src, const float* coef_tgt,
                      const float* coef_neg, float* dense, gtr_stream_t stream);
 
-/* step_dev += 1 (if non-NULL); rng_ctr += 1 (if non-NULL).                    */
-int gtr_step_end(int64_t* step_dev, uint32_t* rng_ctr, gtr_stream_t stream);
+/* step_dev += 1 (if non-NULL); rng_ctr += 1 (if non-NULL); if loss_part != NULL,
+ * loss_out[0] = sum of the 2*nparts (already scaled) loss partials in order.     */
+int gtr_step_end(int64_t* step_dev, uint32_t* rng_ctr, const float* loss_part, int nparts, float* loss_out,
+                 gtr_stream_t stream);
 
 #ifdef __cplusplus
 }
