@@ -73,32 +73,11 @@ def main():
     torch.cuda.set_device(dev)
     cfg = CONFIGS[args.config]
 
-    from etpgt.data.batch import Caps
-    from etpgt.data.synthetic import batch_stats, make_batches, make_sessions_and_graph, random_pe_table
-    from etpgt.model import create_graph_transformer_optimized
-    from etpgt.train.fused import FusedTrainStep
-
     t0 = time.time()
-    data = make_sessions_and_graph(seed=42)
-    T = data.table_rows
-    B = args.batch_size
-    batches = make_batches(data, B, args.num_batches, cfg["n_neg"], seed=42, start=rank * B * args.num_batches)
-    st = batch_stats(batches)
-    log(f"data: T={T} sessions={data.num_sessions} edges={data.edge_keys.size} gen {time.time()-t0:.1f}s {st}")
-
-    torch.manual_seed(42)
-    model = create_graph_transformer_optimized(T, embedding_dim=cfg["D"], hidden_dim=cfg["D"], num_layers=2,
-                                               num_heads=cfg["H"], dropout=0.1, use_laplacian_pe=cfg["K"] > 0,
-                                               laplacian_k=max(cfg["K"], 1))
-    if cfg["K"] > 0:
-        model.laplacian_pe._cached_pe = random_pe_table(T, cfg["K"])
-    model = model.to(dev).train()
-    step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, loss=cfg["loss"], use_graph=not args.no_graph)
-    caps = Caps(max(b.num_nodes for b in batches), B, max(b.num_edges for b in batches), cfg["n_neg"])
-    step._bind(caps)
-    staged = [torch.from_numpy(b.packed(caps)[1]).to(dev) for b in batches]
-    touched = float(np.mean([len(set(b.x.tolist()) | set(b.target_item.tolist()) | set(b.negative_items.tolist()))
-                             for b in batches]))
+    w = build_workload(args.config, args.batch_size, args.num_batches, dev, rank, use_graph=not args.no_graph)
+    step, staged, batches, data, T, B, touched, st = (w[k] for k in ("step", "staged", "batches", "data", "T", "B",
+                                                                   "touched", "stats"))
+    log(f"data: T={T} sessions={data.num_sessions} edges={data.edge_keys.size} setup {time.time()-t0:.1f}s {st}")
 
     def one(i):
         step.load_blob(staged[i % len(staged)])
@@ -129,11 +108,11 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * B * args.steps / elapsed
 
-    # ---- dominant kernel: table sweep (AdamW over untouched rows), HIP events on its stream
-    sweep_ms = measure_sweep(step, staged, args.steps, dev)
+    # ---- dominant kernel: the step tail (AdamW over the whole table), HIP events on its stream
     D = cfg["D"]
-    alg_bytes = 24.0 * (T - touched) * D + 4.0 * T
-    achieved = alg_bytes / (sweep_ms * 1e-3) / 1e9
+    tail_ms = measure_tail(step, args.steps)
+    alg_bytes = tail_bytes(step, T, D, touched)
+    achieved = alg_bytes / (tail_ms * 1e-3) / 1e9
 
     cpu = None
     if rank == 0 and args.cpu_seconds > 0:
@@ -168,14 +147,14 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_adamw_sweep (AdamW over untouched item-table rows)",
+                "kernel": "k_step_tail (AdamW over all item-table rows + small parameters)",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None,
                 "alg_bytes_per_launch": int(alg_bytes),
-                "avg_launch_ms": round(sweep_ms, 5),
+                "avg_launch_ms": round(tail_ms, 5),
             },
             "cpu_baseline": cpu,
         }
@@ -184,32 +163,69 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def measure_sweep(step, staged, iters, dev) -> float:
-    """Average duration of the sweep kernel inside eager steps, bracketed by HIP
-    events recorded on the side stream that launches it."""
+def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, use_graph: bool = True) -> dict:
+    """Synthetic RetailRocket-shaped data, the model of `config`, a bound fused step
+    and `num_batches` packed batches pre-staged in HBM."""
+    from etpgt.data.batch import Caps
+    from etpgt.data.synthetic import batch_stats, make_batches, make_sessions_and_graph, random_pe_table
+    from etpgt.model import create_graph_transformer_optimized
+    from etpgt.train.fused import FusedTrainStep
+
+    cfg = CONFIGS[config]
+    data = make_sessions_and_graph(seed=42)
+    T = data.table_rows
+    batches = make_batches(data, B, num_batches, cfg["n_neg"], seed=42, start=rank * B * num_batches)
+    st = batch_stats(batches)
+    torch.manual_seed(42)
+    model = create_graph_transformer_optimized(T, embedding_dim=cfg["D"], hidden_dim=cfg["D"], num_layers=2,
+                                               num_heads=cfg["H"], dropout=0.1, use_laplacian_pe=cfg["K"] > 0,
+                                               laplacian_k=max(cfg["K"], 1))
+    if cfg["K"] > 0:
+        model.laplacian_pe._cached_pe = random_pe_table(T, cfg["K"])
+    model = model.to(dev).train()
+    step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, loss=cfg["loss"], use_graph=use_graph)
+    caps = Caps(max(b.num_nodes for b in batches), B, max(b.num_edges for b in batches), cfg["n_neg"])
+    step._bind(caps)
+    staged = [torch.from_numpy(b.packed(caps)[1]).to(dev) for b in batches]
+    touched = float(np.mean([len(set(b.x.tolist()) | set(b.target_item.tolist()) | set(b.negative_items.tolist()))
+                             for b in batches]))
+    return dict(step=step, staged=staged, batches=batches, data=data, T=T, B=B, touched=touched, stats=st,
+                caps=caps, model=model)
+
+
+def measure_tail(step, iters) -> float:
+    """Average duration (ms) of the step-tail kernel (AdamW over every item-table row
+    + small parameters), bracketed by HIP events on the stream it is launched on.
+    Re-launches the last step's tail: a valid optimizer update on that step's gradients."""
     from etpgt.backend import _lib as L
     import ctypes as C
 
     lib = L.lib()
     eng = step.eng
+    main = torch.cuda.current_stream()
     durs = []
-    s1 = step.side1
     n = max(10, min(iters, 200))
-    for i in range(n):
-        step.load_blob(staged[i % len(staged)])
-        torch.cuda.synchronize(dev)
-        with torch.cuda.stream(s1):
-            L.check(lib.gtr_contrib_prep(C.byref(step.bs), eng.T, step.keys.data_ptr(), step.vals.data_ptr(),
-                                         step.stamp.data_ptr(), step.step_dev.data_ptr(), s1.cuda_stream), "prep")
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(s1)
-            L.check(lib.gtr_adamw_sweep(eng.T, eng.D, step.stamp.data_ptr(), eng.model.item_embedding.weight.data_ptr(),
-                                        step.m_tab.data_ptr(), step.v_tab.data_ptr(), C.byref(step.adam),
-                                        s1.cuda_stream), "sweep")
-            e1.record(s1)
-        s1.synchronize()
-        durs.append(e0.elapsed_time(e1))
-    return float(np.median(durs))
+    for _ in range(n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(main)
+        L.check(lib.gtr_step_tail(C.byref(step.bs), eng.T, eng.D, C.byref(step.tail), step.segs, step.nseg,
+                                  C.byref(step.adam), main.cuda_stream), "step_tail")
+        e1.record(main)
+        durs.append((e0, e1))
+    torch.cuda.synchronize()
+    return float(np.median([a.elapsed_time(b) for a, b in durs]))
+
+
+def tail_bytes(step, T, D, touched) -> float:
+    """Algorithmic HBM bytes of one step-tail launch (SURVEY.md §8d table term):
+    untouched rows p,m,v read+write (24 B/elem) + their stamps; touched rows p,m,v
+    (24 B/elem) + contribution rows / keys / coefficients; small parameters p,m,v +
+    gradient partials."""
+    caps = step.caps
+    m_cap = caps.n_cap + caps.b_cap * (1 + caps.n_neg)
+    lay = step.eng.flat.layout
+    small = lay.total * (24.0 + 4.0 * step.ws.P)
+    return 24.0 * T * D + 4.0 * T + m_cap * (4.0 * D + 12.0) + small
 
 
 def cpu_baseline(cfg, batches, T, seconds):

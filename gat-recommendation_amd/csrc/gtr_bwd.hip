@@ -15,6 +15,8 @@ namespace {
 
 using namespace gtr;
 
+GTR_PH_DECL
+
 struct ConvBwdK {
   gtr_batch bt;
   int H, C, layer, has_prev, cred, gpart_n;  // gpart_n: partials feeding gsum (-1: hdr G)
@@ -166,24 +168,31 @@ __device__ __forceinline__ void bwd_src_row(const ConvBwdK& a, int s, int sl, co
 template <int D>
 __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
   using G = LayerGeom<D>;
-  constexpr int VPL = G::VPL, RMAX = G::RMAX, AS = G::AS;
+  constexpr int VPL = G::VPL, RMAX = G::RMAX, XS = G::XS, TPR = G::TPR, CH = G::CH;
   constexpr int NCT = D / 16;                                   // dX column tiles
   constexpr int CPW = NCT > CONV_WAVES ? NCT / CONV_WAVES : 1;  // column tiles per wave
+  constexpr int WPC = NCT >= CONV_WAVES ? 1 : CONV_WAVES / NCT; // waves sharing a column tile
   extern __shared__ __attribute__((aligned(16))) float sm[];
-  float* R1 = sm + G::B_R1;
-  float* ALs = sm + G::B_ALPHA;
-  float* DLs = sm + G::B_DLOG;
+  float* Ks = sm + G::B_R;
+  float* Vs = Ks + RMAX * XS;
+  float* Qs = Vs + RMAX * XS;
+  float* DAs = Qs + RMAX * XS;
+  float* AL = sm + G::B_AL;
+  float* DL = sm + G::B_DL;
   int* iptr = reinterpret_cast<int*>(sm + G::B_IPTR);
   int* isrc = reinterpret_cast<int*>(sm + G::B_ISRC);
+  int* edst = reinterpret_cast<int*>(sm + G::B_EDST);
   int* optr = reinterpret_cast<int*>(sm + G::B_OPTR);
   int* oedge = reinterpret_cast<int*>(sm + G::B_OEDGE);
   int* odst = reinterpret_cast<int*>(sm + G::B_ODST);
   float* s_gs = sm + G::B_GS;
+  float* s_bnp = sm + G::B_BNP;
   int* s_flag = reinterpret_cast<int*>(sm + G::B_FLAG);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int N = a.bt.hdr[0];
+  GTR_PH(a.layer, 0);
   const int Gn = a.bt.hdr[4];
+  const int N = a.bt.hdr[0];
   const int g = blockIdx.x;
   if (g >= Gn) return;
   const int r0 = a.bt.grp_row[g], r1 = a.bt.grp_row[g + 1];
@@ -192,15 +201,14 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
   const int e_lo = a.bt.grp_edge[g], e_hi = a.bt.grp_edge[g + 1];
   const int o_lo = e_lo;
   const int nrow = r1 - r0;
-  const int H = a.H;
+  const int H = a.H, C = a.C;
   const int ne = e_hi - e_lo;
-  const bool fast = G::KV && nrow <= RMAX && ne <= G::EMAX && H <= 8;
+  const bool fast = G::KV && nrow <= RMAX && ne <= G::EMAX && ne * H <= G::EH && H <= 8 && C >= CH;
   const uint32_t ctr = a.rng_ctr ? *a.rng_ctr : 0u;
   const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
-  const int d0 = lane * VPL;
-  const bool act = d0 < D;
   const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
   const float invN = 1.0f / (float)N;
+  const int prow = tid / TPR, pchunk = tid - prow * TPR, f0 = pchunk * CH;
 
   // ---- this layer's BatchNorm backward sums: reduce the producer's partials (cred)
   if (a.cred) {
@@ -214,98 +222,221 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
     }
   }
 
-  // ---- stage (fast): CSR slices, alpha slice, K|V rows of the group
   if (fast) {
+    // ---- stage: CSR slices (by destination and by source), alpha, K | V | Q rows
     for (int i = tid; i <= nrow; i += CONV_BLOCK) {
       iptr[i] = a.bt.in_ptr[r0 + i] - e_lo;
       optr[i] = a.bt.out_ptr[r0 + i] - o_lo;
+    }
+    for (int i = tid; i < nrow; i += CONV_BLOCK) {
+      const int k1 = a.bt.in_ptr[r0 + i + 1] - e_lo;
+      for (int k = a.bt.in_ptr[r0 + i] - e_lo; k < k1; ++k) edst[k] = i;
     }
     for (int k = tid; k < ne; k += CONV_BLOCK) {
       isrc[k] = a.bt.in_src[e_lo + k] - r0;
       oedge[k] = a.bt.out_edge[o_lo + k] - e_lo;
       odst[k] = a.bt.out_dst[o_lo + k] - r0;
     }
-    for (int k = tid; k < ne * H; k += CONV_BLOCK) ALs[k] = a.alpha[(size_t)e_lo * H + k];
+    for (int k = tid; k < ne * H; k += CONV_BLOCK) AL[k] = a.alpha[(size_t)e_lo * H + k];
     for (int idx = tid; idx < nrow * (D / 4); idx += CONV_BLOCK) {
       const int i = idx / (D / 4), c = (idx - i * (D / 4)) * 4;
       const float* src = a.qkvs + (size_t)(r0 + i) * (4 * D);
-      *reinterpret_cast<float4*>(R1 + i * D + c) = *reinterpret_cast<const float4*>(src + D + c);
-      *reinterpret_cast<float4*>(R1 + RMAX * D + i * D + c) = *reinterpret_cast<const float4*>(src + 2 * D + c);
+      *reinterpret_cast<float4*>(Ks + i * XS + c) = *reinterpret_cast<const float4*>(src + D + c);
+      *reinterpret_cast<float4*>(Vs + i * XS + c) = *reinterpret_cast<const float4*>(src + 2 * D + c);
+      *reinterpret_cast<float4*>(Qs + i * XS + c) = *reinterpret_cast<const float4*>(src + c);
     }
-  }
-  __syncthreads();
+    __syncthreads();
+    GTR_PH(a.layer, 1);
 
-  float k_g[VPL], k_mean[VPL], k_rstd[VPL], k_s1[VPL], k_s2[VPL];
-  {
-    const int j = act ? d0 : 0;
-    load_vec<VPL>(k_g, a.gamma + j, true);
-    load_vec<VPL>(k_mean, a.stats + j, true);
-    load_vec<VPL>(k_rstd, a.stats + D + j, true);
-    const float* gs = a.cred ? s_gs : a.gsum;
-    load_vec<VPL>(k_s1, gs + j, true);
-    load_vec<VPL>(k_s2, gs + D + j, true);
+    // ---- (D1) BatchNorm backward, beta gate: TPR lanes per destination row, CH features each
+    const bool live = prow < nrow;
+    const int t = r0 + prow;
+    float gv[CH], sv[CH], agv[CH];
+    float dbeta = 0.0f, beta = 0.0f;
+    if (live) {
+      const size_t ro = (size_t)t * D + f0;
+      const float* gs = a.cred ? s_gs : a.gsum;
+      beta = a.gate[t];
 #pragma unroll
-    for (int v = 0; v < VPL; ++v) { k_s1[v] *= invN; k_s2[v] *= invN; }
-  }
+      for (int c = 0; c < CH; c += 4) {
+        const float4 dy4 = *reinterpret_cast<const float4*>(a.dy + ro + c);
+        const float4 o4 = *reinterpret_cast<const float4*>(a.out + ro + c);
+        const float4 ag4 = *reinterpret_cast<const float4*>(a.agg + ro + c);
+        const float4 s4 = *reinterpret_cast<const float4*>(a.qkvs + (size_t)t * (4 * D) + 3 * D + f0 + c);
+        const float dyv[4] = {dy4.x, dy4.y, dy4.z, dy4.w}, ov[4] = {o4.x, o4.y, o4.z, o4.w};
+        const float agl[4] = {ag4.x, ag4.y, ag4.z, ag4.w}, svl[4] = {s4.x, s4.y, s4.z, s4.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int j = f0 + c + q;
+          const float mean = a.stats[j], rstd = a.stats[D + j];
+          const float xh = (ov[q] - mean) * rstd;
+          const float s1 = gs[j] * invN, s2 = gs[D + j] * invN;
+          gv[c + q] = (dyv[q] - s1 - xh * s2) * rstd * a.gamma[j];
+          sv[c + q] = svl[q];
+          agv[c + q] = agl[q];
+          dbeta += gv[c + q] * (svl[q] - agl[q]);
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < TPR; o <<= 1) dbeta += __shfl_xor(dbeta, o);
+    if (live) {
+      const float du = dbeta * beta * (1.0f - beta);
+      if (pchunk == 0) a.du[t] = du;
+#pragma unroll
+      for (int c = 0; c < CH; c += 4) {
+        float dag[4], ds[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int j = f0 + c + q;
+          const float w1 = a.w_beta[j], w2 = a.w_beta[D + j], w3 = a.w_beta[2 * D + j];
+          dag[q] = gv[c + q] * (1.0f - beta) + du * (w1 + w3);
+          ds[q] = gv[c + q] * beta + du * (w2 - w3);
+        }
+        *reinterpret_cast<float4*>(a.dqkvs + (size_t)t * (4 * D) + 3 * D + f0 + c) =
+            make_float4(ds[0], ds[1], ds[2], ds[3]);
+        *reinterpret_cast<float4*>(DAs + prow * XS + f0 + c) = make_float4(dag[0], dag[1], dag[2], dag[3]);
+      }
+    }
+    (void)sv; (void)agv;
+    __syncthreads();
 
-  // ---- phase 1: destination rows
-  if (fast) {
-    for (int t = r0 + wave; t < r1; t += CONV_WAVES)
-      bwd_dst_row<D>(a, t, t - r0, R1, R1 + RMAX * D, D, iptr, isrc, ALs, DLs, e_lo, lane, dr, st_attn,
-                     k_g, k_mean, k_rstd, k_s1, k_s2);
+    // ---- (D2) da of every (edge, head): <dA[dst], V[src]> * dropout mask, SPL lanes per item
+    {
+      const int SPL = C >= 16 ? 4 : 1;
+      const int cw = C / SPL;
+      const int nit = ne * H * SPL;
+      for (int base = 0; base < nit; base += CONV_BLOCK) {
+        const int idx = base + tid;
+        const int it = idx / SPL;
+        float dot = 0.0f;
+        if (idx < nit) {
+          const int sub = idx - it * SPL;
+          const int e = it / H, h = it - e * H;
+          const float* x = DAs + edst[e] * XS + h * C + sub * cw;
+          const float* y = Vs + isrc[e] * XS + h * C + sub * cw;
+          for (int c = 0; c < cw; c += 4) {
+            const float4 p = *reinterpret_cast<const float4*>(x + c);
+            const float4 q = *reinterpret_cast<const float4*>(y + c);
+            dot += p.x * q.x + p.y * q.y + p.z * q.z + p.w * q.w;
+          }
+        }
+        if (SPL == 4) {
+          dot += __shfl_xor(dot, 1);
+          dot += __shfl_xor(dot, 2);
+        }
+        if (idx < nit && idx == it * SPL) DL[it] = dot * dr.mul(st_attn, (uint32_t)(e_lo * H + it));
+      }
+    }
+    __syncthreads();
+
+    // ---- (D3) softmax backward per (destination, head): dlogit = alpha * (da - sum alpha*da)
+    for (int idx = tid; idx < nrow * H; idx += CONV_BLOCK) {
+      const int i = idx / H, h = idx - i * H;
+      const int e0 = iptr[i], e1 = iptr[i + 1];
+      float sdot = 0.0f;
+      for (int e = e0; e < e1; ++e) sdot += AL[e * H + h] * DL[e * H + h];
+      for (int e = e0; e < e1; ++e) {
+        const int k = e * H + h;
+        const float al = AL[k];
+        DL[k] = al * (DL[k] - sdot);
+        AL[k] = al * dr.mul(st_attn, (uint32_t)((e + e_lo) * H + h));
+      }
+    }
+    __syncthreads();
+    GTR_PH(a.layer, 2);
+
+    // ---- (D4) dQ over in-edges, (D5) dK, dV over out-edges: TPR lanes per row
+    if (live) {
+      const int hd = f0 / C;
+      const float isc = 1.0f / a.sqrt_c;
+      float dq[CH], dk[CH], dv[CH];
+#pragma unroll
+      for (int c = 0; c < CH; ++c) { dq[c] = 0.0f; dk[c] = 0.0f; dv[c] = 0.0f; }
+      const int e1 = iptr[prow + 1];
+      for (int e = iptr[prow]; e < e1; ++e) {
+        const float cdl = DL[e * H + hd] * isc;
+        const float* kr = Ks + isrc[e] * XS + f0;
+#pragma unroll
+        for (int c = 0; c < CH; c += 4) {
+          const float4 k4 = *reinterpret_cast<const float4*>(kr + c);
+          dq[c] += cdl * k4.x; dq[c + 1] += cdl * k4.y; dq[c + 2] += cdl * k4.z; dq[c + 3] += cdl * k4.w;
+        }
+      }
+      const int i1 = optr[prow + 1];
+      for (int i = optr[prow]; i < i1; ++i) {
+        const int p = oedge[i], dd = odst[i];
+        const float cdl = DL[p * H + hd] * isc;
+        const float am = AL[p * H + hd];
+        const float* qr = Qs + dd * XS + f0;
+        const float* gr = DAs + dd * XS + f0;
+#pragma unroll
+        for (int c = 0; c < CH; c += 4) {
+          const float4 q4 = *reinterpret_cast<const float4*>(qr + c);
+          const float4 g4 = *reinterpret_cast<const float4*>(gr + c);
+          dk[c] += cdl * q4.x; dk[c + 1] += cdl * q4.y; dk[c + 2] += cdl * q4.z; dk[c + 3] += cdl * q4.w;
+          dv[c] += am * g4.x; dv[c + 1] += am * g4.y; dv[c + 2] += am * g4.z; dv[c + 3] += am * g4.w;
+        }
+      }
+      float* drow = a.dqkvs + (size_t)t * (4 * D) + f0;
+#pragma unroll
+      for (int c = 0; c < CH; c += 4) {
+        *reinterpret_cast<float4*>(drow + c) = make_float4(dq[c], dq[c + 1], dq[c + 2], dq[c + 3]);
+        *reinterpret_cast<float4*>(drow + D + c) = make_float4(dk[c], dk[c + 1], dk[c + 2], dk[c + 3]);
+        *reinterpret_cast<float4*>(drow + 2 * D + c) = make_float4(dv[c], dv[c + 1], dv[c + 2], dv[c + 3]);
+      }
+    }
   } else {
+    __syncthreads();
+    GTR_PH(a.layer, 1);
+    // ---- general path: wave per row against global memory (any group size / dim)
+    const int d0 = lane * VPL;
+    const bool act = d0 < D;
+    float k_g[VPL], k_mean[VPL], k_rstd[VPL], k_s1[VPL], k_s2[VPL];
+    {
+      const int j = act ? d0 : 0;
+      load_vec<VPL>(k_g, a.gamma + j, true);
+      load_vec<VPL>(k_mean, a.stats + j, true);
+      load_vec<VPL>(k_rstd, a.stats + D + j, true);
+      const float* gs = a.cred ? s_gs : a.gsum;
+      load_vec<VPL>(k_s1, gs + j, true);
+      load_vec<VPL>(k_s2, gs + D + j, true);
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) { k_s1[v] *= invN; k_s2[v] *= invN; }
+    }
     for (int t = r0 + wave; t < r1; t += CONV_WAVES)
       bwd_dst_row<D>(a, t, t, a.qkvs + D, a.qkvs + 2 * D, 4 * D, a.bt.in_ptr, a.bt.in_src, a.alpha, a.dlogit, 0,
                      lane, dr, st_attn, k_g, k_mean, k_rstd, k_s1, k_s2);
-  }
-  __syncthreads();
-
-  // ---- phase 2: source rows (fast: Q and dA rows re-staged into R1)
-  if (fast) {
-    for (int idx = tid; idx < nrow * (D / 4); idx += CONV_BLOCK) {
-      const int i = idx / (D / 4), c = (idx - i * (D / 4)) * 4;
-      *reinterpret_cast<float4*>(R1 + i * D + c) =
-          *reinterpret_cast<const float4*>(a.qkvs + (size_t)(r0 + i) * (4 * D) + c);
-      *reinterpret_cast<float4*>(R1 + RMAX * D + i * D + c) =
-          *reinterpret_cast<const float4*>(a.dagg + (size_t)(r0 + i) * D + c);
-    }
     __syncthreads();
-    for (int s = r0 + wave; s < r1; s += CONV_WAVES)
-      bwd_src_row<D>(a, s, s - r0, R1, D, R1 + RMAX * D, D, optr, oedge, odst, ALs, DLs, e_lo, lane, dr, st_attn);
-  } else {
+    GTR_PH(a.layer, 2);
     for (int s = r0 + wave; s < r1; s += CONV_WAVES)
       bwd_src_row<D>(a, s, s, a.qkvs, 4 * D, a.dagg, D, a.bt.out_ptr, a.bt.out_edge, a.bt.out_dst, a.alpha,
                      a.dlogit, 0, lane, dr, st_attn);
   }
   __syncthreads();
+  GTR_PH(a.layer, 3);
 
-  // ---- phase 3: dX = dQKVS . W_all (MFMA f32), + residual; previous layer's dropout mask;
-  //      the previous BatchNorm's backward sums (sum dy, sum dy*xhat) accumulate in the epilogue
+  // ---- phase X: dX = dQKVS . W_all (MFMA f32, operands straight from L2), + residual;
+  //      previous layer's dropout mask; that BatchNorm's backward sums in the epilogue.
+  //      Wave w owns column tile(s) ct = w % NCT (+ CONV_WAVES for CPW = 2) and the row
+  //      tiles rt = rs, rs + WPC, ... with rs = w / NCT.
   const int lr = lane & 15, lg = lane >> 4;
   const uint32_t st_prev = drop_stream(1, (uint32_t)(a.layer - 1), ctr);
-  float* As = R1;
+  const int rs = WPC > 1 ? wave / NCT : 0;
   float s1[CPW], s2[CPW], pm[CPW], pr[CPW];
 #pragma unroll
   for (int c = 0; c < CPW; ++c) {
     s1[c] = 0.0f; s2[c] = 0.0f; pm[c] = 0.0f; pr[c] = 0.0f;
-    const int ct = wave + c * CONV_WAVES;
-    if (a.has_prev && ct < NCT) { pm[c] = a.p_stats[ct * 16 + lr]; pr[c] = a.p_stats[D + ct * 16 + lr]; }
+    const int ct = (WPC > 1 ? wave % NCT : wave) + c * CONV_WAVES;
+    if (a.has_prev) { pm[c] = a.p_stats[ct * 16 + lr]; pr[c] = a.p_stats[D + ct * 16 + lr]; }
   }
-  for (int rt = r0; rt < r1; rt += 16) {
-    for (int idx = tid; idx < 16 * D; idx += CONV_BLOCK) {  // float4 granules
-      const int i = idx / D, c = (idx - i * D) * 4;
-      const int r = rt + i;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (r < r1) v = *reinterpret_cast<const float4*>(a.dqkvs + (size_t)r * (4 * D) + c);
-      *reinterpret_cast<float4*>(As + i * AS + c) = v;
-    }
-    __syncthreads();
+  for (int rt = r0 + rs * 16; rt < r1; rt += 16 * WPC) {
+    const int ar = min(rt + lr, r1 - 1);  // clamp: rows past the group are computed, never stored
+    const float* arow = a.dqkvs + (size_t)ar * (4 * D) + lg * 4;
 #pragma unroll
     for (int c = 0; c < CPW; ++c) {
-      const int ct = wave + c * CONV_WAVES;
-      if (ct >= NCT) continue;
+      const int ct = (WPC > 1 ? wave % NCT : wave) + c * CONV_WAVES;
       f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-      const float* arow = As + lr * AS + lg * 4;
       const float* bcol = a.w_all + (size_t)(lg * 4) * D + ct * 16 + lr;
 #pragma unroll 4
       for (int kb = 0; kb < D / 4; ++kb) {
@@ -331,22 +462,30 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
         }
       }
     }
-    __syncthreads();
   }
 
+  GTR_PH(a.layer, 4);
   if (!a.has_prev) return;
-  // ---- previous layer's BatchNorm backward partials: reduce the 4 row quads of each column
-  float* part = a.p_gpart + (size_t)g * 2 * D;
+  // ---- previous layer's BatchNorm backward partials: reduce the 4 row quads of each
+  //      column, then the WPC waves sharing a column tile (fixed order)
 #pragma unroll
   for (int c = 0; c < CPW; ++c) {
-    const int ct = wave + c * CONV_WAVES;
+    const int ct = (WPC > 1 ? wave % NCT : wave) + c * CONV_WAVES;
     float x1 = s1[c], x2 = s2[c];
     x1 += __shfl_xor(x1, 16); x1 += __shfl_xor(x1, 32);
     x2 += __shfl_xor(x2, 16); x2 += __shfl_xor(x2, 32);
-    if (ct < NCT && lg == 0) {
-      part[ct * 16 + lr] = x1;
-      part[D + ct * 16 + lr] = x2;
+    if (lg == 0) {
+      s_bnp[rs * 2 * D + ct * 16 + lr] = x1;
+      s_bnp[rs * 2 * D + D + ct * 16 + lr] = x2;
     }
+  }
+  __syncthreads();
+  float* part = a.p_gpart + (size_t)g * 2 * D;
+  for (int j = tid; j < 2 * D; j += CONV_BLOCK) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int q = 0; q < WPC; ++q) acc += s_bnp[q * 2 * D + j];
+    part[j] = acc;
   }
   if (a.cred) return;  // the next conv_bwd reduces the partials
   if (!arrive_last(a.p_cnt, (uint32_t)Gn, s_flag)) return;
@@ -482,6 +621,8 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_wgrad(WgradK a) {
 }
 
 }  // namespace
+
+GTR_PH_READER(gtr_dbg_bwd_phases)
 
 extern "C" int gtr_conv_bwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l,
                             float* dx0, gtr_stream_t stream) {

@@ -152,6 +152,41 @@ struct AdamStep {
 
 }  // namespace gtr
 
+// Diagnostic build only (make timing): per-workgroup phase stamps of the layer
+// kernels, s_memrealtime (100 MHz) taken by thread 0; read back by gtr_dbg_*_phases.
+#define GTR_PH_KERNELS 32
+#define GTR_PH_GROUPS 1024
+#define GTR_PH_SLOTS 8
+#ifdef GTR_PHASE_TIMING
+#define GTR_PH_DECL static __device__ unsigned long long g_ph[GTR_PH_KERNELS][GTR_PH_GROUPS][GTR_PH_SLOTS];
+#define GTR_PH(kid, k)                                                                               \
+  do {                                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x < GTR_PH_GROUPS) {                                            \
+      unsigned long long _t;                                                                         \
+      asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                 \
+      g_ph[(kid)][blockIdx.x][(k)] = _t;                                                             \
+    }                                                                                                \
+  } while (0)
+#define GTR_PH_CLK(kid, k)                                                                           \
+  do {                                                                                               \
+    if (threadIdx.x == 0 && blockIdx.x < GTR_PH_GROUPS) {                                            \
+      unsigned long long _t;                                                                         \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(_t)::"memory");                     \
+      g_ph[(kid)][blockIdx.x][(k)] = _t;                                                             \
+    }                                                                                                \
+  } while (0)
+#define GTR_PH_READER(name)                                                                          \
+  extern "C" int name(void* host, size_t bytes) {                                                    \
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ph), bytes < sizeof(g_ph) ? bytes : sizeof(g_ph), 0, \
+                                    hipMemcpyDeviceToHost);                                          \
+  }
+#else
+#define GTR_PH_DECL
+#define GTR_PH(kid, k) do { } while (0)
+#define GTR_PH_CLK(kid, k) do { } while (0)
+#define GTR_PH_READER(name)
+#endif
+
 #define GTR_HIP_CHECK_LAUNCH()                                              \
   do {                                                                      \
     hipError_t _e = hipGetLastError();                                      \

@@ -22,6 +22,8 @@ namespace {
 
 using namespace gtr;
 
+GTR_PH_DECL
+
 struct ConvFwdK {
   gtr_batch bt;
   int H, C, first, train, layer, pe_k, cred, pad0;
@@ -67,14 +69,14 @@ struct ConvFwdK {
 template <int D, int BLK>
 __device__ __forceinline__ void prev_bn_stats(int train, int cred, int G, const float* part, float* stats,
                                               float* rmean, float* rvar, int64_t* nbt, float eps, float mom,
-                                              float* s_mean, float* s_rstd, float* s_uvar) {
+                                              float* s_mean, float* s_rstd, float* s_uvar, float* scr) {
   if (!train) {
     for (int j = threadIdx.x; j < D; j += BLK) {
       s_mean[j] = rmean[j];
       s_rstd[j] = 1.0f / sqrtf(rvar[j] + eps);
     }
   } else if (cred) {
-    bn_stats_from_parts<D, BLK>(part, G, eps, s_mean, s_rstd, s_uvar);
+    bn_stats_from_parts<D, BLK>(part, G, eps, s_mean, s_rstd, s_uvar, scr);
     if (blockIdx.x == 0) {
       for (int j = threadIdx.x; j < D; j += BLK) {
         stats[j] = s_mean[j];
@@ -160,26 +162,33 @@ __device__ __forceinline__ void attn_row(const ConvFwdK& a, int t, int tl, const
 template <int D>
 __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
   using G = LayerGeom<D>;
-  constexpr int VPL = G::VPL, RMAX = G::RMAX, XS = G::XS, KPE = G::KPE;
+  constexpr int VPL = G::VPL, RMAX = G::RMAX, XS = G::XS, KPE = G::KPE, TPR = G::TPR, CH = G::CH;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* XO = sm + G::F_XO;
   float* KVs = sm + G::F_KV;
   float* QSs = sm + G::F_QS;
   float* PEs = sm + G::F_PE;
+  float* LOG = sm + G::F_LOG;
   float* s_bn = sm + G::F_BN;
   int* items = reinterpret_cast<int*>(sm + G::F_ITEMS);
   int* iptr = reinterpret_cast<int*>(sm + G::F_IPTR);
   int* isrc = reinterpret_cast<int*>(sm + G::F_ISRC);
+  int* edst = reinterpret_cast<int*>(sm + G::F_EDST);
   int* s_flag = reinterpret_cast<int*>(sm + G::F_FLAG);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  GTR_PH(a.layer, 0);
+  GTR_PH_CLK(a.layer, 6);
   const int Gn = a.bt.hdr[4];
   const int g = blockIdx.x;
   if (g >= Gn) return;
   const int r0 = a.bt.grp_row[g], r1 = a.bt.grp_row[g + 1];
   const int e_lo = a.bt.grp_edge[g], e_hi = a.bt.grp_edge[g + 1];
   const int nrow = r1 - r0;
-  const bool fast = G::KV && nrow <= RMAX && (e_hi - e_lo) <= G::EMAX;
+  const int ne = e_hi - e_lo;
+  // fast path: the group's rows, edges and (edge, head) logits fit the LDS carve and
+  // every thread's CH-feature chunk lies inside one head
+  const bool fast = G::KV && nrow <= RMAX && ne <= G::EMAX && ne * a.H <= G::EH && a.H <= 8 && a.C >= CH;
   const uint32_t ctr = a.rng_ctr ? *a.rng_ctr : 0u;
   const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
   const bool pe_lds = a.first && a.pe_k > 0 && a.pe_k <= KPE;
@@ -198,19 +207,39 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
 #pragma unroll
     for (int kb = 0; kb < D / 16; ++kb) wpre[pi][kb] = *reinterpret_cast<const float4*>(wrow + kb * 16);
   }
+  // gate weights: the row-parallel fast path holds this thread's CH-feature chunk,
+  // the wave-per-row general path VPL features per lane
+  const int prow = tid / TPR, pchunk = tid - prow * TPR, f0 = pchunk * CH;
+  float w1c[CH], w2c[CH], w3c[CH];
   float w1[VPL], w2[VPL], w3[VPL];
-  load_vec<VPL>(w1, a.w_beta + d0, act);
-  load_vec<VPL>(w2, a.w_beta + D + d0, act);
-  load_vec<VPL>(w3, a.w_beta + 2 * D + d0, act);
+  if (fast) {
+#pragma unroll
+    for (int c = 0; c < CH; c += 4) {
+      const float4 x1 = *reinterpret_cast<const float4*>(a.w_beta + f0 + c);
+      const float4 x2 = *reinterpret_cast<const float4*>(a.w_beta + D + f0 + c);
+      const float4 x3 = *reinterpret_cast<const float4*>(a.w_beta + 2 * D + f0 + c);
+      w1c[c] = x1.x; w1c[c + 1] = x1.y; w1c[c + 2] = x1.z; w1c[c + 3] = x1.w;
+      w2c[c] = x2.x; w2c[c + 1] = x2.y; w2c[c + 2] = x2.z; w2c[c + 3] = x2.w;
+      w3c[c] = x3.x; w3c[c + 1] = x3.y; w3c[c + 2] = x3.z; w3c[c + 3] = x3.w;
+    }
+  } else {
+    load_vec<VPL>(w1, a.w_beta + d0, act);
+    load_vec<VPL>(w2, a.w_beta + D + d0, act);
+    load_vec<VPL>(w3, a.w_beta + 2 * D + d0, act);
+  }
 
   // ---- stage: previous BN stats, CSR slice, node items, LapPE projection weight
   if (!a.first) {
     prev_bn_stats<D, CONV_BLOCK>(a.train, a.cred, Gn, a.p_part, a.p_stats, a.p_rmean, a.p_rvar, a.p_nbt, a.bn_eps,
-                                 a.bn_mom, s_bn, s_bn + D, XO);
+                                 a.bn_mom, s_bn, s_bn + D, XO, LOG);
   }
   if (fast) {
     for (int i = tid; i <= nrow; i += CONV_BLOCK) iptr[i] = a.bt.in_ptr[r0 + i] - e_lo;
-    for (int k = tid; k < e_hi - e_lo; k += CONV_BLOCK) isrc[k] = a.bt.in_src[e_lo + k] - r0;
+    for (int k = tid; k < ne; k += CONV_BLOCK) isrc[k] = a.bt.in_src[e_lo + k] - r0;
+    for (int i = tid; i < nrow; i += CONV_BLOCK) {
+      const int k1 = a.bt.in_ptr[r0 + i + 1] - e_lo;
+      for (int k = a.bt.in_ptr[r0 + i] - e_lo; k < k1; ++k) edst[k] = i;
+    }
   }
   if (pe_lds) {
     for (int idx = tid; idx < D * a.pe_k; idx += CONV_BLOCK) {
@@ -222,6 +251,7 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
     for (int i = tid; i < min(RMAX, nrow); i += CONV_BLOCK) items[i] = a.bt.node_item[r0 + i];
   }
   __syncthreads();
+  GTR_PH(a.layer, 1);
 
   // ---- phase P+M: layer input rows -> LDS -> QKVS projection (MFMA f32), chunks of RMAX rows
   const uint32_t st_prev = drop_stream(1, (uint32_t)(a.layer - 1), ctr);
@@ -286,7 +316,7 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
       const int which = col / D, cc = col - which * D;
       // LDS copies on the fast path: 0 = query -> QS[0], 1 = key -> KV[0], 2 = value -> KV[1], 3 = skip -> QS[1]
       float* ldst = nullptr;
-      if (fast) ldst = (which == 0 ? QSs : which == 1 ? KVs : which == 2 ? KVs + RMAX * D : QSs + RMAX * D) + cc;
+      if (fast) ldst = (which == 0 ? QSs : which == 1 ? KVs : which == 2 ? KVs + RMAX * XS : QSs + RMAX * XS) + cc;
       for (int rt = 0; rt * 16 < m; ++rt) {
         f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
         const float* xrow = XO + (rt * 16 + lr) * XS + lg * 4;
@@ -299,7 +329,7 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
           if (row < m) {
             const float v = acc[i] + bias;
             a.qkvs[(size_t)(rc + row) * (4 * D) + col] = v;
-            if (ldst) ldst[row * D] = v;
+            if (ldst) ldst[row * XS] = v;
           }
         }
       }
@@ -307,12 +337,100 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
     __syncthreads();
   }
 
+  GTR_PH(a.layer, 2);
   // ---- phase A: attention over in-edges + beta gate (wave per destination row)
   const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
   if (fast) {
-    for (int t = r0 + wave; t < r1; t += CONV_WAVES)
-      attn_row<D>(a, t, t - r0, QSs, QSs + RMAX * D, KVs, KVs + RMAX * D, D, iptr, isrc, e_lo, lane, dr, st_attn,
-                  w1, w2, w3, XO + (t - r0) * XS);
+    const int H = a.H, C = a.C;
+    // (L) logits of every (edge, head), the head's C features split over SPL lanes
+    const int SPL = C >= 16 ? 4 : 1;
+    const int cw = C / SPL;
+    const int nit = ne * H * SPL;
+    for (int base = 0; base < nit; base += CONV_BLOCK) {
+      const int idx = base + tid;
+      const int it = idx / SPL;
+      float dot = 0.0f;
+      if (idx < nit) {
+        const int sub = idx - it * SPL;
+        const int e = it / H, h = it - e * H;
+        const float* q = QSs + edst[e] * XS + h * C + sub * cw;
+        const float* k = KVs + isrc[e] * XS + h * C + sub * cw;
+        for (int c = 0; c < cw; c += 4) {
+          const float4 x = *reinterpret_cast<const float4*>(q + c);
+          const float4 y = *reinterpret_cast<const float4*>(k + c);
+          dot += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+        }
+      }
+      if (SPL == 4) {
+        dot += __shfl_xor(dot, 1);
+        dot += __shfl_xor(dot, 2);
+      }
+      if (idx < nit && idx == it * SPL) LOG[it] = dot / a.sqrt_c;
+    }
+    __syncthreads();
+    // (S) softmax over each destination's in-edges per head (PyG softmax: exp(l - max) /
+    //     (sum + 1e-16)); alpha -> HBM for backward, alpha * dropout mask -> LDS
+    for (int idx = tid; idx < nrow * H; idx += CONV_BLOCK) {
+      const int i = idx / H, h = idx - i * H;
+      const int e0 = iptr[i], e1 = iptr[i + 1];
+      float m = -INFINITY;
+      for (int e = e0; e < e1; ++e) m = fmaxf(m, LOG[e * H + h]);
+      float z = 0.0f;
+      for (int e = e0; e < e1; ++e) z += expf(LOG[e * H + h] - m);
+      const float zd = z + 1e-16f;
+      for (int e = e0; e < e1; ++e) {
+        const int eg = (e + e_lo) * H + h;
+        const float al = expf(LOG[e * H + h] - m) / zd;
+        a.alpha[eg] = al;
+        LOG[e * H + h] = al * dr.mul(st_attn, (uint32_t)eg);
+      }
+    }
+    __syncthreads();
+    // (G) aggregation + beta gate: TPR lanes per row, CH features each
+    float ag[CH], sv[CH];
+    float u = 0.0f;
+    const bool live = prow < nrow;
+    if (live) {
+      const int hd = f0 / C;
+#pragma unroll
+      for (int c = 0; c < CH; ++c) ag[c] = 0.0f;
+      const int e1 = iptr[prow + 1];
+      for (int e = iptr[prow]; e < e1; ++e) {
+        const float ad = LOG[e * H + hd];
+        const float* vr = KVs + RMAX * XS + isrc[e] * XS + f0;
+#pragma unroll
+        for (int c = 0; c < CH; c += 4) {
+          const float4 v = *reinterpret_cast<const float4*>(vr + c);
+          ag[c] += ad * v.x; ag[c + 1] += ad * v.y; ag[c + 2] += ad * v.z; ag[c + 3] += ad * v.w;
+        }
+      }
+      const float* srow = QSs + RMAX * XS + prow * XS + f0;
+#pragma unroll
+      for (int c = 0; c < CH; c += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(srow + c);
+        sv[c] = v.x; sv[c + 1] = v.y; sv[c + 2] = v.z; sv[c + 3] = v.w;
+      }
+#pragma unroll
+      for (int c = 0; c < CH; ++c) u += w1c[c] * ag[c] + w2c[c] * sv[c] + w3c[c] * (ag[c] - sv[c]);
+    }
+#pragma unroll
+    for (int o = 1; o < TPR; o <<= 1) u += __shfl_xor(u, o);
+    if (live) {
+      const float beta = 1.0f / (1.0f + expf(-u));
+      const size_t ro = (size_t)(r0 + prow) * D + f0;
+#pragma unroll
+      for (int c = 0; c < CH; c += 4) {
+        float4 o4;
+        o4.x = beta * sv[c] + (1.0f - beta) * ag[c];
+        o4.y = beta * sv[c + 1] + (1.0f - beta) * ag[c + 1];
+        o4.z = beta * sv[c + 2] + (1.0f - beta) * ag[c + 2];
+        o4.w = beta * sv[c + 3] + (1.0f - beta) * ag[c + 3];
+        *reinterpret_cast<float4*>(a.agg + ro + c) = make_float4(ag[c], ag[c + 1], ag[c + 2], ag[c + 3]);
+        *reinterpret_cast<float4*>(a.out + ro + c) = o4;
+        *reinterpret_cast<float4*>(XO + prow * XS + f0 + c) = o4;
+      }
+      if (pchunk == 0) a.gate[r0 + prow] = beta;
+    }
   } else {
     for (int t = r0 + wave; t < r1; t += CONV_WAVES)
       attn_row<D>(a, t, t, a.qkvs, a.qkvs + 3 * D, a.qkvs + D, a.qkvs + 2 * D, 4 * D, a.bt.in_ptr, a.bt.in_src, 0,
@@ -322,9 +440,9 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
 
   // ---- phase S: this group's BatchNorm partial (count, mean, M2); slices of rows per thread
   __syncthreads();
+  GTR_PH(a.layer, 3);
   constexpr int NS = CONV_BLOCK / D >= 1 ? CONV_BLOCK / D : 1;
-  float* red = XO + RMAX * XS - (NS + 1) * D;  // scratch: tail of XO is past the group's rows
-  if (!fast || nrow * XS > RMAX * XS - (NS + 1) * D) red = sm + G::F_PE;  // PE region is free after the prologue
+  float* red = LOG;  // scratch: the logits are consumed
   float* part = a.bn_part + (size_t)g * (1 + 2 * D);
   {
     const int j = tid % D, sl = tid / D;
@@ -360,15 +478,16 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
     }
     if (tid == 0) part[0] = (float)nrow;
   }
+  GTR_PH(a.layer, 4);
+  GTR_PH_CLK(a.layer, 7);
   if (a.cred) return;  // the consuming kernel reduces the partials
   if (!arrive_last(a.cnt, (uint32_t)Gn, s_flag)) return;
-  bn_stats_from_parts<D, CONV_BLOCK>(a.bn_part, Gn, a.bn_eps, s_bn, s_bn + D, red);
-  __syncthreads();
+  bn_stats_from_parts<D, CONV_BLOCK>(a.bn_part, Gn, a.bn_eps, s_bn, s_bn + D, XO, red);
   for (int j = tid; j < D; j += CONV_BLOCK) {
     a.bn_stats[j] = s_bn[j];
     a.bn_stats[D + j] = s_bn[D + j];
     a.bn_rmean[j] = (1.0f - a.bn_mom) * a.bn_rmean[j] + a.bn_mom * s_bn[j];
-    a.bn_rvar[j] = (1.0f - a.bn_mom) * a.bn_rvar[j] + a.bn_mom * red[j];
+    a.bn_rvar[j] = (1.0f - a.bn_mom) * a.bn_rvar[j] + a.bn_mom * XO[j];
   }
   if (tid == 0) {
     reset_counter(a.cnt);
@@ -412,10 +531,12 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_readout(ReadoutK a) {
   constexpr int NB = 8;   // node rows in flight per wave
   constexpr int NK = 8;   // negative rows in flight per wave
   __shared__ float s_bn[3 * D];
+  __shared__ float s_scr[2 * GTR_BLOCK + D];
   __shared__ float s_red[GTR_WAVES][2 * D];
   __shared__ float s_loss[GTR_WAVES][2];
   __shared__ int s_flag;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  GTR_PH(16, 0);
   const int B = a.bt.hdr[1];
   const int n = a.bt.n_neg;
   const int d0 = lane * VPL;
@@ -434,11 +555,12 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_readout(ReadoutK a) {
 
   if (do_fwd) {
     prev_bn_stats<D, GTR_BLOCK>(a.train, a.cred, a.bt.hdr[4], a.part, a.stats, a.rmean, a.rvar, a.nbt, a.bn_eps,
-                                a.bn_mom, s_bn, s_bn + D, s_bn + 2 * D);
+                                a.bn_mom, s_bn, s_bn + D, s_bn + 2 * D, s_scr);
   } else if (do_bwd) {
     for (int j = tid; j < D; j += GTR_BLOCK) { s_bn[j] = a.stats[j]; s_bn[D + j] = a.stats[D + j]; }
   }
   __syncthreads();
+  GTR_PH(16, 1);
   float bm[VPL], br[VPL], bg[VPL], bb[VPL];
   if (do_fwd || do_bwd) {
 #pragma unroll
@@ -605,6 +727,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_readout(ReadoutK a) {
     }
   }
 
+  GTR_PH(16, 2);
   if (!(do_loss || do_bwd)) return;
   // ---- block partials (loss partials pre-scaled by the mean normalisers) in fixed order
   if (lane == 0) { s_loss[wave][0] = lw_sum * (w_lw * inv_b); s_loss[wave][1] = bpr_sum * (w_bpr * inv_bn); }
@@ -625,6 +748,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_readout(ReadoutK a) {
       a.gpart[(size_t)blockIdx.x * 2 * D + j] = acc;
     }
   }
+  GTR_PH(16, 3);
   if (!a.fin) return;  // loss summed by gtr_step_end, BN sums reduced by the consuming conv_bwd
   if (!arrive_last(a.cnt, gridDim.x, &s_flag)) return;
   if (do_loss && tid == 0) {
@@ -666,6 +790,8 @@ void drop_params(const gtr_config* c, uint32_t& thresh, float& scale, int& on) {
 }
 
 }  // namespace
+
+GTR_PH_READER(gtr_dbg_fwd_phases)
 
 extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_embed* emb,
                             const gtr_layer* layers, int l, gtr_stream_t stream) {

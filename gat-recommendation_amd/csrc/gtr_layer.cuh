@@ -22,30 +22,36 @@ struct LayerGeom {
   static constexpr int XS = D + 4;                     // padded LDS row (16B aligned)
   static constexpr int EMAX = 1024;                    // edges of a group staged in LDS
   static constexpr int KPE = 16;                       // LapPE width staged in LDS
-  // ---- forward LDS carve (4-byte words)
+  static constexpr int EH = 4096;                      // (edge, head) pairs of a group staged in LDS
+  static constexpr int TPR = CONV_BLOCK / RMAX;        // threads per row in the row-parallel phases
+  static constexpr int CH = D / TPR;                   // features per thread in those phases
+  // ---- forward LDS carve (4-byte words); row arrays use the padded stride XS
   static constexpr int F_XO = 0;                              // [RMAX][XS]   X rows, then OUT rows
-  static constexpr int F_KV = F_XO + RMAX * XS;               // [2][RMAX][D] K rows | V rows
-  static constexpr int F_QS = F_KV + (KV ? 2 * RMAX * D : 0); // [2][RMAX][D] Q rows | S rows
-  static constexpr int F_PE = F_QS + (KV ? 2 * RMAX * D : 0); // [D][KPE] Wpe | [RMAX][KPE] P rows
-  static constexpr int F_BN = F_PE + (D + RMAX) * KPE;        // [2D] previous BN mean | rstd
+  static constexpr int F_KV = F_XO + RMAX * XS;               // [2][RMAX][XS] K rows | V rows
+  static constexpr int F_QS = F_KV + (KV ? 2 * RMAX * XS : 0);// [2][RMAX][XS] Q rows | S rows
+  static constexpr int F_PE = F_QS + (KV ? 2 * RMAX * XS : 0);// [D][KPE] Wpe | [RMAX][KPE] P rows
+  static constexpr int F_LOG = F_PE + (D + RMAX) * KPE;       // [EH] logits -> alpha*mask; scratch
+  static constexpr int F_BN = F_LOG + EH;                     // [2D] previous BN mean | rstd
   static constexpr int F_ITEMS = F_BN + 2 * D;                // [RMAX] node items
   static constexpr int F_IPTR = F_ITEMS + RMAX;               // [RMAX+1] local in_ptr
   static constexpr int F_ISRC = F_IPTR + RMAX + 4;            // [EMAX] local in_src
-  static constexpr int F_FLAG = F_ISRC + EMAX;
+  static constexpr int F_EDST = F_ISRC + EMAX;                // [EMAX] local dst of each in-edge
+  static constexpr int F_FLAG = F_EDST + EMAX;
   static constexpr int F_WORDS = F_FLAG + 4;
   // ---- backward LDS carve (4-byte words)
-  static constexpr int AS = 4 * D + 4;                        // dQKVS staging row for dX
-  static constexpr int B_R1N = (2 * RMAX * D > 16 * AS) ? 2 * RMAX * D : 16 * AS;
-  static constexpr int B_R1 = 0;                              // K|V rows, then Q|dA rows, then dQKVS tile
-  static constexpr int B_ALPHA = B_R1 + B_R1N;                // [EMAX*8] alpha of group edges
-  static constexpr int B_DLOG = B_ALPHA + EMAX * 8;           // [EMAX*8] dlogit of group edges
-  static constexpr int B_IPTR = B_DLOG + EMAX * 8;            // [RMAX+1]
-  static constexpr int B_ISRC = B_IPTR + RMAX + 4;            // [EMAX]
-  static constexpr int B_OPTR = B_ISRC + EMAX;                // [RMAX+1]
+  static constexpr int B_RN = KV ? 4 * RMAX * XS : 0;
+  static constexpr int B_R = 0;                               // [4][RMAX][XS] K | V | Q | dA rows
+  static constexpr int B_AL = B_R + B_RN;                     // [EH] alpha -> alpha * mask
+  static constexpr int B_DL = B_AL + EH;                      // [EH] da -> dlogit
+  static constexpr int B_IPTR = B_DL + EH;                    // [RMAX+1] local in_ptr
+  static constexpr int B_ISRC = B_IPTR + RMAX + 4;            // [EMAX] local in_src
+  static constexpr int B_EDST = B_ISRC + EMAX;                // [EMAX] local dst of each in-edge
+  static constexpr int B_OPTR = B_EDST + EMAX;                // [RMAX+1] local out_ptr
   static constexpr int B_OEDGE = B_OPTR + RMAX + 4;           // [EMAX] local dst-order position
   static constexpr int B_ODST = B_OEDGE + EMAX;               // [EMAX] local dst row
   static constexpr int B_GS = B_ODST + EMAX;                  // [2D] reduced BN backward sums
-  static constexpr int B_FLAG = B_GS + 2 * D;
+  static constexpr int B_BNP = B_GS + 2 * D;                  // [CONV_WAVES][2D] dX-epilogue BN partials
+  static constexpr int B_FLAG = B_BNP + CONV_WAVES * 2 * D;
   static constexpr int B_WORDS = B_FLAG + 4;
 };
 
@@ -84,31 +90,56 @@ __device__ __forceinline__ void store_vec(float* p, const float (&x)[VPL], bool 
 }
 
 // Consumer-side BatchNorm statistics: combine G per-group (count, mean, M2) partials
-// (layout [G][1+2D]) into mean / rstd; thread per feature, fixed order (deterministic).
+// (layout [G][1+2D]) into mean / rstd / unbiased var.  BLK/D slices of the groups are
+// folded in parallel (Chan's parallel-variance formula), then combined in fixed order
+// (deterministic).  scr: >= 2*BLK + D floats of LDS.  Call with the whole block.
 template <int D, int BLK>
 __device__ __forceinline__ void bn_stats_from_parts(const float* part, int G, float eps, float* s_mean,
-                                                    float* s_rstd, float* s_uvar) {
-  for (int j = threadIdx.x; j < D; j += BLK) {
-    double n = 0.0, sum = 0.0;
-#pragma unroll 8
-    for (int q = 0; q < G; ++q) {
+                                                    float* s_rstd, float* s_uvar, float* scr) {
+  constexpr int NSL = BLK / D >= 1 ? BLK / D : 1;
+  const int tid = threadIdx.x;
+  const int j = tid % D, sl = tid / D;
+  float* s_sum = scr;              // [NSL][D]
+  float* s_n = scr + NSL * D;      // [NSL][D] (the count repeated per feature)
+  float* s_mu = scr + 2 * NSL * D; // [D]
+  if (sl < NSL) {
+    float n = 0.0f, sum = 0.0f;
+    for (int q = sl; q < G; q += NSL) {
       const float* pp = part + (size_t)q * (1 + 2 * D);
-      n += (double)pp[0];
-      sum += (double)pp[0] * (double)pp[1 + j];
+      const float c = pp[0];
+      n += c;
+      sum += c * pp[1 + j];
     }
-    const double mean = sum / n;
-    double m2 = 0.0;
-#pragma unroll 8
-    for (int q = 0; q < G; ++q) {
-      const float* pp = part + (size_t)q * (1 + 2 * D);
-      const double d = (double)pp[1 + j] - mean;
-      m2 += (double)pp[1 + D + j] + (double)pp[0] * d * d;
-    }
-    const float var = (float)(m2 / n);
-    s_mean[j] = (float)mean;
-    s_rstd[j] = 1.0f / sqrtf(var + eps);
-    s_uvar[j] = n > 1.0 ? (float)(m2 / (n - 1.0)) : var;
+    s_sum[sl * D + j] = sum;
+    s_n[sl * D + j] = n;
   }
+  __syncthreads();
+  if (tid < D) {
+    float n = 0.0f, sum = 0.0f;
+    for (int q = 0; q < NSL; ++q) { n += s_n[q * D + tid]; sum += s_sum[q * D + tid]; }
+    s_mu[tid] = sum / n;
+  }
+  __syncthreads();
+  if (sl < NSL) {
+    const float mean = s_mu[j];
+    float m2 = 0.0f;
+    for (int q = sl; q < G; q += NSL) {
+      const float* pp = part + (size_t)q * (1 + 2 * D);
+      const float d = pp[1 + j] - mean;
+      m2 += pp[1 + D + j] + pp[0] * d * d;
+    }
+    s_sum[sl * D + j] = m2;
+  }
+  __syncthreads();
+  if (tid < D) {
+    float n = 0.0f, m2 = 0.0f;
+    for (int q = 0; q < NSL; ++q) { n += s_n[q * D + tid]; m2 += s_sum[q * D + tid]; }
+    const float var = m2 / n;
+    s_mean[tid] = s_mu[tid];
+    s_rstd[tid] = 1.0f / sqrtf(var + eps);
+    s_uvar[tid] = n > 1.0f ? m2 / (n - 1.0f) : var;
+  }
+  __syncthreads();
 }
 
 // Dynamic LDS above 64 KiB needs the per-kernel limit raised once (gfx950: 160 KiB per CU).

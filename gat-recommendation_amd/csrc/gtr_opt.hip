@@ -46,37 +46,39 @@ struct SmallK {
   gtr_segment segs[GTR_SMALL_MAX_SEG];
 };
 
-__global__ __launch_bounds__(GTR_BLOCK) void k_adamw_small(SmallK a) {
-  __shared__ AdamStep s_st;
-  const int64_t e = (int64_t)blockIdx.x * GTR_BLOCK + threadIdx.x;
-  if (a.grad_out == nullptr && threadIdx.x == 0) s_st.init(a.opt, *a.opt.step_dev + 1);
-  __syncthreads();
+// Small parameters: element e of the flat buffer; its segment's gradient partials summed.
+__device__ __forceinline__ void small_body(int64_t e, const gtr_segment* segs, int nseg, float* param, float* m,
+                                           float* v, float* grad_out, const AdamStep& st) {
   int s = -1;
-  for (int i = 0; i < a.nseg; ++i)
-    if (e >= a.segs[i].begin && e < a.segs[i].begin + a.segs[i].len) s = i;
+  for (int i = 0; i < nseg; ++i)
+    if (e >= segs[i].begin && e < segs[i].begin + segs[i].len) s = i;
   if (s < 0) return;
-  const gtr_segment& sg = a.segs[s];
+  const gtr_segment& sg = segs[s];
   const int64_t off = e - sg.begin;
   float g = 0.0f;
   for (int p = 0; p < sg.nparts; ++p) g += sg.src[(int64_t)p * sg.pstride + off];
-  if (a.grad_out) {
-    a.grad_out[e] = g;
+  if (grad_out) {
+    grad_out[e] = g;
     return;
   }
-  const AdamStep st = s_st;
-  float pv = a.param[e], mv = a.m[e], vv = a.v[e];
+  float pv = param[e], mv = m[e], vv = v[e];
   st.apply(pv, mv, vv, g);
-  a.param[e] = pv;
-  a.m[e] = mv;
-  a.v[e] = vv;
+  param[e] = pv;
+  m[e] = mv;
+  v[e] = vv;
 }
 
-__global__ __launch_bounds__(GTR_BLOCK) void k_contrib_prep(gtr_batch bt, int T, int32_t* keys, int32_t* vals,
-                                                            int32_t* stamp, const int64_t* step_dev) {
-  const int j = blockIdx.x * GTR_BLOCK + threadIdx.x;
-  const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
-  if (j >= m_cap) return;
-  const int N = bt.hdr[0], B = bt.hdr[1];
+__global__ __launch_bounds__(GTR_BLOCK) void k_adamw_small(SmallK a) {
+  __shared__ AdamStep s_st;
+  const int64_t e = (int64_t)blockIdx.x * GTR_BLOCK + threadIdx.x;
+  if (a.grad_out == nullptr && threadIdx.x == 0) s_st.init(a.opt, *a.opt.step_dev + a.opt.step_offset);
+  __syncthreads();
+  const AdamStep st = s_st;
+  small_body(e, a.segs, a.nseg, a.param, a.m, a.v, a.grad_out, st);
+}
+
+// Contribution key of slot j (sentinel T for unused slots), see gtr_contrib_prep.
+__device__ __forceinline__ int contrib_key(const gtr_batch& bt, int T, int j, int N, int B) {
   int key = T;
   if (j < bt.n_cap) {
     if (j < N) key = bt.node_item[j];
@@ -88,6 +90,15 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_contrib_prep(gtr_batch bt, int T,
     if (q / bt.n_neg < B) key = bt.negatives[q];
   }
   if (key < 0 || key > T) key = T;
+  return key;
+}
+
+__global__ __launch_bounds__(GTR_BLOCK) void k_contrib_prep(gtr_batch bt, int T, int32_t* keys, int32_t* vals,
+                                                            int32_t* stamp, const int64_t* step_dev) {
+  const int j = blockIdx.x * GTR_BLOCK + threadIdx.x;
+  const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
+  if (j >= m_cap) return;
+  const int key = contrib_key(bt, T, j, bt.hdr[0], bt.hdr[1]);
   keys[j] = key;
   vals[j] = j;
   if (stamp && key > 0 && key < T) stamp[key] = (int32_t)(*step_dev + 1);
@@ -97,17 +108,12 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_contrib_prep(gtr_batch bt, int T,
 // fetched up front (they depend only on the key), the segment's contributions are
 // summed in sorted (stable) order, then AdamW — or the dense gradient is written.
 template <int D>
-__global__ __launch_bounds__(GTR_BLOCK) void k_adamw_rows(gtr_batch bt, int T, const int32_t* skeys,
-                                                          const int32_t* svals, const float* dx0,
-                                                          const float* se, const float* coef_tgt,
-                                                          const float* coef_neg, float* table, float* m,
-                                                          float* v, float* grad_dense, gtr_adam opt) {
+__device__ __forceinline__ void rows_body(int gid, const gtr_batch& bt, int T, const int32_t* skeys,
+                                          const int32_t* svals, const float* dx0, const float* se,
+                                          const float* coef_tgt, const float* coef_neg, float* table, float* m,
+                                          float* v, float* grad_dense, const AdamStep& st) {
   constexpr int C4 = D / 4;
-  __shared__ AdamStep s_st;
-  if (grad_dense == nullptr && threadIdx.x == 0) s_st.init(opt, *opt.step_dev + 1);
-  __syncthreads();
   const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
-  const int gid = blockIdx.x * GTR_BLOCK + threadIdx.x;
   const int i = gid / C4, c = gid - (gid / C4) * C4;
   if (i >= m_cap) return;
   const int key = skeys[i];
@@ -146,7 +152,6 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_adamw_rows(gtr_batch bt, int T, c
     reinterpret_cast<float4*>(grad_dense)[base] = g;
     return;
   }
-  const AdamStep st = s_st;
   st.apply(pv.x, mv.x, vv.x, g.x);
   st.apply(pv.y, mv.y, vv.y, g.y);
   st.apply(pv.z, mv.z, vv.z, g.z);
@@ -156,21 +161,29 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_adamw_rows(gtr_batch bt, int T, c
   reinterpret_cast<float4*>(v)[base] = vv;
 }
 
-// Untouched rows: 16 B per thread per tensor, grid-stride; rows with stamp == step+1 skipped.
-__global__ __launch_bounds__(GTR_BLOCK) void k_adamw_sweep(int64_t nvec, int vpr_log2, const int32_t* stamp,
-                                                           float4* table, float4* m, float4* v, gtr_adam opt) {
+// Touched rows: one thread per (segment start, float4 column).  p/m/v of the row are
+// fetched up front (they depend only on the key), the segment's contributions are
+// summed in sorted (stable) order, then AdamW — or the dense gradient is written.
+template <int D>
+__global__ __launch_bounds__(GTR_BLOCK) void k_adamw_rows(gtr_batch bt, int T, const int32_t* skeys,
+                                                          const int32_t* svals, const float* dx0,
+                                                          const float* se, const float* coef_tgt,
+                                                          const float* coef_neg, float* table, float* m,
+                                                          float* v, float* grad_dense, gtr_adam opt) {
   __shared__ AdamStep s_st;
-  __shared__ int32_t s_t;
-  if (threadIdx.x == 0) {
-    const int64_t t = *opt.step_dev + 1;
-    s_st.init(opt, t);
-    s_t = (int32_t)t;
-  }
+  if (grad_dense == nullptr && threadIdx.x == 0) s_st.init(opt, *opt.step_dev + opt.step_offset);
   __syncthreads();
   const AdamStep st = s_st;
-  const int32_t t = s_t;
-  const int64_t stride = (int64_t)gridDim.x * GTR_BLOCK;
-  for (int64_t i = (int64_t)blockIdx.x * GTR_BLOCK + threadIdx.x; i < nvec; i += stride) {
+  rows_body<D>(blockIdx.x * GTR_BLOCK + threadIdx.x, bt, T, skeys, svals, dx0, se, coef_tgt, coef_neg, table, m, v,
+               grad_dense, st);
+}
+
+// Untouched rows: 16 B per thread per tensor, grid-stride over nblk blocks; rows with
+// stamp == t (touched this step) skipped.
+__device__ __forceinline__ void sweep_body(int blk, int nblk, int64_t nvec, int vpr_log2, const int32_t* stamp,
+                                           int32_t t, float4* table, float4* m, float4* v, const AdamStep& st) {
+  const int64_t stride = (int64_t)nblk * GTR_BLOCK;
+  for (int64_t i = (int64_t)blk * GTR_BLOCK + threadIdx.x; i < nvec; i += stride) {
     const int64_t row = i >> vpr_log2;
     if (stamp[row] == t) continue;
     float4 p = table[i], mm = m[i], vv = v[i];
@@ -182,6 +195,119 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_adamw_sweep(int64_t nvec, int vpr
     m[i] = mm;
     v[i] = vv;
   }
+}
+
+__global__ __launch_bounds__(GTR_BLOCK) void k_adamw_sweep(int64_t nvec, int vpr_log2, const int32_t* stamp,
+                                                           float4* table, float4* m, float4* v, gtr_adam opt) {
+  __shared__ AdamStep s_st;
+  __shared__ int32_t s_t;
+  if (threadIdx.x == 0) {
+    const int64_t t = *opt.step_dev + opt.step_offset;
+    s_st.init(opt, t);
+    s_t = (int32_t)t;
+  }
+  __syncthreads();
+  const AdamStep st = s_st;
+  sweep_body(blockIdx.x, gridDim.x, nvec, vpr_log2, stamp, s_t, table, m, v, st);
+}
+
+// ---- fused step: begin (counters, stamps, sorted contribution list) -------------------
+#define GTR_BEGIN_BLOCK 1024
+#define GTR_BEGIN_MCAP 4096
+
+// One workgroup: composite keys (row << 12 | slot) are unique, so the stable order is
+// the plain order of the composites; each slot's rank = #composites below it
+// (broadcast LDS reads, no atomics, deterministic).
+__global__ __launch_bounds__(GTR_BEGIN_BLOCK) void k_step_begin_small(gtr_batch bt, int T, int32_t* skeys,
+                                                                     int32_t* svals, int32_t* stamp,
+                                                                     int64_t* step_dev, uint32_t* rng_ctr) {
+  __shared__ __attribute__((aligned(16))) uint32_t ck[GTR_BEGIN_MCAP];
+  const int tid = threadIdx.x;
+  const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
+  const int m4 = (m_cap + 3) & ~3;
+  const int N = bt.hdr[0], B = bt.hdr[1];
+  const int32_t tnew = (int32_t)(*step_dev + 1);
+  for (int j = tid; j < m4; j += GTR_BEGIN_BLOCK) {
+    uint32_t c = 0xFFFFFFFFu;
+    if (j < m_cap) {
+      const int key = contrib_key(bt, T, j, N, B);
+      c = ((uint32_t)key << 12) | (uint32_t)j;
+      if (stamp && key > 0 && key < T) stamp[key] = tnew;
+    }
+    ck[j] = c;
+  }
+  __syncthreads();
+  for (int j = tid; j < m_cap; j += GTR_BEGIN_BLOCK) {
+    const uint32_t mine = ck[j];
+    int rank = 0;
+    for (int i = 0; i < m4; i += 4) {
+      const uint4 q = *reinterpret_cast<const uint4*>(ck + i);
+      rank += (q.x < mine) + (q.y < mine) + (q.z < mine) + (q.w < mine);
+    }
+    skeys[rank] = (int32_t)(mine >> 12);
+    svals[rank] = (int32_t)(mine & 0xFFFu);
+  }
+  if (tid == 0) {
+    *step_dev = tnew;
+    if (rng_ctr) *rng_ctr += 1;
+  }
+}
+
+__global__ void k_counters(int64_t* step_dev, uint32_t* rng_ctr) {
+  if (step_dev) *step_dev += 1;
+  if (rng_ctr) *rng_ctr += 1;
+}
+
+// ---- fused step: tail (touched rows | small parameters | untouched rows) ---------------
+struct TailK {
+  gtr_batch bt;
+  gtr_tail tl;
+  gtr_adam opt;
+  int T, nb_rows, nb_small, nb_sweep;
+  int64_t nvec;
+  int vpr_log2, nseg;
+  gtr_segment segs[GTR_SMALL_MAX_SEG];
+};
+
+template <int D>
+__global__ __launch_bounds__(GTR_BLOCK) void k_step_tail(TailK a) {
+  __shared__ AdamStep s_st;
+  __shared__ int32_t s_t;
+  __shared__ float s_acc[GTR_BLOCK];
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    const int64_t t = *a.opt.step_dev + a.opt.step_offset;
+    s_st.init(a.opt, t);
+    s_t = (int32_t)t;
+  }
+  __syncthreads();
+  const AdamStep st = s_st;
+  const int blk = blockIdx.x;
+  if (blk < a.nb_rows) {
+    rows_body<D>(blk * GTR_BLOCK + tid, a.bt, a.T, a.tl.skeys, a.tl.svals, a.tl.dx0, a.tl.se, a.tl.coef_tgt,
+                 a.tl.coef_neg, a.tl.table, a.tl.table_m, a.tl.table_v, nullptr, st);
+    return;
+  }
+  if (blk < a.nb_rows + a.nb_small) {
+    const int sb = blk - a.nb_rows;
+    small_body((int64_t)sb * GTR_BLOCK + tid, a.segs, a.nseg, a.tl.flat, a.tl.flat_m, a.tl.flat_v, nullptr, st);
+    if (sb == 0 && a.tl.loss_part) {  // loss of the step: the readout's partials, fixed order
+      float acc = 0.0f;
+      for (int q = tid; q < a.tl.loss_nparts; q += GTR_BLOCK)
+        acc += a.tl.loss_part[(size_t)q * 2] + a.tl.loss_part[(size_t)q * 2 + 1];
+      s_acc[tid] = acc;
+      __syncthreads();
+      if (tid == 0) {
+        float t = 0.0f;
+        for (int q = 0; q < GTR_BLOCK; ++q) t += s_acc[q];
+        a.tl.loss_out[0] = t;
+      }
+    }
+    return;
+  }
+  sweep_body(blk - a.nb_rows - a.nb_small, a.nb_sweep, a.nvec, a.vpr_log2, a.tl.stamp, s_t,
+             reinterpret_cast<float4*>(a.tl.table), reinterpret_cast<float4*>(a.tl.table_m),
+             reinterpret_cast<float4*>(a.tl.table_v), st);
 }
 
 template <int D>
@@ -389,6 +515,73 @@ int gtr_scatter_rows(const gtr_batch* bt, int dim, int mode, const float* src, c
     case 64: hipLaunchKernelGGL(k_scatter_rows<64>, dim3(blocks), dim3(GTR_BLOCK), 0, s, *bt, mode, src, coef_tgt, coef_neg, dense); break;
     case 128: hipLaunchKernelGGL(k_scatter_rows<128>, dim3(blocks), dim3(GTR_BLOCK), 0, s, *bt, mode, src, coef_tgt, coef_neg, dense); break;
     default: hipLaunchKernelGGL(k_scatter_rows<256>, dim3(blocks), dim3(GTR_BLOCK), 0, s, *bt, mode, src, coef_tgt, coef_neg, dense); break;
+  }
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+int gtr_step_begin(const gtr_batch* bt, int num_items, int32_t* keys, int32_t* vals, int32_t* skeys,
+                   int32_t* svals, int32_t* stamp, int64_t* step_dev, uint32_t* rng_ctr, void* tmp,
+                   size_t tmp_bytes, gtr_stream_t stream) {
+  if (!bt || !skeys || !svals || !step_dev || bt->n_neg <= 0 || num_items <= 0) {
+    set_error("gtr_step_begin: bad arguments");
+    return GTR_E_ARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int m_cap = bt->n_cap + bt->b_cap * (1 + bt->n_neg);
+  if (m_cap <= GTR_BEGIN_MCAP && num_items < (1 << 20)) {
+    hipLaunchKernelGGL(k_step_begin_small, dim3(1), dim3(GTR_BEGIN_BLOCK), 0, s, *bt, num_items, skeys, svals, stamp,
+                       step_dev, rng_ctr);
+    GTR_HIP_CHECK_LAUNCH();
+    return GTR_OK;
+  }
+  if (!keys || !vals || !tmp) { set_error("gtr_step_begin: large batch needs keys/vals/tmp scratch"); return GTR_E_ARG; }
+  int rc = gtr_contrib_prep(bt, num_items, keys, vals, stamp, step_dev, stream);
+  if (rc) return rc;
+  rc = gtr_contrib_sort(keys, vals, skeys, svals, m_cap, num_items, tmp, tmp_bytes, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_counters, dim3(1), dim3(1), 0, s, step_dev, rng_ctr);
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+int gtr_step_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tail, const gtr_segment* segs,
+                  int nseg, const gtr_adam* opt, gtr_stream_t stream) {
+  if (!bt || !tail || !opt || !opt->step_dev || !dim_ok(dim) || num_items <= 0 || nseg < 0 ||
+      nseg > GTR_SMALL_MAX_SEG || (nseg > 0 && !segs)) {
+    set_error("gtr_step_tail: bad arguments");
+    return GTR_E_ARG;
+  }
+  const gtr_tail& t = *tail;
+  if (!t.skeys || !t.svals || !t.dx0 || !t.se || !t.coef_tgt || !t.coef_neg || !t.table || !t.table_m ||
+      !t.table_v || !t.stamp || (nseg > 0 && (!t.flat || !t.flat_m || !t.flat_v)) ||
+      (t.loss_part && (!t.loss_out || t.loss_nparts < 0))) {
+    set_error("gtr_step_tail: missing buffers");
+    return GTR_E_ARG;
+  }
+  TailK k{};
+  k.bt = *bt;
+  k.tl = t;
+  k.opt = *opt;
+  k.T = num_items;
+  const int m_cap = bt->n_cap + bt->b_cap * (1 + bt->n_neg);
+  k.nb_rows = (int)(((int64_t)m_cap * (dim / 4) + GTR_BLOCK - 1) / GTR_BLOCK);
+  k.nb_small = nseg > 0 ? (int)((t.flat_total + GTR_BLOCK - 1) / GTR_BLOCK) : 0;
+  if (k.nb_small == 0 && t.loss_part) k.nb_small = 1;
+  k.nvec = (int64_t)num_items * dim / 4;
+  k.vpr_log2 = 0;
+  while ((1 << k.vpr_log2) < dim / 4) ++k.vpr_log2;
+  int64_t sw = (k.nvec + GTR_BLOCK - 1) / GTR_BLOCK;
+  k.nb_sweep = (int)(sw > 2048 ? 2048 : sw);
+  k.nseg = nseg;
+  for (int i = 0; i < nseg; ++i) k.segs[i] = segs[i];
+  const int grid = k.nb_rows + k.nb_small + k.nb_sweep;
+  hipStream_t s = (hipStream_t)stream;
+  switch (dim) {
+    case 32: hipLaunchKernelGGL(k_step_tail<32>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    case 64: hipLaunchKernelGGL(k_step_tail<64>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    case 128: hipLaunchKernelGGL(k_step_tail<128>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    default: hipLaunchKernelGGL(k_step_tail<256>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
   }
   GTR_HIP_CHECK_LAUNCH();
   return GTR_OK;

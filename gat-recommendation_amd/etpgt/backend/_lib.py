@@ -71,7 +71,16 @@ class GtrSegment(C.Structure):
 class GtrAdam(C.Structure):
     _fields_ = [
         ("lr", f32), ("beta1", f32), ("beta2", f32), ("eps", f32), ("weight_decay", f32),
-        ("decoupled", i32), ("step_dev", P),
+        ("decoupled", i32), ("step_offset", i32), ("step_dev", P),
+    ]
+
+
+class GtrTail(C.Structure):
+    _fields_ = [
+        ("skeys", P), ("svals", P), ("dx0", P), ("se", P), ("coef_tgt", P), ("coef_neg", P),
+        ("table", P), ("table_m", P), ("table_v", P), ("stamp", P),
+        ("flat", P), ("flat_m", P), ("flat_v", P), ("flat_total", i64),
+        ("loss_part", P), ("loss_out", P), ("loss_nparts", i32), ("pad0", i32),
     ]
 
 
@@ -97,6 +106,8 @@ _SIGS = {
     "gtr_adamw_sweep": (C.c_int, [C.c_int, C.c_int, P, P, P, P, P, P]),
     "gtr_scatter_rows": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P]),
     "gtr_step_end": (C.c_int, [P, P, P, C.c_int, P, P]),
+    "gtr_step_begin": (C.c_int, [P, C.c_int, P, P, P, P, P, P, P, P, C.c_size_t, P]),
+    "gtr_step_tail": (C.c_int, [P, C.c_int, C.c_int, P, P, C.c_int, P, P]),
 }
 
 EXPORTS = tuple(_SIGS)

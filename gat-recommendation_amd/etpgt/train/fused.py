@@ -1,26 +1,25 @@
 """Fused training step: forward + loss + backward + (Adam|AdamW) in HIP kernels,
-optionally captured once into a hipGraph and replayed per batch.
+captured once into a hipGraph and replayed per batch.
 
 One step of ``Trainer.train_epoch`` (trainer.py:80-133) with
-``torch.optim.AdamW(lr, weight_decay)`` (train_baseline.py:252-256):
+``torch.optim.AdamW(lr, weight_decay)`` (train_baseline.py:252-256), as nine
+launches on one stream (the blob copy, then):
 
-  main stream:  conv_fwd(0..L-1) -> readout_loss(FWD|LOSS|BWD) -> conv_bwd(L-1..0)
-                -> wgrad -> [join] -> adamw_rows -> adamw_small -> [join] -> step_end
-  side stream 1: contrib_prep (keys + touched-row stamps) -> adamw_sweep (untouched rows)
-  side stream 2: contrib_sort (stable radix sort of the table-gradient contributions)
+  step_begin -> conv_fwd(0..L-1) -> readout_loss(FWD|LOSS|BWD) -> conv_bwd(L-1..0)
+  -> wgrad(all layers) -> step_tail
 
-The item table never gets a dense gradient: untouched rows take the g = 0 AdamW
-update (same arithmetic as the dense reference update, 24 B/element instead of
-32) concurrently with the forward/backward chain; touched rows are updated from
-their segment sums once the backward is done.  Optimizer state (exp_avg,
-exp_avg_sq, step) lives in this object; ``export_optimizer_state`` writes it back
-into a ``torch.optim.AdamW`` state_dict layout.
+step_begin advances the step / dropout counters, stamps the touched table rows and
+builds the sorted table-gradient contribution list; step_tail applies AdamW to the
+touched rows (segment sums of the contributions), to the untouched rows (g = 0: the
+same arithmetic as the dense reference update, 24 B/element instead of 32) and to
+every small parameter, and sums the loss.  The item table never gets a dense
+gradient.  Optimizer state (exp_avg, exp_avg_sq, step) lives in this object;
+``export_optimizer_state`` writes it into a ``torch.optim.AdamW`` state layout.
 """
 
 from __future__ import annotations
 
 import ctypes as C
-import os
 
 import torch
 
@@ -43,8 +42,6 @@ class FusedTrainStep:
         self.temperature = float(temperature)
         self.alpha = float(alpha)
         self.use_graph = use_graph
-        # experiment knob: run the untouched-row sweep after the chain instead of beside it
-        self.serial_sweep = os.environ.get("GTR_SERIAL_SWEEP", "1") == "1"
         eng = self.eng
         T, D = eng.T, eng.D
         self.adam = L.GtrAdam()
@@ -52,6 +49,7 @@ class FusedTrainStep:
         self.adam.eps, self.adam.weight_decay, self.adam.decoupled = float(eps), float(weight_decay), int(decoupled)
         self.step_dev = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self.adam.step_dev = self.step_dev.data_ptr()
+        self.adam.step_offset = 0  # kernels after gtr_step_begin see the current step
         self.m_tab = torch.zeros(T, D, dtype=torch.float32, device=self.dev)
         self.v_tab = torch.zeros(T, D, dtype=torch.float32, device=self.dev)
         self.m_flat = torch.zeros_like(eng.flat.flat)
@@ -86,9 +84,20 @@ class FusedTrainStep:
         self.sort_tmp = torch.zeros(max(int(nb.value), 16), dtype=torch.uint8, device=self.dev)
         self.segs, self.nseg = eng.segments(self.ws)
         self.cfg = eng.config(self.ws, True)
-        self.side1 = torch.cuda.Stream(self.dev)
-        self.side2 = torch.cuda.Stream(self.dev)
-        self.side3 = torch.cuda.Stream(self.dev)
+        ws = self.ws
+        t = L.GtrTail()
+        t.skeys, t.svals = self.skeys.data_ptr(), self.svals.data_ptr()
+        t.dx0, t.se = ws.dx0.data_ptr(), ws.se.data_ptr()
+        t.coef_tgt, t.coef_neg = ws.coef_tgt.data_ptr(), ws.coef_neg.data_ptr()
+        t.table = eng.model.item_embedding.weight.data_ptr()
+        t.table_m, t.table_v, t.stamp = self.m_tab.data_ptr(), self.v_tab.data_ptr(), self.stamp.data_ptr()
+        t.flat, t.flat_m, t.flat_v = eng.flat.flat.data_ptr(), self.m_flat.data_ptr(), self.v_flat.data_ptr()
+        t.flat_total = eng.flat.layout.total
+        # with consumer-side reduction the readout leaves its loss partials to the tail
+        t.loss_part = ws.loss_part.data_ptr() if self.cfg.consumer_reduce else None
+        t.loss_out = ws.loss_out.data_ptr()
+        t.loss_nparts = readout_grid(caps.b_cap)
+        self.tail = t
         self.graph = None
         self.graph_pe = None
 
@@ -125,50 +134,15 @@ class FusedTrainStep:
         lib = L.lib()
         ws, cfg = self.ws, self.cfg
         bs = self.bs_pe if with_pe else self.bs
-        main = torch.cuda.current_stream(self.dev)
-        ev0 = torch.cuda.Event()
-        ev0.record(main)
-        # side 1: keys/stamps -> sweep of untouched rows
-        self.side1.wait_event(ev0)
-        with torch.cuda.stream(self.side1):
-            s1 = self.side1.cuda_stream
-            L.check(lib.gtr_contrib_prep(C.byref(bs), eng.T, self.keys.data_ptr(), self.vals.data_ptr(),
-                                         self.stamp.data_ptr(), self.step_dev.data_ptr(), s1), "contrib_prep")
-            ev_prep = torch.cuda.Event()
-            ev_prep.record(self.side1)
-            if not self.serial_sweep:
-                self._sweep(s1)
-        # side 2: sort contributions by row
-        self.side2.wait_event(ev_prep)
-        with torch.cuda.stream(self.side2):
-            L.check(lib.gtr_contrib_sort(self.keys.data_ptr(), self.vals.data_ptr(), self.skeys.data_ptr(),
-                                         self.svals.data_ptr(), self.m_cap, eng.T, self.sort_tmp.data_ptr(),
-                                         self.sort_tmp.numel(), self.side2.cuda_stream), "contrib_sort")
-        # main: forward, loss, backward, weight gradients
+        st = torch.cuda.current_stream(self.dev).cuda_stream
+        L.check(lib.gtr_step_begin(C.byref(bs), eng.T, self.keys.data_ptr(), self.vals.data_ptr(),
+                                   self.skeys.data_ptr(), self.svals.data_ptr(), self.stamp.data_ptr(),
+                                   self.step_dev.data_ptr(), eng.rng_ctr.data_ptr(), self.sort_tmp.data_ptr(),
+                                   self.sort_tmp.numel(), st), "step_begin")
         eng.run_forward(ws, cfg, bs, L.RO_FWD | L.RO_LOSS | L.RO_BWD, self.loss_kind, self.temperature, self.alpha)
-        eng.run_backward(ws, cfg, bs, side=self.side3)
-        main.wait_stream(self.side3)
-        main.wait_stream(self.side2)
-        st = main.cuda_stream
-        L.check(lib.gtr_adamw_rows(C.byref(bs), eng.T, eng.D, self.skeys.data_ptr(), self.svals.data_ptr(),
-                                   ws.dx0.data_ptr(), ws.se.data_ptr(), ws.coef_tgt.data_ptr(), ws.coef_neg.data_ptr(),
-                                   eng.model.item_embedding.weight.data_ptr(), self.m_tab.data_ptr(),
-                                   self.v_tab.data_ptr(), None, C.byref(self.adam), st), "adamw_rows")
-        L.check(lib.gtr_adamw_small(eng.flat.flat.data_ptr(), self.m_flat.data_ptr(), self.v_flat.data_ptr(), None,
-                                    eng.flat.layout.total, self.segs, self.nseg, C.byref(self.adam), st), "adamw_small")
-        main.wait_stream(self.side1)
-        if self.serial_sweep:
-            self._sweep(st)
-        # with consumer-side reduction the readout leaves its loss partials to step_end
-        lp = ws.loss_part.data_ptr() if cfg.consumer_reduce else None
-        L.check(lib.gtr_step_end(self.step_dev.data_ptr(), eng.rng_ctr.data_ptr(), lp,
-                                 readout_grid(self.caps.b_cap), ws.loss_out.data_ptr(), st), "step_end")
-
-    def _sweep(self, stream_handle):
-        eng = self.eng
-        L.check(L.lib().gtr_adamw_sweep(eng.T, eng.D, self.stamp.data_ptr(), eng.model.item_embedding.weight.data_ptr(),
-                                        self.m_tab.data_ptr(), self.v_tab.data_ptr(), C.byref(self.adam),
-                                        stream_handle), "sweep")
+        eng.run_backward(ws, cfg, bs)
+        L.check(lib.gtr_step_tail(C.byref(bs), eng.T, eng.D, C.byref(self.tail), self.segs, self.nseg,
+                                  C.byref(self.adam), st), "step_tail")
 
     def capture(self, with_pe: bool = False):
         """Capture one step into a hipGraph (after one eager warm-up step)."""

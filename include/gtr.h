@@ -200,8 +200,11 @@ typedef struct gtr_segment {
 
 typedef struct gtr_adam {
   float lr, beta1, beta2, eps, weight_decay;
-  int32_t decoupled;          /* 1 = AdamW, 0 = Adam (L2 into the gradient) */
-  const int64_t* step_dev;    /* completed optimizer steps (device)          */
+  int32_t decoupled;          /* 1 = AdamW, 0 = Adam (L2 into the gradient)            */
+  int32_t step_offset;        /* the update is step t = *step_dev + step_offset:
+                                 1 when *step_dev counts completed steps (eager entry
+                                 points), 0 after gtr_step_begin advanced it           */
+  const int64_t* step_dev;    /* optimizer step counter (device)                       */
 } gtr_adam;
 
 #define GTR_SMALL_MAX_SEG 48
@@ -235,6 +238,43 @@ int gtr_adamw_sweep(int num_items, int dim, const int32_t* stamp, float* table, 
  * mode 0: node rows (src = dx0, coef 1); mode 1: score rows (src = se).       */
 int gtr_scatter_rows(const gtr_batch* bt, int dim, int mode, const float* src, const float* coef_tgt,
                      const float* coef_neg, float* dense, gtr_stream_t stream);
+
+/* ---- fused training step (etpgt.train.fused.FusedTrainStep) ------------------
+ * gtr_step_begin: advance the step (*step_dev += 1) and dropout-stream counters,
+ * stamp the touched table rows (stamp[row] = new step) and build the sorted
+ * contribution list skeys/svals (keys/vals/tmp: scratch for large batches, sized
+ * by gtr_contrib_sort_bytes).  One workgroup when m_cap <= 4096 and T < 2^20.    */
+int gtr_step_begin(const gtr_batch* bt, int num_items, int32_t* keys, int32_t* vals, int32_t* skeys,
+                   int32_t* svals, int32_t* stamp, int64_t* step_dev, uint32_t* rng_ctr, void* tmp,
+                   size_t tmp_bytes, gtr_stream_t stream);
+
+/* Inputs of the optimizer tail of a fused step.                                  */
+typedef struct gtr_tail {
+  const int32_t* skeys;   /* sorted contribution list (gtr_step_begin)             */
+  const int32_t* svals;
+  const float* dx0;       /* [n_cap, D] layer-0 input gradient                      */
+  const float* se;        /* [b_cap, D] session embeddings                          */
+  const float* coef_tgt;  /* [b_cap] d loss / d score(target)                        */
+  const float* coef_neg;  /* [b_cap*n] d loss / d score(negative)                    */
+  float* table;           /* [T, D] item table, its AdamW moments                    */
+  float* table_m;
+  float* table_v;
+  const int32_t* stamp;   /* [T] last step each row was touched                     */
+  float* flat;            /* flat small-parameter buffer + moments                   */
+  float* flat_m;
+  float* flat_v;
+  int64_t flat_total;
+  const float* loss_part; /* [loss_nparts, 2] pre-scaled loss partials (or NULL)     */
+  float* loss_out;        /* [1] loss of the step                                   */
+  int32_t loss_nparts;
+  int32_t pad0;
+} gtr_tail;
+
+/* One launch: AdamW of the touched table rows (segmented sums), of the untouched
+ * rows (zero gradient) and of every small parameter (segments), plus the loss sum.
+ * opt->step_offset must be 0 (runs after gtr_step_begin).                        */
+int gtr_step_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tail,
+                  const gtr_segment* segs, int nseg, const gtr_adam* opt, gtr_stream_t stream);
 
 /* step_dev += 1 (if non-NULL); rng_ctr += 1 (if non-NULL); if loss_part != NULL,
  * loss_out[0] = sum of the 2*nparts (already scaled) loss partials in order.     */
