@@ -648,8 +648,7 @@ extern "C" int gtr_conv_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   // partials feeding this layer's sums: the readout grid for the last layer, else the conv groups
   k.gpart_n = -1;
   if (l == cfg->num_layers - 1) {
-    int rg = (bt->b_cap + GTR_WAVES - 1) / GTR_WAVES;
-    k.gpart_n = rg > 256 ? 256 : rg;
+    k.gpart_n = gtr_readout_grid(bt->b_cap);
   }
   k.has_prev = l > 0;
   k.sqrt_c = (float)sqrt((double)k.C);

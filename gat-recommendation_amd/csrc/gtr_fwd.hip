@@ -241,10 +241,10 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
       for (int k = a.bt.in_ptr[r0 + i] - e_lo; k < k1; ++k) edst[k] = i;
     }
   }
-  if (pe_lds) {
-    for (int idx = tid; idx < D * a.pe_k; idx += CONV_BLOCK) {
-      const int j = idx / a.pe_k, k = idx - j * a.pe_k;
-      PEs[j * KPE + k] = a.wpe[idx];
+  if (pe_lds) {  // LapPE projection weight [D][KPE], zero-padded past pe_k
+    for (int idx = tid; idx < D * KPE; idx += CONV_BLOCK) {
+      const int j = idx / KPE, k = idx - j * KPE;
+      PEs[idx] = k < a.pe_k ? a.wpe[j * a.pe_k + k] : 0.0f;
     }
   }
   if (a.first) {
@@ -261,42 +261,57 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
       for (int i = tid; i < m; i += CONV_BLOCK) items[i] = a.bt.node_item[rc + i];
       __syncthreads();
     }
-    if (pe_lds) {
-      for (int idx = tid; idx < m * a.pe_k; idx += CONV_BLOCK) {
-        const int i = idx / a.pe_k, k = idx - i * a.pe_k;
-        const float* pr = a.bt.node_pe ? a.bt.node_pe + (size_t)(rc + i) * a.pe_k
-                                       : a.pe_tab + (size_t)items[i] * a.pe_k;
-        PEs[D * KPE + i * KPE + k] = pr[k];
-      }
-      __syncthreads();
-    }
-    for (int idx = tid; idx < m * D; idx += CONV_BLOCK) {
-      const int i = idx / D, j = idx - i * D;
+    // layer input rows, float4 per thread: item row + LapPE projection (layer 0) or
+    // drop(bn(prev out) + prev in) (layers >= 1); both global gathers of a row in flight together
+    constexpr int C4 = D / 4;
+    for (int idx = tid; idx < m * C4; idx += CONV_BLOCK) {
+      const int i = idx / C4, j = (idx - i * C4) * 4;
       const int r = rc + i;
       const size_t o = (size_t)r * D + j;
-      float val;
+      float4 val;
       if (a.first) {
-        val = a.table[(size_t)items[i] * D + j];
+        val = *reinterpret_cast<const float4*>(a.table + (size_t)items[i] * D + j);
         if (a.pe_k > 0) {
-          float acc = 0.0f;
-          if (pe_lds) {
-            const float* pr = PEs + D * KPE + i * KPE;
-            const float* wr = PEs + j * KPE;
-            for (int k = 0; k < a.pe_k; ++k) acc += pr[k] * wr[k];
+          const float* pr = a.bt.node_pe ? a.bt.node_pe + (size_t)r * a.pe_k : a.pe_tab + (size_t)items[i] * a.pe_k;
+          float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+          if (pe_lds && (a.pe_k & 3) == 0) {
+            for (int k = 0; k < a.pe_k; k += 4) {
+              const float4 p4 = *reinterpret_cast<const float4*>(pr + k);
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const float4 w4 = *reinterpret_cast<const float4*>(PEs + (j + q) * KPE + k);
+                acc[q] += p4.x * w4.x;
+                acc[q] += p4.y * w4.y;
+                acc[q] += p4.z * w4.z;
+                acc[q] += p4.w * w4.w;
+              }
+            }
           } else {
-            const float* pr = a.bt.node_pe ? a.bt.node_pe + (size_t)r * a.pe_k : a.pe_tab + (size_t)items[i] * a.pe_k;
-            const float* wr = a.wpe + (size_t)j * a.pe_k;
-            for (int k = 0; k < a.pe_k; ++k) acc += pr[k] * wr[k];
+            for (int k = 0; k < a.pe_k; ++k) {
+              const float pk = pr[k];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) acc[q] += pk * a.wpe[(size_t)(j + q) * a.pe_k + k];
+            }
           }
-          val = val + (acc + a.bpe[j]);
+          val.x = val.x + (acc[0] + a.bpe[j]);
+          val.y = val.y + (acc[1] + a.bpe[j + 1]);
+          val.z = val.z + (acc[2] + a.bpe[j + 2]);
+          val.w = val.w + (acc[3] + a.bpe[j + 3]);
         }
       } else {
-        float y = (a.p_out[o] - s_bn[j]) * s_bn[D + j] * a.p_gamma[j] + a.p_beta[j];
-        y = y + a.p_xin[o];
-        val = y * dr.mul(st_prev, (uint32_t)o);
+        const float4 po = *reinterpret_cast<const float4*>(a.p_out + o);
+        const float4 px = *reinterpret_cast<const float4*>(a.p_xin + o);
+        const float4 pg = *reinterpret_cast<const float4*>(a.p_gamma + j);
+        const float4 pb = *reinterpret_cast<const float4*>(a.p_beta + j);
+        const float4 mu = *reinterpret_cast<const float4*>(s_bn + j);
+        const float4 rs = *reinterpret_cast<const float4*>(s_bn + D + j);
+        val.x = (((po.x - mu.x) * rs.x * pg.x + pb.x) + px.x) * dr.mul(st_prev, (uint32_t)o);
+        val.y = (((po.y - mu.y) * rs.y * pg.y + pb.y) + px.y) * dr.mul(st_prev, (uint32_t)(o + 1));
+        val.z = (((po.z - mu.z) * rs.z * pg.z + pb.z) + px.z) * dr.mul(st_prev, (uint32_t)(o + 2));
+        val.w = (((po.w - mu.w) * rs.w * pg.w + pb.w) + px.w) * dr.mul(st_prev, (uint32_t)(o + 3));
       }
-      a.xin[o] = val;
-      XO[i * XS + j] = val;
+      *reinterpret_cast<float4*>(a.xin + o) = val;
+      *reinterpret_cast<float4*>(XO + i * XS + j) = val;
     }
     __syncthreads();
 #pragma unroll
@@ -525,15 +540,24 @@ struct ReadoutK {
   float* gsum;
 };
 
+// Block per session (grid-strided): RO_WAVES waves split the session's node rows and
+// its scoring rows.  The target / negative rows are requested before the session
+// embedding exists (they depend only on the batch), held in registers (KR rows per
+// wave) and reused by the coefficient pass; chunks beyond RO_WAVES*KR rows reload.
+#define RO_BLOCK 512
+#define RO_WAVES (RO_BLOCK / 64)
+
 template <int D>
-__global__ __launch_bounds__(GTR_BLOCK) void k_readout(ReadoutK a) {
+__global__ __launch_bounds__(RO_BLOCK) void k_readout(ReadoutK a) {
   constexpr int VPL = D >= 64 ? D / 64 : 1;
-  constexpr int NB = 8;   // node rows in flight per wave
-  constexpr int NK = 8;   // negative rows in flight per wave
+  constexpr int KR = 32 / VPL;       // scoring rows per wave held in registers
+  constexpr int CHN = RO_WAVES * KR; // negatives per chunk
   __shared__ float s_bn[3 * D];
-  __shared__ float s_scr[2 * GTR_BLOCK + D];
-  __shared__ float s_red[GTR_WAVES][2 * D];
-  __shared__ float s_loss[GTR_WAVES][2];
+  __shared__ float s_scr[2 * RO_BLOCK + D];
+  __shared__ __attribute__((aligned(16))) float s_vec[RO_WAVES][D];
+  __shared__ float s_w[RO_WAVES][4];
+  __shared__ float s_red[RO_WAVES][2 * D];
+  __shared__ float s_loss[RO_WAVES][2];
   __shared__ int s_flag;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   GTR_PH(16, 0);
@@ -552,12 +576,13 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_readout(ReadoutK a) {
   const float inv_bn = 1.0f / ((float)B * (float)n);  // BPR mean over B*n
   const float inv_b = 1.0f / (float)B;                // listwise mean over B
   const float inv_t = 1.0f / a.temperature;
+  const int nchunk = do_loss ? (n + CHN - 1) / CHN : 0;
 
   if (do_fwd) {
-    prev_bn_stats<D, GTR_BLOCK>(a.train, a.cred, a.bt.hdr[4], a.part, a.stats, a.rmean, a.rvar, a.nbt, a.bn_eps,
-                                a.bn_mom, s_bn, s_bn + D, s_bn + 2 * D, s_scr);
+    prev_bn_stats<D, RO_BLOCK>(a.train, a.cred, a.bt.hdr[4], a.part, a.stats, a.rmean, a.rvar, a.nbt, a.bn_eps,
+                               a.bn_mom, s_bn, s_bn + D, s_bn + 2 * D, s_scr);
   } else if (do_bwd) {
-    for (int j = tid; j < D; j += GTR_BLOCK) { s_bn[j] = a.stats[j]; s_bn[D + j] = a.stats[D + j]; }
+    for (int j = tid; j < D; j += RO_BLOCK) { s_bn[j] = a.stats[j]; s_bn[D + j] = a.stats[D + j]; }
   }
   __syncthreads();
   GTR_PH(16, 1);
@@ -575,154 +600,218 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_readout(ReadoutK a) {
   for (int v = 0; v < VPL; ++v) { gs[v] = 0.0f; gx[v] = 0.0f; }
   float lw_sum = 0.0f, bpr_sum = 0.0f;
 
-  for (int b = blockIdx.x * GTR_WAVES + wave; b < B; b += gridDim.x * GTR_WAVES) {
+  for (int b = blockIdx.x; b < B; b += gridDim.x) {
     const int n0 = a.bt.node_ptr[b], n1 = a.bt.node_ptr[b + 1];
     const float cnt = (float)(n1 - n0);
-    float se[VPL], dse[VPL];
+    const int* negs = a.bt.negatives + (size_t)b * n;
+    // ---- (1) scoring rows of chunk 0 requested first (independent of the embedding)
+    float tv[VPL], rv[KR][VPL], sk[KR];
+    if (do_loss) {
+      load_vec<VPL>(tv, a.table + (size_t)a.bt.target[b] * D + d0, act);
+      const int kq = wave + lane * RO_WAVES;
+      const int nid = (lane < KR && kq < n) ? negs[kq] : 0;
 #pragma unroll
-    for (int v = 0; v < VPL; ++v) dse[v] = 0.0f;
+      for (int q = 0; q < KR; ++q) {
+        const int id = __shfl(nid, q);
+        if (wave + q * RO_WAVES < n) load_vec<VPL>(rv[q], a.table + (size_t)id * D + d0, act);
+      }
+    }
+    // ---- (2) session embedding: mean over node rows of drop(bn(out) + xin)
+    float se[VPL];
+    constexpr int NBR = 2;  // node rows per wave whose conv output stays in registers for (5)
+    float oc[NBR][VPL];
     if (do_fwd) {
       float acc[VPL];
 #pragma unroll
       for (int v = 0; v < VPL; ++v) acc[v] = 0.0f;
-      for (int i0 = n0; i0 < n1; i0 += NB) {
-        float ov[NB][VPL], xv[NB][VPL];
+      for (int i = n0 + wave, q = 0; i < n1; i += RO_WAVES, ++q) {
+        float ov[VPL], xv[VPL];
+        load_vec<VPL>(ov, a.out + (size_t)i * D + d0, act);
+        load_vec<VPL>(xv, a.xin + (size_t)i * D + d0, act);
 #pragma unroll
-        for (int q = 0; q < NB; ++q) {
-          const bool ok = act && (i0 + q < n1);
-          load_vec<VPL>(ov[q], a.out + (size_t)(i0 + q) * D + d0, ok);
-          load_vec<VPL>(xv[q], a.xin + (size_t)(i0 + q) * D + d0, ok);
-        }
+        for (int c = 0; c < NBR; ++c)
+          if (q == c) {
 #pragma unroll
-        for (int q = 0; q < NB; ++q) {
-          if (i0 + q < n1) {
-#pragma unroll
-            for (int v = 0; v < VPL; ++v) {
-              const size_t o = (size_t)(i0 + q) * D + d0 + v;
-              float y = (ov[q][v] - bm[v]) * br[v] * bg[v] + bb[v];
-              y = y + xv[q][v];
-              acc[v] += y * dr.mul(st, (uint32_t)o);
-            }
+            for (int v = 0; v < VPL; ++v) oc[c][v] = ov[v];
           }
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) {
+          const size_t o = (size_t)i * D + d0 + v;
+          float y = (ov[v] - bm[v]) * br[v] * bg[v] + bb[v];
+          y = y + xv[v];
+          acc[v] += y * dr.mul(st, (uint32_t)o);
         }
       }
+      if (act) {
 #pragma unroll
-      for (int v = 0; v < VPL; ++v) se[v] = acc[v] / cnt;
-      store_vec<VPL>(a.se + (size_t)b * D + d0, se, act);
+        for (int v = 0; v < VPL; ++v) s_vec[wave][d0 + v] = acc[v];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) {
+        float t = 0.0f;
+#pragma unroll
+        for (int w = 0; w < RO_WAVES; ++w) t += act ? s_vec[w][d0 + v] : 0.0f;
+        se[v] = t / cnt;
+      }
+      if (wave == 0) store_vec<VPL>(a.se + (size_t)b * D + d0, se, act);
+      __syncthreads();
     } else {
       load_vec<VPL>(se, a.se + (size_t)b * D + d0, act);
     }
 
+    float dse[VPL];
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) dse[v] = 0.0f;
     if (do_loss) {
-      const float* trow = a.table + (size_t)a.bt.target[b] * D;
-      const int* negs = a.bt.negatives + (size_t)b * n;
-      float tv[VPL];
-      load_vec<VPL>(tv, trow + d0, act);
       float pos = 0.0f;
 #pragma unroll
       for (int v = 0; v < VPL; ++v) pos += se[v] * tv[v];
       pos = wave_sum(pos);
       float dpos = 0.0f;
-      float m = pos * inv_t, z = 1.0f;
-      int nid = 0;
-      // pass 1: BPR terms (+ coefficients when BPR only) and online log-sum-exp for listwise
-      for (int k0 = 0; k0 < n; k0 += NK) {
-        if ((k0 & 63) == 0) nid = (k0 + lane < n) ? negs[k0 + lane] : 0;
-        float rv[NK][VPL];
+      float m = wave == 0 ? pos * inv_t : -INFINITY, z = wave == 0 ? 1.0f : 0.0f;
+      // ---- (3) pass 1: scores, BPR terms, per-wave online log-sum-exp
+      for (int c = 0; c < nchunk; ++c) {
+        const int kb = c * CHN;
+        if (c > 0) {
+          const int kq = kb + wave + lane * RO_WAVES;
+          const int nid = (lane < KR && kq < n) ? negs[kq] : 0;
 #pragma unroll
-        for (int q = 0; q < NK; ++q) {
-          const int id = __shfl(nid, (k0 + q) & 63);
-          load_vec<VPL>(rv[q], a.table + (size_t)id * D + d0, act && (k0 + q < n));
+          for (int q = 0; q < KR; ++q) {
+            const int id = __shfl(nid, q);
+            if (kb + wave + q * RO_WAVES < n) load_vec<VPL>(rv[q], a.table + (size_t)id * D + d0, act);
+          }
         }
 #pragma unroll
-        for (int q = 0; q < NK; ++q) {
-          const int k = k0 + q;
-          if (k >= n) break;
-          float sk = 0.0f;
+        for (int q = 0; q < KR; ++q) {
+          const int k = kb + wave + q * RO_WAVES;
+          if (k < n) {
+          float d = 0.0f;
 #pragma unroll
-          for (int v = 0; v < VPL; ++v) sk += se[v] * rv[q][v];
-          sk = wave_sum(sk);
-          float cb = 0.0f;
-          if (use_bpr) {
-            const float sg = 1.0f / (1.0f + expf(-(pos - sk)));
-            bpr_sum += -logf(sg + 1e-8f);
-            const float dz = -(sg * (1.0f - sg)) / (sg + 1e-8f) * inv_bn * w_bpr;
-            dpos += dz;
-            cb = -dz;
+          for (int v = 0; v < VPL; ++v) d += se[v] * rv[q][v];
+          d = wave_sum(d);
+          sk[q] = d;
+          {
+            if (use_bpr) {
+              const float sg = 1.0f / (1.0f + expf(-(pos - d)));
+              bpr_sum += -logf(sg + 1e-8f);
+              const float dz = -(sg * (1.0f - sg)) / (sg + 1e-8f) * inv_bn * w_bpr;
+              dpos += dz;
+              if (!use_lw) {
+                if (lane == 0) a.coef_neg[(size_t)b * n + k] = -dz;
+#pragma unroll
+                for (int v = 0; v < VPL; ++v) dse[v] += -dz * rv[q][v];
+              }
+            }
+            if (use_lw) {
+              const float l = d * inv_t;
+              const float mn = fmaxf(m, l);
+              z = z * expf(m - mn) + expf(l - mn);
+              m = mn;
+            }
           }
-          if (use_lw) {
-            const float l = sk * inv_t;
-            const float mn = fmaxf(m, l);
-            z = z * expf(m - mn) + expf(l - mn);
-            m = mn;
-          } else {
-            if (lane == 0) a.coef_neg[(size_t)b * n + k] = cb;
-#pragma unroll
-            for (int v = 0; v < VPL; ++v) dse[v] += cb * rv[q][v];
           }
         }
       }
       if (use_lw) {
-        const float lse = m + logf(z);
-        lw_sum += lse - pos * inv_t;
-        dpos += (expf(pos * inv_t - lse) - 1.0f) * inv_b * inv_t * w_lw;
-        // pass 2: softmax coefficients (+ BPR coefficients for dual)
-        for (int k0 = 0; k0 < n; k0 += NK) {
-          if ((k0 & 63) == 0) nid = (k0 + lane < n) ? negs[k0 + lane] : 0;
-          float rv[NK][VPL];
+        if (lane == 0) { s_w[wave][0] = m; s_w[wave][1] = z; }
+        __syncthreads();
+        float M = -INFINITY;
 #pragma unroll
-          for (int q = 0; q < NK; ++q) {
-            const int id = __shfl(nid, (k0 + q) & 63);
-            load_vec<VPL>(rv[q], a.table + (size_t)id * D + d0, act && (k0 + q < n));
+        for (int w = 0; w < RO_WAVES; ++w) M = fmaxf(M, s_w[w][0]);
+        float Z = 0.0f;
+#pragma unroll
+        for (int w = 0; w < RO_WAVES; ++w) Z += s_w[w][1] * expf(s_w[w][0] - M);
+        const float lse = M + logf(Z);
+        if (wave == 0) {
+          lw_sum += lse - pos * inv_t;
+          dpos += (expf(pos * inv_t - lse) - 1.0f) * inv_b * inv_t * w_lw;
+        }
+        // ---- pass 2: softmax (+ BPR) coefficients; rows still in registers for one chunk
+        for (int c = 0; c < nchunk; ++c) {
+          const int kb = c * CHN;
+          if (nchunk > 1) {
+            const int kq = kb + wave + lane * RO_WAVES;
+            const int nid = (lane < KR && kq < n) ? negs[kq] : 0;
+#pragma unroll
+            for (int q = 0; q < KR; ++q) {
+              const int id = __shfl(nid, q);
+              if (kb + wave + q * RO_WAVES < n) load_vec<VPL>(rv[q], a.table + (size_t)id * D + d0, act);
+            }
+#pragma unroll
+            for (int q = 0; q < KR; ++q) {
+              if (kb + wave + q * RO_WAVES < n) {
+                float d = 0.0f;
+#pragma unroll
+                for (int v = 0; v < VPL; ++v) d += se[v] * rv[q][v];
+                sk[q] = wave_sum(d);
+              }
+            }
           }
 #pragma unroll
-          for (int q = 0; q < NK; ++q) {
-            const int k = k0 + q;
-            if (k >= n) break;
-            float sk = 0.0f;
+          for (int q = 0; q < KR; ++q) {
+            const int k = kb + wave + q * RO_WAVES;
+            if (k < n) {
+              float cb = expf(sk[q] * inv_t - lse) * inv_b * inv_t * w_lw;
+              if (use_bpr) {
+                const float sg = 1.0f / (1.0f + expf(-(pos - sk[q])));
+                cb += (sg * (1.0f - sg)) / (sg + 1e-8f) * inv_bn * w_bpr;
+              }
+              if (lane == 0) a.coef_neg[(size_t)b * n + k] = cb;
 #pragma unroll
-            for (int v = 0; v < VPL; ++v) sk += se[v] * rv[q][v];
-            sk = wave_sum(sk);
-            float cb = expf(sk * inv_t - lse) * inv_b * inv_t * w_lw;
-            if (use_bpr) {
-              const float sg = 1.0f / (1.0f + expf(-(pos - sk)));
-              cb += (sg * (1.0f - sg)) / (sg + 1e-8f) * inv_bn * w_bpr;
+              for (int v = 0; v < VPL; ++v) dse[v] += cb * rv[q][v];
             }
-            if (lane == 0) a.coef_neg[(size_t)b * n + k] = cb;
-#pragma unroll
-            for (int v = 0; v < VPL; ++v) dse[v] += cb * rv[q][v];
           }
         }
       }
-      if (lane == 0) a.coef_tgt[b] = dpos;
+      // ---- (4) dse = sum of the waves' partials + dpos * target row
+      if (act) {
 #pragma unroll
-      for (int v = 0; v < VPL; ++v) dse[v] += dpos * tv[v];
-      if (a.dse_out) store_vec<VPL>(a.dse_out + (size_t)b * D + d0, dse, act);
+        for (int v = 0; v < VPL; ++v) s_vec[wave][d0 + v] = dse[v];
+      }
+      if (lane == 0) s_w[wave][2] = dpos;
+      __syncthreads();
+      float dp = 0.0f;
+#pragma unroll
+      for (int w = 0; w < RO_WAVES; ++w) dp += s_w[w][2];
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) {
+        float t = 0.0f;
+#pragma unroll
+        for (int w = 0; w < RO_WAVES; ++w) t += act ? s_vec[w][d0 + v] : 0.0f;
+        dse[v] = t + dp * tv[v];
+      }
+      if (tid == 0) a.coef_tgt[b] = dp;
+      if (wave == 0 && a.dse_out) store_vec<VPL>(a.dse_out + (size_t)b * D + d0, dse, act);
+      __syncthreads();
     } else if (do_bwd) {
       load_vec<VPL>(dse, a.dse_in + (size_t)b * D + d0, act);
     }
 
+    // ---- (5) readout backward into the node rows + the last BatchNorm's backward sums
     if (do_bwd) {
       const float inv_cnt = 1.0f / cnt;
-      for (int i0 = n0; i0 < n1; i0 += NB) {
-        float ov[NB][VPL];
+      for (int i = n0 + wave, q = 0; i < n1; i += RO_WAVES, ++q) {
+        float ov[VPL], dyv[VPL];
+        if (do_fwd && q < NBR) {
 #pragma unroll
-        for (int q = 0; q < NB; ++q) load_vec<VPL>(ov[q], a.out + (size_t)(i0 + q) * D + d0, act && (i0 + q < n1));
+          for (int c = 0; c < NBR; ++c)
+            if (q == c) {
 #pragma unroll
-        for (int q = 0; q < NB; ++q) {
-          if (i0 + q < n1) {
-            float dyv[VPL];
-#pragma unroll
-            for (int v = 0; v < VPL; ++v) {
-              const size_t o = (size_t)(i0 + q) * D + d0 + v;
-              dyv[v] = dse[v] * inv_cnt * dr.mul(st, (uint32_t)o);
-              const float xh = (ov[q][v] - bm[v]) * br[v];
-              gs[v] += dyv[v];
-              gx[v] += dyv[v] * xh;
+              for (int v = 0; v < VPL; ++v) ov[v] = oc[c][v];
             }
-            store_vec<VPL>(a.dy + (size_t)(i0 + q) * D + d0, dyv, act);
-          }
+        } else {
+          load_vec<VPL>(ov, a.out + (size_t)i * D + d0, act);
         }
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) {
+          const size_t o = (size_t)i * D + d0 + v;
+          dyv[v] = dse[v] * inv_cnt * dr.mul(st, (uint32_t)o);
+          const float xh = (ov[v] - bm[v]) * br[v];
+          gs[v] += dyv[v];
+          gx[v] += dyv[v] * xh;
+        }
+        store_vec<VPL>(a.dy + (size_t)i * D + d0, dyv, act);
       }
     }
   }
@@ -738,18 +827,18 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_readout(ReadoutK a) {
   __syncthreads();
   if (do_loss && tid < 2) {
     float acc = 0.0f;
-    for (int w = 0; w < GTR_WAVES; ++w) acc += s_loss[w][tid];
+    for (int w = 0; w < RO_WAVES; ++w) acc += s_loss[w][tid];
     a.loss_part[(size_t)blockIdx.x * 2 + tid] = acc;
   }
   if (do_bwd) {
-    for (int j = tid; j < 2 * D; j += GTR_BLOCK) {
+    for (int j = tid; j < 2 * D; j += RO_BLOCK) {
       float acc = 0.0f;
-      for (int w = 0; w < GTR_WAVES; ++w) acc += s_red[w][j];
+      for (int w = 0; w < RO_WAVES; ++w) acc += s_red[w][j];
       a.gpart[(size_t)blockIdx.x * 2 * D + j] = acc;
     }
   }
   GTR_PH(16, 3);
-  if (!a.fin) return;  // loss summed by gtr_step_end, BN sums reduced by the consuming conv_bwd
+  if (!a.fin) return;  // loss summed by the step tail, BN sums reduced by the consuming conv_bwd
   if (!arrive_last(a.cnt, gridDim.x, &s_flag)) return;
   if (do_loss && tid == 0) {
     float loss = 0.0f;
@@ -757,7 +846,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_readout(ReadoutK a) {
     a.loss_out[0] = loss;
   }
   if (do_bwd) {
-    for (int j = tid; j < 2 * D; j += GTR_BLOCK) {
+    for (int j = tid; j < 2 * D; j += RO_BLOCK) {
       float acc = 0.0f;
 #pragma unroll 4
       for (int q = 0; q < (int)gridDim.x; ++q) acc += a.gpart[(size_t)q * 2 * D + j];
@@ -887,15 +976,13 @@ extern "C" int gtr_readout_loss(const gtr_config* cfg, const gtr_batch* bt, cons
   k.coef_neg = head->coef_neg;
   k.loss_part = head->loss_part; k.loss_out = head->loss_out; k.cnt = head->cnt;
   k.dy = L.dy; k.gpart = L.bn_gpart; k.gsum = L.bn_gsum;
-  int grid = (bt->b_cap + GTR_WAVES - 1) / GTR_WAVES;
-  if (grid > 256) grid = 256;
-  if (grid <= 0) return GTR_OK;
+  const int grid = gtr_readout_grid(bt->b_cap);
   hipStream_t s = (hipStream_t)stream;
   switch (cfg->dim) {
-    case 32: hipLaunchKernelGGL(k_readout<32>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
-    case 64: hipLaunchKernelGGL(k_readout<64>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
-    case 128: hipLaunchKernelGGL(k_readout<128>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
-    default: hipLaunchKernelGGL(k_readout<256>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    case 32: hipLaunchKernelGGL(k_readout<32>, dim3(grid), dim3(RO_BLOCK), 0, s, k); break;
+    case 64: hipLaunchKernelGGL(k_readout<64>, dim3(grid), dim3(RO_BLOCK), 0, s, k); break;
+    case 128: hipLaunchKernelGGL(k_readout<128>, dim3(grid), dim3(RO_BLOCK), 0, s, k); break;
+    default: hipLaunchKernelGGL(k_readout<256>, dim3(grid), dim3(RO_BLOCK), 0, s, k); break;
   }
   GTR_HIP_CHECK_LAUNCH();
   return GTR_OK;

@@ -213,41 +213,54 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_adamw_sweep(int64_t nvec, int vpr
 
 // ---- fused step: begin (counters, stamps, sorted contribution list) -------------------
 #define GTR_BEGIN_BLOCK 1024
-#define GTR_BEGIN_MCAP 4096
+#define GTR_BEGIN_WAVES (GTR_BEGIN_BLOCK / 64)
+#define GTR_BEGIN_MCAP 8192
+#define GTR_BEGIN_KEY_LIMIT (1 << 19)
 
-// One workgroup: composite keys (row << 12 | slot) are unique, so the stable order is
-// the plain order of the composites; each slot's rank = #composites below it
-// (broadcast LDS reads, no atomics, deterministic).
-__global__ __launch_bounds__(GTR_BEGIN_BLOCK) void k_step_begin_small(gtr_batch bt, int T, int32_t* skeys,
-                                                                     int32_t* svals, int32_t* stamp,
-                                                                     int64_t* step_dev, uint32_t* rng_ctr) {
+// Rank sort: composite keys (row << 13 | slot) are unique, so the stable order by row
+// is the plain order of the composites and slot j goes to rank #{composites < c_j}.
+// Every workgroup stages all composites in LDS and ranks 64 slots, its 16 waves each
+// counting over one slice of the composites (broadcast LDS reads; no atomics,
+// deterministic).  Workgroup 0 also stamps the touched rows and advances the counters.
+__global__ __launch_bounds__(GTR_BEGIN_BLOCK) void k_step_begin(gtr_batch bt, int T, int32_t* skeys, int32_t* svals,
+                                                               int32_t* stamp, int64_t* step_dev, uint32_t* rng_ctr) {
   __shared__ __attribute__((aligned(16))) uint32_t ck[GTR_BEGIN_MCAP];
-  const int tid = threadIdx.x;
+  __shared__ int s_part[GTR_BEGIN_WAVES][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
   const int m4 = (m_cap + 3) & ~3;
   const int N = bt.hdr[0], B = bt.hdr[1];
-  const int32_t tnew = (int32_t)(*step_dev + 1);
+  const bool lead = blockIdx.x == 0;
+  const int32_t tnew = lead ? (int32_t)(*step_dev + 1) : 0;
   for (int j = tid; j < m4; j += GTR_BEGIN_BLOCK) {
     uint32_t c = 0xFFFFFFFFu;
     if (j < m_cap) {
       const int key = contrib_key(bt, T, j, N, B);
-      c = ((uint32_t)key << 12) | (uint32_t)j;
-      if (stamp && key > 0 && key < T) stamp[key] = tnew;
+      c = ((uint32_t)key << 13) | (uint32_t)j;
+      if (lead && stamp && key > 0 && key < T) stamp[key] = tnew;
     }
     ck[j] = c;
   }
   __syncthreads();
-  for (int j = tid; j < m_cap; j += GTR_BEGIN_BLOCK) {
-    const uint32_t mine = ck[j];
-    int rank = 0;
-    for (int i = 0; i < m4; i += 4) {
-      const uint4 q = *reinterpret_cast<const uint4*>(ck + i);
-      rank += (q.x < mine) + (q.y < mine) + (q.z < mine) + (q.w < mine);
-    }
-    skeys[rank] = (int32_t)(mine >> 12);
-    svals[rank] = (int32_t)(mine & 0xFFFu);
+  const int j = blockIdx.x * 64 + lane;
+  const uint32_t mine = j < m_cap ? ck[j] : 0u;
+  const int S = ((m4 / GTR_BEGIN_WAVES) + 4) & ~3;
+  const int i0 = wave * S, i1 = min(m4, i0 + S);
+  int rank = 0;
+  for (int i = i0; i < i1; i += 4) {
+    const uint4 q = *reinterpret_cast<const uint4*>(ck + i);
+    rank += (q.x < mine) + (q.y < mine) + (q.z < mine) + (q.w < mine);
   }
-  if (tid == 0) {
+  s_part[wave][lane] = rank;
+  __syncthreads();
+  if (wave == 0 && j < m_cap) {
+    int r = 0;
+#pragma unroll
+    for (int w = 0; w < GTR_BEGIN_WAVES; ++w) r += s_part[w][lane];
+    skeys[r] = (int32_t)(mine >> 13);
+    svals[r] = (int32_t)(mine & 0x1FFFu);
+  }
+  if (lead && tid == 0) {
     *step_dev = tnew;
     if (rng_ctr) *rng_ctr += 1;
   }
@@ -381,6 +394,7 @@ bool dim_ok(int D) { return D == 32 || D == 64 || D == 128 || D == 256; }
 extern "C" {
 
 int gtr_version(void) { return 100; }
+int gtr_readout_grid(int b_cap) { return b_cap < 1 ? 1 : (b_cap > 256 ? 256 : b_cap); }
 int gtr_abi_version(void) { return GTR_ABI_VERSION; }
 const char* gtr_last_error(void) { return gtr::g_err; }
 
@@ -529,9 +543,9 @@ int gtr_step_begin(const gtr_batch* bt, int num_items, int32_t* keys, int32_t* v
   }
   hipStream_t s = (hipStream_t)stream;
   const int m_cap = bt->n_cap + bt->b_cap * (1 + bt->n_neg);
-  if (m_cap <= GTR_BEGIN_MCAP && num_items < (1 << 20)) {
-    hipLaunchKernelGGL(k_step_begin_small, dim3(1), dim3(GTR_BEGIN_BLOCK), 0, s, *bt, num_items, skeys, svals, stamp,
-                       step_dev, rng_ctr);
+  if (m_cap <= GTR_BEGIN_MCAP && num_items < GTR_BEGIN_KEY_LIMIT) {
+    hipLaunchKernelGGL(k_step_begin, dim3((m_cap + 63) / 64), dim3(GTR_BEGIN_BLOCK), 0, s, *bt, num_items, skeys,
+                       svals, stamp, step_dev, rng_ctr);
     GTR_HIP_CHECK_LAUNCH();
     return GTR_OK;
   }

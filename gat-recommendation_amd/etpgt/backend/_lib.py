@@ -106,6 +106,7 @@ _SIGS = {
     "gtr_adamw_sweep": (C.c_int, [C.c_int, C.c_int, P, P, P, P, P, P]),
     "gtr_scatter_rows": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P]),
     "gtr_step_end": (C.c_int, [P, P, P, C.c_int, P, P]),
+    "gtr_readout_grid": (C.c_int, [C.c_int]),
     "gtr_step_begin": (C.c_int, [P, C.c_int, P, P, P, P, P, P, P, P, C.c_size_t, P]),
     "gtr_step_tail": (C.c_int, [P, C.c_int, C.c_int, P, P, C.c_int, P, P]),
 }

@@ -147,7 +147,7 @@ def _f32(*shape, device):
 
 def readout_grid(b_cap: int) -> int:
     """Workgroups of gtr_readout_loss (= its loss / BN-sum partial count)."""
-    return max(1, min((b_cap + 3) // 4, 256))
+    return int(L.lib().gtr_readout_grid(int(b_cap)))
 
 
 class Workspace:

@@ -243,7 +243,8 @@ int gtr_scatter_rows(const gtr_batch* bt, int dim, int mode, const float* src, c
  * gtr_step_begin: advance the step (*step_dev += 1) and dropout-stream counters,
  * stamp the touched table rows (stamp[row] = new step) and build the sorted
  * contribution list skeys/svals (keys/vals/tmp: scratch for large batches, sized
- * by gtr_contrib_sort_bytes).  One workgroup when m_cap <= 4096 and T < 2^20.    */
+ * by gtr_contrib_sort_bytes).  One launch (rank sort, 64 slots per workgroup) when
+ * m_cap <= 8192 and T < 2^19; else contrib_prep + radix sort + counter update.  */
 int gtr_step_begin(const gtr_batch* bt, int num_items, int32_t* keys, int32_t* vals, int32_t* skeys,
                    int32_t* svals, int32_t* stamp, int64_t* step_dev, uint32_t* rng_ctr, void* tmp,
                    size_t tmp_bytes, gtr_stream_t stream);
@@ -275,6 +276,10 @@ typedef struct gtr_tail {
  * opt->step_offset must be 0 (runs after gtr_step_begin).                        */
 int gtr_step_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tail,
                   const gtr_segment* segs, int nseg, const gtr_adam* opt, gtr_stream_t stream);
+
+/* Workgroups of gtr_readout_loss = the number of its loss / BatchNorm-sum partials
+ * (gtr_tail.loss_nparts; the last layer's bn_gpart rows).                         */
+int gtr_readout_grid(int b_cap);
 
 /* step_dev += 1 (if non-NULL); rng_ctr += 1 (if non-NULL); if loss_part != NULL,
  * loss_out[0] = sum of the 2*nparts (already scaled) loss partials in order.     */
