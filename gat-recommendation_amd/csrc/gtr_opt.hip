@@ -381,6 +381,183 @@ __global__ void k_step_end(int64_t* step_dev, uint32_t* rng_ctr, const float* lo
   }
 }
 
+
+// ---- data-parallel step: pack (local gradients) and tail (rank-averaged update) ----------
+struct DpPackK {
+  gtr_batch bt;
+  gtr_tail tl;
+  gtr_dp_layout lay;
+  float* pack;
+  int T, nb_rows, nb_small, nseg;
+  gtr_segment segs[GTR_SMALL_MAX_SEG];
+};
+
+template <int D>
+__global__ __launch_bounds__(GTR_BLOCK) void k_dp_pack(DpPackK a) {
+  constexpr int C4 = D / 4;
+  __shared__ float s_acc[GTR_BLOCK];
+  const int tid = threadIdx.x;
+  const int blk = blockIdx.x;
+  const int m_cap = a.lay.m_cap;
+  int32_t* keys = reinterpret_cast<int32_t*>(a.pack + a.lay.keys_off);
+  float* rows = a.pack + a.lay.rows_off;
+  if (blk < a.nb_rows) {
+    const int gid = blk * GTR_BLOCK + tid;
+    const int i = gid / C4, c = gid - i * C4;
+    if (i >= m_cap) return;
+    const int key = a.tl.skeys[i];
+    if (c == 0) keys[i] = key;
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+    const bool start = key > 0 && key < a.T && (i == 0 || a.tl.skeys[i - 1] != key);
+    if (start) {
+      const gtr_batch& bt = a.bt;
+      int k = i;
+      do {
+        const int j = a.tl.svals[k];
+        const float* src;
+        float cf;
+        if (j < bt.n_cap) {
+          src = a.tl.dx0 + (size_t)j * D;
+          cf = 1.0f;
+        } else if (j < bt.n_cap + bt.b_cap) {
+          const int b = j - bt.n_cap;
+          src = a.tl.se + (size_t)b * D;
+          cf = a.tl.coef_tgt[b];
+        } else {
+          const int qn = j - bt.n_cap - bt.b_cap;
+          src = a.tl.se + (size_t)(qn / bt.n_neg) * D;
+          cf = a.tl.coef_neg[qn];
+        }
+        const float4 sv = reinterpret_cast<const float4*>(src)[c];
+        g.x += cf * sv.x; g.y += cf * sv.y; g.z += cf * sv.z; g.w += cf * sv.w;
+        ++k;
+      } while (k < m_cap && a.tl.skeys[k] == key);
+    }
+    reinterpret_cast<float4*>(rows + (size_t)i * D)[c] = g;
+    return;
+  }
+  const int sb = blk - a.nb_rows;
+  const AdamStep unused{};
+  small_body((int64_t)sb * GTR_BLOCK + tid, a.segs, a.nseg, nullptr, nullptr, nullptr, a.pack, unused);
+  if (sb == 0) {  // local loss
+    float acc = 0.0f;
+    if (a.tl.loss_part)
+      for (int q = tid; q < a.tl.loss_nparts; q += GTR_BLOCK)
+        acc += a.tl.loss_part[(size_t)q * 2] + a.tl.loss_part[(size_t)q * 2 + 1];
+    s_acc[tid] = acc;
+    __syncthreads();
+    if (tid == 0) {
+      float t = 0.0f;
+      if (a.tl.loss_part) {
+        for (int q = 0; q < GTR_BLOCK; ++q) t += s_acc[q];
+      } else {
+        t = a.tl.loss_out[0];
+      }
+      a.pack[a.lay.loss_off] = t;
+    }
+  }
+}
+
+// Union of the ranks' touched rows: stamp them and record, per (row, rank), the
+// segment-start slot holding that rank's summed gradient row.
+__global__ __launch_bounds__(GTR_BLOCK) void k_dp_stamp(gtr_dp_layout lay, int T, const float* recv, int32_t* stamp,
+                                                        int2* slot, const int64_t* step_dev, int step_offset) {
+  const int gid = blockIdx.x * GTR_BLOCK + threadIdx.x;
+  const int r = gid / lay.m_cap, i = gid - r * lay.m_cap;
+  if (r >= lay.world) return;
+  const int32_t* keys = reinterpret_cast<const int32_t*>(recv + (size_t)r * lay.words + lay.keys_off);
+  const int k = keys[i];
+  if (k <= 0 || k >= T || (i > 0 && keys[i - 1] == k)) return;
+  const int32_t t = (int32_t)(*step_dev + step_offset);
+  stamp[k] = t;
+  slot[(size_t)k * lay.world + r] = make_int2(t, i);
+}
+
+struct DpTailK {
+  gtr_tail tl;
+  gtr_dp_layout lay;
+  gtr_adam opt;
+  const float* recv;
+  const int2* slot;
+  int T, nb_rows, nb_small, nb_sweep;
+  int64_t nvec;
+  int vpr_log2, pad0;
+};
+
+template <int D>
+__global__ __launch_bounds__(GTR_BLOCK) void k_dp_tail(DpTailK a) {
+  constexpr int C4 = D / 4;
+  __shared__ AdamStep s_st;
+  __shared__ int32_t s_t;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    const int64_t t = *a.opt.step_dev + a.opt.step_offset;
+    s_st.init(a.opt, t);
+    s_t = (int32_t)t;
+  }
+  __syncthreads();
+  const AdamStep st = s_st;
+  const int32_t t = s_t;
+  const int W = a.lay.world;
+  const float inv_w = 1.0f / (float)W;
+  const int blk = blockIdx.x;
+  if (blk < a.nb_rows) {
+    // owner = lowest rank holding the row; it sums every rank's row in rank order
+    const int gid = blk * GTR_BLOCK + tid;
+    const int ri = gid / C4, c = gid - ri * C4;
+    const int r = ri / a.lay.m_cap, i = ri - r * a.lay.m_cap;
+    if (r >= W) return;
+    const int32_t* keys = reinterpret_cast<const int32_t*>(a.recv + (size_t)r * a.lay.words + a.lay.keys_off);
+    const int k = keys[i];
+    if (k <= 0 || k >= a.T || (i > 0 && keys[i - 1] == k)) return;
+    const int2* sl = a.slot + (size_t)k * W;
+    for (int q = 0; q < r; ++q)
+      if (sl[q].x == t) return;
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int q = r; q < W; ++q) {
+      const int2 e = sl[q];
+      if (e.x != t) continue;
+      const float4 v = reinterpret_cast<const float4*>(a.recv + (size_t)q * a.lay.words + a.lay.rows_off +
+                                                       (size_t)e.y * D)[c];
+      g.x += v.x; g.y += v.y; g.z += v.z; g.w += v.w;
+    }
+    g.x *= inv_w; g.y *= inv_w; g.z *= inv_w; g.w *= inv_w;
+    const size_t base = (size_t)k * C4 + c;
+    float4 pv = reinterpret_cast<const float4*>(a.tl.table)[base];
+    float4 mv = reinterpret_cast<const float4*>(a.tl.table_m)[base];
+    float4 vv = reinterpret_cast<const float4*>(a.tl.table_v)[base];
+    st.apply(pv.x, mv.x, vv.x, g.x);
+    st.apply(pv.y, mv.y, vv.y, g.y);
+    st.apply(pv.z, mv.z, vv.z, g.z);
+    st.apply(pv.w, mv.w, vv.w, g.w);
+    reinterpret_cast<float4*>(a.tl.table)[base] = pv;
+    reinterpret_cast<float4*>(a.tl.table_m)[base] = mv;
+    reinterpret_cast<float4*>(a.tl.table_v)[base] = vv;
+    return;
+  }
+  if (blk < a.nb_rows + a.nb_small) {
+    const int64_t e = (int64_t)(blk - a.nb_rows) * GTR_BLOCK + tid;
+    if (e < a.lay.flat_total) {
+      float g = 0.0f;
+      for (int q = 0; q < W; ++q) g += a.recv[(size_t)q * a.lay.words + e];
+      g *= inv_w;
+      float pv = a.tl.flat[e], mv = a.tl.flat_m[e], vv = a.tl.flat_v[e];
+      st.apply(pv, mv, vv, g);
+      a.tl.flat[e] = pv;
+      a.tl.flat_m[e] = mv;
+      a.tl.flat_v[e] = vv;
+    } else if (e == a.lay.flat_total && a.tl.loss_out) {
+      float l = 0.0f;
+      for (int q = 0; q < W; ++q) l += a.recv[(size_t)q * a.lay.words + a.lay.loss_off];
+      a.tl.loss_out[0] = l * inv_w;
+    }
+    return;
+  }
+  sweep_body(blk - a.nb_rows - a.nb_small, a.nb_sweep, a.nvec, a.vpr_log2, a.tl.stamp, t,
+             reinterpret_cast<float4*>(a.tl.table), reinterpret_cast<float4*>(a.tl.table_m),
+             reinterpret_cast<float4*>(a.tl.table_v), st);
+}
+
 int key_bits(int T) {
   int b = 1;
   while ((1LL << b) <= (long long)T) ++b;
@@ -596,6 +773,81 @@ int gtr_step_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* t
     case 64: hipLaunchKernelGGL(k_step_tail<64>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
     case 128: hipLaunchKernelGGL(k_step_tail<128>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
     default: hipLaunchKernelGGL(k_step_tail<256>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+  }
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+static bool dp_layout_ok(const gtr_dp_layout* l, int dim) {
+  return l && l->world >= 1 && l->m_cap > 0 && l->flat_total >= 0 && l->loss_off >= l->flat_total &&
+         l->keys_off > l->loss_off && l->rows_off >= l->keys_off + l->m_cap && (l->rows_off & 3) == 0 &&
+         l->words >= l->rows_off + (int64_t)l->m_cap * dim && (l->words & 3) == 0;
+}
+
+int gtr_dp_pack(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tail, const gtr_segment* segs, int nseg,
+                const gtr_dp_layout* lay, float* pack, gtr_stream_t stream) {
+  if (!bt || !tail || !pack || !dim_ok(dim) || !dp_layout_ok(lay, dim) || nseg < 0 || nseg > GTR_SMALL_MAX_SEG ||
+      lay->m_cap != bt->n_cap + bt->b_cap * (1 + bt->n_neg) || !tail->skeys || !tail->svals || !tail->dx0 ||
+      !tail->se || !tail->coef_tgt || !tail->coef_neg || (!tail->loss_part && !tail->loss_out)) {
+    set_error("gtr_dp_pack: bad arguments");
+    return GTR_E_ARG;
+  }
+  DpPackK k{};
+  k.bt = *bt;
+  k.tl = *tail;
+  k.lay = *lay;
+  k.pack = pack;
+  k.T = num_items;
+  k.nb_rows = (int)(((int64_t)lay->m_cap * (dim / 4) + GTR_BLOCK - 1) / GTR_BLOCK);
+  k.nb_small = (int)((lay->flat_total + GTR_BLOCK - 1) / GTR_BLOCK);
+  if (k.nb_small == 0) k.nb_small = 1;
+  k.nseg = nseg;
+  for (int i = 0; i < nseg; ++i) k.segs[i] = segs[i];
+  const int grid = k.nb_rows + k.nb_small;
+  hipStream_t s = (hipStream_t)stream;
+  switch (dim) {
+    case 32: hipLaunchKernelGGL(k_dp_pack<32>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    case 64: hipLaunchKernelGGL(k_dp_pack<64>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    case 128: hipLaunchKernelGGL(k_dp_pack<128>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    default: hipLaunchKernelGGL(k_dp_pack<256>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+  }
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+int gtr_dp_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tail, const gtr_dp_layout* lay,
+                const float* recv, int32_t* slot, const gtr_adam* opt, gtr_stream_t stream) {
+  if (!bt || !tail || !recv || !slot || !opt || !opt->step_dev || !dim_ok(dim) || !dp_layout_ok(lay, dim) ||
+      num_items <= 0 || !tail->table || !tail->table_m || !tail->table_v || !tail->stamp ||
+      (lay->flat_total > 0 && (!tail->flat || !tail->flat_m || !tail->flat_v))) {
+    set_error("gtr_dp_tail: bad arguments");
+    return GTR_E_ARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t slots = (int64_t)lay->world * lay->m_cap;
+  hipLaunchKernelGGL(k_dp_stamp, dim3((unsigned)((slots + GTR_BLOCK - 1) / GTR_BLOCK)), dim3(GTR_BLOCK), 0, s, *lay,
+                     num_items, recv, tail->stamp, reinterpret_cast<int2*>(slot), opt->step_dev, opt->step_offset);
+  GTR_HIP_CHECK_LAUNCH();
+  DpTailK k{};
+  k.tl = *tail;
+  k.lay = *lay;
+  k.opt = *opt;
+  k.recv = recv;
+  k.slot = reinterpret_cast<const int2*>(slot);
+  k.T = num_items;
+  k.nb_rows = (int)((slots * (dim / 4) + GTR_BLOCK - 1) / GTR_BLOCK);
+  k.nb_small = (int)((lay->flat_total + 1 + GTR_BLOCK - 1) / GTR_BLOCK);
+  k.nvec = (int64_t)num_items * dim / 4;
+  k.vpr_log2 = 0;
+  while ((1 << k.vpr_log2) < dim / 4) ++k.vpr_log2;
+  int64_t sw = (k.nvec + GTR_BLOCK - 1) / GTR_BLOCK;
+  k.nb_sweep = (int)(sw > 2048 ? 2048 : sw);
+  const int grid = k.nb_rows + k.nb_small + k.nb_sweep;
+  switch (dim) {
+    case 32: hipLaunchKernelGGL(k_dp_tail<32>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    case 64: hipLaunchKernelGGL(k_dp_tail<64>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    case 128: hipLaunchKernelGGL(k_dp_tail<128>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    default: hipLaunchKernelGGL(k_dp_tail<256>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
   }
   GTR_HIP_CHECK_LAUNCH();
   return GTR_OK;

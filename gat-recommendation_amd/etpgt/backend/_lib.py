@@ -84,6 +84,13 @@ class GtrTail(C.Structure):
     ]
 
 
+class GtrDpLayout(C.Structure):
+    _fields_ = [
+        ("flat_total", i64), ("loss_off", i64), ("keys_off", i64), ("rows_off", i64), ("words", i64),
+        ("m_cap", i32), ("world", i32),
+    ]
+
+
 GTR_LOSS = {"none": 0, "bpr": 1, "listwise": 2, "sampled_softmax": 2, "dual": 3}
 RO_FWD, RO_LOSS, RO_BWD = 1, 2, 4
 SMALL_MAX_SEG = 48
@@ -107,6 +114,8 @@ _SIGS = {
     "gtr_scatter_rows": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P]),
     "gtr_step_end": (C.c_int, [P, P, P, C.c_int, P, P]),
     "gtr_readout_grid": (C.c_int, [C.c_int]),
+    "gtr_dp_pack": (C.c_int, [P, C.c_int, C.c_int, P, P, C.c_int, P, P, P]),
+    "gtr_dp_tail": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P]),
     "gtr_step_begin": (C.c_int, [P, C.c_int, P, P, P, P, P, P, P, P, C.c_size_t, P]),
     "gtr_step_tail": (C.c_int, [P, C.c_int, C.c_int, P, P, C.c_int, P, P]),
 }

@@ -32,7 +32,7 @@ class FusedTrainStep:
     def __init__(self, model, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 1e-5, decoupled: bool = True, loss: str = "bpr",
                  temperature: float = 1.0, alpha: float = 0.7, caps: Caps | None = None,
-                 use_graph: bool = True):
+                 use_graph: bool = True, data_parallel: bool | None = None, process_group=None):
         if loss not in ("bpr", "listwise", "dual", "sampled_softmax"):
             raise ValueError(f"Unknown loss type: {loss}")
         self.model = model
@@ -42,6 +42,16 @@ class FusedTrainStep:
         self.temperature = float(temperature)
         self.alpha = float(alpha)
         self.use_graph = use_graph
+        # data parallel (one process per GPU): gradients averaged over the ranks by one
+        # all-gather per step (etpgt.train.distributed); default: on when the default
+        # process group spans more than one rank
+        from etpgt.train.distributed import world_info
+
+        self.group = process_group
+        self.rank, self.world = world_info(process_group)
+        self.data_parallel = (self.world > 1) if data_parallel is None else bool(data_parallel)
+        self.dp = None
+        self.graph_b = None
         eng = self.eng
         T, D = eng.T, eng.D
         self.adam = L.GtrAdam()
@@ -61,8 +71,21 @@ class FusedTrainStep:
             self._bind(caps)
 
     # ------------------------------------------------------------------ buffers
+    def _agree(self, caps: Caps) -> Caps:
+        """DP: every rank binds the same capacities (the packs are all-gathered)."""
+        if not (self.data_parallel and self.world > 1):
+            return caps
+        import torch.distributed as dist
+
+        dev = self.dev if dist.get_backend(self.group) != "gloo" else "cpu"
+        t = torch.tensor([caps.n_cap, caps.b_cap, caps.e_cap], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        n, b, e = (int(v) for v in t.tolist())
+        return Caps(n, b, e, caps.n_neg)
+
     def _bind(self, caps: Caps):
         eng = self.eng
+        caps = self._agree(caps)
         self.caps = caps
         self.ws = eng.workspace(caps)
         from etpgt.data.batch import blob_layout
@@ -98,11 +121,23 @@ class FusedTrainStep:
         t.loss_out = ws.loss_out.data_ptr()
         t.loss_nparts = readout_grid(caps.b_cap)
         self.tail = t
+        if self.data_parallel:
+            from etpgt.train.distributed import DpExchange
+
+            self.dp = DpExchange(self, self.group)
         self.graph = None
         self.graph_pe = None
+        self.graph_b = None
 
     def ensure_caps(self, batch: SessionBatch):
         N, B, E, n = batch.sizes()
+        if self.data_parallel and self.world > 1:  # collective: the ranks grow together
+            import torch.distributed as dist
+
+            dev = self.dev if dist.get_backend(self.group) != "gloo" else "cpu"
+            t = torch.tensor([N, B, E], dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            N, B, E = (int(v) for v in t.tolist())
         if self.caps is None:
             self._bind(Caps.bucket(2 * N, B, 2 * E, n))
         elif not self.caps.fits(N, B, E, n):
@@ -129,7 +164,8 @@ class FusedTrainStep:
         self.blob.copy_(blob, non_blocking=True)
 
     # ------------------------------------------------------------------ launches
-    def _launch(self, with_pe: bool):
+    def _launch_a(self, with_pe: bool):
+        """step_begin -> forward + loss -> backward (+ the DP pack)."""
         eng = self.eng
         lib = L.lib()
         ws, cfg = self.ws, self.cfg
@@ -141,21 +177,48 @@ class FusedTrainStep:
                                    self.sort_tmp.numel(), st), "step_begin")
         eng.run_forward(ws, cfg, bs, L.RO_FWD | L.RO_LOSS | L.RO_BWD, self.loss_kind, self.temperature, self.alpha)
         eng.run_backward(ws, cfg, bs)
-        L.check(lib.gtr_step_tail(C.byref(bs), eng.T, eng.D, C.byref(self.tail), self.segs, self.nseg,
-                                  C.byref(self.adam), st), "step_tail")
+        if self.dp is not None:
+            self.dp.launch_pack(bs, st)
 
-    def capture(self, with_pe: bool = False):
-        """Capture one step into a hipGraph (after one eager warm-up step)."""
+    def _launch_b(self, with_pe: bool):
+        """Optimizer tail: local (step_tail) or rank-averaged (dp_tail)."""
+        eng = self.eng
+        bs = self.bs_pe if with_pe else self.bs
+        st = torch.cuda.current_stream(self.dev).cuda_stream
+        if self.dp is not None:
+            self.dp.launch_tail(bs, st)
+        else:
+            L.check(L.lib().gtr_step_tail(C.byref(bs), eng.T, eng.D, C.byref(self.tail), self.segs, self.nseg,
+                                          C.byref(self.adam), st), "step_tail")
+
+    def _launch(self, with_pe: bool):
+        self._launch_a(with_pe)
+        if self.dp is not None:
+            self.dp.exchange()
+        self._launch_b(with_pe)
+
+    def _capture(self, fn):
         g = torch.cuda.CUDAGraph()
         s = torch.cuda.Stream(self.dev)
         s.wait_stream(torch.cuda.current_stream(self.dev))
         with torch.cuda.graph(g, stream=s):
-            self._launch(with_pe)
+            fn()
         torch.cuda.current_stream(self.dev).wait_stream(s)
-        if with_pe:
-            self.graph_pe = g
+        return g
+
+    def capture(self, with_pe: bool = False):
+        """Capture one step into hipGraphs (after one eager warm-up step): the whole
+        step single-GPU; the halves before / after the all-gather in DP mode."""
+        if self.dp is None:
+            g = self._capture(lambda: self._launch(with_pe))
+            gb = None
         else:
-            self.graph = g
+            g = self._capture(lambda: self._launch_a(with_pe))
+            gb = self._capture(lambda: self._launch_b(with_pe))
+        if with_pe:
+            self.graph_pe, self.graph_b_pe = g, gb
+        else:
+            self.graph, self.graph_b = g, gb
         return g
 
     def run(self, with_pe: bool = False):
@@ -171,6 +234,9 @@ class FusedTrainStep:
                 self.capture(with_pe)
                 return self.ws.loss_out[0]
             g.replay()
+            if self.dp is not None:
+                self.dp.exchange()
+                (self.graph_b_pe if with_pe else self.graph_b).replay()
         else:
             self._launch(with_pe)
         return self.ws.loss_out[0]

@@ -260,7 +260,7 @@ typedef struct gtr_tail {
   float* table;           /* [T, D] item table, its AdamW moments                    */
   float* table_m;
   float* table_v;
-  const int32_t* stamp;   /* [T] last step each row was touched                     */
+  int32_t* stamp;         /* [T] last step each row was touched (dp_tail writes) */
   float* flat;            /* flat small-parameter buffer + moments                   */
   float* flat_m;
   float* flat_v;
@@ -276,6 +276,28 @@ typedef struct gtr_tail {
  * opt->step_offset must be 0 (runs after gtr_step_begin).                        */
 int gtr_step_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tail,
                   const gtr_segment* segs, int nseg, const gtr_adam* opt, gtr_stream_t stream);
+
+/* ---- data-parallel step (one process per GPU; etpgt.train.distributed) --------
+ * Each rank packs its gradients into `pack` (words per rank = layout.words):
+ *   [0, flat_total)          summed small-parameter gradient (flat layout)
+ *   [loss_off]               local loss
+ *   [keys_off, +m_cap)       sorted contribution keys (int32 bits; sentinel T)
+ *   [rows_off, +m_cap*D)     per-segment-start summed table-gradient rows
+ * After an all-gather of the packs (RCCL), every rank runs gtr_dp_tail on the
+ * same [world][words] buffer: AdamW with the rank-averaged gradient on the union
+ * of touched rows, the untouched rows and the small parameters — replicas stay
+ * identical without exchanging parameters.                                       */
+typedef struct gtr_dp_layout {
+  int64_t flat_total, loss_off, keys_off, rows_off, words;
+  int32_t m_cap, world;
+} gtr_dp_layout;
+
+int gtr_dp_pack(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tail, const gtr_segment* segs,
+                int nseg, const gtr_dp_layout* lay, float* pack, gtr_stream_t stream);
+
+/* slot: [T][world] int2 {step, segment-start index} scratch (init to -1).          */
+int gtr_dp_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tail, const gtr_dp_layout* lay,
+                const float* recv, int32_t* slot, const gtr_adam* opt, gtr_stream_t stream);
 
 /* Workgroups of gtr_readout_loss = the number of its loss / BatchNorm-sum partials
  * (gtr_tail.loss_nparts; the last layer's bn_gpart rows).                         */

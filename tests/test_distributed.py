@@ -1,0 +1,159 @@
+"""Data-parallel protocol on CPU (gloo, world size 2): the gradient pack / all-gather /
+rank-average of etpgt.train.distributed, driven with the oracle's autograd gradients,
+equals one AdamW step on the averaged gradients, and the replicas stay identical.
+(The device kernels of the same protocol: tests/test_gpu_parity.py::test_dp_*.)"""
+
+from __future__ import annotations
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+T, D, H, L_, B, NNEG = 300, 32, 2, 2, 8, 5
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _model():
+    import etpgt_ref as R
+
+    torch.manual_seed(0)
+    return R.ref_create_graph_transformer_optimized(T, embedding_dim=D, hidden_dim=D, num_layers=L_, num_heads=H,
+                                                    dropout=0.0, use_laplacian_pe=False)
+
+
+def _batches(world):
+    from etpgt.data.synthetic import make_batches, make_sessions_and_graph
+
+    data = make_sessions_and_graph(num_items=T, num_sessions=500, num_edges=1500, seed=3)
+    return make_batches(data, B, world, NNEG, seed=7)
+
+
+def _grads(model, sb):
+    """Forward + loss + backward of one rank's batch (trainer.py:80-122, BPR)."""
+    import etpgt_ref as R
+
+    rb = R.ref_batch_from(sb)
+    model.train()
+    model.zero_grad()
+    se = model(rb)
+    loss = R.ref_loss("bpr", se, rb.target_item, rb.negative_items.view(B, NNEG), model.item_embedding)
+    loss.backward()
+    return loss.detach()
+
+
+def _flat_grad(model, layout):
+    from etpgt.backend.engine import model_param_map
+
+    flat = torch.zeros(layout.total)
+    for name, p, row in model_param_map(model):
+        s = layout.seg(name)
+        start = s.begin + row * (D if name.endswith("w_all") else 1)
+        flat[start: start + p.numel()] = p.grad.reshape(-1)
+    return flat
+
+
+def _set_grads(model, layout, flat, rows):
+    from etpgt.backend.engine import model_param_map
+
+    for name, p, row in model_param_map(model):
+        s = layout.seg(name)
+        start = s.begin + row * (D if name.endswith("w_all") else 1)
+        p.grad = flat[start: start + p.numel()].view(p.shape).clone()
+    g = torch.zeros(T, D)
+    for k, v in rows.items():
+        g[k] = v
+    model.item_embedding.weight.grad = g
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from etpgt.backend.engine import ParamLayout
+    from etpgt.train import distributed as DP
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        model = _model()
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=1e-2)
+        layout = ParamLayout(D, L_, 0)
+        sb = _batches(world)[rank]
+        m_cap = 64 + B * (1 + NNEG) + 64
+        lay = DP.DpLayout(layout.total, m_cap, D, world)
+        loss = _grads(model, sb)
+        keys = torch.cat([torch.as_tensor(sb.x), torch.as_tensor(sb.target_item),
+                          torch.as_tensor(sb.negative_items).reshape(-1)])
+        pack = DP.pack_reference(lay, _flat_grad(model, layout), float(loss), model.item_embedding.weight.grad,
+                                 keys, T)
+        recv = torch.zeros(world, lay.words)
+        DP.all_gather_packs(recv, pack)
+        flat, rows, loss_avg = DP.combine_reference(lay, recv, T)
+        _set_grads(model, layout, flat, rows)
+        opt.step()
+        # numpy payload: tensors would travel as shared-memory handles that die with the process
+        q.put((rank, loss_avg, {k: v.detach().numpy().copy() for k, v in model.state_dict().items()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_protocol_matches_averaged_step():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        rank, loss, state = q.get(timeout=240)
+        res[rank] = (loss, {k: torch.from_numpy(v) for k, v in state.items()})
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # replicas identical (parameters; BatchNorm running statistics are rank-local, as in
+    # DistributedDataParallel without SyncBatchNorm / buffer broadcast)
+    is_buffer = lambda k: "running_" in k or "num_batches" in k  # noqa: E731
+    for k, v in res[0][1].items():
+        if not is_buffer(k):
+            assert torch.equal(v, res[1][1][k]), k
+    # single process: average of the two ranks' gradients, one AdamW step
+    model = _model()
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-2, weight_decay=1e-2)
+    bl = _batches(world)
+    gsum = {}
+    losses = []
+    for sb in bl:
+        losses.append(float(_grads(model, sb)))
+        for n, p in model.named_parameters():
+            gsum[n] = gsum.get(n, 0) + p.grad.clone()
+    for n, p in model.named_parameters():
+        p.grad = gsum[n] / world
+    opt.step()
+    assert abs(res[0][0] - sum(losses) / world) < 1e-6
+    for k, v in model.state_dict().items():
+        if not is_buffer(k):
+            torch.testing.assert_close(res[0][1][k], v, rtol=1e-5, atol=1e-6, msg=k)
+
+
+def test_dp_layout_is_aligned_and_packed():
+    from etpgt.train.distributed import DpLayout
+
+    for F, m, d, w in ((34000, 342, 64, 8), (1, 1, 32, 1), (133123, 3382, 128, 2)):
+        lay = DpLayout(F, m, d, w)
+        assert lay.loss_off == F and lay.keys_off == F + 1
+        assert lay.rows_off % 4 == 0 and lay.rows_off >= lay.keys_off + m
+        assert lay.words % 4 == 0 and lay.words >= lay.rows_off + m * d
+        s = lay.struct()
+        assert (s.flat_total, s.loss_off, s.keys_off, s.rows_off, s.words, s.m_cap, s.world) == (
+            F, lay.loss_off, lay.keys_off, lay.rows_off, lay.words, m, w)

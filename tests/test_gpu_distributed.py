@@ -1,0 +1,120 @@
+"""GPU: the data-parallel step kernels (gtr_dp_pack / gtr_dp_tail) — world size 1
+against the single-GPU fused step, and two ranks sharing the GPU over a gloo group
+against the oracle's rank-averaged AdamW trajectory (replicas must stay identical)."""
+
+from __future__ import annotations
+
+import copy
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover - collected only on the GPU box
+    pytest.skip("no GPU", allow_module_level=True)
+
+from gpu_helpers import assert_close_norm, batches, make_pair, ref_batch, small_data  # noqa: E402
+
+from etpgt.train.fused import FusedTrainStep  # noqa: E402
+
+D, H, STEPS, B, NNEG = 64, 2, 3, 16, 5
+
+
+def test_dp_world1_equals_fused_step():
+    data = small_data()
+    T = data.table_rows
+    m1, _ = make_pair(T, D, H, K=0, seed=21)
+    m2 = copy.deepcopy(m1)
+    m1.train(); m2.train()
+    f1 = FusedTrainStep(m1, lr=1e-2, weight_decay=1e-2, loss="bpr")
+    f2 = FusedTrainStep(m2, lr=1e-2, weight_decay=1e-2, loss="bpr", data_parallel=True)
+    assert f2.world == 1
+    for sb in batches(data, B, NNEG, STEPS, seed=22):
+        l1 = float(f1(sb.to("cuda")))
+        l2 = float(f2(sb.to("cuda")))
+        assert abs(l1 - l2) <= 1e-6 * max(1.0, abs(l1))
+    assert f2.dp is not None
+    for (n, a), b in zip(m1.named_parameters(), m2.parameters()):
+        torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7, msg=n)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        data = small_data()
+        T = data.table_rows
+        m, _ = make_pair(T, D, H, K=0, seed=23)
+        m.train()
+        f = FusedTrainStep(m, lr=1e-2, weight_decay=1e-2, loss="bpr")
+        assert f.data_parallel and f.world == world
+        bl = batches(data, B, NNEG, STEPS * world, seed=24)
+        losses = [float(f(bl[s * world + rank].to("cuda"))) for s in range(STEPS)]
+        q.put((rank, losses, {n: p.detach().cpu().numpy().copy() for n, p in m.named_parameters()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_two_ranks_match_oracle_average():
+    import etpgt_ref as R
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            rank, losses, params = q.get(timeout=400)
+            res[rank] = (losses, {k: torch.from_numpy(v) for k, v in params.items()})
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    for k, v in res[0][1].items():
+        assert torch.equal(v, res[1][1][k]), f"replicas diverged: {k}"
+    # oracle: per step, each rank's batch through its own BatchNorm statistics, the
+    # gradients averaged, one AdamW step
+    data = small_data()
+    T = data.table_rows
+    _, ref = make_pair(T, D, H, K=0, seed=23)
+    opt = torch.optim.AdamW(ref.parameters(), lr=1e-2, weight_decay=1e-2)
+    bl = batches(data, B, NNEG, STEPS * world, seed=24)
+    for s in range(STEPS):
+        gsum, ls = {}, []
+        for r in range(world):
+            rb = ref_batch(bl[s * world + r])
+            ref.train()
+            ref.zero_grad()
+            se = ref(rb)
+            loss = R.ref_loss("bpr", se, rb.target_item, rb.negative_items.view(B, NNEG), ref.item_embedding)
+            loss.backward()
+            ls.append(float(loss))
+            for n, p in ref.named_parameters():
+                gsum[n] = gsum.get(n, 0) + p.grad.clone()
+        for n, p in ref.named_parameters():
+            p.grad = gsum[n] / world
+        opt.step()
+        assert abs(res[0][0][s] - sum(ls) / world) <= 1e-3 * abs(sum(ls) / world)
+    for n, p in ref.named_parameters():
+        if n.endswith("lin_key.bias"):  # softmax-invariant: zero gradient, Adam-amplified rounding
+            assert float((res[0][1][n] - p.detach()).abs().max()) <= 2 * 1e-2 * STEPS + 1e-6
+            continue
+        assert_close_norm(res[0][1][n], p, rtol=1e-3, name=n)
