@@ -13,8 +13,9 @@ BPR with 5 negatives, dropout 0.1, AdamW(lr 1e-3, wd 1e-5), B = 32 sessions per
 GPU (params.yaml:6).  ``--config c3`` runs configs[2] (d=128, 4 heads, LapPE
 k=16, listwise with 100 negatives).
 
-Multi-GPU (torchrun): data-parallel replicas, B per GPU fixed ("weak" scaling);
-see DESIGN.md §6 for the exchange.
+Multi-GPU (torchrun, one process per GPU): data parallel, B per GPU fixed ("weak"
+scaling); gradients averaged by one RCCL all-gather of a fixed-size pack per step
+(etpgt.train.distributed, DESIGN.md).
 
 Prints ONE JSON line (rank 0).
 """
@@ -105,6 +106,12 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss)
+    replicas_identical = None
+    if world > 1:  # data parallel: every rank must hold the same parameters
+        chk = torch.stack([step.model.item_embedding.weight.double().sum(), step.eng.flat.flat.double().sum()])
+        allc = [torch.zeros_like(chk) for _ in range(world)]
+        torch.distributed.all_gather(allc, chk)
+        replicas_identical = all(torch.equal(allc[0], c) for c in allc)
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * B * args.steps / elapsed
 
@@ -144,6 +151,7 @@ def main():
                 "hip_graph": not args.no_graph,
                 "gpu_ms_per_step_events": round(gpu_ms / args.steps, 4),
                 "final_loss": round(final_loss, 6),
+                "replicas_identical": replicas_identical,
             },
             "roofline": {
                 "bound": "hbm",

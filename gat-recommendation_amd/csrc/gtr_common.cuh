@@ -141,6 +141,9 @@ struct AdamStep {
     decay_mul = (float)(1.0 - (double)o.lr * (double)o.weight_decay);
   }
   __device__ __forceinline__ void apply(float& p, float& m, float& v, float g) const {
+    // no FMA contraction: the same rounding in every kernel that applies the update
+    // (single-GPU tail, data-parallel tail, eager entry points)
+#pragma clang fp contract(off)
     if (decoupled) p = p * decay_mul;
     else g = g + wd * p;
     m = m + (1.0f - b1) * (g - m);          // exp_avg.lerp_(grad, 1 - beta1)
