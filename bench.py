@@ -120,6 +120,7 @@ def main():
     tail_ms = measure_tail(step, args.steps)
     alg_bytes = tail_bytes(step, T, D, touched)
     achieved = alg_bytes / (tail_ms * 1e-3) / 1e9
+    traffic, traffic_src = load_traffic(args.config)
 
     cpu = None
     if rank == 0 and args.cpu_seconds > 0:
@@ -160,7 +161,9 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": None if traffic is None else round(traffic),
+                "traffic_unit": "bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                "traffic_source": traffic_src,
                 "alg_bytes_per_launch": int(alg_bytes),
                 "avg_launch_ms": round(tail_ms, 5),
             },
@@ -199,6 +202,22 @@ def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, us
                              for b in batches]))
     return dict(step=step, staged=staged, batches=batches, data=data, T=T, B=B, touched=touched, stats=st,
                 caps=caps, model=model)
+
+
+def load_traffic(config: str, kernel: str = "k_step_tail"):
+    """Per-launch HBM bytes of `kernel` from the newest committed PMC summary
+    (profiles/rNN/<config>_pmc.json: scripts/gpu_pmc.sh = two rocprofv3 --pmc passes,
+    FETCH_SIZE doubled per the gfx950 note + WRITE_SIZE, scripts/pmc_parse.py)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"{config}_pmc.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        rec = json.load(f).get(kernel)
+    if not rec:
+        return None, None
+    return float(rec["hbm_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
 
 
 def measure_tail(step, iters) -> float:

@@ -24,6 +24,15 @@
  *                     (trainer.py:125-127) over the item table and the dense params.
  *   gtr_scatter_rows  eager (autograd) path: dense table gradient.
  *   gtr_step_end      step / dropout-stream counters.
+ *   gtr_step_begin / gtr_step_tail
+ *                     one whole Trainer.train_epoch iteration (trainer.py:80-133)
+ *                     is begin -> conv_fwd.. -> readout_loss -> conv_bwd.. -> wgrad
+ *                     -> tail: zero_grad/backward/optimizer.step() of trainer.py:
+ *                     123-127 without a dense table gradient.
+ *   gtr_dp_pack / gtr_dp_tail
+ *                     the data-parallel version of that step (one process per GPU);
+ *                     the reference has no multi-GPU path.
+ *   gtr_readout_grid  partial count of gtr_readout_loss (host sizing).
  *
  * Conventions: plain pointers + sizes, no torch types; every
  * pointer is a device pointer unless marked (host); stream is a hipStream_t;

@@ -39,6 +39,33 @@ def edge_case_batch(n_neg=5, T=300) -> SessionBatch:
     return collate_sessions(out)
 
 
+def long_session_batch(n_neg=5, T=300) -> SessionBatch:
+    """Groups past the LDS fast path of the layer kernels: a 70-node session
+    (> RMAX rows), a 40-node complete graph (1600 edges > EMAX), next to short ones."""
+    rng = np.random.default_rng(1)
+    items = []
+    xs = rng.choice(np.arange(1, T), size=70, replace=False)
+    src, dst = [], []
+    for a in range(70):
+        for b in range(max(0, a - 5), min(70, a + 6)):
+            src.append(a); dst.append(b)
+    items.append({"x": xs, "edge_index": [src, dst]})
+    xs = rng.choice(np.arange(1, T), size=40, replace=False)
+    items.append({"x": xs, "edge_index": [[a for a in range(40) for b in range(40)],
+                                          [b for a in range(40) for b in range(40)]]})
+    for _ in range(4):
+        xs = rng.choice(np.arange(1, T), size=4, replace=False)
+        items.append({"x": xs, "edge_index": [[0, 1, 2, 3, 1], [1, 2, 3, 0, 1]]})
+    out = []
+    for it in items:
+        x = np.asarray(it["x"], np.int64)
+        seen = set(x.tolist())
+        negs = [v for v in rng.integers(1, T, size=4 * n_neg) if int(v) not in seen][:n_neg]
+        out.append({"x": x, "edge_index": np.array(it["edge_index"], np.int64).reshape(2, -1),
+                    "target_item": int(rng.integers(1, T)), "negative_items": np.array(negs, np.int64)})
+    return collate_sessions(out)
+
+
 def make_pair(T, D, H, L=2, K=0, dropout=0.0, seed=0, pe_table=None):
     """HIP model (cuda) + oracle model (cpu) with identical parameters."""
     torch.manual_seed(seed)

@@ -17,7 +17,8 @@ if not torch.cuda.is_available():  # pragma: no cover - collected only on the GP
     pytest.skip("no GPU", allow_module_level=True)
 
 import etpgt_ref as R  # noqa: E402
-from gpu_helpers import assert_close, assert_close_norm, batches, edge_case_batch, make_pair, ref_batch, small_data  # noqa: E402
+from gpu_helpers import (assert_close, assert_close_norm, batches, edge_case_batch, long_session_batch,  # noqa: E402
+                         make_pair, ref_batch, small_data)
 
 from etpgt.train.fused import FusedTrainStep  # noqa: E402
 from etpgt.train.losses import create_loss_function  # noqa: E402
@@ -117,6 +118,30 @@ def test_edge_cases_train():
     se_ref = ref(rb)
     L_ref = ref.compute_loss(se_ref, rb.target_item, rb.negative_items.view(sb.num_graphs, 5))
     L_ref.backward()
+    assert_close(L_hip.reshape(1), L_ref.reshape(1), name="loss")
+    hp = dict(m.named_parameters())
+    gscale = max(float(p.grad.abs().max()) for p in ref.parameters())
+    for name, p in ref.named_parameters():
+        assert_close(hp[name].grad, p.grad, rtol=2e-3, name=f"grad {name}", floor=1e-6 * gscale)
+
+
+@pytest.mark.parametrize("D,H", [(64, 2), (128, 4)])
+def test_long_sessions_general_path_train(D, H):
+    """Row groups beyond the LDS carve (70-row session, 1600-edge session) run the
+    general global-memory path next to fast-path groups of the same batch."""
+    T = data().table_rows
+    m, ref = make_pair(T, D, H, K=0, seed=4)
+    m.train(); ref.train()
+    sb = long_session_batch(5, T)
+    dsb = sb.to("cuda")
+    se = m(dsb)
+    L_hip = m.compute_loss(se, dsb.target_item, dsb.negative_items.view(sb.num_graphs, 5))
+    L_hip.backward()
+    rb = ref_batch(sb)
+    se_ref = ref(rb)
+    L_ref = ref.compute_loss(se_ref, rb.target_item, rb.negative_items.view(sb.num_graphs, 5))
+    L_ref.backward()
+    assert_close(se, se_ref, name="se")
     assert_close(L_hip.reshape(1), L_ref.reshape(1), name="loss")
     hp = dict(m.named_parameters())
     gscale = max(float(p.grad.abs().max()) for p in ref.parameters())
