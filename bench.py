@@ -60,6 +60,7 @@ def main():
     ap.add_argument("--num-batches", type=int, default=64, help="distinct pre-staged batches per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--dp", action="store_true", help="force the data-parallel step (exchange) even at N=1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -75,7 +76,8 @@ def main():
     cfg = CONFIGS[args.config]
 
     t0 = time.time()
-    w = build_workload(args.config, args.batch_size, args.num_batches, dev, rank, use_graph=not args.no_graph)
+    w = build_workload(args.config, args.batch_size, args.num_batches, dev, rank, use_graph=not args.no_graph,
+                       data_parallel=True if args.dp else None)
     step, staged, batches, data, T, B, touched, st = (w[k] for k in ("step", "staged", "batches", "data", "T", "B",
                                                                    "touched", "stats"))
     log(f"data: T={T} sessions={data.num_sessions} edges={data.edge_keys.size} setup {time.time()-t0:.1f}s {st}")
@@ -149,6 +151,7 @@ def main():
                 "nodes_per_session": round(st["nodes_per_session"], 3),
                 "edges_per_session": round(st["edges_per_session"], 3),
                 "parallelism": f"dp{world}",
+                "dp_exchange": step.dp is not None,
                 "hip_graph": not args.no_graph,
                 "gpu_ms_per_step_events": round(gpu_ms / args.steps, 4),
                 "final_loss": round(final_loss, 6),
@@ -174,7 +177,8 @@ def main():
         torch.distributed.destroy_process_group()
 
 
-def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, use_graph: bool = True) -> dict:
+def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, use_graph: bool = True,
+                   data_parallel: bool | None = None) -> dict:
     """Synthetic RetailRocket-shaped data, the model of `config`, a bound fused step
     and `num_batches` packed batches pre-staged in HBM."""
     from etpgt.data.batch import Caps
@@ -194,7 +198,8 @@ def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, us
     if cfg["K"] > 0:
         model.laplacian_pe._cached_pe = random_pe_table(T, cfg["K"])
     model = model.to(dev).train()
-    step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, loss=cfg["loss"], use_graph=use_graph)
+    step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, loss=cfg["loss"], use_graph=use_graph,
+                          data_parallel=data_parallel)
     caps = Caps(max(b.num_nodes for b in batches), B, max(b.num_edges for b in batches), cfg["n_neg"])
     step._bind(caps)
     staged = [torch.from_numpy(b.packed(caps)[1]).to(dev) for b in batches]

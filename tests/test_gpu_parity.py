@@ -158,6 +158,23 @@ def test_long_sessions_general_path_train(D, H):
 def test_fused_steps(D, H, K, loss, opt, use_graph):
     """k fused steps (forward+loss+backward+optimizer, hipGraph replay) == k
     reference trainer steps (trainer.py:80-133) with torch.optim.AdamW/Adam."""
+    _fused_vs_reference(D, H, K, loss, opt, use_graph, B=32, steps=4)
+
+
+def test_fused_steps_last_arriver_reductions(monkeypatch):
+    """The large-grid BatchNorm reduction mode (last arriving workgroup combines the
+    partials, agent-scope fences) on the C2 shape."""
+    monkeypatch.setenv("GTR_CONSUMER_REDUCE", "0")
+    _fused_vs_reference(64, 1, 0, "bpr", "adamw", True, B=32, steps=3)
+
+
+def test_fused_steps_large_batch():
+    """B = 1400: > 64 row groups (last-arriver reductions), > 8192 table-gradient
+    contributions (prep + radix-sort begin path), readout grid-stride over sessions."""
+    _fused_vs_reference(64, 2, 0, "bpr", "adamw", True, B=1400, steps=2)
+
+
+def _fused_vs_reference(D, H, K, loss, opt, use_graph, B, steps):
     T = data().table_rows
     n = 5 if loss != "listwise" else 100
     m, ref = make_pair(T, D, H, K=K, seed=4)
@@ -169,7 +186,7 @@ def test_fused_steps(D, H, K, loss, opt, use_graph):
         ropt = torch.optim.AdamW(ref.parameters(), lr=lr, weight_decay=wd)
     else:
         ropt = torch.optim.Adam(ref.parameters(), lr=lr)
-    bl = batches(data(), 32, n, 4, seed=11)
+    bl = batches(data(), B, n, steps, seed=11)
     losses, rlosses = [], []
     for sb in bl:
         losses.append(float(fused(sb.to("cuda"))))
