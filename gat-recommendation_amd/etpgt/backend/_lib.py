@@ -118,6 +118,8 @@ _SIGS = {
     "gtr_dp_tail": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P]),
     "gtr_step_begin": (C.c_int, [P, C.c_int, P, P, P, P, P, P, P, P, C.c_size_t, P]),
     "gtr_step_tail": (C.c_int, [P, C.c_int, C.c_int, P, P, C.c_int, P, P]),
+    "gtr_topk_workspace_bytes": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_size_t)]),
+    "gtr_score_topk": (C.c_int, [P, C.c_int, C.c_int, P, C.c_int, C.c_int, P, P, P, C.c_size_t, P]),
 }
 
 EXPORTS = tuple(_SIGS)

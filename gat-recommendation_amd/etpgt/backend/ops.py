@@ -137,3 +137,42 @@ class GraphTransformerFn(torch.autograd.Function):
                                          eng.stream()), "scatter_rows")
         grads = eng.flat.grad_views(flat_grad)
         return (None, None, None, None, None, None, None, dtab, *grads)
+
+
+_TOPK_WS: dict = {}
+
+
+def score_topk(se: torch.Tensor, table: torch.Tensor, k: int) -> tuple[torch.Tensor, torch.Tensor]:
+    """Full-catalog scores ``se @ table.T`` and their top-k (base.py:59-78) on the HIP
+    kernel (gtr_score_topk): returns (item ids [B, k] int64, scores [B, k] fp32), best
+    first; ties resolve to the lower item id.  No [B, T] score matrix is materialised."""
+    if isinstance(table, torch.nn.Embedding):
+        table = table.weight
+    if se.device.type != "cuda":
+        raise RuntimeError("predict runs on the MI355X HIP path only (tensors are on CPU)")
+    if se.dim() != 2 or table.dim() != 2 or se.shape[1] != table.shape[1]:
+        raise ValueError(f"session embeddings {tuple(se.shape)} do not match the item table {tuple(table.shape)}")
+    B, D = se.shape
+    T = table.shape[0]
+    if k > T:
+        raise RuntimeError(f"selected index k out of range (k={k} > {T} items)")
+    dev = se.device
+    idx = torch.empty(B, k, dtype=torch.int64, device=dev)
+    sc = torch.empty(B, k, dtype=torch.float32, device=dev)
+    if B == 0:
+        return idx, sc
+    lib = L.lib()
+    nb = C.c_size_t(0)
+    L.check(lib.gtr_topk_workspace_bytes(B, T, k, C.byref(nb)), "topk_workspace_bytes")
+    key = (str(dev), int(nb.value))
+    ws = _TOPK_WS.get(key)
+    if ws is None:
+        _TOPK_WS.clear()
+        ws = torch.empty(int(nb.value), dtype=torch.uint8, device=dev)
+        _TOPK_WS[key] = ws
+    s = se.detach().float().contiguous()
+    t = table.detach().float().contiguous()
+    st = torch.cuda.current_stream(dev).cuda_stream
+    L.check(lib.gtr_score_topk(s.data_ptr(), B, D, t.data_ptr(), T, int(k), idx.data_ptr(), sc.data_ptr(),
+                               ws.data_ptr(), ws.numel(), st), "score_topk")
+    return idx, sc

@@ -13,7 +13,7 @@ from abc import ABC, abstractmethod
 import torch
 import torch.nn as nn
 
-from etpgt.backend.ops import score_loss
+from etpgt.backend.ops import score_loss, score_topk
 
 
 class BaseRecommendationModel(nn.Module, ABC):
@@ -37,9 +37,9 @@ class BaseRecommendationModel(nn.Module, ABC):
 
     def predict(self, session_embeddings: torch.Tensor, k: int = 20) -> torch.Tensor:
         """Top-k item ids by dot product over the full catalog (base.py:59-78; no
-        masking of seen items or row 0, as in the reference)."""
-        scores = torch.matmul(session_embeddings, self.get_item_embeddings().t())
-        return torch.topk(scores, k=k, dim=1)[1]
+        masking of seen items or row 0, as in the reference), fused scoring + top-k
+        on the HIP kernel (gtr_score_topk, MFMA scores, no [B, T] matrix)."""
+        return score_topk(session_embeddings, self.get_item_embeddings(), k)[0]
 
     def compute_loss(self, session_embeddings: torch.Tensor, target_items: torch.Tensor,
                      negative_items: torch.Tensor) -> torch.Tensor:

@@ -33,6 +33,8 @@
  *                     the data-parallel version of that step (one process per GPU);
  *                     the reference has no multi-GPU path.
  *   gtr_readout_grid  partial count of gtr_readout_loss (host sizing).
+ *   gtr_score_topk    base.py:59-78 predict (full-catalog scores + top-k), the
+ *                     Recall@K / NDCG@K evaluation of trainer.py:138-173.
  *
  * Conventions: plain pointers + sizes, no torch types; every
  * pointer is a device pointer unless marked (host); stream is a hipStream_t;
@@ -307,6 +309,17 @@ int gtr_dp_pack(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tai
 /* slot: [T][world] int2 {step, segment-start index} scratch (init to -1).          */
 int gtr_dp_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tail, const gtr_dp_layout* lay,
                 const float* recv, int32_t* slot, const gtr_adam* opt, gtr_stream_t stream);
+
+/* ---- evaluation: full-catalog scoring + top-k (etpgt.model.base.predict) ---------
+ * Replaces base.py:59-78 (scores = se @ item_embedding.weight.T; torch.topk(scores, k))
+ * as called by Trainer.evaluate (trainer.py:138-173) for Recall@K / NDCG@K.
+ * se [B, dim], table [num_items, dim] fp32 row-major; out_idx [B, k] int64 item ids and
+ * out_score [B, k] fp32 scores, best first (score descending, item id ascending on ties;
+ * row 0 and seen items are not masked, as in the reference).  1 <= k <= 128, k <= T.
+ * Workspace (device, caller-provided) of gtr_topk_workspace_bytes(B, T, k) bytes.      */
+int gtr_topk_workspace_bytes(int B, int num_items, int k, size_t* bytes);
+int gtr_score_topk(const float* se, int B, int dim, const float* table, int num_items, int k,
+                   int64_t* out_idx, float* out_score, void* ws, size_t ws_bytes, gtr_stream_t stream);
 
 /* Workgroups of gtr_readout_loss = the number of its loss / BatchNorm-sum partials
  * (gtr_tail.loss_nparts; the last layer's bn_gpart rows).                         */
