@@ -856,6 +856,352 @@ __global__ __launch_bounds__(RO_BLOCK) void k_readout(ReadoutK a) {
   if (tid == 0) reset_counter(a.cnt);
 }
 
+// Large-batch readout (b_cap >= ro_wave_min_b(), D <= 128): wave per session, grid-strided;
+// 16 lanes per row so one wave instruction moves 4 rows (node rows and scoring rows);
+// the scoring rows are streamed in rounds of 4*KQ and the listwise softmax is
+// accumulated online (running max / sum / sum of exp-weighted rows per row group), so
+// every table row is read once.  Semantics and outputs identical to k_readout.
+#define RW_BLOCK 512
+#define RW_WAVES (RW_BLOCK / 64)
+#define RW_NMAX 256  // negatives per session whose raw scores stay in LDS
+
+template <int EPL>
+__device__ __forceinline__ void ld_row(float (&x)[EPL], const float* p, bool act) {
+  if constexpr (EPL == 2) {
+    const float2 t = act ? *reinterpret_cast<const float2*>(p) : make_float2(0.f, 0.f);
+    x[0] = t.x; x[1] = t.y;
+  } else {
+#pragma unroll
+    for (int c = 0; c < EPL / 4; ++c) {
+      const float4 t = act ? reinterpret_cast<const float4*>(p)[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+      x[4 * c] = t.x; x[4 * c + 1] = t.y; x[4 * c + 2] = t.z; x[4 * c + 3] = t.w;
+    }
+  }
+}
+
+template <int EPL>
+__device__ __forceinline__ void st_row(float* p, const float (&x)[EPL]) {
+  if constexpr (EPL == 2) {
+    *reinterpret_cast<float2*>(p) = make_float2(x[0], x[1]);
+  } else {
+#pragma unroll
+    for (int c = 0; c < EPL / 4; ++c)
+      reinterpret_cast<float4*>(p)[c] = make_float4(x[4 * c], x[4 * c + 1], x[4 * c + 2], x[4 * c + 3]);
+  }
+}
+
+// sum over the 4 row groups (lanes l, l^16, l^32, l^48)
+__device__ __forceinline__ float sum_groups(float x) {
+  x += __shfl_xor(x, 16);
+  x += __shfl_xor(x, 32);
+  return x;
+}
+
+// Round r of a session's scoring rows: slot q of row group rg loads negative
+// k = r*4*KQ + q*4 + rg (ids fetched by the first 4*KQ lanes, then shuffled).
+template <int D, int KQ>
+__device__ __forceinline__ void issue_round(float (&rv)[KQ][D / 16], const float* table, const int* negs, int n,
+                                            int r, int lane, int rg, int c0) {
+  constexpr int RND = 4 * KQ;
+  const int kl = r * RND + lane;
+  const int nid = (lane < RND && kl < n) ? negs[kl] : 0;
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) {
+    const int id = __shfl(nid, q * 4 + rg);
+    ld_row<D / 16>(rv[q], table + (size_t)id * D + c0, r * RND + q * 4 + rg < n);
+  }
+}
+
+// Per-session scoring accumulators of one wave (row group rg's share until combined).
+template <int EPL>
+struct ScoreAcc {
+  float dse[EPL];   // BPR part of d loss / d se (sum of -dz * row)
+  float accl[EPL];  // listwise: sum of exp(l - mg) * row (online rescaled)
+  float mg, zg, dpos, bpr_sum;
+};
+
+// Scores of one round's rows (slot q of row group rg = negative k) -> BPR terms and the
+// online listwise softmax; raw listwise scores go to sc (LDS, or coef_neg when sc null).
+template <int D, int KQ>
+__device__ __forceinline__ void consume_round(ScoreAcc<D / 16>& A, const float (&rv)[KQ][D / 16],
+                                              const float (&se)[D / 16], float pos, int r, int n, int rg, bool lead,
+                                              bool use_bpr, bool use_lw, float inv_bn, float w_bpr, float inv_t,
+                                              float* sc, float* coef_row) {
+  constexpr int EPL = D / 16, RND = 4 * KQ;
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) {
+    const int k = r * RND + q * 4 + rg;
+    float d = 0.0f;
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) d += se[e] * rv[q][e];
+    d = group_sum(d, 16);
+    if (k < n) {
+      if (use_bpr) {
+        const float sg = 1.0f / (1.0f + expf(-(pos - d)));
+        if (lead) A.bpr_sum += -logf(sg + 1e-8f);
+        const float dz = -(sg * (1.0f - sg)) / (sg + 1e-8f) * inv_bn * w_bpr;
+        A.dpos += dz;
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) A.dse[e] += -dz * rv[q][e];
+        if (!use_lw && lead) coef_row[k] = -dz;
+      }
+      if (use_lw) {
+        const float l = d * inv_t;
+        const float mn = fmaxf(A.mg, l);
+        const float c = expf(A.mg - mn), p = expf(l - mn);
+        A.zg = A.zg * c + p;
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) A.accl[e] = A.accl[e] * c + p * rv[q][e];
+        A.mg = mn;
+        if (lead) {
+          if (sc) sc[k] = d; else coef_row[k] = d;  // raw score; coefficient once lse is known
+        }
+      }
+    }
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
+  constexpr int EPL = D / 16;              // features per lane (16 lanes per row)
+  constexpr int KQ = 4;                    // row slots per lane per round
+  constexpr int RND = 4 * KQ;              // scoring rows per wave round
+  __shared__ float s_bn[3 * D];            // mean | rstd | unbiased var (prologue)
+  __shared__ float s_gb[2 * D];            // gamma | beta
+  __shared__ float s_scr[2 * RW_BLOCK + D];
+  __shared__ float s_red[RW_WAVES][2 * D];
+  __shared__ float s_loss[RW_WAVES][2];
+  __shared__ float s_sc[RW_WAVES][RW_NMAX];  // raw listwise scores of the wave's session
+  __shared__ int s_flag;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int rg = lane >> 4, c0 = (lane & 15) * EPL;
+  const bool lead = (lane & 15) == 0;
+  const int B = a.bt.hdr[1];
+  const int n = a.bt.n_neg;
+  const uint32_t ctr = a.rng_ctr ? *a.rng_ctr : 0u;
+  const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
+  const uint32_t st = drop_stream(1, (uint32_t)a.L1, ctr);
+  const bool do_fwd = a.flags & GTR_RO_FWD, do_loss = a.flags & GTR_RO_LOSS, do_bwd = a.flags & GTR_RO_BWD;
+  const bool use_lw = a.loss_kind == GTR_LOSS_LISTWISE || a.loss_kind == GTR_LOSS_DUAL;
+  const bool use_bpr = a.loss_kind == GTR_LOSS_BPR || a.loss_kind == GTR_LOSS_DUAL;
+  const float w_lw = a.loss_kind == GTR_LOSS_DUAL ? a.dual_alpha : 1.0f;
+  const float w_bpr = a.loss_kind == GTR_LOSS_DUAL ? 1.0f - a.dual_alpha : 1.0f;
+  const float inv_bn = 1.0f / ((float)B * (float)n);
+  const float inv_b = 1.0f / (float)B;
+  const float inv_t = 1.0f / a.temperature;
+
+  if (do_fwd) {
+    prev_bn_stats<D, RW_BLOCK>(a.train, a.cred, a.bt.hdr[4], a.part, a.stats, a.rmean, a.rvar, a.nbt, a.bn_eps,
+                               a.bn_mom, s_bn, s_bn + D, s_bn + 2 * D, s_scr);
+  } else if (do_bwd) {
+    for (int j = tid; j < D; j += RW_BLOCK) { s_bn[j] = a.stats[j]; s_bn[D + j] = a.stats[D + j]; }
+  }
+  if (do_fwd || do_bwd)
+    for (int j = tid; j < D; j += RW_BLOCK) { s_gb[j] = a.gamma[j]; s_gb[D + j] = a.beta[j]; }
+  for (int j = lane; j < 2 * D; j += 64) s_red[wave][j] = 0.0f;  // this wave's BN-backward sums
+  __syncthreads();
+
+  float lw_sum = 0.0f, bpr_sum = 0.0f;
+
+#pragma unroll 1
+  for (int b = blockIdx.x * RW_WAVES + wave; b < B; b += gridDim.x * RW_WAVES) {
+    const int n0 = a.bt.node_ptr[b], n1 = a.bt.node_ptr[b + 1];
+    const float cnt = (float)(n1 - n0);
+    const int* negs = a.bt.negatives + (size_t)b * n;
+    float tv[EPL], rv[KQ][EPL], rv2[KQ][EPL];
+    if (do_loss) {
+      ld_row<EPL>(tv, a.table + (size_t)a.bt.target[b] * D + c0, true);
+      issue_round<D, KQ>(rv, a.table, negs, n, 0, lane, rg, c0);
+    }
+    // ---- session embedding: mean over node rows of drop(bn(out) + xin)
+    float se[EPL];
+    if (do_fwd) {
+      float acc[EPL];
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) acc[e] = 0.0f;
+#pragma unroll 1
+      for (int i = n0 + rg; i < n1; i += 4) {
+        float ov[EPL], xv[EPL];
+        ld_row<EPL>(ov, a.out + (size_t)i * D + c0, true);
+        ld_row<EPL>(xv, a.xin + (size_t)i * D + c0, true);
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) {
+          const int j = c0 + e;
+          float y = (ov[e] - s_bn[j]) * s_bn[D + j] * s_gb[j] + s_gb[D + j];
+          y = y + xv[e];
+          acc[e] += y * dr.mul(st, (uint32_t)((size_t)i * D + j));
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) se[e] = sum_groups(acc[e]) / cnt;
+      if (rg == 0) st_row<EPL>(a.se + (size_t)b * D + c0, se);
+    } else {
+      ld_row<EPL>(se, a.se + (size_t)b * D + c0, true);
+    }
+
+    float dse[EPL];
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) dse[e] = 0.0f;
+    if (do_loss) {
+      float pos = 0.0f;
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) pos += se[e] * tv[e];
+      pos = group_sum(pos, 16);
+      ScoreAcc<EPL> A;
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) { A.dse[e] = 0.0f; A.accl[e] = 0.0f; }
+      A.mg = rg == 0 ? pos * inv_t : -INFINITY;
+      A.zg = rg == 0 ? 1.0f : 0.0f;
+      A.dpos = 0.0f;
+      A.bpr_sum = 0.0f;
+      float* coef_row = a.coef_neg + (size_t)b * n;
+      float* sc = n <= RW_NMAX ? s_sc[wave] : nullptr;
+      const int nr = (n + RND - 1) / RND;
+      // double-buffered rounds: round r+1's rows are in flight while round r is scored
+#pragma unroll 1
+      for (int r = 0; r < nr; r += 2) {
+        if (r + 1 < nr) issue_round<D, KQ>(rv2, a.table, negs, n, r + 1, lane, rg, c0);
+        consume_round<D, KQ>(A, rv, se, pos, r, n, rg, lead, use_bpr, use_lw, inv_bn, w_bpr, inv_t, sc, coef_row);
+        if (r + 1 < nr) {
+          if (r + 2 < nr) issue_round<D, KQ>(rv, a.table, negs, n, r + 2, lane, rg, c0);
+          consume_round<D, KQ>(A, rv2, se, pos, r + 1, n, rg, lead, use_bpr, use_lw, inv_bn, w_bpr, inv_t, sc,
+                               coef_row);
+        }
+      }
+      bpr_sum += A.bpr_sum;
+      float dpos = sum_groups(A.dpos);
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) dse[e] = sum_groups(A.dse[e]);
+      if (use_lw) {
+        float M = fmaxf(A.mg, __shfl_xor(A.mg, 16));
+        M = fmaxf(M, __shfl_xor(M, 32));
+        const float f = A.zg > 0.0f ? expf(A.mg - M) : 0.0f;
+        const float Z = sum_groups(A.zg * f);
+        const float lse = M + logf(Z);
+        if (lane == 0) lw_sum += lse - pos * inv_t;
+        dpos += (expf(pos * inv_t - lse) - 1.0f) * inv_b * inv_t * w_lw;
+        const float cf = inv_b * inv_t * w_lw / Z;
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) dse[e] += sum_groups(A.accl[e] * f) * cf;
+        if (sc) {
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll 1
+          for (int k = lane; k < n; k += 64) {
+            const float d = sc[k];
+            float cb = expf(d * inv_t - lse) * inv_b * inv_t * w_lw;
+            if (use_bpr) {
+              const float sg = 1.0f / (1.0f + expf(-(pos - d)));
+              cb += (sg * (1.0f - sg)) / (sg + 1e-8f) * inv_bn * w_bpr;
+            }
+            coef_row[k] = cb;
+          }
+          __builtin_amdgcn_wave_barrier();  // sc is reused by the wave's next session
+        } else if (lead) {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this lane's raw-score stores
+#pragma unroll 1
+          for (int k = rg; k < n; k += 4) {
+            const float d = coef_row[k];
+            float cb = expf(d * inv_t - lse) * inv_b * inv_t * w_lw;
+            if (use_bpr) {
+              const float sg = 1.0f / (1.0f + expf(-(pos - d)));
+              cb += (sg * (1.0f - sg)) / (sg + 1e-8f) * inv_bn * w_bpr;
+            }
+            coef_row[k] = cb;
+          }
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) dse[e] += dpos * tv[e];
+      if (lane == 0) a.coef_tgt[b] = dpos;
+      if (rg == 0 && a.dse_out) st_row<EPL>(a.dse_out + (size_t)b * D + c0, dse);
+    } else if (do_bwd) {
+      ld_row<EPL>(dse, a.dse_in + (size_t)b * D + c0, true);
+    }
+
+    // ---- readout backward into the node rows + the last BatchNorm's backward sums
+    if (do_bwd) {
+      const float inv_cnt = 1.0f / cnt;
+      float gs[EPL], gx[EPL];
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) { gs[e] = 0.0f; gx[e] = 0.0f; }
+#pragma unroll 1
+      for (int i = n0 + rg; i < n1; i += 4) {
+        float ov[EPL], dyv[EPL];
+        ld_row<EPL>(ov, a.out + (size_t)i * D + c0, true);
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) {
+          const int j = c0 + e;
+          dyv[e] = dse[e] * inv_cnt * dr.mul(st, (uint32_t)((size_t)i * D + j));
+          const float xh = (ov[e] - s_bn[j]) * s_bn[D + j];
+          gs[e] += dyv[e];
+          gx[e] += dyv[e] * xh;
+        }
+        st_row<EPL>(a.dy + (size_t)i * D + c0, dyv);
+      }
+      // fold into the wave's running sums (sessions in order, row groups by xor tree)
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {
+        const float g1 = sum_groups(gs[e]), g2 = sum_groups(gx[e]);
+        if (rg == 0) { s_red[wave][c0 + e] += g1; s_red[wave][D + c0 + e] += g2; }
+      }
+    }
+  }
+
+  if (!(do_loss || do_bwd)) return;
+  // ---- block partials in fixed order (waves)
+  const float bsum = wave_sum(bpr_sum);
+  if (lane == 0) { s_loss[wave][0] = lw_sum * (w_lw * inv_b); s_loss[wave][1] = bsum * (w_bpr * inv_bn); }
+  __syncthreads();
+  if (do_loss && tid < 2) {
+    float acc = 0.0f;
+    for (int w = 0; w < RW_WAVES; ++w) acc += s_loss[w][tid];
+    a.loss_part[(size_t)blockIdx.x * 2 + tid] = acc;
+  }
+  if (do_bwd) {
+    for (int j = tid; j < 2 * D; j += RW_BLOCK) {
+      float acc = 0.0f;
+      for (int w = 0; w < RW_WAVES; ++w) acc += s_red[w][j];
+      a.gpart[(size_t)blockIdx.x * 2 * D + j] = acc;
+    }
+  }
+  if (!a.fin) return;
+  if (!arrive_last(a.cnt, gridDim.x, &s_flag)) return;
+  if (do_loss && tid == 0) {
+    float loss = 0.0f;
+    for (int q = 0; q < (int)gridDim.x; ++q) loss += a.loss_part[(size_t)q * 2] + a.loss_part[(size_t)q * 2 + 1];
+    a.loss_out[0] = loss;
+  }
+  if (do_bwd) {
+    // NSL slices of the partials per column, summed in fixed order
+    constexpr int NSL = RW_BLOCK / (2 * D) >= 1 ? RW_BLOCK / (2 * D) : 1;
+    const int j = tid % (2 * D), sl = tid / (2 * D);
+    float acc = 0.0f;
+    if (sl < NSL) {
+#pragma unroll 8
+      for (int q = sl; q < (int)gridDim.x; q += NSL) acc += a.gpart[(size_t)q * 2 * D + j];
+    }
+    __syncthreads();
+    float* red = s_scr;  // >= NSL * 2D floats (NSL * 2D <= RW_BLOCK)
+    if (sl < NSL) red[sl * 2 * D + j] = acc;
+    __syncthreads();
+    for (int jj = tid; jj < 2 * D; jj += RW_BLOCK) {
+      float t = 0.0f;
+      for (int q = 0; q < NSL; ++q) t += red[q * 2 * D + jj];
+      a.gsum[jj] = t;
+    }
+  }
+  if (tid == 0) reset_counter(a.cnt);
+}
+
+// Sessions per batch from which the wave-per-session readout runs (env GTR_RO_WAVE_MIN_B
+// overrides, for tests); below it the block-per-session kernel has the lower latency.
+int ro_wave_min_b() {
+  const char* e = getenv("GTR_RO_WAVE_MIN_B");
+  return e ? atoi(e) : 2048;
+}
+
 bool check_dims(const gtr_config* c, const char* fn) {
   const int D = c->dim, H = c->heads;
   if (!(D == 32 || D == 64 || D == 128 || D == 256)) {
@@ -978,6 +1324,15 @@ extern "C" int gtr_readout_loss(const gtr_config* cfg, const gtr_batch* bt, cons
   k.dy = L.dy; k.gpart = L.bn_gpart; k.gsum = L.bn_gsum;
   const int grid = gtr_readout_grid(bt->b_cap);
   hipStream_t s = (hipStream_t)stream;
+  if (bt->b_cap >= ro_wave_min_b() && cfg->dim <= 128) {
+    switch (cfg->dim) {
+      case 32: hipLaunchKernelGGL(k_readout_wave<32>, dim3(grid), dim3(RW_BLOCK), 0, s, k); break;
+      case 64: hipLaunchKernelGGL(k_readout_wave<64>, dim3(grid), dim3(RW_BLOCK), 0, s, k); break;
+      default: hipLaunchKernelGGL(k_readout_wave<128>, dim3(grid), dim3(RW_BLOCK), 0, s, k); break;
+    }
+    GTR_HIP_CHECK_LAUNCH();
+    return GTR_OK;
+  }
   switch (cfg->dim) {
     case 32: hipLaunchKernelGGL(k_readout<32>, dim3(grid), dim3(RO_BLOCK), 0, s, k); break;
     case 64: hipLaunchKernelGGL(k_readout<64>, dim3(grid), dim3(RO_BLOCK), 0, s, k); break;

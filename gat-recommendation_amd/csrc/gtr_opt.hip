@@ -277,10 +277,163 @@ struct TailK {
   gtr_tail tl;
   gtr_adam opt;
   int T, nb_rows, nb_small, nb_sweep;
+  int windowed, pad_w;  // 1: rows part = one block per TW-slot window of the sorted list
   int64_t nvec;
   int vpr_log2, nseg;
   gtr_segment segs[GTR_SMALL_MAX_SEG];
 };
+
+
+// ---- large batches: windowed segmented sums -----------------------------------------
+// The sorted contribution list is cut into windows of TW slots.  A row's segment that
+// starts in window w is summed by window w's block over its in-window part; the part
+// lying in each following window w' (it can span many: hot Zipf items collect thousands
+// of node contributions) is a "carry" summed beforehand by k_tail_carry, so no thread
+// walks a long segment serially.  Sums run in slot order inside a piece and pieces are
+// added in window order: deterministic.
+#define TW 128
+
+// Sum of contributions in slots [s, e) for column float4 `gl` by the C4 = D/4 lanes of
+// one group (group base lane gb): slot ids are fetched one per lane, decoded to a source
+// row (dx0 node row, or se session row for target / negative slots) + coefficient,
+// then broadcast 8 at a time so 8 row loads are in flight per lane.
+template <int D>
+__device__ __forceinline__ float4 piece_sum(const gtr_batch& bt, const int32_t* svals, int s, int e, const float* dx0,
+                                            const float* se, const float* coef_tgt, const float* coef_neg, int gl,
+                                            int gb) {
+  constexpr int C4 = D / 4;
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int base = s; base < e; base += C4) {
+    const int cnt = min(C4, e - base);
+    int code = 0;
+    float cf = 0.0f;
+    if (gl < cnt) {
+      const int j = svals[base + gl];
+      if (j < bt.n_cap) {
+        code = j;
+        cf = 1.0f;
+      } else if (j < bt.n_cap + bt.b_cap) {
+        const int b = j - bt.n_cap;
+        code = (int)(0x80000000u | (uint32_t)b);
+        cf = coef_tgt[b];
+      } else {
+        const int q = j - bt.n_cap - bt.b_cap;
+        code = (int)(0x80000000u | (uint32_t)(q / bt.n_neg));
+        cf = coef_neg[q];
+      }
+    }
+    for (int q0 = 0; q0 < cnt; q0 += 8) {
+      float4 v[8];
+      float f[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int cq = __shfl(code, gb + ((q0 + u) & (C4 - 1)));
+        f[u] = __shfl(cf, gb + ((q0 + u) & (C4 - 1)));
+        const float* src = cq < 0 ? se + (size_t)(cq & 0x7FFFFFFF) * D : dx0 + (size_t)cq * D;
+        v[u] = q0 + u < cnt ? reinterpret_cast<const float4*>(src)[gl] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (q0 + u < cnt) {
+          g.x += f[u] * v[u].x; g.y += f[u] * v[u].y; g.z += f[u] * v[u].z; g.w += f[u] * v[u].w;
+        }
+      }
+    }
+  }
+  return g;
+}
+
+// Carry of window w (>= 1) whose first slot continues the previous window's segment:
+// the sum over [w*TW, first key change in w), split over the block's groups in fixed
+// contiguous pieces and combined in group order.  carry: [nwin][D].
+template <int D>
+__global__ __launch_bounds__(GTR_BLOCK) void k_tail_carry(gtr_batch bt, int T, gtr_tail tl) {
+  constexpr int C4 = D / 4, NG = GTR_BLOCK / C4;
+  __shared__ int s_end;
+  __shared__ __attribute__((aligned(16))) float4 s_part[NG][C4];
+  const int tid = threadIdx.x;
+  const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
+  const int w = blockIdx.x + 1;
+  const int w0 = w * TW, w1 = min(w0 + TW, m_cap);
+  const int key = tl.skeys[w0];
+  if (key <= 0 || key >= T || tl.skeys[w0 - 1] != key) return;  // block-uniform
+  if (tid == 0) s_end = w1;
+  __syncthreads();
+  if (tid < TW && w0 + tid < w1 && tl.skeys[w0 + tid] != key) atomicMin(&s_end, w0 + tid);
+  __syncthreads();
+  const int e = s_end;
+  const int grp = tid / C4, gl = tid % C4;
+  const int len = e - w0, per = (len + NG - 1) / NG;
+  const int ps = min(e, w0 + grp * per), pe = min(e, ps + per);
+  s_part[grp][gl] = piece_sum<D>(bt, tl.svals, ps, pe, tl.dx0, tl.se, tl.coef_tgt, tl.coef_neg, gl, grp * C4 % 64);
+  __syncthreads();
+  if (tid < C4) {
+    float4 g = s_part[0][tid];
+    for (int q = 1; q < NG; ++q) {
+      const float4 t = s_part[q][tid];
+      g.x += t.x; g.y += t.y; g.z += t.z; g.w += t.w;
+    }
+    reinterpret_cast<float4*>(tl.carry)[(size_t)w * C4 + tid] = g;
+  }
+}
+
+// Rows part of the tail for window w = blk: every segment starting in the window is
+// summed (in-window piece + carries of the following windows) and AdamW-updated.
+template <int D>
+__device__ __forceinline__ void window_rows(int w, const gtr_batch& bt, int T, const gtr_tail& tl, const AdamStep& st) {
+  constexpr int C4 = D / 4, NG = GTR_BLOCK / C4;
+  __shared__ int s_bnd[TW + 1];
+  __shared__ int s_nb;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
+  const int w0 = w * TW, w1 = min(w0 + TW, m_cap);
+  // boundaries (key changes) of the window in slot order: ballot + prefix per wave
+  if (tid == 0) s_nb = 0;
+  __syncthreads();
+  const int i = w0 + tid;
+  bool bnd = false;
+  if (tid < TW && i < w1) bnd = (i == 0) || tl.skeys[i] != tl.skeys[i - 1];
+  __shared__ int s_wcnt[GTR_WAVES];
+  const unsigned long long bal = __ballot(bnd);
+  if (lane == 0) s_wcnt[tid >> 6] = __popcll(bal);
+  __syncthreads();
+  int off = 0;
+  for (int q = 0; q < (tid >> 6); ++q) off += s_wcnt[q];
+  if (bnd) s_bnd[off + __popcll(bal & ((1ull << lane) - 1ull))] = i;
+  if (tid == 0) {
+    int tot = 0;
+    for (int q = 0; q < GTR_WAVES; ++q) tot += s_wcnt[q];
+    s_nb = tot;
+  }
+  __syncthreads();
+  const int nb = s_nb;
+  const int grp = tid / C4, gl = tid % C4, gb = grp * C4 % 64;
+  for (int q = grp; q < nb; q += NG) {
+    const int s0 = s_bnd[q];
+    const int key = tl.skeys[s0];
+    if (key <= 0 || key >= T) continue;
+    const int e = q + 1 < nb ? s_bnd[q + 1] : w1;
+    const size_t base = (size_t)key * C4 + gl;
+    float4 pv = reinterpret_cast<const float4*>(tl.table)[base];
+    float4 mv = reinterpret_cast<const float4*>(tl.table_m)[base];
+    float4 vv = reinterpret_cast<const float4*>(tl.table_v)[base];
+    float4 g = piece_sum<D>(bt, tl.svals, s0, e, tl.dx0, tl.se, tl.coef_tgt, tl.coef_neg, gl, gb);
+    if (e == w1) {  // the segment may continue: add the carries in window order
+      for (int w2 = w + 1; w2 * TW < m_cap && tl.skeys[w2 * TW] == key; ++w2) {
+        const float4 c = reinterpret_cast<const float4*>(tl.carry)[(size_t)w2 * C4 + gl];
+        g.x += c.x; g.y += c.y; g.z += c.z; g.w += c.w;
+        if (tl.skeys[min((w2 + 1) * TW, m_cap) - 1] != key) break;
+      }
+    }
+    st.apply(pv.x, mv.x, vv.x, g.x);
+    st.apply(pv.y, mv.y, vv.y, g.y);
+    st.apply(pv.z, mv.z, vv.z, g.z);
+    st.apply(pv.w, mv.w, vv.w, g.w);
+    reinterpret_cast<float4*>(tl.table)[base] = pv;
+    reinterpret_cast<float4*>(tl.table_m)[base] = mv;
+    reinterpret_cast<float4*>(tl.table_v)[base] = vv;
+  }
+}
 
 template <int D>
 __global__ __launch_bounds__(GTR_BLOCK) void k_step_tail(TailK a) {
@@ -296,6 +449,10 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_step_tail(TailK a) {
   __syncthreads();
   const AdamStep st = s_st;
   const int blk = blockIdx.x;
+  if (blk < a.nb_rows && a.windowed) {
+    window_rows<D>(blk, a.bt, a.T, a.tl, st);
+    return;
+  }
   if (blk < a.nb_rows) {
     rows_body<D>(blk * GTR_BLOCK + tid, a.bt, a.T, a.tl.skeys, a.tl.svals, a.tl.dx0, a.tl.se, a.tl.coef_tgt,
                  a.tl.coef_neg, a.tl.table, a.tl.table_m, a.tl.table_v, nullptr, st);
@@ -570,6 +727,10 @@ bool dim_ok(int D) { return D == 32 || D == 64 || D == 128 || D == 256; }
 
 extern "C" {
 
+int gtr_tail_carry_floats(int m_cap, int dim) {
+  return m_cap > GTR_BEGIN_MCAP ? ((m_cap + TW - 1) / TW) * dim : 0;
+}
+
 int gtr_version(void) { return 100; }
 int gtr_readout_grid(int b_cap) { return b_cap < 1 ? 1 : (b_cap > 256 ? 256 : b_cap); }
 int gtr_abi_version(void) { return GTR_ABI_VERSION; }
@@ -756,7 +917,26 @@ int gtr_step_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* t
   k.opt = *opt;
   k.T = num_items;
   const int m_cap = bt->n_cap + bt->b_cap * (1 + bt->n_neg);
-  k.nb_rows = (int)(((int64_t)m_cap * (dim / 4) + GTR_BLOCK - 1) / GTR_BLOCK);
+  hipStream_t s = (hipStream_t)stream;
+  k.windowed = m_cap > GTR_BEGIN_MCAP ? 1 : 0;
+  if (k.windowed) {
+    if (!t.carry) { set_error("gtr_step_tail: large batch (m_cap > %d) needs the carry scratch", GTR_BEGIN_MCAP); return GTR_E_ARG; }
+    const int nwin = (m_cap + TW - 1) / TW;
+    k.nb_rows = nwin;
+    if (nwin > 1) {
+#define GTR_CARRY(DD) hipLaunchKernelGGL(k_tail_carry<DD>, dim3(nwin - 1), dim3(GTR_BLOCK), 0, s, *bt, num_items, t)
+      switch (dim) {
+        case 32: GTR_CARRY(32); break;
+        case 64: GTR_CARRY(64); break;
+        case 128: GTR_CARRY(128); break;
+        default: GTR_CARRY(256); break;
+      }
+#undef GTR_CARRY
+      GTR_HIP_CHECK_LAUNCH();
+    }
+  } else {
+    k.nb_rows = (int)(((int64_t)m_cap * (dim / 4) + GTR_BLOCK - 1) / GTR_BLOCK);
+  }
   k.nb_small = nseg > 0 ? (int)((t.flat_total + GTR_BLOCK - 1) / GTR_BLOCK) : 0;
   if (k.nb_small == 0 && t.loss_part) k.nb_small = 1;
   k.nvec = (int64_t)num_items * dim / 4;
@@ -767,7 +947,6 @@ int gtr_step_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* t
   k.nseg = nseg;
   for (int i = 0; i < nseg; ++i) k.segs[i] = segs[i];
   const int grid = k.nb_rows + k.nb_small + k.nb_sweep;
-  hipStream_t s = (hipStream_t)stream;
   switch (dim) {
     case 32: hipLaunchKernelGGL(k_step_tail<32>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
     case 64: hipLaunchKernelGGL(k_step_tail<64>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;

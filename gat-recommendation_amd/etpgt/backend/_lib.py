@@ -80,7 +80,7 @@ class GtrTail(C.Structure):
         ("skeys", P), ("svals", P), ("dx0", P), ("se", P), ("coef_tgt", P), ("coef_neg", P),
         ("table", P), ("table_m", P), ("table_v", P), ("stamp", P),
         ("flat", P), ("flat_m", P), ("flat_v", P), ("flat_total", i64),
-        ("loss_part", P), ("loss_out", P), ("loss_nparts", i32), ("pad0", i32),
+        ("loss_part", P), ("loss_out", P), ("loss_nparts", i32), ("pad0", i32), ("carry", P),
     ]
 
 
@@ -118,6 +118,7 @@ _SIGS = {
     "gtr_dp_tail": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P]),
     "gtr_step_begin": (C.c_int, [P, C.c_int, P, P, P, P, P, P, P, P, C.c_size_t, P]),
     "gtr_step_tail": (C.c_int, [P, C.c_int, C.c_int, P, P, C.c_int, P, P]),
+    "gtr_tail_carry_floats": (C.c_int, [C.c_int, C.c_int]),
     "gtr_topk_workspace_bytes": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_size_t)]),
     "gtr_score_topk": (C.c_int, [P, C.c_int, C.c_int, P, C.c_int, C.c_int, P, P, P, C.c_size_t, P]),
 }

@@ -120,6 +120,9 @@ class FusedTrainStep:
         t.loss_part = ws.loss_part.data_ptr() if self.cfg.consumer_reduce else None
         t.loss_out = ws.loss_out.data_ptr()
         t.loss_nparts = readout_grid(caps.b_cap)
+        nc = int(L.lib().gtr_tail_carry_floats(m_cap, eng.D))
+        self.carry = torch.zeros(max(nc, 4), dtype=torch.float32, device=self.dev) if nc > 0 else None
+        t.carry = self.carry.data_ptr() if self.carry is not None else None
         self.tail = t
         if self.data_parallel:
             from etpgt.train.distributed import DpExchange

@@ -280,10 +280,17 @@ typedef struct gtr_tail {
   float* loss_out;        /* [1] loss of the step                                   */
   int32_t loss_nparts;
   int32_t pad0;
+  float* carry;           /* large batches (m_cap > 8192): [gtr_tail_carry_floats] scratch
+                             for segment pieces spanning windows of the sorted list; else NULL */
 } gtr_tail;
+
+/* Floats of gtr_tail.carry needed at contribution capacity m_cap (0: not used).      */
+int gtr_tail_carry_floats(int m_cap, int dim);
 
 /* One launch: AdamW of the touched table rows (segmented sums), of the untouched
  * rows (zero gradient) and of every small parameter (segments), plus the loss sum.
+ * Large batches (m_cap > 8192) add a first launch summing the segment pieces that
+ * span windows of the sorted list (tail->carry); the rows part then runs per window.
  * opt->step_offset must be 0 (runs after gtr_step_begin).                        */
 int gtr_step_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tail,
                   const gtr_segment* segs, int nseg, const gtr_adam* opt, gtr_stream_t stream);

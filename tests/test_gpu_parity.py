@@ -244,3 +244,26 @@ def test_table_untouched_rows_follow_dense_adamw():
     # rows never in a batch: pure decay + zero-gradient moment updates, elementwise
     assert_close(m.item_embedding.weight[untouched.cuda()], ref.item_embedding.weight[untouched], rtol=1e-5,
                  name="untouched rows")
+
+
+@pytest.mark.parametrize("D,H,K,loss", [(64, 1, 0, "model_bpr"), (128, 4, 16, "listwise"), (32, 2, 0, "dual")])
+def test_train_grads_wave_readout(D, H, K, loss, monkeypatch):
+    """The large-batch readout kernel (wave per session, online listwise softmax),
+    forced at B = 32: forward (RO_FWD), loss (RO_LOSS) and readout backward (RO_BWD)
+    as separate launches of the autograd path."""
+    monkeypatch.setenv("GTR_RO_WAVE_MIN_B", "1")
+    test_train_grads(D, H, K, loss)
+
+
+@pytest.mark.parametrize("D,H,K,loss", [(64, 1, 0, "bpr"), (128, 4, 16, "listwise"), (32, 2, 0, "dual")])
+def test_fused_steps_wave_readout(D, H, K, loss, monkeypatch):
+    """Fused steps through the wave-per-session readout (FWD|LOSS|BWD in one launch)."""
+    monkeypatch.setenv("GTR_RO_WAVE_MIN_B", "1")
+    _fused_vs_reference(D, H, K, loss, "adamw", True, B=64, steps=3)
+
+
+def test_fused_steps_wave_readout_large_batch(monkeypatch):
+    """B = 2100 at the default switch-over: > 64 row groups, radix-sort begin, wave readout
+    with several sessions per wave (grid-stride), 100 listwise negatives."""
+    monkeypatch.delenv("GTR_RO_WAVE_MIN_B", raising=False)
+    _fused_vs_reference(64, 2, 0, "listwise", "adamw", True, B=2100, steps=2)
