@@ -71,13 +71,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal on a one-GPU box (GTR_SHARE_DEVICE=1): every rank on cuda:0, gloo transport
+    share = os.environ.get("GTR_SHARE_DEVICE") == "1"
+    backend = "gloo" if share else "nccl"
+    dev_index = 0 if share else local
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev_index)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group("gloo")
+    dev = torch.device("cuda", dev_index)
     torch.cuda.set_device(dev)
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")
     cfg = CONFIGS[args.config]
 
     t0 = time.time()
@@ -109,13 +117,14 @@ def main():
     elapsed = time.perf_counter() - t_start
     gpu_ms = ev0.elapsed_time(ev1)
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=coll_dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss)
     replicas_identical = None
     if world > 1:  # data parallel: every rank must hold the same parameters
         chk = torch.stack([step.model.item_embedding.weight.double().sum(), step.eng.flat.flat.double().sum()])
+        chk = chk.to(coll_dev)
         allc = [torch.zeros_like(chk) for _ in range(world)]
         torch.distributed.all_gather(allc, chk)
         replicas_identical = all(torch.equal(allc[0], c) for c in allc)
@@ -127,10 +136,10 @@ def main():
     tail_ms = measure_tail(step, args.steps)
     alg_bytes = tail_bytes(step, T, D, touched)
     achieved = alg_bytes / (tail_ms * 1e-3) / 1e9
-    traffic, traffic_src = load_traffic(args.config)
+    traffic, traffic_src = load_traffic(args.config) if step.dp is None else (None, None)
 
     cpu = None
-    if rank == 0 and args.cpu_seconds > 0:
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(cfg, batches, T, args.cpu_seconds)
     gather = None
     if rank == 0 and world == 1 and args.gather_batch > 0:
@@ -162,6 +171,7 @@ def main():
                 "nodes_per_session": round(st["nodes_per_session"], 3),
                 "edges_per_session": round(st["edges_per_session"], 3),
                 "parallelism": f"dp{world}",
+                "transport": "rccl" if backend == "nccl" else "gloo (shared-device rehearsal)",
                 "dp_exchange": step.dp is not None,
                 "hip_graph": not args.no_graph,
                 "gpu_ms_per_step_events": round(gpu_ms / args.steps, 4),
@@ -170,7 +180,9 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_step_tail (AdamW over all item-table rows + small parameters)",
+                "kernel": ("k_dp_tail (rank-averaged AdamW over all item-table rows + small parameters)"
+                           if step.dp is not None else
+                           "k_step_tail (AdamW over all item-table rows + small parameters)"),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -214,7 +226,8 @@ def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, us
     step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, loss=cfg["loss"], use_graph=use_graph,
                           data_parallel=data_parallel)
     caps = Caps(max(b.num_nodes for b in batches), B, max(b.num_edges for b in batches), cfg["n_neg"])
-    step._bind(caps)
+    step._bind(caps)  # data parallel: the ranks agree on the largest capacities
+    caps = step.caps
     staged = [torch.from_numpy(b.packed(caps)[1]).to(dev) for b in batches]
     touched = float(np.mean([len(set(b.x.tolist()) | set(b.target_item.tolist()) | set(b.negative_items.tolist()))
                              for b in batches]))
@@ -253,8 +266,11 @@ def measure_tail(step, iters) -> float:
     for _ in range(n):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(main)
-        L.check(lib.gtr_step_tail(C.byref(step.bs), eng.T, eng.D, C.byref(step.tail), step.segs, step.nseg,
-                                  C.byref(step.adam), main.cuda_stream), "step_tail")
+        if step.dp is not None:  # data parallel: the rank-averaged tail (k_dp_stamp + k_dp_tail)
+            step.dp.launch_tail(step.bs, main.cuda_stream)
+        else:
+            L.check(lib.gtr_step_tail(C.byref(step.bs), eng.T, eng.D, C.byref(step.tail), step.segs, step.nseg,
+                                      C.byref(step.adam), main.cuda_stream), "step_tail")
         e1.record(main)
         durs.append((e0, e1))
     torch.cuda.synchronize()

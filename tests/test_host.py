@@ -241,3 +241,36 @@ def test_metrics_and_seed():
     p = torch.tensor([[1, 2, 3, 4, 5], [6, 7, 8, 9, 10], [11, 12, 13, 14, 15]])
     assert compute_recall_at_k(p, torch.tensor([2, 9, 20]), 5) == pytest.approx(2 / 3)
     assert compute_ndcg_at_k(p, torch.tensor([1, 9, 20]), 5) == pytest.approx(0.4769, abs=1e-4)
+
+
+def test_c1_pipeline_batch_semantics():
+    """run_full_pipeline.py:85-179 batch construction: sorted unique context items as
+    nodes, induced co-event edges in both directions (self loops if none), the first
+    n catalogue items outside the session as negatives, remapped ids."""
+    from etpgt.pipeline import build_co_event_graph, create_batch_from_sessions, generate_synthetic_events
+
+    ev = generate_synthetic_events(num_sessions=100, num_items=1000, seed=42)
+    assert ev["session_id"].nunique() == 100
+    lens = ev.groupby("session_id").size()
+    assert lens.min() >= 3 and lens.max() <= 20
+    g = build_co_event_graph(ev)
+    assert bool((g["item_i"] <= g["item_j"]).all()) and bool((g["count"] >= 1).all())
+    batch, T = create_batch_from_sessions(ev, g, batch_size=16, num_negatives=5)
+    assert T == ev["itemid"].nunique()
+    assert batch.num_graphs == 16 and tuple(batch.negative_items.shape) == (16, 5)
+    ptr = batch.ptr.numpy()
+    ei = batch.edge_index.numpy()
+    items = sorted(ev["itemid"].unique())
+    idx = {it: k for k, it in enumerate(items)}
+    for b, sid in enumerate(ev["session_id"].unique()[:16]):
+        sd = ev[ev["session_id"] == sid].sort_values("timestamp", kind="stable")["itemid"].to_numpy()
+        x = batch.x.numpy()[ptr[b]:ptr[b + 1]]
+        assert x.tolist() == sorted({idx[i] for i in sd[:-1]})
+        assert int(batch.target_item[b]) == idx[sd[-1]]
+        seen = {idx[i] for i in sd}
+        assert batch.negative_items[b].tolist() == [i for i in range(T) if i not in seen][:5]
+        m = (ei[0] >= ptr[b]) & (ei[0] < ptr[b + 1])
+        e = ei[:, m] - ptr[b]
+        pairs = set(zip(e[0].tolist(), e[1].tolist()))
+        assert all((d, s) in pairs for s, d in pairs)  # both directions
+        assert e.shape[1] > 0
