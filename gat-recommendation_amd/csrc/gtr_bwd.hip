@@ -47,6 +47,8 @@ struct ConvBwdK {
   float* p_gsum;
   uint32_t* p_cnt;
   float* dx0;
+  gtr_sweep sw;         // untouched-row AdamW slice run by blocks >= main_grid
+  int sw_slot, main_grid;
 };
 
 // Destination-row backward: BatchNorm backward, beta gate, softmax backward, dQ, dS.
@@ -189,6 +191,10 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
   float* s_bnp = sm + G::B_BNP;
   int* s_flag = reinterpret_cast<int*>(sm + G::B_FLAG);
 
+  if ((int)blockIdx.x >= a.main_grid) {  // extra workgroups: untouched-row AdamW slice
+    sweep_slice(a.sw, a.sw_slot, blockIdx.x - a.main_grid, gridDim.x - a.main_grid);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   GTR_PH(a.layer, 0);
   const int Gn = a.bt.hdr[4];
@@ -667,8 +673,17 @@ extern "C" int gtr_conv_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     k.p_gsum = P.bn_gsum; k.p_cnt = P.cnt + 1;
   }
   k.dx0 = dx0;
-  const int grid = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;
+  int grid = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;
   if (grid <= 0) return GTR_OK;
+  k.main_grid = grid;
+  {
+    const int slot = 2 * cfg->num_layers - l;  // after the forward slots and the readout's
+    if (cfg->sweep && slot < GTR_SWEEP_SLOTS && cfg->sweep->bounds[slot + 1] > cfg->sweep->bounds[slot]) {
+      k.sw = *cfg->sweep;
+      k.sw_slot = slot;
+      grid += cfg->sweep->blocks;
+    }
+  }
   hipStream_t s = (hipStream_t)stream;
 #define GTR_BWD(DD) set_lds_limit<DD>(k_conv_bwd<DD>, (size_t)LayerGeom<DD>::B_WORDS * 4); \
   hipLaunchKernelGGL(k_conv_bwd<DD>, dim3(grid), dim3(CONV_BLOCK), \

@@ -153,6 +153,56 @@ struct AdamStep {
   }
 };
 
+// Untouched-row AdamW slice of a fused-step launch (see gtr_sweep in gtr.h): workgroup
+// blk of nblk streams float4s of rows [bounds[slot], bounds[slot+1]) whose stamp is not
+// the current step, SW_U float4 per thread in flight per tensor (one workgroup per CU
+// next to the layer kernels' LDS-heavy groups, so each thread keeps several in flight).
+#define SW_U 4
+__device__ __forceinline__ void sweep_slice(const gtr_sweep& sw, int slot, int blk, int nblk) {
+  __shared__ AdamStep s_sw_st;
+  __shared__ int32_t s_sw_t;
+  const int64_t r0 = sw.bounds[slot], r1 = sw.bounds[slot + 1];
+  if (r1 <= r0) return;
+  if (threadIdx.x == 0) {
+    const int64_t t = *sw.opt.step_dev + sw.opt.step_offset;
+    s_sw_st.init(sw.opt, t);
+    s_sw_t = (int32_t)t;
+  }
+  __syncthreads();
+  const AdamStep st = s_sw_st;
+  const int32_t tcur = s_sw_t;
+  int lg = 0;
+  while ((1 << lg) < sw.dim / 4) ++lg;
+  const int64_t v0 = r0 << lg, v1 = r1 << lg;
+  const int64_t stride = (int64_t)nblk * blockDim.x;
+  float4* P = reinterpret_cast<float4*>(sw.table);
+  float4* M = reinterpret_cast<float4*>(sw.m);
+  float4* V = reinterpret_cast<float4*>(sw.v);
+  for (int64_t i = v0 + (int64_t)blk * blockDim.x + threadIdx.x; i < v1; i += SW_U * stride) {
+    bool on[SW_U];
+    float4 p[SW_U], m[SW_U], q[SW_U];
+#pragma unroll
+    for (int u = 0; u < SW_U; ++u) {
+      const int64_t j = i + u * stride;
+      on[u] = j < v1 && sw.stamp[j >> lg] != tcur;
+    }
+#pragma unroll
+    for (int u = 0; u < SW_U; ++u) {
+      const int64_t j = i + u * stride;
+      if (on[u]) { p[u] = P[j]; m[u] = M[j]; q[u] = V[j]; }
+    }
+#pragma unroll
+    for (int u = 0; u < SW_U; ++u) {
+      const int64_t j = i + u * stride;
+      if (on[u]) {
+        st.apply(p[u].x, m[u].x, q[u].x, 0.0f); st.apply(p[u].y, m[u].y, q[u].y, 0.0f);
+        st.apply(p[u].z, m[u].z, q[u].z, 0.0f); st.apply(p[u].w, m[u].w, q[u].w, 0.0f);
+        P[j] = p[u]; M[j] = m[u]; V[j] = q[u];
+      }
+    }
+  }
+}
+
 }  // namespace gtr
 
 // Diagnostic build only (make timing): per-workgroup phase stamps of the layer

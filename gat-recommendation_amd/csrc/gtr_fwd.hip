@@ -59,6 +59,8 @@ struct ConvFwdK {
   float* bn_rmean;
   float* bn_rvar;
   int64_t* bn_nbt;
+  gtr_sweep sw;         // untouched-row AdamW slice run by blocks >= main_grid
+  int sw_slot, main_grid;
 };
 
 // Block prologue shared by k_conv_fwd (previous layer) and k_readout (last layer):
@@ -176,6 +178,10 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
   int* edst = reinterpret_cast<int*>(sm + G::F_EDST);
   int* s_flag = reinterpret_cast<int*>(sm + G::F_FLAG);
 
+  if ((int)blockIdx.x >= a.main_grid) {  // extra workgroups: untouched-row AdamW slice
+    sweep_slice(a.sw, a.sw_slot, blockIdx.x - a.main_grid, gridDim.x - a.main_grid);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   GTR_PH(a.layer, 0);
   GTR_PH_CLK(a.layer, 6);
@@ -538,6 +544,8 @@ struct ReadoutK {
   float* dy;
   float* gpart;
   float* gsum;
+  gtr_sweep sw;         // untouched-row AdamW slice run by blocks >= main_grid
+  int sw_slot, main_grid;
 };
 
 // Block per session (grid-strided): RO_WAVES waves split the session's node rows and
@@ -559,6 +567,10 @@ __global__ __launch_bounds__(RO_BLOCK) void k_readout(ReadoutK a) {
   __shared__ float s_red[RO_WAVES][2 * D];
   __shared__ float s_loss[RO_WAVES][2];
   __shared__ int s_flag;
+  if ((int)blockIdx.x >= a.main_grid) {  // extra workgroups: untouched-row AdamW slice
+    sweep_slice(a.sw, a.sw_slot, blockIdx.x - a.main_grid, gridDim.x - a.main_grid);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   GTR_PH(16, 0);
   const int B = a.bt.hdr[1];
@@ -600,7 +612,7 @@ __global__ __launch_bounds__(RO_BLOCK) void k_readout(ReadoutK a) {
   for (int v = 0; v < VPL; ++v) { gs[v] = 0.0f; gx[v] = 0.0f; }
   float lw_sum = 0.0f, bpr_sum = 0.0f;
 
-  for (int b = blockIdx.x; b < B; b += gridDim.x) {
+  for (int b = blockIdx.x; b < B; b += a.main_grid) {
     const int n0 = a.bt.node_ptr[b], n1 = a.bt.node_ptr[b + 1];
     const float cnt = (float)(n1 - n0);
     const int* negs = a.bt.negatives + (size_t)b * n;
@@ -839,17 +851,17 @@ __global__ __launch_bounds__(RO_BLOCK) void k_readout(ReadoutK a) {
   }
   GTR_PH(16, 3);
   if (!a.fin) return;  // loss summed by the step tail, BN sums reduced by the consuming conv_bwd
-  if (!arrive_last(a.cnt, gridDim.x, &s_flag)) return;
+  if (!arrive_last(a.cnt, (uint32_t)a.main_grid, &s_flag)) return;
   if (do_loss && tid == 0) {
     float loss = 0.0f;
-    for (int q = 0; q < (int)gridDim.x; ++q) loss += a.loss_part[(size_t)q * 2] + a.loss_part[(size_t)q * 2 + 1];
+    for (int q = 0; q < a.main_grid; ++q) loss += a.loss_part[(size_t)q * 2] + a.loss_part[(size_t)q * 2 + 1];
     a.loss_out[0] = loss;
   }
   if (do_bwd) {
     for (int j = tid; j < 2 * D; j += RO_BLOCK) {
       float acc = 0.0f;
 #pragma unroll 4
-      for (int q = 0; q < (int)gridDim.x; ++q) acc += a.gpart[(size_t)q * 2 * D + j];
+      for (int q = 0; q < a.main_grid; ++q) acc += a.gpart[(size_t)q * 2 * D + j];
       a.gsum[j] = acc;
     }
   }
@@ -973,6 +985,10 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
   __shared__ float s_loss[RW_WAVES][2];
   __shared__ float s_sc[RW_WAVES][RW_NMAX];  // raw listwise scores of the wave's session
   __shared__ int s_flag;
+  if ((int)blockIdx.x >= a.main_grid) {  // extra workgroups: untouched-row AdamW slice
+    sweep_slice(a.sw, a.sw_slot, blockIdx.x - a.main_grid, gridDim.x - a.main_grid);
+    return;
+  }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int rg = lane >> 4, c0 = (lane & 15) * EPL;
   const bool lead = (lane & 15) == 0;
@@ -1004,7 +1020,7 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
   float lw_sum = 0.0f, bpr_sum = 0.0f;
 
 #pragma unroll 1
-  for (int b = blockIdx.x * RW_WAVES + wave; b < B; b += gridDim.x * RW_WAVES) {
+  for (int b = blockIdx.x * RW_WAVES + wave; b < B; b += a.main_grid * RW_WAVES) {
     const int n0 = a.bt.node_ptr[b], n1 = a.bt.node_ptr[b + 1];
     const float cnt = (float)(n1 - n0);
     const int* negs = a.bt.negatives + (size_t)b * n;
@@ -1167,10 +1183,10 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
     }
   }
   if (!a.fin) return;
-  if (!arrive_last(a.cnt, gridDim.x, &s_flag)) return;
+  if (!arrive_last(a.cnt, (uint32_t)a.main_grid, &s_flag)) return;
   if (do_loss && tid == 0) {
     float loss = 0.0f;
-    for (int q = 0; q < (int)gridDim.x; ++q) loss += a.loss_part[(size_t)q * 2] + a.loss_part[(size_t)q * 2 + 1];
+    for (int q = 0; q < a.main_grid; ++q) loss += a.loss_part[(size_t)q * 2] + a.loss_part[(size_t)q * 2 + 1];
     a.loss_out[0] = loss;
   }
   if (do_bwd) {
@@ -1180,7 +1196,7 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
     float acc = 0.0f;
     if (sl < NSL) {
 #pragma unroll 8
-      for (int q = sl; q < (int)gridDim.x; q += NSL) acc += a.gpart[(size_t)q * 2 * D + j];
+      for (int q = sl; q < a.main_grid; q += NSL) acc += a.gpart[(size_t)q * 2 * D + j];
     }
     __syncthreads();
     float* red = s_scr;  // >= NSL * 2D floats (NSL * 2D <= RW_BLOCK)
@@ -1268,8 +1284,14 @@ extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   k.xin = L.xin; k.qkvs = L.qkvs; k.alpha = L.alpha; k.agg = L.agg; k.gate = L.gate; k.out = L.out;
   k.bn_part = L.bn_part; k.cnt = L.cnt; k.bn_stats = L.bn_stats; k.bn_rmean = L.bn_rmean;
   k.bn_rvar = L.bn_rvar; k.bn_nbt = L.bn_nbt;
-  const int grid = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;
+  int grid = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;
   if (grid <= 0) return GTR_OK;
+  k.main_grid = grid;
+  if (cfg->sweep && l < GTR_SWEEP_SLOTS && cfg->sweep->bounds[l + 1] > cfg->sweep->bounds[l]) {
+    k.sw = *cfg->sweep;
+    k.sw_slot = l;
+    grid += cfg->sweep->blocks;
+  }
   hipStream_t s = (hipStream_t)stream;
 #define GTR_FWD(DD) set_lds_limit<DD>(k_conv_fwd<DD>, (size_t)LayerGeom<DD>::F_WORDS * 4); \
   hipLaunchKernelGGL(k_conv_fwd<DD>, dim3(grid), dim3(CONV_BLOCK), (size_t)LayerGeom<DD>::F_WORDS * 4, s, k)
@@ -1322,7 +1344,14 @@ extern "C" int gtr_readout_loss(const gtr_config* cfg, const gtr_batch* bt, cons
   k.coef_neg = head->coef_neg;
   k.loss_part = head->loss_part; k.loss_out = head->loss_out; k.cnt = head->cnt;
   k.dy = L.dy; k.gpart = L.bn_gpart; k.gsum = L.bn_gsum;
-  const int grid = gtr_readout_grid(bt->b_cap);
+  int grid = gtr_readout_grid(bt->b_cap);
+  k.main_grid = grid;
+  if (cfg->sweep && cfg->num_layers < GTR_SWEEP_SLOTS &&
+      cfg->sweep->bounds[cfg->num_layers + 1] > cfg->sweep->bounds[cfg->num_layers]) {
+    k.sw = *cfg->sweep;
+    k.sw_slot = cfg->num_layers;
+    grid += cfg->sweep->blocks;
+  }
   hipStream_t s = (hipStream_t)stream;
   if (bt->b_cap >= ro_wave_min_b() && cfg->dim <= 128) {
     switch (cfg->dim) {

@@ -181,9 +181,10 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_adamw_rows(gtr_batch bt, int T, c
 // Untouched rows: 16 B per thread per tensor, grid-stride over nblk blocks; rows with
 // stamp == t (touched this step) skipped.
 __device__ __forceinline__ void sweep_body(int blk, int nblk, int64_t nvec, int vpr_log2, const int32_t* stamp,
-                                           int32_t t, float4* table, float4* m, float4* v, const AdamStep& st) {
+                                           int32_t t, float4* table, float4* m, float4* v, const AdamStep& st,
+                                           int64_t vbegin = 0) {
   const int64_t stride = (int64_t)nblk * GTR_BLOCK;
-  for (int64_t i = (int64_t)blk * GTR_BLOCK + threadIdx.x; i < nvec; i += stride) {
+  for (int64_t i = vbegin + (int64_t)blk * GTR_BLOCK + threadIdx.x; i < nvec; i += stride) {
     const int64_t row = i >> vpr_log2;
     if (stamp[row] == t) continue;
     float4 p = table[i], mm = m[i], vv = v[i];
@@ -278,6 +279,7 @@ struct TailK {
   gtr_adam opt;
   int T, nb_rows, nb_small, nb_sweep;
   int windowed, pad_w;  // 1: rows part = one block per TW-slot window of the sorted list
+  int64_t vbegin;       // first float4 of the untouched-row sweep (rows below: swept in the chain)
   int64_t nvec;
   int vpr_log2, nseg;
   gtr_segment segs[GTR_SMALL_MAX_SEG];
@@ -477,7 +479,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_step_tail(TailK a) {
   }
   sweep_body(blk - a.nb_rows - a.nb_small, a.nb_sweep, a.nvec, a.vpr_log2, a.tl.stamp, s_t,
              reinterpret_cast<float4*>(a.tl.table), reinterpret_cast<float4*>(a.tl.table_m),
-             reinterpret_cast<float4*>(a.tl.table_v), st);
+             reinterpret_cast<float4*>(a.tl.table_v), st, a.vbegin);
 }
 
 template <int D>
@@ -942,7 +944,9 @@ int gtr_step_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* t
   k.nvec = (int64_t)num_items * dim / 4;
   k.vpr_log2 = 0;
   while ((1 << k.vpr_log2) < dim / 4) ++k.vpr_log2;
-  int64_t sw = (k.nvec + GTR_BLOCK - 1) / GTR_BLOCK;
+  const int64_t from = t.sweep_from < 0 ? 0 : (t.sweep_from > num_items ? num_items : t.sweep_from);
+  k.vbegin = from * (dim / 4);
+  int64_t sw = (k.nvec - k.vbegin + GTR_BLOCK - 1) / GTR_BLOCK;
   k.nb_sweep = (int)(sw > 2048 ? 2048 : sw);
   k.nseg = nseg;
   for (int i = 0; i < nseg; ++i) k.segs[i] = segs[i];

@@ -37,6 +37,7 @@ class GtrConfig(C.Structure):
         ("num_items", i32), ("dim", i32), ("heads", i32), ("pe_k", i32), ("num_layers", i32),
         ("row_group", i32), ("training", i32), ("dropout", f32), ("bn_eps", f32),
         ("bn_momentum", f32), ("seed", u32), ("rng_ctr", P), ("consumer_reduce", i32), ("pad0", i32),
+        ("sweep", P),
     ]
 
 
@@ -81,6 +82,17 @@ class GtrTail(C.Structure):
         ("table", P), ("table_m", P), ("table_v", P), ("stamp", P),
         ("flat", P), ("flat_m", P), ("flat_v", P), ("flat_total", i64),
         ("loss_part", P), ("loss_out", P), ("loss_nparts", i32), ("pad0", i32), ("carry", P),
+        ("sweep_from", i64),
+    ]
+
+
+SWEEP_SLOTS = 8
+
+
+class GtrSweep(C.Structure):
+    _fields_ = [
+        ("table", P), ("m", P), ("v", P), ("stamp", P), ("opt", GtrAdam), ("bounds", i64 * (SWEEP_SLOTS + 1)),
+        ("dim", i32), ("blocks", i32),
     ]
 
 

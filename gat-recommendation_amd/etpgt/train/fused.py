@@ -20,6 +20,7 @@ gradient.  Optimizer state (exp_avg, exp_avg_sq, step) lives in this object;
 from __future__ import annotations
 
 import ctypes as C
+import os
 
 import torch
 
@@ -120,6 +121,34 @@ class FusedTrainStep:
         t.loss_part = ws.loss_part.data_ptr() if self.cfg.consumer_reduce else None
         t.loss_out = ws.loss_out.data_ptr()
         t.loss_nparts = readout_grid(caps.b_cap)
+        # untouched-row AdamW spread over the layer kernels' idle CUs (single GPU, small
+        # grids): the chain's 2L launches each sweep a slice of the table (gtr_sweep)
+        self.sweep = None
+        t.sweep_from = 0
+        chain = os.environ.get("GTR_CHAIN_SWEEP", "1") != "0"
+        # slots: conv_fwd(l) -> l, readout -> L, conv_bwd(l) -> 2L - l; weighted by the
+        # launches' measured slack (the readout is shorter than a layer kernel)
+        wts = [1.0] * eng.L + [0.75] + [1.0] * eng.L
+        if os.environ.get("GTR_SWEEP_WTS"):  # experiments: comma-separated slot weights
+            wts = [float(x) for x in os.environ["GTR_SWEEP_WTS"].split(",")]
+        slots = len(wts)
+        if chain and not self.data_parallel and self.ws.g_cap <= 128 and slots <= L.SWEEP_SLOTS:
+            sw = L.GtrSweep()
+            sw.table = eng.model.item_embedding.weight.data_ptr()
+            sw.m, sw.v, sw.stamp = self.m_tab.data_ptr(), self.v_tab.data_ptr(), self.stamp.data_ptr()
+            sw.opt = self.adam  # copied by value (step_dev: device counter)
+            tot, acc = sum(wts), 0.0
+            for i in range(L.SWEEP_SLOTS + 1):
+                sw.bounds[i] = eng.T if i >= slots else int(eng.T * acc / tot)
+                if i < slots:
+                    acc += wts[i]
+            sw.dim = eng.D
+            # 64 extra workgroups per launch measured best (C2 271.7k, C3 168.7k sessions/s;
+            # more of them raise the latency-bound groups' load latency)
+            sw.blocks = int(os.environ.get("GTR_SWEEP_BLOCKS", 64))
+            self.sweep = sw
+            self.cfg.sweep = C.addressof(sw)
+            t.sweep_from = eng.T
         nc = int(L.lib().gtr_tail_carry_floats(m_cap, eng.D))
         self.carry = torch.zeros(max(nc, 4), dtype=torch.float32, device=self.dev) if nc > 0 else None
         t.carry = self.carry.data_ptr() if self.carry is not None else None

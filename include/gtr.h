@@ -85,6 +85,8 @@ typedef struct gtr_batch {
   int32_t n_cap, b_cap, e_cap, n_neg;
 } gtr_batch;
 
+typedef struct gtr_sweep gtr_sweep;
+
 typedef struct gtr_config {
   int32_t num_items;  /* T: table rows                          */
   int32_t dim;        /* D = embedding_dim = hidden_dim          */
@@ -103,7 +105,11 @@ typedef struct gtr_config {
                               kernel (no inter-workgroup fences; for <= 64 row groups);
                               0: the producer's last-arriving workgroup finalises them */
   int32_t pad0;
+  const gtr_sweep* sweep;  /* optional (fused single-GPU step): untouched-row AdamW
+                              slices run by extra workgroups of the layer kernels */
 } gtr_config;
+
+
 
 /* Parameters + saved activations of one TransformerConv/BatchNorm layer.
  * w_all = [lin_query; lin_key; lin_value; lin_skip].weight stacked [4D, D],
@@ -218,6 +224,24 @@ typedef struct gtr_adam {
   const int64_t* step_dev;    /* optimizer step counter (device)                       */
 } gtr_adam;
 
+/* AdamW (g = 0) of the item-table rows NOT touched by the step, spread over the layer
+ * kernels of the fused step: launch slot s (conv_fwd of layer l -> slot l, conv_bwd of
+ * layer l -> slot 2L-1-l) appends `blocks` workgroups that update rows
+ * [bounds[s], bounds[s+1]) whose stamp != step, on the CUs the latency-bound row
+ * groups leave idle.  The forward/backward never reads those rows (only touched rows
+ * are gathered), so the slices are race-free; gtr_tail.sweep_from then skips them.    */
+#define GTR_SWEEP_SLOTS 8
+typedef struct gtr_sweep {
+  float* table;
+  float* m;
+  float* v;
+  const int32_t* stamp;
+  gtr_adam opt;       /* by value: the kernels copy it (opt.step_dev is a device pointer) */
+  int64_t bounds[GTR_SWEEP_SLOTS + 1];
+  int32_t dim;
+  int32_t blocks;
+} gtr_sweep;
+
 #define GTR_SMALL_MAX_SEG 48
 /* Sum each segment's gradient partials and apply (Adam|AdamW) — or, when
  * grad_out != NULL, only write the summed gradient there (eager path).        */
@@ -282,6 +306,7 @@ typedef struct gtr_tail {
   int32_t pad0;
   float* carry;           /* large batches (m_cap > 8192): [gtr_tail_carry_floats] scratch
                              for segment pieces spanning windows of the sorted list; else NULL */
+  int64_t sweep_from;     /* untouched rows below this were updated during the chain (gtr_sweep) */
 } gtr_tail;
 
 /* Floats of gtr_tail.carry needed at contribution capacity m_cap (0: not used).      */

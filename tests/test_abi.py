@@ -57,7 +57,8 @@ def test_struct_layouts_match_header():
     src = open(HEADER).read()
     for cname, py in (("gtr_batch", _lib.GtrBatch), ("gtr_config", _lib.GtrConfig), ("gtr_layer", _lib.GtrLayer),
                       ("gtr_embed", _lib.GtrEmbed), ("gtr_head", _lib.GtrHead), ("gtr_segment", _lib.GtrSegment),
-                      ("gtr_adam", _lib.GtrAdam), ("gtr_tail", _lib.GtrTail), ("gtr_dp_layout", _lib.GtrDpLayout)):
+                      ("gtr_adam", _lib.GtrAdam), ("gtr_tail", _lib.GtrTail), ("gtr_dp_layout", _lib.GtrDpLayout),
+                      ("gtr_sweep", _lib.GtrSweep)):
         body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), src, re.S).group(1)
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
         names = []
@@ -68,7 +69,7 @@ def test_struct_layouts_match_header():
             parts = decl.replace("*", " ").split()
             # "int32_t n_cap, b_cap, e_cap" declares several fields
             tail = " ".join(parts[1:]) if parts[0] != "const" else " ".join(parts[2:])
-            names += [n.strip() for n in tail.split(",") if n.strip()]
+            names += [n.split("[")[0].strip() for n in tail.split(",") if n.strip()]  # arrays: name only
         assert [f[0] for f in py._fields_] == names, cname
 
 
