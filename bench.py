@@ -131,12 +131,14 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     value = world * B * args.steps / elapsed
 
-    # ---- dominant kernel: the step tail (AdamW over the whole table), HIP events on its stream
+    # ---- roofline: the fused step (one hipGraph launch) against HBM; the table AdamW
+    # sweep rides in the layer kernels, so the step is the unit that streams the table
     D = cfg["D"]
-    tail_ms = measure_tail(step, args.steps)
-    alg_bytes = tail_bytes(step, T, D, touched)
-    achieved = alg_bytes / (tail_ms * 1e-3) / 1e9
+    step_ms = gpu_ms / args.steps
+    alg_bytes = step_bytes(step, cfg, T, st["nodes_per_session"] * B, B)
+    achieved = alg_bytes / (step_ms * 1e-3) / 1e9
     traffic, traffic_src = load_traffic(args.config) if step.dp is None else (None, None)
+    tail_ms = measure_tail(step, args.steps)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -180,18 +182,22 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": ("k_dp_tail (rank-averaged AdamW over all item-table rows + small parameters)"
-                           if step.dp is not None else
-                           "k_step_tail (AdamW over all item-table rows + small parameters)"),
+                "kernel": "fused training step = one hipGraph launch (begin, conv_fwd x2, readout, conv_bwd x2, "
+                          "wgrad, tail; the untouched-row AdamW sweep runs as extra workgroups of the layer "
+                          "kernels)" + (" + RCCL all-gather + dp tail" if step.dp is not None else ""),
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None if traffic is None else round(traffic),
-                "traffic_unit": "bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                "traffic_unit": "HBM bytes per step (PMC FETCH_SIZE x2 + WRITE_SIZE, summed over the step's kernels)",
                 "traffic_source": traffic_src,
                 "alg_bytes_per_launch": int(alg_bytes),
-                "avg_launch_ms": round(tail_ms, 5),
+                "alg_bytes_terms": "24*T*D table p/m/v + 4*T stamps + gathered rows/ids + 36*4*N*D per layer "
+                                   "+ small params (24 + 4*P slab partials per element)",
+                "avg_launch_ms": round(step_ms, 5),
+                "tail_kernel": {"name": "k_dp_tail" if step.dp is not None else "k_step_tail",
+                                "avg_launch_ms": round(tail_ms, 5)},
             },
             "cpu_baseline": cpu,
             "gather_roofline": gather,
@@ -235,20 +241,21 @@ def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, us
                 caps=caps, model=model)
 
 
-def load_traffic(config: str, kernel: str = "k_step_tail"):
-    """Per-launch HBM bytes of `kernel` from the newest committed PMC summary
+def load_traffic(config: str):
+    """HBM bytes per training step from the newest committed PMC summary
     (profiles/rNN/<config>_pmc.json: scripts/gpu_pmc.sh = two rocprofv3 --pmc passes,
-    FETCH_SIZE doubled per the gfx950 note + WRITE_SIZE, scripts/pmc_parse.py)."""
+    FETCH_SIZE doubled per the gfx950 note + WRITE_SIZE, summed over the step's kernels
+    by scripts/pmc_parse.py)."""
     import glob
 
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"{config}_pmc.json")))
     if not files:
         return None, None
     with open(files[-1]) as f:
-        rec = json.load(f).get(kernel)
+        rec = json.load(f).get("_per_step")
     if not rec:
         return None, None
-    return float(rec["hbm_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
+    return float(rec["hbm_bytes_per_step"]), os.path.relpath(files[-1], ROOT)
 
 
 def measure_tail(step, iters) -> float:
@@ -277,16 +284,18 @@ def measure_tail(step, iters) -> float:
     return float(np.median([a.elapsed_time(b) for a, b in durs]))
 
 
-def tail_bytes(step, T, D, touched) -> float:
-    """Algorithmic HBM bytes of one step-tail launch (SURVEY.md §8d table term):
-    untouched rows p,m,v read+write (24 B/elem) + their stamps; touched rows p,m,v
-    (24 B/elem) + contribution rows / keys / coefficients; small parameters p,m,v +
-    gradient partials."""
-    caps = step.caps
-    m_cap = caps.n_cap + caps.b_cap * (1 + caps.n_neg)
-    lay = step.eng.flat.layout
-    small = lay.total * (24.0 + 4.0 * step.ws.P)
-    return 24.0 * T * D + 4.0 * T + m_cap * (4.0 * D + 12.0) + small
+def step_bytes(step, cfg, T, N, B) -> float:
+    """Algorithmic HBM bytes of one training step (each distinct tensor
+    read or written once): the table AdamW (p, m, v read + write = 24 B per element; no
+    dense gradient) + touched-row stamps; the gathered node / PE / scoring rows and
+    their ids; layer activations (12 forward + 24 backward D-vectors per node and
+    layer, §8d); the small parameters (p, m, v + one read of each split-K partial)."""
+    D, K, n = cfg["D"], cfg["K"], cfg["n_neg"]
+    table = 24.0 * T * D + 4.0 * T
+    gather = 4.0 * N * D + 4.0 * N * K + 4.0 * B * (1 + n) * D + 4.0 * (N + B * (1 + n))
+    acts = step.eng.L * 36 * 4.0 * N * D
+    small = step.eng.flat.layout.total * (24.0 + 4.0 * step.ws.P)
+    return table + gather + acts + small
 
 
 def gather_probe(dev, B, nbatch=2, steps=20):
@@ -329,6 +338,15 @@ def gather_probe(dev, B, nbatch=2, steps=20):
     rows = 4.0 * Bl * (1 + n) * D
     alg = rows + 4.0 * Bl * (1 + n) + 4.0 * (Bl + 1) + 3 * 4.0 * N * D + 4.0 * Bl * D + 4.0 * Bl * (1 + n)
     ach = alg / (ms * 1e-3) / 1e9
+    traffic, src = None, None
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"c3_b{B}_pmc.json")))
+    if files:
+        with open(files[-1]) as f:
+            rec = json.load(f).get("k_readout_wave")
+        if rec:
+            traffic, src = round(float(rec["hbm_bytes_per_launch"])), os.path.relpath(files[-1], ROOT)
     return {
         "bound": "hbm",
         "kernel": "k_readout_wave (mean readout + sampled scoring gather + listwise loss fwd/bwd)",
@@ -337,6 +355,9 @@ def gather_probe(dev, B, nbatch=2, steps=20):
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": round(ach / HBM_PEAK_GBS, 4),
+        "traffic": traffic,
+        "traffic_unit": "bytes/launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+        "traffic_source": src,
         "alg_bytes_per_launch": int(alg),
         "scoring_row_bytes_per_launch": int(rows),
         "avg_launch_ms": round(ms, 5),

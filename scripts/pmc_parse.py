@@ -44,6 +44,15 @@ def main():
             # rocprofv3 FETCH_SIZE / WRITE_SIZE are in KiB; FETCH doubled on gfx950
             "hbm_bytes_per_launch": (2 * fa * 1024 if fa is not None else 0) + (wa * 1024 if wa is not None else 0),
         }
+    # per training step: every kernel's bytes x its launches, over the step count (one
+    # k_step_begin per step; copies included)
+    steps = out.get("k_step_begin", out.get("k_counters", {})).get("dispatches", 0)
+    if steps:
+        # HIP kernels of the library (k_*, incl. the rocprim sort's) + the blob copy;
+        # torch fill kernels belong to setup, not to the step
+        tot = sum(v["hbm_bytes_per_launch"] * v["dispatches"] for k, v in out.items()
+                  if k.startswith("k_") or k.startswith("__amd_rocclr_copyBuffer"))
+        out["_per_step"] = {"steps": steps, "hbm_bytes_per_step": tot / steps}
     print(json.dumps(out, indent=1))
 
 
