@@ -89,6 +89,13 @@ class GtrTail(C.Structure):
 SWEEP_SLOTS = 8
 
 
+class GtrSessions(C.Structure):
+    _fields_ = [
+        ("sess_ptr", P), ("sess_items", P), ("sess_nodes", P), ("sess_edges", P),
+        ("num_sessions", i32), ("num_items", i32),
+    ]
+
+
 class GtrSweep(C.Structure):
     _fields_ = [
         ("table", P), ("m", P), ("v", P), ("stamp", P), ("opt", GtrAdam), ("bounds", i64 * (SWEEP_SLOTS + 1)),
@@ -131,6 +138,10 @@ _SIGS = {
     "gtr_step_begin": (C.c_int, [P, C.c_int, P, P, P, P, P, P, P, P, C.c_size_t, P]),
     "gtr_step_tail": (C.c_int, [P, C.c_int, C.c_int, P, P, C.c_int, P, P]),
     "gtr_tail_carry_floats": (C.c_int, [C.c_int, C.c_int]),
+    "gtr_edge_hash_slots": (C.c_int, [i64, C.POINTER(i64)]),
+    "gtr_edge_hash_build": (C.c_int, [P, i64, P, i64, P]),
+    "gtr_session_counts": (C.c_int, [P, P, i64, C.c_int, P, P, P]),
+    "gtr_build_batch": (C.c_int, [P, P, i64, C.c_int, P, P, C.c_int, C.c_int, u32, P, P, P, P, P]),
     "gtr_topk_workspace_bytes": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_size_t)]),
     "gtr_score_topk": (C.c_int, [P, C.c_int, C.c_int, P, C.c_int, C.c_int, P, P, P, C.c_size_t, P]),
 }

@@ -1,0 +1,148 @@
+"""GPU batch constructor: SessionDataset.__getitem__ + collate_fn
+(etpgt/train/dataloader.py:64-202) as HIP kernels (libgtr_hip ``gtr_build_batch``).
+
+``GpuSessionStore`` keeps a dataset resident in HBM: the click sequences (CSR by
+session), an open-addressing hash of the co-occurrence edge keys item_i * T + item_j
+(graph_edges.csv, item_i <= item_j) and every session's node / edge counts.
+``GpuBatchBuilder`` walks an epoch order of session ids with a device cursor and writes
+each batch straight into a fused step's packed batch image — the training step then
+runs without any host work per batch, and the build is captured in the step's hipGraph
+(``FusedTrainStep.attach_builder``).
+
+Semantics per session: the last ``max_session_length`` clicks, target = the last,
+nodes = sorted unique context ids, edges = graph edges with both endpoints in the
+context (directed item_i -> item_j, (src, dst) order), ``num_negatives`` negatives
+uniform in [1, T) rejecting the session's clicks.  The reference draws negatives with
+``torch.randint`` on the host; here they come from a counter-based hash of (seed, batch
+position, draw) — the same distribution, reproducible on the device
+(oracle/batch_ref.py restates the stream for the parity tests).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from etpgt.backend import _lib as L
+from etpgt.data.batch import Caps, blob_layout
+
+
+class GpuSessionStore:
+    def __init__(self, session_ptr, session_items, edge_keys, num_items: int, device, max_session_length: int = 50):
+        ptr = np.asarray(session_ptr, np.int64)
+        items = np.asarray(session_items, np.int64)
+        if ptr.ndim != 1 or ptr.size < 2 or ptr[0] != 0 or np.any(np.diff(ptr) < 0) or ptr[-1] != items.size:
+            raise ValueError("session_ptr must be a CSR offset array over session_items")
+        if np.any(np.diff(ptr) < 2):
+            raise ValueError("every session needs at least 2 clicks (a context and a target)")
+        if not 2 <= max_session_length <= 64:
+            raise ValueError("max_session_length must be in [2, 64] on the GPU batch constructor")
+        if items.size and (items.min() < 0 or items.max() >= num_items):
+            raise IndexError(f"session items outside [0, {num_items})")
+        if items.size >= 2**31:
+            raise ValueError("more than 2^31 clicks")
+        self.device = torch.device(device)
+        self.T = int(num_items)
+        self.S = int(ptr.size - 1)
+        self.max_len = int(max_session_length)
+        dev = self.device
+        self.ptr_d = torch.from_numpy(ptr.astype(np.int32)).to(dev)
+        self.items_d = torch.from_numpy(items.astype(np.int32)).to(dev)
+        keys = np.asarray(edge_keys, np.int64)
+        lib = L.lib()
+        ns = C.c_int64(0)
+        L.check(lib.gtr_edge_hash_slots(int(keys.size), C.byref(ns)), "edge_hash_slots")
+        self.num_slots = int(ns.value)
+        self.slots = torch.empty(self.num_slots, dtype=torch.int64, device=dev)
+        keys_d = torch.from_numpy(keys).to(dev)
+        st = torch.cuda.current_stream(dev).cuda_stream
+        L.check(lib.gtr_edge_hash_build(keys_d.data_ptr(), int(keys.size), self.slots.data_ptr(), self.num_slots, st),
+                "edge_hash_build")
+        self.nodes_d = torch.zeros(self.S, dtype=torch.int32, device=dev)
+        self.edges_d = torch.zeros(self.S, dtype=torch.int32, device=dev)
+        self.ss = L.GtrSessions()
+        self.ss.sess_ptr, self.ss.sess_items = self.ptr_d.data_ptr(), self.items_d.data_ptr()
+        self.ss.sess_nodes, self.ss.sess_edges = self.nodes_d.data_ptr(), self.edges_d.data_ptr()
+        self.ss.num_sessions, self.ss.num_items = self.S, self.T
+        L.check(lib.gtr_session_counts(C.byref(self.ss), self.slots.data_ptr(), self.num_slots, self.max_len,
+                                       self.nodes_d.data_ptr(), self.edges_d.data_ptr(), st), "session_counts")
+        self.nodes = self.nodes_d.cpu().numpy().astype(np.int64)
+        self.edges = self.edges_d.cpu().numpy().astype(np.int64)
+
+    @classmethod
+    def from_synthetic(cls, data, device, max_session_length: int = 50) -> "GpuSessionStore":
+        return cls(data.session_ptr, data.session_items, data.edge_keys, data.table_rows, device, max_session_length)
+
+    @classmethod
+    def from_dataset(cls, ds, device) -> "GpuSessionStore":
+        """From an etpgt.train.SessionDataset (sessions in session-id order)."""
+        ei = ds.edge_index.numpy()
+        keys = np.unique(ei[0].astype(np.int64) * ds.num_items + ei[1].astype(np.int64))
+        return cls(ds._ptr, ds._items, keys, ds.num_items, device, ds.max_session_length)
+
+
+class GpuBatchBuilder:
+    """Batches of ``batch_size`` sessions in epoch order, built on the device."""
+
+    def __init__(self, store: GpuSessionStore, batch_size: int, num_negatives: int, seed: int = 0):
+        if batch_size <= 0 or batch_size > 16384:
+            raise ValueError("batch_size must be in [1, 16384] on the GPU batch constructor")
+        if num_negatives <= 0:
+            raise ValueError("num_negatives must be positive")
+        self.store = store
+        self.B = int(batch_size)
+        self.n_neg = int(num_negatives)
+        self.seed = int(seed) & 0x7FFFFFFF
+        dev = store.device
+        self.cursor = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.start = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.scratch = None
+        self.order_h = np.arange(store.S, dtype=np.int64)
+        self.order_d = torch.from_numpy(self.order_h.astype(np.int32)).to(dev)
+
+    def set_epoch_order(self, order, position: int = 0) -> None:
+        """Session ids in visiting order (e.g. a permutation); batches wrap around."""
+        o = np.asarray(order, np.int64)
+        if o.ndim != 1 or o.size == 0 or o.min() < 0 or o.max() >= self.store.S:
+            raise ValueError("order must list session ids in [0, S)")
+        self.order_h = o
+        self.order_d = torch.from_numpy(o.astype(np.int32)).to(self.store.device)
+        self.cursor.fill_(int(position))
+
+    def batch_sizes(self, num_batches: int, position: int = 0) -> tuple[np.ndarray, np.ndarray]:
+        """(N, E) of the next ``num_batches`` batches from ``position`` (host, from the counts)."""
+        idx = (position + np.arange(num_batches * self.B)) % self.order_h.size
+        sess = self.order_h[idx].reshape(num_batches, self.B)
+        return self.store.nodes[sess].sum(1), self.store.edges[sess].sum(1)
+
+    def plan_caps(self, num_batches: int | None = None, position: int = 0) -> Caps:
+        """Capacities covering the next ``num_batches`` batches (default: one epoch)."""
+        if num_batches is None:
+            num_batches = max(1, -(-self.order_h.size // self.B))
+        N, E = self.batch_sizes(num_batches, position)
+        return Caps.bucket(int(N.max()), self.B, max(int(E.max()), 1), self.n_neg)
+
+    def launch(self, bs: L.GtrBatch, caps: Caps, stream: int) -> None:
+        """Build the next batch into the batch image ``bs`` (capacities ``caps``)."""
+        if self.scratch is None or self.scratch.numel() < 2 * caps.b_cap:
+            self.scratch = torch.zeros(2 * caps.b_cap, dtype=torch.int32, device=self.store.device)
+        st = self.store
+        L.check(L.lib().gtr_build_batch(C.byref(st.ss), st.slots.data_ptr(), st.num_slots, st.max_len,
+                                        self.order_d.data_ptr(), self.cursor.data_ptr(), self.B, caps.R,
+                                        self.seed, C.byref(bs), self.scratch.data_ptr(), self.start.data_ptr(),
+                                        self.status.data_ptr(), stream), "build_batch")
+
+    def build(self, caps: Caps | None = None) -> tuple[Caps, torch.Tensor]:
+        """Build the next batch into a fresh blob (eager; tests and tools)."""
+        from etpgt.backend.engine import Engine
+
+        caps = caps or self.plan_caps(1, int(self.cursor.item()))
+        blob = torch.zeros(blob_layout(caps)["_total"], dtype=torch.int32, device=self.store.device)
+        bs = Engine.batch_struct(caps, blob)
+        self.launch(bs, caps, torch.cuda.current_stream(self.store.device).cuda_stream)
+        if int(self.status.item()) != 0:
+            raise RuntimeError("GPU batch exceeded its capacities")
+        return caps, blob

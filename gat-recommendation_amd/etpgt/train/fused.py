@@ -68,6 +68,7 @@ class FusedTrainStep:
         self.stamp = torch.zeros(T, dtype=torch.int32, device=self.dev)
         self.caps = None
         self.graph = None
+        self.builder = None
         if caps is not None:
             self._bind(caps)
 
@@ -195,14 +196,33 @@ class FusedTrainStep:
         """D2D copy of a pre-staged packed blob of the same capacities."""
         self.blob.copy_(blob, non_blocking=True)
 
+    def attach_builder(self, builder, num_batches: int | None = None):
+        """Build every batch on the device inside the step (etpgt.data.gpu_batch): each
+        ``run()`` first writes the builder's next batch into the batch image, and the
+        build is captured in the step's hipGraph with the rest.  Capacities cover the
+        builder's next ``num_batches`` batches (default: one epoch of its order)."""
+        caps = builder.plan_caps(num_batches, int(builder.cursor.item()))
+        if caps.n_neg != (self.caps.n_neg if self.caps is not None else caps.n_neg):
+            raise ValueError("the number of negatives per session must stay fixed")
+        if self.caps is None or not self.caps.fits(caps.n_cap, caps.b_cap, caps.e_cap, caps.n_neg):
+            self._bind(caps if self.caps is None else self.caps.grow(caps.n_cap, caps.b_cap, caps.e_cap, caps.n_neg))
+        self.builder = builder
+        self.graph = self.graph_pe = self.graph_b = None
+
+    def detach_builder(self):
+        self.builder = None
+        self.graph = self.graph_pe = self.graph_b = None
+
     # ------------------------------------------------------------------ launches
     def _launch_a(self, with_pe: bool):
-        """step_begin -> forward + loss -> backward (+ the DP pack)."""
+        """[device batch build] -> step_begin -> forward + loss -> backward (+ the DP pack)."""
         eng = self.eng
         lib = L.lib()
         ws, cfg = self.ws, self.cfg
         bs = self.bs_pe if with_pe else self.bs
         st = torch.cuda.current_stream(self.dev).cuda_stream
+        if self.builder is not None:
+            self.builder.launch(bs, self.caps, st)
         L.check(lib.gtr_step_begin(C.byref(bs), eng.T, self.keys.data_ptr(), self.vals.data_ptr(),
                                    self.skeys.data_ptr(), self.svals.data_ptr(), self.stamp.data_ptr(),
                                    self.step_dev.data_ptr(), eng.rng_ctr.data_ptr(), self.sort_tmp.data_ptr(),

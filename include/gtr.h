@@ -35,6 +35,8 @@
  *   gtr_readout_grid  partial count of gtr_readout_loss (host sizing).
  *   gtr_score_topk    base.py:59-78 predict (full-catalog scores + top-k), the
  *                     Recall@K / NDCG@K evaluation of trainer.py:138-173.
+ *   gtr_build_batch   dataloader.py:64-202 SessionDataset.__getitem__ + collate_fn on
+ *                     the device (+ gtr_edge_hash_build, gtr_session_counts).
  *
  * Conventions: plain pointers + sizes, no torch types; every
  * pointer is a device pointer unless marked (host); stream is a hipStream_t;
@@ -352,6 +354,39 @@ int gtr_dp_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tai
 int gtr_topk_workspace_bytes(int B, int num_items, int k, size_t* bytes);
 int gtr_score_topk(const float* se, int B, int dim, const float* table, int num_items, int k,
                    int64_t* out_idx, float* out_score, void* ws, size_t ws_bytes, gtr_stream_t stream);
+
+/* ---- GPU batch constructor (etpgt.data.gpu_batch) ----------------------------------
+ * SessionDataset.__getitem__ + collate_fn (dataloader.py:64-202) on the device, writing
+ * the packed batch image (gtr_batch) the training step consumes.  Per session: the last
+ * max_len clicks, target = the last, nodes = sorted unique context ids, edges = graph
+ * edges (item_i <= item_j, directed item_i -> item_j) with both ends in the context in
+ * (src, dst) order, n_neg negatives uniform in [1, T) rejecting the session's clicks
+ * (counter-based hash stream of (seed, batch position, draw)).                          */
+typedef struct gtr_sessions {
+  const int32_t* sess_ptr;   /* [S+1] click offsets                              */
+  const int32_t* sess_items; /* clicks in click order                            */
+  const int32_t* sess_nodes; /* [S] unique context ids (gtr_session_counts)      */
+  const int32_t* sess_edges; /* [S] induced edges (gtr_session_counts)           */
+  int32_t num_sessions;      /* S                                                */
+  int32_t num_items;         /* T (table rows)                                   */
+} gtr_sessions;
+
+/* Power-of-two slot count (>= 2 * num_edges) of the edge hash.                        */
+int gtr_edge_hash_slots(int64_t num_edges, int64_t* slots);
+/* Open-addressing hash of the edge keys item_i * T + item_j.                           */
+int gtr_edge_hash_build(const int64_t* keys, int64_t num_edges, uint64_t* slots, int64_t num_slots,
+                        gtr_stream_t stream);
+/* nodes[s], edges[s] of every session (capacity planning and batch offsets).           */
+int gtr_session_counts(const gtr_sessions* ss, const uint64_t* slots, int64_t num_slots, int max_len,
+                       int32_t* nodes, int32_t* edges, gtr_stream_t stream);
+/* One batch of the B sessions order[(*cursor + b) % S] into *out (device blob arrays;
+ * hdr sizes live), then *cursor += B.  scratch: [2 * b_cap] int32; start: [1] int64;
+ * status[0] = 1 (and an empty header) if the batch exceeds out's capacities.
+ * row_group = the layer kernels' R for out's n_cap.  B <= 16384, max_len <= 64.        */
+int gtr_build_batch(const gtr_sessions* ss, const uint64_t* slots, int64_t num_slots, int max_len,
+                    const int32_t* order, int64_t* cursor, int B, int row_group, uint32_t seed,
+                    const gtr_batch* out, int32_t* scratch, int64_t* start, int32_t* status,
+                    gtr_stream_t stream);
 
 /* Workgroups of gtr_readout_loss = the number of its loss / BatchNorm-sum partials
  * (gtr_tail.loss_nparts; the last layer's bn_gpart rows).                         */
