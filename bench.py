@@ -64,6 +64,8 @@ def main():
     ap.add_argument("--recall-steps", type=int, default=100,
                     help="Recall@10 parity leg: training steps of the HIP and oracle trainers (0 = skip)")
     ap.add_argument("--recall-sessions", type=int, default=2048, help="held-out sessions of the Recall@10 leg")
+    ap.add_argument("--e2e-steps", type=int, default=200,
+                    help="end-to-end leg: steps with the batch built on the device inside the step (0 = skip)")
     ap.add_argument("--gather-batch", type=int, default=8192,
                     help="embedding-gather roofline leg: C3 shape (d=128, 100 negatives) at this batch (0 = skip)")
     args = ap.parse_args()
@@ -143,6 +145,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(cfg, batches, T, args.cpu_seconds)
+    e2e = None
+    if rank == 0 and world == 1 and args.e2e_steps > 0:
+        e2e = e2e_probe(cfg, data, dev, B, args.e2e_steps)
     gather = None
     if rank == 0 and world == 1 and args.gather_batch > 0:
         gather = gather_probe(dev, args.gather_batch)
@@ -200,6 +205,7 @@ def main():
                                 "avg_launch_ms": round(tail_ms, 5)},
             },
             "cpu_baseline": cpu,
+            "end_to_end": e2e,
             "gather_roofline": gather,
             "recall_parity": recall,
         }
@@ -296,6 +302,70 @@ def step_bytes(step, cfg, T, N, B) -> float:
     acts = step.eng.L * 36 * 4.0 * N * D
     small = step.eng.flat.layout.total * (24.0 + 4.0 * step.ws.P)
     return table + gather + acts + small
+
+
+def e2e_probe(cfg, data, dev, B, steps):
+    """End to end from resident session data: the batch is built
+    on the device (etpgt.data.gpu_batch: SessionDataset.__getitem__ + collate_fn as
+    kernels) inside the captured step, walking a shuffled epoch order.  Beside it, the
+    host pipeline: per-session example + collate + pack on the host, one H2D copy, the
+    same fused step."""
+    from etpgt.data.batch import collate_sessions
+    from etpgt.data.gpu_batch import GpuBatchBuilder, GpuSessionStore
+    from etpgt.data.synthetic import random_pe_table, session_example
+    from etpgt.model import create_graph_transformer_optimized
+    from etpgt.train.fused import FusedTrainStep
+
+    T = data.table_rows
+    kw = dict(embedding_dim=cfg["D"], hidden_dim=cfg["D"], num_layers=2, num_heads=cfg["H"], dropout=0.1,
+              use_laplacian_pe=cfg["K"] > 0, laplacian_k=max(cfg["K"], 1))
+    torch.manual_seed(42)
+    model = create_graph_transformer_optimized(T, **kw)
+    if cfg["K"] > 0:
+        model.laplacian_pe._cached_pe = random_pe_table(T, cfg["K"])
+    model = model.to(dev).train()
+    t0 = time.perf_counter()
+    store = GpuSessionStore.from_synthetic(data, dev)
+    torch.cuda.synchronize(dev)
+    store_s = time.perf_counter() - t0
+    bld = GpuBatchBuilder(store, B, cfg["n_neg"], seed=9)
+    order = np.random.default_rng(9).permutation(data.num_sessions)
+    bld.set_epoch_order(order)
+    step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, loss=cfg["loss"])
+    step.attach_builder(bld)  # capacities for the whole epoch order
+    for _ in range(20):
+        step.run()
+    torch.cuda.synchronize(dev)
+    t = time.perf_counter()
+    for _ in range(steps):
+        step.run()
+    torch.cuda.synchronize(dev)
+    dev_s = (time.perf_counter() - t) / steps
+    # host pipeline on the same model / step object (builder detached)
+    step.detach_builder()
+    rng = np.random.default_rng(10)
+    hs = max(10, steps // 10)
+    pos = 0
+    for i in range(3 + hs):
+        if i == 3:
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+        ids = order[(pos + np.arange(B)) % order.size]
+        pos += B
+        sb = collate_sessions([session_example(data, int(s), cfg["n_neg"], rng) for s in ids])
+        step(sb)
+    torch.cuda.synchronize(dev)
+    host_s = (time.perf_counter() - t) / hs
+    return {
+        "device_batch_build_sessions_per_s": round(B / dev_s, 1),
+        "device_ms_per_step": round(dev_s * 1e3, 4),
+        "host_batch_build_sessions_per_s": round(B / host_s, 1),
+        "host_ms_per_step": round(host_s * 1e3, 3),
+        "batch": B,
+        "store_setup_s": round(store_s, 3),
+        "note": "device: k_bb_scan + k_bb_write in the captured step, epoch order walked by a device cursor; "
+                "host: per-session example + collate + pack + H2D per step",
+    }
 
 
 def gather_probe(dev, B, nbatch=2, steps=20):
