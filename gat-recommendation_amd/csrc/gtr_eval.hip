@@ -63,10 +63,14 @@ __device__ __forceinline__ void group_topk(uint64_t (&key)[NV], int k, F&& emit)
 
 // Stage 1.  blockIdx.x = chunk (rows [c*TK_CH, +TK_CH)), blockIdx.y = session group.
 // out: cand[(b * nchunk + c) * k + j].
+// excl_ptr / excl_ids (optional): per-session sorted item ids that may not be returned
+// (serving: the session's own items and the padding row, recommender.py:128-129).
 template <int D, int NSW>
 __global__ __launch_bounds__(64 * NSW) void k_topk_chunk(const float* __restrict__ se, int B,
                                                          const float* __restrict__ table, int T, int k,
-                                                         int nchunk, uint64_t* __restrict__ cand) {
+                                                         int nchunk, uint64_t* __restrict__ cand,
+                                                         const int32_t* __restrict__ excl_ptr,
+                                                         const int32_t* __restrict__ excl_ids) {
   constexpr int KC = D / 16;
   constexpr int NT = TK_CH / 16;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -109,6 +113,19 @@ __global__ __launch_bounds__(64 * NSW) void k_topk_chunk(const float* __restrict
     for (int t = 0; t < NT; ++t) {
       const int row = r0 + t * 16 + lr;
       key[t] = row < T ? make_key(sc[t][i], row) : 0ull;
+    }
+    if (excl_ptr && s < B) {
+      const int e0 = excl_ptr[s], e1 = excl_ptr[s + 1];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int row = r0 + t * 16 + lr;
+        int lo = e0, hi = e1;  // sorted ids: binary search
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (excl_ids[mid] < row) lo = mid + 1; else hi = mid;
+        }
+        if (lo < e1 && excl_ids[lo] == row) key[t] = 0ull;
+      }
     }
     uint64_t* out = cand + ((size_t)s * nchunk + c) * k;
     const bool wr = s < B && lr == 0;
@@ -173,9 +190,24 @@ extern "C" int gtr_topk_workspace_bytes(int B, int num_items, int k, size_t* byt
   return GTR_OK;
 }
 
+extern "C" int gtr_score_topk_masked(const float* se, int B, int dim, const float* table, int num_items, int k,
+                                     const int32_t* excl_ptr, const int32_t* excl_ids, int64_t* out_idx,
+                                     float* out_score, void* ws, size_t ws_bytes, gtr_stream_t stream);
+
 extern "C" int gtr_score_topk(const float* se, int B, int dim, const float* table, int num_items, int k,
                               int64_t* out_idx, float* out_score, void* ws, size_t ws_bytes,
                               gtr_stream_t stream) {
+  return gtr_score_topk_masked(se, B, dim, table, num_items, k, nullptr, nullptr, out_idx, out_score, ws,
+                               ws_bytes, stream);
+}
+
+extern "C" int gtr_score_topk_masked(const float* se, int B, int dim, const float* table, int num_items, int k,
+                                     const int32_t* excl_ptr, const int32_t* excl_ids, int64_t* out_idx,
+                                     float* out_score, void* ws, size_t ws_bytes, gtr_stream_t stream) {
+  if ((excl_ptr == nullptr) != (excl_ids == nullptr)) {
+    set_error("gtr_score_topk_masked: excl_ptr and excl_ids go together");
+    return GTR_E_ARG;
+  }
   size_t need = 0;
   if (int e = gtr_topk_workspace_bytes(B, num_items, k, &need)) return e;
   if (!se || !table || !out_idx || !out_score || !ws || ws_bytes < need) {
@@ -194,7 +226,7 @@ extern "C" int gtr_score_topk(const float* se, int B, int dim, const float* tabl
   const int nsw = B > 32 ? 4 : (B > 16 ? 2 : 1);
   const dim3 g1(nc, (B + 16 * nsw - 1) / (16 * nsw));
 #define TK_LAUNCH(DD, NS) hipLaunchKernelGGL((k_topk_chunk<DD, NS>), g1, dim3(64 * NS), 0, s, se, B, table, \
-                                             num_items, k, nc, buf0)
+                                             num_items, k, nc, buf0, excl_ptr, excl_ids)
 #define TK_DIM(DD)                                  \
   if (nsw == 4) TK_LAUNCH(DD, 4);                   \
   else if (nsw == 2) TK_LAUNCH(DD, 2);              \

@@ -142,10 +142,13 @@ class GraphTransformerFn(torch.autograd.Function):
 _TOPK_WS: dict = {}
 
 
-def score_topk(se: torch.Tensor, table: torch.Tensor, k: int) -> tuple[torch.Tensor, torch.Tensor]:
+def score_topk(se: torch.Tensor, table: torch.Tensor, k: int, exclude: list | None = None
+               ) -> tuple[torch.Tensor, torch.Tensor]:
     """Full-catalog scores ``se @ table.T`` and their top-k (base.py:59-78) on the HIP
     kernel (gtr_score_topk): returns (item ids [B, k] int64, scores [B, k] fp32), best
-    first; ties resolve to the lower item id.  No [B, T] score matrix is materialised."""
+    first; ties resolve to the lower item id.  No [B, T] score matrix is materialised.
+    ``exclude``: per-session iterables of item ids that may not be returned (serving's
+    seen-item / padding mask); missing results come back as id -1, score -inf."""
     if isinstance(table, torch.nn.Embedding):
         table = table.weight
     if se.device.type != "cuda":
@@ -173,6 +176,20 @@ def score_topk(se: torch.Tensor, table: torch.Tensor, k: int) -> tuple[torch.Ten
     s = se.detach().float().contiguous()
     t = table.detach().float().contiguous()
     st = torch.cuda.current_stream(dev).cuda_stream
-    L.check(lib.gtr_score_topk(s.data_ptr(), B, D, t.data_ptr(), T, int(k), idx.data_ptr(), sc.data_ptr(),
-                               ws.data_ptr(), ws.numel(), st), "score_topk")
+    if exclude is None:
+        L.check(lib.gtr_score_topk(s.data_ptr(), B, D, t.data_ptr(), T, int(k), idx.data_ptr(), sc.data_ptr(),
+                                   ws.data_ptr(), ws.numel(), st), "score_topk")
+        return idx, sc
+    if len(exclude) != B:
+        raise ValueError("exclude needs one id list per session")
+    lists = [sorted(set(int(v) for v in e)) for e in exclude]
+    ptr = [0]
+    for e in lists:
+        ptr.append(ptr[-1] + len(e))
+    ids = [v for e in lists for v in e] or [0]
+    ptr_d = torch.tensor(ptr, dtype=torch.int32, device=dev)
+    ids_d = torch.tensor(ids, dtype=torch.int32, device=dev)
+    L.check(lib.gtr_score_topk_masked(s.data_ptr(), B, D, t.data_ptr(), T, int(k), ptr_d.data_ptr(),
+                                      ids_d.data_ptr(), idx.data_ptr(), sc.data_ptr(), ws.data_ptr(), ws.numel(),
+                                      st), "score_topk_masked")
     return idx, sc

@@ -354,6 +354,13 @@ int gtr_dp_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tai
 int gtr_topk_workspace_bytes(int B, int num_items, int k, size_t* bytes);
 int gtr_score_topk(const float* se, int B, int dim, const float* table, int num_items, int k,
                    int64_t* out_idx, float* out_score, void* ws, size_t ws_bytes, gtr_stream_t stream);
+/* Same with per-session excluded ids (serving, etpgt/serving/recommender.py:126-131:
+ * the session's items and the padding row never come back): session b excludes the
+ * ascending ids excl_ids[excl_ptr[b] .. excl_ptr[b+1]).  If fewer than k ids remain,
+ * the tail of out_idx is -1 (score -inf).                                           */
+int gtr_score_topk_masked(const float* se, int B, int dim, const float* table, int num_items, int k,
+                          const int32_t* excl_ptr, const int32_t* excl_ids, int64_t* out_idx, float* out_score,
+                          void* ws, size_t ws_bytes, gtr_stream_t stream);
 
 /* ---- GPU batch constructor (etpgt.data.gpu_batch) ----------------------------------
  * SessionDataset.__getitem__ + collate_fn (dataloader.py:64-202) on the device, writing
