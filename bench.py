@@ -42,6 +42,11 @@ CONFIGS = {
                name="C2 RetailRocket 82k-node/738k-edge, d=64, 2 layers, 1 head, BPR (5 neg)"),
     "c3": dict(D=128, H=4, K=16, loss="listwise", n_neg=100,
                name="C3 RetailRocket 82k-node/738k-edge, d=128, 2 layers, 4 heads, LapPE k=16, listwise (100 neg)"),
+    # configs[4] on one GPU (the strong-scaling curve's N=1 point): C3 model on the
+    # Yoochoose-scale graph, global batch 8192
+    "c5": dict(D=128, H=4, K=16, loss="listwise", n_neg=100, scale="yoochoose", batch=8192,
+               name="C5 Yoochoose-scale synthetic 1M-node/9M-edge, d=128, 2 layers, 4 heads, LapPE k=16, "
+                    "listwise (100 neg)"),
 }
 
 
@@ -56,7 +61,7 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
-    ap.add_argument("--batch-size", type=int, default=32)
+    ap.add_argument("--batch-size", type=int, default=None, help="sessions per GPU (default 32; c5: 8192)")
     ap.add_argument("--num-batches", type=int, default=64, help="distinct pre-staged batches per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-graph", action="store_true")
@@ -89,6 +94,8 @@ def main():
     torch.cuda.set_device(dev)
     coll_dev = dev if backend == "nccl" else torch.device("cpu")
     cfg = CONFIGS[args.config]
+    if args.batch_size is None:
+        args.batch_size = cfg.get("batch", 32)
 
     t0 = time.time()
     w = build_workload(args.config, args.batch_size, args.num_batches, dev, rank, use_graph=not args.no_graph,
@@ -168,7 +175,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "fp32",
-            "data": "synthetic RetailRocket-shaped sessions/graph (seed 42), random-init weights",
+            "data": ("synthetic Yoochoose-scale" if cfg.get("scale") else "synthetic RetailRocket-shaped")
+                    + " sessions/graph (seed 42), random-init weights",
             "config": {
                 "workload": cfg["name"],
                 "global_batch": B * world,
@@ -224,7 +232,12 @@ def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, us
     from etpgt.train.fused import FusedTrainStep
 
     cfg = CONFIGS[config]
-    data = make_sessions_and_graph(seed=42)
+    if cfg.get("scale") == "yoochoose":
+        from etpgt.data.synthetic import YOOCHOOSE_SCALE
+
+        data = make_sessions_and_graph(seed=42, **YOOCHOOSE_SCALE)
+    else:
+        data = make_sessions_and_graph(seed=42)
     T = data.table_rows
     batches = make_batches(data, B, num_batches, cfg["n_neg"], seed=42, start=rank * B * num_batches)
     st = batch_stats(batches)
