@@ -44,7 +44,7 @@ CONFIGS = {
                name="C3 RetailRocket 82k-node/738k-edge, d=128, 2 layers, 4 heads, LapPE k=16, listwise (100 neg)"),
     # configs[4] on one GPU (the strong-scaling curve's N=1 point): C3 model on the
     # Yoochoose-scale graph, global batch 8192
-    "c5": dict(D=128, H=4, K=16, loss="listwise", n_neg=100, scale="yoochoose", batch=8192,
+    "c5": dict(D=128, H=4, K=16, loss="listwise", n_neg=100, scale="yoochoose", batch=8192, lazy=True,
                name="C5 Yoochoose-scale synthetic 1M-node/9M-edge, d=128, 2 layers, 4 heads, LapPE k=16, "
                     "listwise (100 neg)"),
 }
@@ -66,6 +66,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--dp", action="store_true", help="force the data-parallel step (exchange) even at N=1")
+    ap.add_argument("--lazy", type=int, default=None,
+                    help="deferred zero-gradient AdamW of untouched table rows (1/0; default: per config)")
     ap.add_argument("--recall-steps", type=int, default=100,
                     help="Recall@10 parity leg: training steps of the HIP and oracle trainers (0 = skip)")
     ap.add_argument("--recall-sessions", type=int, default=2048, help="held-out sessions of the Recall@10 leg")
@@ -98,8 +100,9 @@ def main():
         args.batch_size = cfg.get("batch", 32)
 
     t0 = time.time()
+    lazy = bool(args.lazy) if args.lazy is not None else bool(cfg.get("lazy", False))
     w = build_workload(args.config, args.batch_size, args.num_batches, dev, rank, use_graph=not args.no_graph,
-                       data_parallel=True if args.dp else None)
+                       data_parallel=True if args.dp else None, lazy=lazy)
     step, staged, batches, data, T, B, touched, st = (w[k] for k in ("step", "staged", "batches", "data", "T", "B",
                                                                    "touched", "stats"))
     log(f"data: T={T} sessions={data.num_sessions} edges={data.edge_keys.size} setup {time.time()-t0:.1f}s {st}")
@@ -130,6 +133,7 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss)
+    step.flush()  # lazy table: bring every row to the last step before reading it
     replicas_identical = None
     if world > 1:  # data parallel: every rank must hold the same parameters
         chk = torch.stack([step.model.item_embedding.weight.double().sum(), step.eng.flat.flat.double().sum()])
@@ -189,6 +193,7 @@ def main():
                 "transport": "rccl" if backend == "nccl" else "gloo (shared-device rehearsal)",
                 "dp_exchange": step.dp is not None,
                 "hip_graph": not args.no_graph,
+                "lazy_table": lazy,
                 "gpu_ms_per_step_events": round(gpu_ms / args.steps, 4),
                 "final_loss": round(final_loss, 6),
                 "replicas_identical": replicas_identical,
@@ -223,7 +228,7 @@ def main():
 
 
 def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, use_graph: bool = True,
-                   data_parallel: bool | None = None) -> dict:
+                   data_parallel: bool | None = None, lazy: bool = False) -> dict:
     """Synthetic RetailRocket-shaped data, the model of `config`, a bound fused step
     and `num_batches` packed batches pre-staged in HBM."""
     from etpgt.data.batch import Caps
@@ -249,7 +254,7 @@ def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, us
         model.laplacian_pe._cached_pe = random_pe_table(T, cfg["K"])
     model = model.to(dev).train()
     step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, loss=cfg["loss"], use_graph=use_graph,
-                          data_parallel=data_parallel)
+                          data_parallel=data_parallel, lazy=lazy)
     caps = Caps(max(b.num_nodes for b in batches), B, max(b.num_edges for b in batches), cfg["n_neg"])
     step._bind(caps)  # data parallel: the ranks agree on the largest capacities
     caps = step.caps

@@ -111,7 +111,8 @@ template <int D>
 __device__ __forceinline__ void rows_body(int gid, const gtr_batch& bt, int T, const int32_t* skeys,
                                           const int32_t* svals, const float* dx0, const float* se,
                                           const float* coef_tgt, const float* coef_neg, float* table, float* m,
-                                          float* v, float* grad_dense, const AdamStep& st) {
+                                          float* v, float* grad_dense, const AdamStep& st,
+                                          int32_t* lazy_stamp = nullptr, int32_t lazy_t = 0) {
   constexpr int C4 = D / 4;
   const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
   const int i = gid / C4, c = gid - (gid / C4) * C4;
@@ -159,6 +160,7 @@ __device__ __forceinline__ void rows_body(int gid, const gtr_batch& bt, int T, c
   reinterpret_cast<float4*>(table)[base] = pv;
   reinterpret_cast<float4*>(m)[base] = mv;
   reinterpret_cast<float4*>(v)[base] = vv;
+  if (lazy_stamp && c == 0) lazy_stamp[key] = lazy_t;  // lazy table: current through this step
 }
 
 // Touched rows: one thread per (segment start, float4 column).  p/m/v of the row are
@@ -210,6 +212,78 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_adamw_sweep(int64_t nvec, int vpr
   __syncthreads();
   const AdamStep st = s_st;
   sweep_body(blockIdx.x, gridDim.x, nvec, vpr_log2, stamp, s_t, table, m, v, st);
+}
+
+
+// Lazy table: bring one float4 column of a row from its stamp to step `upto` with the
+// zero-gradient update of each step in order (AdamStep with step t's scalars from
+// consts[t]): the same float operations as the eager sweep applies, so bitwise equal.
+__device__ __forceinline__ void catch_up4(float4& p, float4& m, float4& v, int from, int upto, const gtr_adam& o,
+                                          const float* consts) {
+  if (from >= upto) return;
+  AdamStep st;
+  st.lr = o.lr; st.b1 = o.beta1; st.b2 = o.beta2; st.eps = o.eps; st.wd = o.weight_decay;
+  st.decoupled = o.decoupled;
+  st.decay_mul = (float)(1.0 - (double)o.lr * (double)o.weight_decay);
+  for (int t = from + 1; t <= upto; ++t) {
+    const float2 c = reinterpret_cast<const float2*>(consts)[t];
+    st.step_size = c.x;
+    st.bc2_sqrt = c.y;
+    st.apply(p.x, m.x, v.x, 0.0f);
+    st.apply(p.y, m.y, v.y, 0.0f);
+    st.apply(p.z, m.z, v.z, 0.0f);
+    st.apply(p.w, m.w, v.w, 0.0f);
+  }
+}
+
+// consts[t] exactly as AdamStep::init computes the step's scalars.
+__device__ __forceinline__ void lazy_consts_for(const gtr_adam& o, int64_t t, float* consts) {
+  AdamStep st;
+  st.init(o, t);
+  reinterpret_cast<float2*>(consts)[t] = make_float2(st.step_size, st.bc2_sqrt);
+}
+
+// Claim row `key` for catch-up to step t-1 (first claimer gets the old stamp; later
+// claimers of the same row see t-1) and bring it forward with the 16 lanes of a group
+// (lanes gl = 0..15 at gbase; they cover the row's float4 columns).  The per-step
+// scalars are fetched 16 steps at a time (one per lane) and broadcast by shuffles, so
+// the serial chain of updates never waits on memory.
+__device__ __forceinline__ void lazy_claim_row(int key, int T, int D, int32_t t, int gl, int gbase,
+                                               int32_t* stamp, const gtr_lazy& lz) {
+  int old = 0;
+  if (gl == 0 && key > 0 && key < T) old = atomicExch(stamp + key, t - 1);
+  old = __shfl(old, gbase);
+  if (!(key > 0 && key < T) || old >= t - 1) return;
+  const int C4 = D / 4;
+  float4* P = reinterpret_cast<float4*>(lz.table) + (size_t)key * C4;
+  float4* M = reinterpret_cast<float4*>(lz.m) + (size_t)key * C4;
+  float4* V = reinterpret_cast<float4*>(lz.v) + (size_t)key * C4;
+  const gtr_adam& o = lz.opt;
+  AdamStep st;
+  st.lr = o.lr; st.b1 = o.beta1; st.b2 = o.beta2; st.eps = o.eps; st.wd = o.weight_decay;
+  st.decoupled = o.decoupled;
+  st.decay_mul = (float)(1.0 - (double)o.lr * (double)o.weight_decay);
+  for (int c0 = 0; c0 < C4; c0 += 16) {  // D = 256: two column passes
+    const int c = c0 + gl;
+    const bool on = c < C4;
+    float4 p, m, v;
+    if (on) { p = P[c]; m = M[c]; v = V[c]; }
+    for (int t0 = old + 1; t0 <= t - 1; t0 += 16) {
+      const int cnt = min(16, t - t0);
+      const float2 cc = gl < cnt ? reinterpret_cast<const float2*>(lz.consts)[t0 + gl] : make_float2(0.f, 0.f);
+      for (int q = 0; q < cnt; ++q) {
+        st.step_size = __shfl(cc.x, gbase + q);
+        st.bc2_sqrt = __shfl(cc.y, gbase + q);
+        if (on) {
+          st.apply(p.x, m.x, v.x, 0.0f);
+          st.apply(p.y, m.y, v.y, 0.0f);
+          st.apply(p.z, m.z, v.z, 0.0f);
+          st.apply(p.w, m.w, v.w, 0.0f);
+        }
+      }
+    }
+    if (on) { P[c] = p; M[c] = m; V[c] = v; }
+  }
 }
 
 // ---- fused step: begin (counters, stamps, sorted contribution list) -------------------
@@ -265,6 +339,99 @@ __global__ __launch_bounds__(GTR_BEGIN_BLOCK) void k_step_begin(gtr_batch bt, in
     *step_dev = tnew;
     if (rng_ctr) *rng_ctr += 1;
   }
+}
+
+// Lazy variant: the same rank sort; each workgroup also claims and brings forward the
+// rows of its 64 slots (16 lanes per slot); the last arriving workgroup writes
+// consts[t] and advances the counters (every workgroup read the step first).
+__global__ __launch_bounds__(GTR_BEGIN_BLOCK) void k_step_begin_lazy(gtr_batch bt, int T, int D, int32_t* skeys,
+                                                                    int32_t* svals, int32_t* stamp,
+                                                                    int64_t* step_dev, uint32_t* rng_ctr,
+                                                                    gtr_lazy lz) {
+  __shared__ __attribute__((aligned(16))) uint32_t ck[GTR_BEGIN_MCAP];
+  __shared__ int s_part[GTR_BEGIN_WAVES][64];
+  __shared__ int s_flag;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
+  const int m4 = (m_cap + 3) & ~3;
+  const int N = bt.hdr[0], B = bt.hdr[1];
+  const int64_t t64 = *step_dev + 1;
+  const int32_t t = (int32_t)t64;
+  for (int j = tid; j < m4; j += GTR_BEGIN_BLOCK) {
+    uint32_t c = 0xFFFFFFFFu;
+    if (j < m_cap) c = ((uint32_t)contrib_key(bt, T, j, N, B) << 13) | (uint32_t)j;
+    ck[j] = c;
+  }
+  __syncthreads();
+  const int j = blockIdx.x * 64 + lane;
+  const uint32_t mine = j < m_cap ? ck[j] : 0u;
+  const int S = ((m4 / GTR_BEGIN_WAVES) + 4) & ~3;
+  const int i0 = wave * S, i1 = min(m4, i0 + S);
+  int rank = 0;
+  for (int i = i0; i < i1; i += 4) {
+    const uint4 q = *reinterpret_cast<const uint4*>(ck + i);
+    rank += (q.x < mine) + (q.y < mine) + (q.z < mine) + (q.w < mine);
+  }
+  s_part[wave][lane] = rank;
+  __syncthreads();
+  if (wave == 0 && j < m_cap) {
+    int r = 0;
+#pragma unroll
+    for (int w = 0; w < GTR_BEGIN_WAVES; ++w) r += s_part[w][lane];
+    skeys[r] = (int32_t)(mine >> 13);
+    svals[r] = (int32_t)(mine & 0x1FFFu);
+  }
+  {  // catch-up of this workgroup's 64 slots: 16 lanes per slot
+    const int slot = blockIdx.x * 64 + tid / 16;
+    const int key = slot < m_cap ? (int)(ck[slot] >> 13) : T;
+    lazy_claim_row(key, T, D, t, tid & 15, lane & ~15, stamp, lz);
+  }
+  if (!arrive_last(lz.cnt, gridDim.x, &s_flag)) return;
+  if (tid == 0) {
+    lazy_consts_for(lz.opt, t64, lz.consts);
+    *step_dev = t64;
+    if (rng_ctr) *rng_ctr += 1;
+    reset_counter(lz.cnt);
+  }
+}
+
+// Lazy catch-up for the large-batch (radix) path: 16 lanes per contribution slot.
+__global__ __launch_bounds__(GTR_BLOCK) void k_lazy_catchup(gtr_batch bt, int T, int D, int32_t* stamp,
+                                                            const int64_t* step_dev, gtr_lazy lz) {
+  const int gid = blockIdx.x * GTR_BLOCK + threadIdx.x;
+  const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
+  const int slot = gid / 16;
+  const int key = slot < m_cap ? contrib_key(bt, T, slot, bt.hdr[0], bt.hdr[1]) : T;
+  lazy_claim_row(key, T, D, (int32_t)(*step_dev + 1), threadIdx.x & 15, (threadIdx.x & 63) & ~15, stamp, lz);
+}
+
+__global__ void k_counters_lazy(int64_t* step_dev, uint32_t* rng_ctr, gtr_lazy lz) {
+  const int64_t t = *step_dev + 1;
+  lazy_consts_for(lz.opt, t, lz.consts);
+  *step_dev = t;
+  if (rng_ctr) *rng_ctr += 1;
+}
+
+// Bring every row to step *step_dev.
+__global__ __launch_bounds__(GTR_BLOCK) void k_lazy_flush(int T, int D, int32_t* stamp, const int64_t* step_dev,
+                                                          gtr_lazy lz) {
+  const int C4 = D / 4;
+  const int64_t gid = (int64_t)blockIdx.x * GTR_BLOCK + threadIdx.x;
+  const int64_t row = gid / C4;
+  const int c = (int)(gid - row * C4);
+  if (row >= T) return;
+  const int32_t t = (int32_t)*step_dev;
+  const int old = stamp[row];  // every column lane reads before lane 0 writes (same wave)
+  if (old >= t) return;
+  const size_t i = (size_t)row * C4 + c;
+  float4 p = reinterpret_cast<float4*>(lz.table)[i], m = reinterpret_cast<float4*>(lz.m)[i],
+         v = reinterpret_cast<float4*>(lz.v)[i];
+  catch_up4(p, m, v, old, t, lz.opt, lz.consts);
+  reinterpret_cast<float4*>(lz.table)[i] = p;
+  reinterpret_cast<float4*>(lz.m)[i] = m;
+  reinterpret_cast<float4*>(lz.v)[i] = v;
+  __builtin_amdgcn_wave_barrier();
+  if (c == 0) stamp[row] = t;
 }
 
 __global__ void k_counters(int64_t* step_dev, uint32_t* rng_ctr) {
@@ -382,7 +549,8 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_tail_carry(gtr_batch bt, int T, g
 // Rows part of the tail for window w = blk: every segment starting in the window is
 // summed (in-window piece + carries of the following windows) and AdamW-updated.
 template <int D>
-__device__ __forceinline__ void window_rows(int w, const gtr_batch& bt, int T, const gtr_tail& tl, const AdamStep& st) {
+__device__ __forceinline__ void window_rows(int w, const gtr_batch& bt, int T, const gtr_tail& tl, const AdamStep& st,
+                                            int32_t* lazy_stamp, int32_t lazy_t) {
   constexpr int C4 = D / 4, NG = GTR_BLOCK / C4;
   __shared__ int s_bnd[TW + 1];
   __shared__ int s_nb;
@@ -434,6 +602,7 @@ __device__ __forceinline__ void window_rows(int w, const gtr_batch& bt, int T, c
     reinterpret_cast<float4*>(tl.table)[base] = pv;
     reinterpret_cast<float4*>(tl.table_m)[base] = mv;
     reinterpret_cast<float4*>(tl.table_v)[base] = vv;
+    if (lazy_stamp && gl == 0) lazy_stamp[key] = lazy_t;
   }
 }
 
@@ -452,12 +621,13 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_step_tail(TailK a) {
   const AdamStep st = s_st;
   const int blk = blockIdx.x;
   if (blk < a.nb_rows && a.windowed) {
-    window_rows<D>(blk, a.bt, a.T, a.tl, st);
+    window_rows<D>(blk, a.bt, a.T, a.tl, st, a.tl.lazy_consts ? a.tl.stamp : nullptr, s_t);
     return;
   }
   if (blk < a.nb_rows) {
     rows_body<D>(blk * GTR_BLOCK + tid, a.bt, a.T, a.tl.skeys, a.tl.svals, a.tl.dx0, a.tl.se, a.tl.coef_tgt,
-                 a.tl.coef_neg, a.tl.table, a.tl.table_m, a.tl.table_v, nullptr, st);
+                 a.tl.coef_neg, a.tl.table, a.tl.table_m, a.tl.table_v, nullptr, st,
+                 a.tl.lazy_consts ? a.tl.stamp : nullptr, s_t);
     return;
   }
   if (blk < a.nb_rows + a.nb_small) {
@@ -628,7 +798,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_dp_stamp(gtr_dp_layout lay, int T
   const int k = keys[i];
   if (k <= 0 || k >= T || (i > 0 && keys[i - 1] == k)) return;
   const int32_t t = (int32_t)(*step_dev + step_offset);
-  stamp[k] = t;
+  if (stamp) stamp[k] = t;  // eager: marks the row for the sweep; lazy: dp_tail stamps after catch-up
   slot[(size_t)k * lay.world + r] = make_int2(t, i);
 }
 
@@ -685,6 +855,10 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_dp_tail(DpTailK a) {
     float4 pv = reinterpret_cast<const float4*>(a.tl.table)[base];
     float4 mv = reinterpret_cast<const float4*>(a.tl.table_m)[base];
     float4 vv = reinterpret_cast<const float4*>(a.tl.table_v)[base];
+    if (a.tl.lazy_consts) {  // rows only other ranks touched are still behind
+      const int old = a.tl.stamp[k];
+      catch_up4(pv, mv, vv, old, t - 1, a.opt, a.tl.lazy_consts);
+    }
     st.apply(pv.x, mv.x, vv.x, g.x);
     st.apply(pv.y, mv.y, vv.y, g.y);
     st.apply(pv.z, mv.z, vv.z, g.z);
@@ -692,6 +866,10 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_dp_tail(DpTailK a) {
     reinterpret_cast<float4*>(a.tl.table)[base] = pv;
     reinterpret_cast<float4*>(a.tl.table_m)[base] = mv;
     reinterpret_cast<float4*>(a.tl.table_v)[base] = vv;
+    if (a.tl.lazy_consts) {
+      __builtin_amdgcn_wave_barrier();  // the row's column lanes (one wave) read the stamp above
+      if (c == 0) a.tl.stamp[k] = t;
+    }
     return;
   }
   if (blk < a.nb_rows + a.nb_small) {
@@ -899,6 +1077,49 @@ int gtr_step_begin(const gtr_batch* bt, int num_items, int32_t* keys, int32_t* v
   return GTR_OK;
 }
 
+int gtr_step_begin_lazy(const gtr_batch* bt, int num_items, int dim, int32_t* keys, int32_t* vals, int32_t* skeys,
+                        int32_t* svals, int32_t* stamp, int64_t* step_dev, uint32_t* rng_ctr, void* tmp,
+                        size_t tmp_bytes, const gtr_lazy* lazy, gtr_stream_t stream) {
+  if (!bt || !skeys || !svals || !step_dev || !stamp || bt->n_neg <= 0 || num_items <= 0 || !dim_ok(dim) || !lazy ||
+      !lazy->consts || !lazy->cnt || !lazy->table || !lazy->m || !lazy->v) {
+    set_error("gtr_step_begin_lazy: bad arguments");
+    return GTR_E_ARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int m_cap = bt->n_cap + bt->b_cap * (1 + bt->n_neg);
+  if (m_cap <= GTR_BEGIN_MCAP && num_items < GTR_BEGIN_KEY_LIMIT) {
+    hipLaunchKernelGGL(k_step_begin_lazy, dim3((m_cap + 63) / 64), dim3(GTR_BEGIN_BLOCK), 0, s, *bt, num_items, dim,
+                       skeys, svals, stamp, step_dev, rng_ctr, *lazy);
+    GTR_HIP_CHECK_LAUNCH();
+    return GTR_OK;
+  }
+  if (!keys || !vals || !tmp) { set_error("gtr_step_begin_lazy: large batch needs keys/vals/tmp scratch"); return GTR_E_ARG; }
+  int rc = gtr_contrib_prep(bt, num_items, keys, vals, nullptr, step_dev, stream);
+  if (rc) return rc;
+  rc = gtr_contrib_sort(keys, vals, skeys, svals, m_cap, num_items, tmp, tmp_bytes, stream);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_lazy_catchup, dim3((unsigned)(((int64_t)m_cap * 16 + GTR_BLOCK - 1) / GTR_BLOCK)),
+                     dim3(GTR_BLOCK), 0, s, *bt, num_items, dim, stamp, step_dev, *lazy);
+  GTR_HIP_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_counters_lazy, dim3(1), dim3(1), 0, s, step_dev, rng_ctr, *lazy);
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+int gtr_lazy_flush(int num_items, int dim, int32_t* stamp, const int64_t* step_dev, const gtr_lazy* lazy,
+                   gtr_stream_t stream) {
+  if (!stamp || !step_dev || !dim_ok(dim) || num_items <= 0 || !lazy || !lazy->consts || !lazy->table ||
+      !lazy->m || !lazy->v) {
+    set_error("gtr_lazy_flush: bad arguments");
+    return GTR_E_ARG;
+  }
+  const int64_t threads = (int64_t)num_items * (dim / 4);
+  hipLaunchKernelGGL(k_lazy_flush, dim3((unsigned)((threads + GTR_BLOCK - 1) / GTR_BLOCK)), dim3(GTR_BLOCK), 0,
+                     (hipStream_t)stream, num_items, dim, stamp, step_dev, *lazy);
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
 int gtr_step_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tail, const gtr_segment* segs,
                   int nseg, const gtr_adam* opt, gtr_stream_t stream) {
   if (!bt || !tail || !opt || !opt->step_dev || !dim_ok(dim) || num_items <= 0 || nseg < 0 ||
@@ -944,7 +1165,8 @@ int gtr_step_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* t
   k.nvec = (int64_t)num_items * dim / 4;
   k.vpr_log2 = 0;
   while ((1 << k.vpr_log2) < dim / 4) ++k.vpr_log2;
-  const int64_t from = t.sweep_from < 0 ? 0 : (t.sweep_from > num_items ? num_items : t.sweep_from);
+  const int64_t from = t.lazy_consts ? num_items  // lazy: no untouched-row sweep
+                                      : (t.sweep_from < 0 ? 0 : (t.sweep_from > num_items ? num_items : t.sweep_from));
   k.vbegin = from * (dim / 4);
   int64_t sw = (k.nvec - k.vbegin + GTR_BLOCK - 1) / GTR_BLOCK;
   k.nb_sweep = (int)(sw > 2048 ? 2048 : sw);
@@ -1009,7 +1231,8 @@ int gtr_dp_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tai
   hipStream_t s = (hipStream_t)stream;
   const int64_t slots = (int64_t)lay->world * lay->m_cap;
   hipLaunchKernelGGL(k_dp_stamp, dim3((unsigned)((slots + GTR_BLOCK - 1) / GTR_BLOCK)), dim3(GTR_BLOCK), 0, s, *lay,
-                     num_items, recv, tail->stamp, reinterpret_cast<int2*>(slot), opt->step_dev, opt->step_offset);
+                     num_items, recv, tail->lazy_consts ? nullptr : tail->stamp, reinterpret_cast<int2*>(slot),
+                     opt->step_dev, opt->step_offset);
   GTR_HIP_CHECK_LAUNCH();
   DpTailK k{};
   k.tl = *tail;
@@ -1024,7 +1247,7 @@ int gtr_dp_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tai
   k.vpr_log2 = 0;
   while ((1 << k.vpr_log2) < dim / 4) ++k.vpr_log2;
   int64_t sw = (k.nvec + GTR_BLOCK - 1) / GTR_BLOCK;
-  k.nb_sweep = (int)(sw > 2048 ? 2048 : sw);
+  k.nb_sweep = tail->lazy_consts ? 0 : (int)(sw > 2048 ? 2048 : sw);  // lazy: no untouched-row sweep
   const int grid = k.nb_rows + k.nb_small + k.nb_sweep;
   switch (dim) {
     case 32: hipLaunchKernelGGL(k_dp_tail<32>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;

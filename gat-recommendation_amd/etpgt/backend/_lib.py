@@ -82,11 +82,17 @@ class GtrTail(C.Structure):
         ("table", P), ("table_m", P), ("table_v", P), ("stamp", P),
         ("flat", P), ("flat_m", P), ("flat_v", P), ("flat_total", i64),
         ("loss_part", P), ("loss_out", P), ("loss_nparts", i32), ("pad0", i32), ("carry", P),
-        ("sweep_from", i64),
+        ("sweep_from", i64), ("lazy_consts", P),
     ]
 
 
 SWEEP_SLOTS = 8
+
+
+class GtrLazy(C.Structure):
+    _fields_ = [
+        ("consts", P), ("cap", i32), ("pad", i32), ("cnt", P), ("table", P), ("m", P), ("v", P), ("opt", GtrAdam),
+    ]
 
 
 class GtrSessions(C.Structure):
@@ -137,6 +143,8 @@ _SIGS = {
     "gtr_dp_tail": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P]),
     "gtr_step_begin": (C.c_int, [P, C.c_int, P, P, P, P, P, P, P, P, C.c_size_t, P]),
     "gtr_step_tail": (C.c_int, [P, C.c_int, C.c_int, P, P, C.c_int, P, P]),
+    "gtr_step_begin_lazy": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P, P, P, C.c_size_t, P, P]),
+    "gtr_lazy_flush": (C.c_int, [C.c_int, C.c_int, P, P, P, P]),
     "gtr_tail_carry_floats": (C.c_int, [C.c_int, C.c_int]),
     "gtr_edge_hash_slots": (C.c_int, [i64, C.POINTER(i64)]),
     "gtr_edge_hash_build": (C.c_int, [P, i64, P, i64, P]),

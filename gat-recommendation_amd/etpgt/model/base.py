@@ -32,7 +32,19 @@ class BaseRecommendationModel(nn.Module, ABC):
     def forward(self, batch):
         ...
 
+    def _sync_lazy(self) -> None:
+        """A fused step in lazy mode defers untouched rows' zero-gradient AdamW updates;
+        bring the table up to date before anything outside the step reads it."""
+        cb = self.__dict__.get("_lazy_sync")
+        if cb is not None:
+            cb()
+
+    def state_dict(self, *args, **kwargs):
+        self._sync_lazy()
+        return super().state_dict(*args, **kwargs)
+
     def get_item_embeddings(self) -> torch.Tensor:
+        self._sync_lazy()
         return self.item_embedding.weight
 
     def predict(self, session_embeddings: torch.Tensor, k: int = 20) -> torch.Tensor:

@@ -118,6 +118,7 @@ class GraphTransformer(BaseRecommendationModel):
         """Session embeddings [B, hidden_dim] for a PyG-style batch (graph_transformer.py:126-182)."""
         from etpgt.backend.ops import GraphTransformerFn
 
+        self._sync_lazy()
         dev = self.item_embedding.weight.device
         if dev.type != "cuda":
             raise RuntimeError("GraphTransformer runs on the MI355X HIP path only; move the model to 'cuda'")

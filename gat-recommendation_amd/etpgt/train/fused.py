@@ -33,7 +33,8 @@ class FusedTrainStep:
     def __init__(self, model, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 1e-5, decoupled: bool = True, loss: str = "bpr",
                  temperature: float = 1.0, alpha: float = 0.7, caps: Caps | None = None,
-                 use_graph: bool = True, data_parallel: bool | None = None, process_group=None):
+                 use_graph: bool = True, data_parallel: bool | None = None, process_group=None,
+                 lazy: bool = False):
         if loss not in ("bpr", "listwise", "dual", "sampled_softmax"):
             raise ValueError(f"Unknown loss type: {loss}")
         self.model = model
@@ -66,11 +67,49 @@ class FusedTrainStep:
         self.m_flat = torch.zeros_like(eng.flat.flat)
         self.v_flat = torch.zeros_like(eng.flat.flat)
         self.stamp = torch.zeros(T, dtype=torch.int32, device=self.dev)
+        # deferred zero-gradient AdamW of untouched table rows (gtr_lazy in gtr.h):
+        # bitwise-identical to the dense update, applied when a row is next read or on flush()
+        self.lazy = bool(lazy)
+        self._host_steps = 0
+        self._dirty = False
+        self.lz = None
+        if self.lazy:
+            self._lazy_alloc(1 << 16)
+            model.__dict__["_lazy_sync"] = self.flush  # forward / predict / state_dict bring rows up to date
         self.caps = None
         self.graph = None
         self.builder = None
         if caps is not None:
             self._bind(caps)
+
+    # ------------------------------------------------------------------ lazy table
+    def _lazy_alloc(self, cap: int):
+        consts = torch.zeros(cap, 2, dtype=torch.float32, device=self.dev)
+        old = getattr(self, "lazy_consts", None)
+        if old is not None:
+            keep = min(cap, old.shape[0])
+            consts[:keep].copy_(old[:keep])
+        self.lazy_consts = consts
+        if getattr(self, "lazy_cnt", None) is None:
+            self.lazy_cnt = torch.zeros(4, dtype=torch.int32, device=self.dev)
+        lz = L.GtrLazy()
+        lz.consts, lz.cap, lz.cnt = consts.data_ptr(), cap, self.lazy_cnt.data_ptr()
+        lz.table = self.eng.model.item_embedding.weight.data_ptr()
+        lz.m, lz.v = self.m_tab.data_ptr(), self.v_tab.data_ptr()
+        lz.opt = self.adam
+        self.lz = lz
+        if getattr(self, "tail", None) is not None:
+            self.tail.lazy_consts = consts.data_ptr()
+        self.graph = self.graph_pe = self.graph_b = None  # captured pointers changed
+
+    def flush(self):
+        """Bring every table row up to the current step (lazy mode; no-op otherwise)."""
+        if not self.lazy or not self._dirty:
+            return
+        L.check(L.lib().gtr_lazy_flush(self.eng.T, self.eng.D, self.stamp.data_ptr(), self.step_dev.data_ptr(),
+                                       C.byref(self.lz), torch.cuda.current_stream(self.dev).cuda_stream),
+                "lazy_flush")
+        self._dirty = False
 
     # ------------------------------------------------------------------ buffers
     def _agree(self, caps: Caps) -> Caps:
@@ -126,7 +165,7 @@ class FusedTrainStep:
         # grids): the chain's 2L launches each sweep a slice of the table (gtr_sweep)
         self.sweep = None
         t.sweep_from = 0
-        chain = os.environ.get("GTR_CHAIN_SWEEP", "1") != "0"
+        chain = os.environ.get("GTR_CHAIN_SWEEP", "1") != "0" and not self.lazy
         # slots: conv_fwd(l) -> l, readout -> L, conv_bwd(l) -> 2L - l; weighted by the
         # launches' measured slack (the readout is shorter than a layer kernel)
         wts = [1.0] * eng.L + [0.75] + [1.0] * eng.L
@@ -150,6 +189,7 @@ class FusedTrainStep:
             self.sweep = sw
             self.cfg.sweep = C.addressof(sw)
             t.sweep_from = eng.T
+        t.lazy_consts = self.lazy_consts.data_ptr() if self.lazy else None
         nc = int(L.lib().gtr_tail_carry_floats(m_cap, eng.D))
         self.carry = torch.zeros(max(nc, 4), dtype=torch.float32, device=self.dev) if nc > 0 else None
         t.carry = self.carry.data_ptr() if self.carry is not None else None
@@ -223,10 +263,17 @@ class FusedTrainStep:
         st = torch.cuda.current_stream(self.dev).cuda_stream
         if self.builder is not None:
             self.builder.launch(bs, self.caps, st)
-        L.check(lib.gtr_step_begin(C.byref(bs), eng.T, self.keys.data_ptr(), self.vals.data_ptr(),
-                                   self.skeys.data_ptr(), self.svals.data_ptr(), self.stamp.data_ptr(),
-                                   self.step_dev.data_ptr(), eng.rng_ctr.data_ptr(), self.sort_tmp.data_ptr(),
-                                   self.sort_tmp.numel(), st), "step_begin")
+        if self.lazy:
+            L.check(lib.gtr_step_begin_lazy(C.byref(bs), eng.T, eng.D, self.keys.data_ptr(), self.vals.data_ptr(),
+                                            self.skeys.data_ptr(), self.svals.data_ptr(), self.stamp.data_ptr(),
+                                            self.step_dev.data_ptr(), eng.rng_ctr.data_ptr(),
+                                            self.sort_tmp.data_ptr(), self.sort_tmp.numel(), C.byref(self.lz), st),
+                    "step_begin_lazy")
+        else:
+            L.check(lib.gtr_step_begin(C.byref(bs), eng.T, self.keys.data_ptr(), self.vals.data_ptr(),
+                                       self.skeys.data_ptr(), self.svals.data_ptr(), self.stamp.data_ptr(),
+                                       self.step_dev.data_ptr(), eng.rng_ctr.data_ptr(), self.sort_tmp.data_ptr(),
+                                       self.sort_tmp.numel(), st), "step_begin")
         eng.run_forward(ws, cfg, bs, L.RO_FWD | L.RO_LOSS | L.RO_BWD, self.loss_kind, self.temperature, self.alpha)
         eng.run_backward(ws, cfg, bs)
         if self.dp is not None:
@@ -278,6 +325,11 @@ class FusedTrainStep:
         self.eng.check_intact()
         if not self.model.training:
             raise RuntimeError("FusedTrainStep requires model.train()")
+        if self.lazy:
+            if self._host_steps + 2 >= self.lz.cap:
+                self._lazy_alloc(2 * self.lz.cap)
+            self._host_steps += 1
+            self._dirty = True
         if self.use_graph:
             g = self.graph_pe if with_pe else self.graph
             if g is None:
@@ -309,6 +361,7 @@ class FusedTrainStep:
 
     def export_optimizer_state(self, optimizer: torch.optim.Optimizer):
         """Write exp_avg / exp_avg_sq / step into a torch Adam(W) optimizer's state."""
+        self.flush()
         t = torch.tensor(float(self.steps))
         tab = self.model.item_embedding.weight
         views_m = self.eng.flat.grad_views(self.m_flat)

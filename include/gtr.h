@@ -286,6 +286,37 @@ int gtr_step_begin(const gtr_batch* bt, int num_items, int32_t* keys, int32_t* v
                    int32_t* svals, int32_t* stamp, int64_t* step_dev, uint32_t* rng_ctr, void* tmp,
                    size_t tmp_bytes, gtr_stream_t stream);
 
+/* ---- deferred zero-gradient AdamW ("lazy" table, bitwise-identical) ---------------
+ * The reference's dense AdamW updates every table row every step; a row the batch does
+ * not touch takes the g = 0 update, whose only inputs are the row's own p, m, v and the
+ * step's scalars.  In lazy mode those updates are deferred: stamp[row] = the step through
+ * which the row is current, and a row is brought forward -- the same per-step update,
+ * applied step by step with that step's scalars, so the floats are identical to eager
+ * sweeping -- right before it is read (gtr_step_begin_lazy, gtr_dp_tail) or on demand
+ * (gtr_lazy_flush: evaluation, checkpoints).  The step tail then updates only the
+ * touched rows.  consts[t] = {lr / (1 - beta1^t), sqrt(1 - beta2^t)} (fp32 of the
+ * double expressions, exactly as the eager kernels compute them), filled by the begin
+ * kernel of step t; cap = its capacity in steps.                                      */
+typedef struct gtr_lazy {
+  float* consts;   /* [cap][2] */
+  int32_t cap;
+  int32_t pad;
+  uint32_t* cnt;   /* [1] arrival counter (zero-initialised once) */
+  float* table;
+  float* m;
+  float* v;
+  gtr_adam opt;    /* by value */
+} gtr_lazy;
+
+/* gtr_step_begin + the lazy catch-up of every touched row (stamp[row] -> t-1) and
+ * consts[t]; the step counter advances after every workgroup has read it.          */
+int gtr_step_begin_lazy(const gtr_batch* bt, int num_items, int dim, int32_t* keys, int32_t* vals, int32_t* skeys,
+                        int32_t* svals, int32_t* stamp, int64_t* step_dev, uint32_t* rng_ctr, void* tmp,
+                        size_t tmp_bytes, const gtr_lazy* lazy, gtr_stream_t stream);
+/* Bring every row forward to step *step_dev (stamp[row] = *step_dev).               */
+int gtr_lazy_flush(int num_items, int dim, int32_t* stamp, const int64_t* step_dev, const gtr_lazy* lazy,
+                   gtr_stream_t stream);
+
 /* Inputs of the optimizer tail of a fused step.                                  */
 typedef struct gtr_tail {
   const int32_t* skeys;   /* sorted contribution list (gtr_step_begin)             */
@@ -309,6 +340,8 @@ typedef struct gtr_tail {
   float* carry;           /* large batches (m_cap > 8192): [gtr_tail_carry_floats] scratch
                              for segment pieces spanning windows of the sorted list; else NULL */
   int64_t sweep_from;     /* untouched rows below this were updated during the chain (gtr_sweep) */
+  const float* lazy_consts; /* lazy mode (gtr_lazy.consts): no untouched-row sweep; touched rows
+                               are stamped with the step; the dp tail catches rows up first */
 } gtr_tail;
 
 /* Floats of gtr_tail.carry needed at contribution capacity m_cap (0: not used).      */

@@ -58,7 +58,8 @@ def test_struct_layouts_match_header():
     for cname, py in (("gtr_batch", _lib.GtrBatch), ("gtr_config", _lib.GtrConfig), ("gtr_layer", _lib.GtrLayer),
                       ("gtr_embed", _lib.GtrEmbed), ("gtr_head", _lib.GtrHead), ("gtr_segment", _lib.GtrSegment),
                       ("gtr_adam", _lib.GtrAdam), ("gtr_tail", _lib.GtrTail), ("gtr_dp_layout", _lib.GtrDpLayout),
-                      ("gtr_sweep", _lib.GtrSweep), ("gtr_sessions", _lib.GtrSessions)):
+                      ("gtr_sweep", _lib.GtrSweep), ("gtr_sessions", _lib.GtrSessions),
+                      ("gtr_lazy", _lib.GtrLazy)):
         body = re.search(r"typedef struct %s \{(.*?)\} %s;" % (cname, cname), src, re.S).group(1)
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
         names = []

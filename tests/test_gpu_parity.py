@@ -267,3 +267,60 @@ def test_fused_steps_wave_readout_large_batch(monkeypatch):
     with several sessions per wave (grid-stride), 100 listwise negatives."""
     monkeypatch.delenv("GTR_RO_WAVE_MIN_B", raising=False)
     _fused_vs_reference(64, 2, 0, "listwise", "adamw", True, B=2100, steps=2)
+
+
+def _lazy_vs_eager(D, H, K, loss, opt, B, steps, dropout=0.1, use_graph=True, dp=None, cap=None):
+    T = data().table_rows
+    n = 5 if loss != "listwise" else 100
+    m1, _ = make_pair(T, D, H, K=K, dropout=dropout, seed=7)
+    m2 = copy.deepcopy(m1)
+    m1.train(); m2.train()
+    kw = dict(lr=1e-3, weight_decay=1e-2, decoupled=opt == "adamw", loss=loss, use_graph=use_graph,
+              data_parallel=dp)
+    f1 = FusedTrainStep(m1, **kw)
+    f2 = FusedTrainStep(m2, lazy=True, **kw)
+    if cap is not None:
+        f2._lazy_alloc(cap)
+    for sb in batches(data(), B, n, steps, seed=13):
+        l1 = float(f1(sb.to("cuda")))
+        l2 = float(f2(sb.to("cuda")))
+        assert l1 == l2
+    sd1, sd2 = m1.state_dict(), m2.state_dict()  # state_dict() flushes the lazy table
+    for k in sd1:
+        assert torch.equal(sd1[k], sd2[k]), k
+    assert torch.equal(f1.m_tab, f2.m_tab) and torch.equal(f1.v_tab, f2.v_tab)
+    assert torch.equal(f1.m_flat, f2.m_flat) and torch.equal(f1.v_flat, f2.v_flat)
+    return f2
+
+
+@pytest.mark.parametrize("D,H,K,loss,opt", [(64, 1, 0, "bpr", "adamw"), (128, 4, 16, "listwise", "adam"),
+                                            (32, 2, 0, "dual", "adamw")])
+def test_lazy_table_bitwise_equals_dense_adamw(D, H, K, loss, opt):
+    """Deferred zero-gradient AdamW (gtr_step_begin_lazy / gtr_lazy_flush): after k steps
+    the table, its moments and every parameter equal the eager dense update bit for bit
+    (dropout on: both use the same device streams)."""
+    _lazy_vs_eager(D, H, K, loss, opt, B=32, steps=5)
+
+
+def test_lazy_table_large_batch_and_capacity_growth():
+    """Radix-sort begin path (B = 1400) + consts table growth (capacity 4 -> 8 -> 16)."""
+    _lazy_vs_eager(64, 2, 0, "bpr", "adamw", B=1400, steps=2)
+    _lazy_vs_eager(64, 1, 0, "bpr", "adamw", B=32, steps=10, cap=4)
+
+
+def test_lazy_table_data_parallel_world1():
+    """Data-parallel tail in lazy mode (catch-up of union rows in gtr_dp_tail)."""
+    _lazy_vs_eager(64, 2, 0, "bpr", "adamw", B=32, steps=4, dp=True)
+
+
+def test_lazy_table_flushes_before_eval_forward():
+    """model(batch) in eval mode after lazy steps sees the up-to-date table (forward hook)."""
+    f2 = _lazy_vs_eager(64, 1, 0, "bpr", "adamw", B=32, steps=3)
+    m2 = f2.model
+    sb = batches(data(), 32, 5, 1, seed=99)[0]
+    f2(sb.to("cuda"))  # dirty again
+    assert f2._dirty
+    m2.eval()
+    with torch.no_grad():
+        m2(sb.to("cuda"))
+    assert not f2._dirty
