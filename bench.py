@@ -66,6 +66,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--dp", action="store_true", help="force the data-parallel step (exchange) even at N=1")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="strong scaling: fixed global batch split over the ranks, SyncBN (1 GPU semantics)")
+    ap.add_argument("--sync-bn", action="store_true", help="BatchNorm statistics over every rank's batch")
     ap.add_argument("--lazy", type=int, default=None,
                     help="deferred zero-gradient AdamW of untouched table rows (1/0; default: per config)")
     ap.add_argument("--recall-steps", type=int, default=100,
@@ -96,13 +99,20 @@ def main():
     torch.cuda.set_device(dev)
     coll_dev = dev if backend == "nccl" else torch.device("cpu")
     cfg = CONFIGS[args.config]
+    strong = args.global_batch is not None
+    if strong:
+        if args.global_batch % world:
+            raise SystemExit("--global-batch must divide by the number of GPUs")
+        args.batch_size = args.global_batch // world
+        args.sync_bn = True
     if args.batch_size is None:
         args.batch_size = cfg.get("batch", 32)
 
     t0 = time.time()
     lazy = bool(args.lazy) if args.lazy is not None else bool(cfg.get("lazy", False))
     w = build_workload(args.config, args.batch_size, args.num_batches, dev, rank, use_graph=not args.no_graph,
-                       data_parallel=True if args.dp else None, lazy=lazy)
+                       data_parallel=True if (args.dp or args.sync_bn) else None, lazy=lazy,
+                       sync_bn=args.sync_bn and world > 1)
     step, staged, batches, data, T, B, touched, st = (w[k] for k in ("step", "staged", "batches", "data", "T", "B",
                                                                    "touched", "stats"))
     log(f"data: T={T} sessions={data.num_sessions} edges={data.edge_keys.size} setup {time.time()-t0:.1f}s {st}")
@@ -176,7 +186,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "fp32",
             "data": ("synthetic Yoochoose-scale" if cfg.get("scale") else "synthetic RetailRocket-shaped")
@@ -194,6 +204,7 @@ def main():
                 "dp_exchange": step.dp is not None,
                 "hip_graph": not args.no_graph,
                 "lazy_table": lazy,
+                "sync_bn": bool(args.sync_bn and world > 1),
                 "gpu_ms_per_step_events": round(gpu_ms / args.steps, 4),
                 "final_loss": round(final_loss, 6),
                 "replicas_identical": replicas_identical,
@@ -228,7 +239,7 @@ def main():
 
 
 def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, use_graph: bool = True,
-                   data_parallel: bool | None = None, lazy: bool = False) -> dict:
+                   data_parallel: bool | None = None, lazy: bool = False, sync_bn: bool = False) -> dict:
     """Synthetic RetailRocket-shaped data, the model of `config`, a bound fused step
     and `num_batches` packed batches pre-staged in HBM."""
     from etpgt.data.batch import Caps
@@ -254,7 +265,7 @@ def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, us
         model.laplacian_pe._cached_pe = random_pe_table(T, cfg["K"])
     model = model.to(dev).train()
     step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, loss=cfg["loss"], use_graph=use_graph,
-                          data_parallel=data_parallel, lazy=lazy)
+                          data_parallel=data_parallel, lazy=lazy, sync_bn=sync_bn)
     caps = Caps(max(b.num_nodes for b in batches), B, max(b.num_edges for b in batches), cfg["n_neg"])
     step._bind(caps)  # data parallel: the ranks agree on the largest capacities
     caps = step.caps

@@ -49,6 +49,9 @@ struct ConvBwdK {
   float* dx0;
   gtr_sweep sw;         // untouched-row AdamW slice run by blocks >= main_grid
   int sw_slot, main_grid;
+  int sync, nparts_bwd, nparts_fwd, pad_s;  // SyncBN: every rank's partials (this layer)
+  const float* gpart_all;
+  const float* part_all;
 };
 
 // Destination-row backward: BatchNorm backward, beta gate, softmax backward, dQ, dS.
@@ -198,9 +201,18 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   GTR_PH(a.layer, 0);
   const int Gn = a.bt.hdr[4];
-  const int N = a.bt.hdr[0];
+  int N = a.bt.hdr[0];
   const int g = blockIdx.x;
-  if (g >= Gn) return;
+  if (g >= Gn) {
+    if (a.sync && a.has_prev)  // SyncBN: an empty group's backward partial is zero
+      for (int j = threadIdx.x; j < 2 * D; j += CONV_BLOCK) a.p_gpart[(size_t)g * 2 * D + j] = 0.0f;
+    return;
+  }
+  if (a.sync) {  // BatchNorm over every rank's nodes: N = the sum of all partial counts
+    float n = 0.0f;
+    for (int q = 0; q < a.nparts_fwd; ++q) n += a.part_all[(size_t)q * (1 + 2 * D)];
+    N = (int)(n + 0.5f);
+  }
   const int r0 = a.bt.grp_row[g], r1 = a.bt.grp_row[g + 1];
   // groups hold whole sessions, so the group's out-edges (CSR by source) start at the
   // same offset as its in-edges: edges with src < r0 are exactly those with dst < r0
@@ -218,11 +230,12 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
 
   // ---- this layer's BatchNorm backward sums: reduce the producer's partials (cred)
   if (a.cred) {
-    const int np = a.gpart_n >= 0 ? a.gpart_n : Gn;
+    const int np = a.sync ? a.nparts_bwd : (a.gpart_n >= 0 ? a.gpart_n : Gn);
+    const float* gp = a.sync ? a.gpart_all : a.gpart;
     for (int j = tid; j < 2 * D; j += CONV_BLOCK) {
       float acc = 0.0f;
 #pragma unroll 8
-      for (int q = 0; q < np; ++q) acc += a.gpart[(size_t)q * 2 * D + j];
+      for (int q = 0; q < np; ++q) acc += gp[(size_t)q * 2 * D + j];
       s_gs[j] = acc;
       if (g == 0) a.gsum[j] = acc;
     }
@@ -673,6 +686,16 @@ extern "C" int gtr_conv_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     k.p_gsum = P.bn_gsum; k.p_cnt = P.cnt + 1;
   }
   k.dx0 = dx0;
+  k.sync = cfg->sync_bn;
+  k.gpart_all = L.bn_gpart_all;
+  k.nparts_bwd = L.nparts_bwd;
+  k.part_all = L.bn_part_all;
+  k.nparts_fwd = L.nparts_fwd;
+  if (cfg->sync_bn && (!cfg->consumer_reduce || !L.bn_gpart_all || !L.bn_part_all || L.nparts_bwd <= 0 ||
+                       L.nparts_fwd <= 0)) {
+    set_error("gtr_conv_bwd: sync_bn needs consumer_reduce and the gathered partials of layer %d", l);
+    return GTR_E_ARG;
+  }
   int grid = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;
   if (grid <= 0) return GTR_OK;
   k.main_grid = grid;

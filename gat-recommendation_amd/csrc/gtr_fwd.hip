@@ -61,6 +61,8 @@ struct ConvFwdK {
   int64_t* bn_nbt;
   gtr_sweep sw;         // untouched-row AdamW slice run by blocks >= main_grid
   int sw_slot, main_grid;
+  int sync, p_nparts;   // SyncBN: previous layer's partials of every rank (p_part_all, p_nparts)
+  const float* p_part_all;
 };
 
 // Block prologue shared by k_conv_fwd (previous layer) and k_readout (last layer):
@@ -187,7 +189,11 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
   GTR_PH_CLK(a.layer, 6);
   const int Gn = a.bt.hdr[4];
   const int g = blockIdx.x;
-  if (g >= Gn) return;
+  if (g >= Gn) {
+    if (a.sync && a.train)  // SyncBN: an empty group contributes a zero-count partial
+      for (int j = threadIdx.x; j < 1 + 2 * D; j += CONV_BLOCK) a.bn_part[(size_t)g * (1 + 2 * D) + j] = 0.0f;
+    return;
+  }
   const int r0 = a.bt.grp_row[g], r1 = a.bt.grp_row[g + 1];
   const int e_lo = a.bt.grp_edge[g], e_hi = a.bt.grp_edge[g + 1];
   const int nrow = r1 - r0;
@@ -236,7 +242,8 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
 
   // ---- stage: previous BN stats, CSR slice, node items, LapPE projection weight
   if (!a.first) {
-    prev_bn_stats<D, CONV_BLOCK>(a.train, a.cred, Gn, a.p_part, a.p_stats, a.p_rmean, a.p_rvar, a.p_nbt, a.bn_eps,
+    prev_bn_stats<D, CONV_BLOCK>(a.train, a.cred, a.sync ? a.p_nparts : Gn, a.sync ? a.p_part_all : a.p_part,
+                                 a.p_stats, a.p_rmean, a.p_rvar, a.p_nbt, a.bn_eps,
                                  a.bn_mom, s_bn, s_bn + D, XO, LOG);
   }
   if (fast) {
@@ -546,6 +553,8 @@ struct ReadoutK {
   float* gsum;
   gtr_sweep sw;         // untouched-row AdamW slice run by blocks >= main_grid
   int sw_slot, main_grid;
+  int sync, nparts;     // SyncBN: the last layer's partials of every rank (part_all, nparts)
+  const float* part_all;
 };
 
 // Block per session (grid-strided): RO_WAVES waves split the session's node rows and
@@ -591,7 +600,8 @@ __global__ __launch_bounds__(RO_BLOCK) void k_readout(ReadoutK a) {
   const int nchunk = do_loss ? (n + CHN - 1) / CHN : 0;
 
   if (do_fwd) {
-    prev_bn_stats<D, RO_BLOCK>(a.train, a.cred, a.bt.hdr[4], a.part, a.stats, a.rmean, a.rvar, a.nbt, a.bn_eps,
+    prev_bn_stats<D, RO_BLOCK>(a.train, a.cred, a.sync ? a.nparts : a.bt.hdr[4], a.sync ? a.part_all : a.part,
+                               a.stats, a.rmean, a.rvar, a.nbt, a.bn_eps,
                                a.bn_mom, s_bn, s_bn + D, s_bn + 2 * D, s_scr);
   } else if (do_bwd) {
     for (int j = tid; j < D; j += RO_BLOCK) { s_bn[j] = a.stats[j]; s_bn[D + j] = a.stats[D + j]; }
@@ -1007,7 +1017,8 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
   const float inv_t = 1.0f / a.temperature;
 
   if (do_fwd) {
-    prev_bn_stats<D, RW_BLOCK>(a.train, a.cred, a.bt.hdr[4], a.part, a.stats, a.rmean, a.rvar, a.nbt, a.bn_eps,
+    prev_bn_stats<D, RW_BLOCK>(a.train, a.cred, a.sync ? a.nparts : a.bt.hdr[4], a.sync ? a.part_all : a.part,
+                               a.stats, a.rmean, a.rvar, a.nbt, a.bn_eps,
                                a.bn_mom, s_bn, s_bn + D, s_bn + 2 * D, s_scr);
   } else if (do_bwd) {
     for (int j = tid; j < D; j += RW_BLOCK) { s_bn[j] = a.stats[j]; s_bn[D + j] = a.stats[D + j]; }
@@ -1273,10 +1284,18 @@ extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   drop_params(cfg, k.thresh, k.scale, k.drop_on);
   k.seed = cfg->seed;
   k.rng_ctr = cfg->rng_ctr;
+  k.sync = cfg->sync_bn;
+  if (cfg->sync_bn && !cfg->consumer_reduce) { set_error("gtr_conv_fwd: sync_bn needs consumer_reduce"); return GTR_E_ARG; }
   if (l == 0) {
     k.table = emb->table; k.pe_tab = emb->pe_tab; k.wpe = emb->wpe; k.bpe = emb->bpe;
   } else {
     const gtr_layer& P = layers[l - 1];
+    k.p_part_all = P.bn_part_all;
+    k.p_nparts = P.nparts_fwd;
+    if (cfg->sync_bn && cfg->training && (!P.bn_part_all || P.nparts_fwd <= 0)) {
+      set_error("gtr_conv_fwd: sync_bn needs the gathered partials of layer %d", l - 1);
+      return GTR_E_ARG;
+    }
     k.p_out = P.out; k.p_xin = P.xin; k.p_stats = P.bn_stats; k.p_part = P.bn_part; k.p_gamma = P.bn_gamma;
     k.p_beta = P.bn_beta; k.p_rmean = P.bn_rmean; k.p_rvar = P.bn_rvar; k.p_nbt = P.bn_nbt;
   }
@@ -1344,6 +1363,13 @@ extern "C" int gtr_readout_loss(const gtr_config* cfg, const gtr_batch* bt, cons
   k.coef_neg = head->coef_neg;
   k.loss_part = head->loss_part; k.loss_out = head->loss_out; k.cnt = head->cnt;
   k.dy = L.dy; k.gpart = L.bn_gpart; k.gsum = L.bn_gsum;
+  k.sync = cfg->sync_bn;
+  k.part_all = L.bn_part_all;
+  k.nparts = L.nparts_fwd;
+  if (cfg->sync_bn && ((head->flags & GTR_RO_FWD) && cfg->training) && (!L.bn_part_all || L.nparts_fwd <= 0 || !cfg->consumer_reduce)) {
+    set_error("gtr_readout_loss: sync_bn needs consumer_reduce and the gathered partials of the last layer");
+    return GTR_E_ARG;
+  }
   int grid = gtr_readout_grid(bt->b_cap);
   k.main_grid = grid;
   if (cfg->sweep && cfg->num_layers < GTR_SWEEP_SLOTS &&

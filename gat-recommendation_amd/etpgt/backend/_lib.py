@@ -36,7 +36,7 @@ class GtrConfig(C.Structure):
     _fields_ = [
         ("num_items", i32), ("dim", i32), ("heads", i32), ("pe_k", i32), ("num_layers", i32),
         ("row_group", i32), ("training", i32), ("dropout", f32), ("bn_eps", f32),
-        ("bn_momentum", f32), ("seed", u32), ("rng_ctr", P), ("consumer_reduce", i32), ("pad0", i32),
+        ("bn_momentum", f32), ("seed", u32), ("rng_ctr", P), ("consumer_reduce", i32), ("sync_bn", i32),
         ("sweep", P),
     ]
 
@@ -48,6 +48,7 @@ class GtrLayer(C.Structure):
         ("xin", P), ("qkvs", P), ("alpha", P), ("agg", P), ("gate", P), ("out", P),
         ("bn_stats", P), ("bn_part", P), ("bn_gsum", P), ("bn_gpart", P), ("cnt", P),
         ("dy", P), ("dqkvs", P), ("du", P), ("dlogit", P), ("dagg", P),
+        ("bn_part_all", P), ("bn_gpart_all", P), ("nparts_fwd", i32), ("nparts_bwd", i32),
     ]
 
 

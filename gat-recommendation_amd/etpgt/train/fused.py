@@ -34,7 +34,7 @@ class FusedTrainStep:
                  weight_decay: float = 1e-5, decoupled: bool = True, loss: str = "bpr",
                  temperature: float = 1.0, alpha: float = 0.7, caps: Caps | None = None,
                  use_graph: bool = True, data_parallel: bool | None = None, process_group=None,
-                 lazy: bool = False):
+                 lazy: bool = False, sync_bn: bool = False):
         if loss not in ("bpr", "listwise", "dual", "sampled_softmax"):
             raise ValueError(f"Unknown loss type: {loss}")
         self.model = model
@@ -52,6 +52,11 @@ class FusedTrainStep:
         self.group = process_group
         self.rank, self.world = world_info(process_group)
         self.data_parallel = (self.world > 1) if data_parallel is None else bool(data_parallel)
+        # SyncBN: BatchNorm statistics over every rank's batch (all-gathered partials per
+        # BatchNorm), so N ranks train exactly like one GPU on the concatenated batch
+        self.sync_bn = bool(sync_bn)
+        if self.sync_bn and not self.data_parallel:
+            raise ValueError("sync_bn needs the data-parallel step")
         self.dp = None
         self.graph_b = None
         eng = self.eng
@@ -198,6 +203,8 @@ class FusedTrainStep:
             from etpgt.train.distributed import DpExchange
 
             self.dp = DpExchange(self, self.group)
+        if self.sync_bn:
+            self._sync_alloc()
         self.graph = None
         self.graph_pe = None
         self.graph_b = None
@@ -254,13 +261,40 @@ class FusedTrainStep:
         self.graph = self.graph_pe = self.graph_b = None
 
     # ------------------------------------------------------------------ launches
-    def _launch_a(self, with_pe: bool):
-        """[device batch build] -> step_begin -> forward + loss -> backward (+ the DP pack)."""
+    def _sync_alloc(self):
+        """Gather buffers of the SyncBN partials: per layer, every rank's forward
+        (count, mean, M2) rows and backward (sum dy, sum dy*xhat) rows."""
+        eng, ws, W = self.eng, self.ws, self.world
+        D, Lc = eng.D, eng.L
+        g = ws.g_cap
+        rg = readout_grid(self.caps.b_cap)
+        self.sync_bufs = []
+        for l in range(Lc):
+            rows_b = rg if l == Lc - 1 else g
+            pa = torch.zeros(W, g * (1 + 2 * D), dtype=torch.float32, device=self.dev)
+            ga = torch.zeros(W, rows_b * 2 * D, dtype=torch.float32, device=self.dev)
+            st = ws.structs[l]
+            st.bn_part_all, st.bn_gpart_all = pa.data_ptr(), ga.data_ptr()
+            st.nparts_fwd, st.nparts_bwd = W * g, W * rows_b
+            self.sync_bufs.append((pa, ga, g * (1 + 2 * D), rows_b * 2 * D))
+        self.cfg.consumer_reduce = 1
+        self.cfg.sync_bn = 1
+
+    def _gather_fwd(self, l):
+        from etpgt.train.distributed import all_gather_packs
+
+        pa, _, n, _ = self.sync_bufs[l]
+        all_gather_packs(pa, self.ws.layers[l]["bn_part"].view(-1)[:n], self.group)
+
+    def _gather_bwd(self, l):
+        from etpgt.train.distributed import all_gather_packs
+
+        _, ga, _, n = self.sync_bufs[l]
+        all_gather_packs(ga, self.ws.layers[l]["bn_gpart"].view(-1)[:n], self.group)
+
+    def _begin(self, bs, st):
         eng = self.eng
         lib = L.lib()
-        ws, cfg = self.ws, self.cfg
-        bs = self.bs_pe if with_pe else self.bs
-        st = torch.cuda.current_stream(self.dev).cuda_stream
         if self.builder is not None:
             self.builder.launch(bs, self.caps, st)
         if self.lazy:
@@ -274,6 +308,14 @@ class FusedTrainStep:
                                        self.skeys.data_ptr(), self.svals.data_ptr(), self.stamp.data_ptr(),
                                        self.step_dev.data_ptr(), eng.rng_ctr.data_ptr(), self.sort_tmp.data_ptr(),
                                        self.sort_tmp.numel(), st), "step_begin")
+
+    def _launch_a(self, with_pe: bool):
+        """[device batch build] -> step_begin -> forward + loss -> backward (+ the DP pack)."""
+        eng = self.eng
+        ws, cfg = self.ws, self.cfg
+        bs = self.bs_pe if with_pe else self.bs
+        st = torch.cuda.current_stream(self.dev).cuda_stream
+        self._begin(bs, st)
         eng.run_forward(ws, cfg, bs, L.RO_FWD | L.RO_LOSS | L.RO_BWD, self.loss_kind, self.temperature, self.alpha)
         eng.run_backward(ws, cfg, bs)
         if self.dp is not None:
@@ -290,11 +332,58 @@ class FusedTrainStep:
             L.check(L.lib().gtr_step_tail(C.byref(bs), eng.T, eng.D, C.byref(self.tail), self.segs, self.nseg,
                                           C.byref(self.adam), st), "step_tail")
 
+    def _pieces(self, with_pe: bool):
+        """The step as (launches, collective-after) pieces: one piece single-GPU; the
+        halves around the gradient all-gather in DP mode; with SyncBN also a cut after
+        every producer of BatchNorm partials (all-gather of the partials)."""
+        if self.dp is None:
+            def whole():
+                self._launch_a(with_pe)
+                self._launch_b(with_pe)
+            return [(whole, None)]
+        if not self.sync_bn:
+            return [(lambda: self._launch_a(with_pe), self.dp.exchange), (lambda: self._launch_b(with_pe), None)]
+        eng, ws, cfg = self.eng, self.ws, self.cfg
+        bs = self.bs_pe if with_pe else self.bs
+        lib = L.lib()
+        Lc = eng.L
+
+        def st():
+            return torch.cuda.current_stream(self.dev).cuda_stream
+
+        def fwd(l):
+            def f():
+                if l == 0:
+                    self._begin(bs, st())
+                L.check(lib.gtr_conv_fwd(C.byref(cfg), C.byref(bs), C.byref(eng.fill_embed()), ws.structs, l, st()),
+                        "conv_fwd")
+            return f
+
+        def head():
+            eng.run_head(ws, cfg, bs, L.RO_FWD | L.RO_LOSS | L.RO_BWD, self.loss_kind, self.temperature, self.alpha)
+
+        def bwd(l):
+            def f():
+                L.check(lib.gtr_conv_bwd(C.byref(cfg), C.byref(bs), ws.structs, l, ws.dx0.data_ptr(), st()),
+                        "conv_bwd")
+                if l == 0:
+                    eng._wgrad(ws, cfg, bs, 0, Lc, st())
+                    self.dp.launch_pack(bs, st())
+            return f
+
+        pieces = [(fwd(l), (lambda l=l: self._gather_fwd(l))) for l in range(Lc)]
+        pieces.append((head, lambda: self._gather_bwd(Lc - 1)))
+        for l in range(Lc - 1, 0, -1):
+            pieces.append((bwd(l), (lambda l=l: self._gather_bwd(l - 1))))
+        pieces.append((bwd(0), self.dp.exchange))
+        pieces.append((lambda: self._launch_b(with_pe), None))
+        return pieces
+
     def _launch(self, with_pe: bool):
-        self._launch_a(with_pe)
-        if self.dp is not None:
-            self.dp.exchange()
-        self._launch_b(with_pe)
+        for launch, coll in self._pieces(with_pe):
+            launch()
+            if coll is not None:
+                coll()
 
     def _capture(self, fn):
         g = torch.cuda.CUDAGraph()
@@ -306,19 +395,14 @@ class FusedTrainStep:
         return g
 
     def capture(self, with_pe: bool = False):
-        """Capture one step into hipGraphs (after one eager warm-up step): the whole
-        step single-GPU; the halves before / after the all-gather in DP mode."""
-        if self.dp is None:
-            g = self._capture(lambda: self._launch(with_pe))
-            gb = None
-        else:
-            g = self._capture(lambda: self._launch_a(with_pe))
-            gb = self._capture(lambda: self._launch_b(with_pe))
+        """Capture the step's pieces into hipGraphs (after one eager warm-up step): the
+        whole step single-GPU; the pieces between collectives in DP mode."""
+        graphs = [(self._capture(launch), coll) for launch, coll in self._pieces(with_pe)]
         if with_pe:
-            self.graph_pe, self.graph_b_pe = g, gb
+            self.graph_pe = graphs
         else:
-            self.graph, self.graph_b = g, gb
-        return g
+            self.graph = graphs
+        return graphs
 
     def run(self, with_pe: bool = False):
         """One training step over the batch currently in the device blob."""
@@ -331,16 +415,16 @@ class FusedTrainStep:
             self._host_steps += 1
             self._dirty = True
         if self.use_graph:
-            g = self.graph_pe if with_pe else self.graph
-            if g is None:
+            graphs = self.graph_pe if with_pe else self.graph
+            if graphs is None:
                 self._launch(with_pe)  # eager warm-up (first touch of every code path)
                 torch.cuda.synchronize(self.dev)
                 self.capture(with_pe)
                 return self.ws.loss_out[0]
-            g.replay()
-            if self.dp is not None:
-                self.dp.exchange()
-                (self.graph_b_pe if with_pe else self.graph_b).replay()
+            for g, coll in graphs:
+                g.replay()
+                if coll is not None:
+                    coll()
         else:
             self._launch(with_pe)
         return self.ws.loss_out[0]

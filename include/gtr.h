@@ -106,7 +106,10 @@ typedef struct gtr_config {
                               reduced from the producer's per-group partials by the CONSUMING
                               kernel (no inter-workgroup fences; for <= 64 row groups);
                               0: the producer's last-arriving workgroup finalises them */
-  int32_t pad0;
+  int32_t sync_bn;         /* 1: BatchNorm statistics over every rank's batch (SyncBN): the
+                              consumers reduce gtr_layer.bn_part_all / bn_gpart_all (the
+                              all-gathered partials of all ranks; requires consumer_reduce)
+                              and producers zero the partial rows of their empty groups */
   const gtr_sweep* sweep;  /* optional (fused single-GPU step): untouched-row AdamW
                               slices run by extra workgroups of the layer kernels */
 } gtr_config;
@@ -141,6 +144,10 @@ typedef struct gtr_layer {
   float* du;       /* [n_cap]     grad wrt gate logit                 */
   float* dlogit;   /* [e_cap, H]                                     */
   float* dagg;     /* [n_cap, D]                                     */
+  const float* bn_part_all;  /* sync_bn: every rank's forward partials [nparts_fwd][1+2D]  */
+  const float* bn_gpart_all; /* sync_bn: every rank's backward partials [nparts_bwd][2D]   */
+  int32_t nparts_fwd;
+  int32_t nparts_bwd;
 } gtr_layer;
 
 /* Embedding + LapPE inputs of layer 0. */

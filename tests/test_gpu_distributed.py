@@ -5,6 +5,8 @@ against the oracle's rank-averaged AdamW trajectory (replicas must stay identica
 from __future__ import annotations
 
 import copy
+
+import numpy as np
 import os
 import socket
 
@@ -118,3 +120,77 @@ def test_dp_two_ranks_match_oracle_average():
             assert float((res[0][1][n] - p.detach()).abs().max()) <= 2 * 1e-2 * STEPS + 1e-6
             continue
         assert_close_norm(res[0][1][n], p, rtol=1e-3, name=n)
+
+
+def _concat(b0, b1):
+    """The global batch: b0's sessions then b1's (PyG Batch.from_data_list order)."""
+    from etpgt.data.batch import SessionBatch
+
+    n0 = b0.num_nodes
+    return SessionBatch(torch.cat([b0.x, b1.x]), torch.cat([b0.edge_index, b1.edge_index + n0], dim=1),
+                        torch.cat([b0.batch, b1.batch + b0.num_graphs]),
+                        torch.cat([b0.target_item, b1.target_item]),
+                        torch.cat([b0.negative_items.reshape(-1), b1.negative_items.reshape(-1)]),
+                        num_graphs=b0.num_graphs + b1.num_graphs)
+
+
+def _sync_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        data = small_data()
+        T = data.table_rows
+        m, _ = make_pair(T, D, H, K=0, seed=25)
+        m.train()
+        f = FusedTrainStep(m, lr=1e-2, weight_decay=1e-2, loss="listwise", sync_bn=True)
+        assert f.data_parallel and f.world == world and f.sync_bn
+        bl = batches(data, B, NNEG, STEPS * world, seed=26)
+        losses = [float(f(bl[s * world + rank].to("cuda"))) for s in range(STEPS)]
+        bufs = {n: b.detach().cpu().numpy().copy() for n, b in m.named_buffers() if "running" in n}
+        q.put((rank, losses, {n: p.detach().cpu().numpy().copy() for n, p in m.named_parameters()}, bufs))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sync_bn_two_ranks_equal_one_gpu_on_the_global_batch():
+    """SyncBN data parallel (2 ranks sharing the GPU, gloo transport for the partials and
+    the gradient packs) trains exactly like the single-GPU fused step on the
+    concatenated global batch: same losses, parameters and BatchNorm running stats up to
+    reduction order."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sync_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            rank, losses, params, bufs = q.get(timeout=400)
+            res[rank] = (losses, params, bufs)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    for k, v in res[0][1].items():
+        assert np.array_equal(v, res[1][1][k]), f"replicas diverged: {k}"
+    data = small_data()
+    T = data.table_rows
+    m, _ = make_pair(T, D, H, K=0, seed=25)
+    m.train()
+    f = FusedTrainStep(m, lr=1e-2, weight_decay=1e-2, loss="listwise")
+    bl = batches(data, B, NNEG, STEPS * world, seed=26)
+    for s in range(STEPS):
+        g = float(f(_concat(bl[s * world], bl[s * world + 1]).to("cuda")))
+        avg = (res[0][0][s] + res[1][0][s]) / 2
+        assert abs(g - avg) <= 1e-5 * max(1.0, abs(g)), (s, g, res[0][0][s], res[1][0][s])
+    for n, p in m.named_parameters():
+        if n.endswith("lin_key.bias"):
+            continue
+        assert_close_norm(torch.from_numpy(res[0][1][n]), p, rtol=1e-4, name=n)
+    for n, b in m.named_buffers():
+        if "running" in n:
+            assert_close_norm(torch.from_numpy(res[0][2][n]), b, rtol=1e-4, name=n)
