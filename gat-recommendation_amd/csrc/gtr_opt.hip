@@ -802,6 +802,17 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_dp_stamp(gtr_dp_layout lay, int T
   slot[(size_t)k * lay.world + r] = make_int2(t, i);
 }
 
+// Early union stamp (data parallel): every rank's sorted contribution keys, all-gathered
+// right after step_begin, mark the union of the step's touched rows before the backward
+// so the untouched-row sweep can ride in the backward kernels (gtr_sweep).
+__global__ __launch_bounds__(GTR_BLOCK) void k_dp_union_stamp(const int32_t* keys_all, int64_t n, int T,
+                                                              int32_t* stamp, const int64_t* step_dev) {
+  const int64_t i = (int64_t)blockIdx.x * GTR_BLOCK + threadIdx.x;
+  if (i >= n) return;
+  const int k = keys_all[i];
+  if (k > 0 && k < T) stamp[k] = (int32_t)*step_dev;
+}
+
 struct DpTailK {
   gtr_tail tl;
   gtr_dp_layout lay;
@@ -809,7 +820,7 @@ struct DpTailK {
   const float* recv;
   const int2* slot;
   int T, nb_rows, nb_small, nb_sweep;
-  int64_t nvec;
+  int64_t nvec, vbegin;
   int vpr_log2, pad0;
 };
 
@@ -892,7 +903,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_dp_tail(DpTailK a) {
   }
   sweep_body(blk - a.nb_rows - a.nb_small, a.nb_sweep, a.nvec, a.vpr_log2, a.tl.stamp, t,
              reinterpret_cast<float4*>(a.tl.table), reinterpret_cast<float4*>(a.tl.table_m),
-             reinterpret_cast<float4*>(a.tl.table_v), st);
+             reinterpret_cast<float4*>(a.tl.table_v), st, a.vbegin);
 }
 
 int key_bits(int T) {
@@ -1077,6 +1088,19 @@ int gtr_step_begin(const gtr_batch* bt, int num_items, int32_t* keys, int32_t* v
   return GTR_OK;
 }
 
+int gtr_dp_union_stamp(const int32_t* keys_all, int64_t n, int num_items, int32_t* stamp, const int64_t* step_dev,
+                       gtr_stream_t stream) {
+  if (!keys_all || n < 0 || num_items <= 0 || !stamp || !step_dev) {
+    set_error("gtr_dp_union_stamp: bad arguments");
+    return GTR_E_ARG;
+  }
+  if (n == 0) return GTR_OK;
+  hipLaunchKernelGGL(k_dp_union_stamp, dim3((unsigned)((n + GTR_BLOCK - 1) / GTR_BLOCK)), dim3(GTR_BLOCK), 0,
+                     (hipStream_t)stream, keys_all, n, num_items, stamp, step_dev);
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
 int gtr_step_begin_lazy(const gtr_batch* bt, int num_items, int dim, int32_t* keys, int32_t* vals, int32_t* skeys,
                         int32_t* svals, int32_t* stamp, int64_t* step_dev, uint32_t* rng_ctr, void* tmp,
                         size_t tmp_bytes, const gtr_lazy* lazy, gtr_stream_t stream) {
@@ -1246,8 +1270,11 @@ int gtr_dp_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tai
   k.nvec = (int64_t)num_items * dim / 4;
   k.vpr_log2 = 0;
   while ((1 << k.vpr_log2) < dim / 4) ++k.vpr_log2;
-  int64_t sw = (k.nvec + GTR_BLOCK - 1) / GTR_BLOCK;
-  k.nb_sweep = tail->lazy_consts ? 0 : (int)(sw > 2048 ? 2048 : sw);  // lazy: no untouched-row sweep
+  // rows below sweep_from were swept inside the backward (early union stamp + gtr_sweep)
+  const int64_t from = tail->sweep_from < 0 ? 0 : (tail->sweep_from > num_items ? num_items : tail->sweep_from);
+  k.vbegin = from * (dim / 4);
+  int64_t sw = (k.nvec - k.vbegin + GTR_BLOCK - 1) / GTR_BLOCK;
+  k.nb_sweep = (tail->lazy_consts || sw <= 0) ? 0 : (int)(sw > 2048 ? 2048 : sw);  // lazy: no sweep
   const int grid = k.nb_rows + k.nb_small + k.nb_sweep;
   switch (dim) {
     case 32: hipLaunchKernelGGL(k_dp_tail<32>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;

@@ -142,6 +142,7 @@ _SIGS = {
     "gtr_readout_grid": (C.c_int, [C.c_int]),
     "gtr_dp_pack": (C.c_int, [P, C.c_int, C.c_int, P, P, C.c_int, P, P, P]),
     "gtr_dp_tail": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P]),
+    "gtr_dp_union_stamp": (C.c_int, [P, i64, C.c_int, P, P, P]),
     "gtr_step_begin": (C.c_int, [P, C.c_int, P, P, P, P, P, P, P, P, C.c_size_t, P]),
     "gtr_step_tail": (C.c_int, [P, C.c_int, C.c_int, P, P, C.c_int, P, P]),
     "gtr_step_begin_lazy": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P, P, P, C.c_size_t, P, P]),

@@ -95,6 +95,26 @@ def all_gather_packs(recv: torch.Tensor, pack: torch.Tensor, group=None) -> None
         dist.all_gather_into_tensor(recv.view(-1), pack.reshape(-1), group=group)
 
 
+class _Done:
+    def wait(self):
+        return None
+
+
+def start_all_gather(out: torch.Tensor, inp: torch.Tensor, group=None):
+    """Asynchronous all-gather (out[world, n] <- every rank's inp[n]) on the collective
+    stream; ``.wait()`` makes the current stream wait for it (RCCL).  gloo (CPU
+    transport) completes it before returning."""
+    if not (dist.is_available() and dist.is_initialized()):
+        out[0].copy_(inp)
+        return _Done()
+    if dist.get_backend(group) == "gloo":
+        host = torch.empty(out.numel(), dtype=inp.dtype)
+        dist.all_gather_into_tensor(host, inp.detach().cpu().reshape(-1), group=group)
+        out.copy_(host.view_as(out))
+        return _Done()
+    return dist.all_gather_into_tensor(out.view(-1), inp.reshape(-1), group=group, async_op=True)
+
+
 # ---------------------------------------------------------------------------------
 # CPU restatement of the protocol (tests; mirrors gtr_dp_pack / gtr_dp_tail)
 # ---------------------------------------------------------------------------------

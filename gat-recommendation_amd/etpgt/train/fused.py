@@ -176,13 +176,23 @@ class FusedTrainStep:
         wts = [1.0] * eng.L + [0.75] + [1.0] * eng.L
         if os.environ.get("GTR_SWEEP_WTS"):  # experiments: comma-separated slot weights
             wts = [float(x) for x in os.environ["GTR_SWEEP_WTS"].split(",")]
+        # data parallel: the union of the ranks' touched rows is known once the sorted keys
+        # are all-gathered (early, overlapped with the forward), so only the launches after
+        # the union stamp (readout, conv_bwd) can sweep
+        self.early_union = (self.data_parallel and chain and not self.sync_bn
+                            and os.environ.get("GTR_DP_EARLY", "0") == "1")
+        if self.early_union:
+            wts = [0.0] * eng.L + wts[eng.L:]
         slots = len(wts)
-        if chain and not self.data_parallel and self.ws.g_cap <= 128 and slots <= L.SWEEP_SLOTS:
+        if chain and (not self.data_parallel or self.early_union) and self.ws.g_cap <= 128 \
+                and slots <= L.SWEEP_SLOTS:
             sw = L.GtrSweep()
             sw.table = eng.model.item_embedding.weight.data_ptr()
             sw.m, sw.v, sw.stamp = self.m_tab.data_ptr(), self.v_tab.data_ptr(), self.stamp.data_ptr()
             sw.opt = self.adam  # copied by value (step_dev: device counter)
             tot, acc = sum(wts), 0.0
+            if self.early_union:
+                self.keys_all = torch.zeros(self.world, m_cap, dtype=torch.int32, device=self.dev)
             for i in range(L.SWEEP_SLOTS + 1):
                 sw.bounds[i] = eng.T if i >= slots else int(eng.T * acc / tot)
                 if i < slots:
@@ -341,8 +351,10 @@ class FusedTrainStep:
                 self._launch_a(with_pe)
                 self._launch_b(with_pe)
             return [(whole, None)]
-        if not self.sync_bn:
+        if not self.sync_bn and not (self.early_union and self.sweep is not None):
             return [(lambda: self._launch_a(with_pe), self.dp.exchange), (lambda: self._launch_b(with_pe), None)]
+        if not self.sync_bn:
+            return self._early_pieces(with_pe)
         eng, ws, cfg = self.eng, self.ws, self.cfg
         bs = self.bs_pe if with_pe else self.bs
         lib = L.lib()
@@ -378,6 +390,45 @@ class FusedTrainStep:
         pieces.append((bwd(0), self.dp.exchange))
         pieces.append((lambda: self._launch_b(with_pe), None))
         return pieces
+
+    def _early_pieces(self, with_pe: bool):
+        """DP with the early union: begin | all-gather the sorted keys (async, overlapped
+        with the forward) | forward | wait + union stamp + readout + backward (carrying the
+        sweep slices) + pack | all-gather the packs | dp tail (touched rows only)."""
+        from etpgt.train.distributed import start_all_gather
+
+        eng, ws, cfg = self.eng, self.ws, self.cfg
+        bs = self.bs_pe if with_pe else self.bs
+        lib = L.lib()
+
+        def st():
+            return torch.cuda.current_stream(self.dev).cuda_stream
+
+        pending = {}
+
+        def begin():
+            self._begin(bs, st())
+
+        def keys_start():
+            pending["w"] = start_all_gather(self.keys_all, self.skeys, self.group)
+
+        def fwd():
+            emb = eng.fill_embed()
+            for l in range(eng.L):
+                L.check(lib.gtr_conv_fwd(C.byref(cfg), C.byref(bs), C.byref(emb), ws.structs, l, st()), "conv_fwd")
+
+        def keys_wait():
+            pending.pop("w").wait()
+
+        def rest():
+            L.check(lib.gtr_dp_union_stamp(self.keys_all.data_ptr(), self.keys_all.numel(), eng.T,
+                                           self.stamp.data_ptr(), self.step_dev.data_ptr(), st()), "dp_union_stamp")
+            eng.run_head(ws, cfg, bs, L.RO_FWD | L.RO_LOSS | L.RO_BWD, self.loss_kind, self.temperature, self.alpha)
+            eng.run_backward(ws, cfg, bs)
+            self.dp.launch_pack(bs, st())
+
+        return [(begin, keys_start), (fwd, keys_wait), (rest, self.dp.exchange),
+                (lambda: self._launch_b(with_pe), None)]
 
     def _launch(self, with_pe: bool):
         for launch, coll in self._pieces(with_pe):

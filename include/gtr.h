@@ -380,6 +380,13 @@ typedef struct gtr_dp_layout {
 int gtr_dp_pack(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tail, const gtr_segment* segs,
                 int nseg, const gtr_dp_layout* lay, float* pack, gtr_stream_t stream);
 
+/* Early union stamp: keys_all = every rank's sorted contribution keys (all-gathered
+ * right after gtr_step_begin, n = world * m_cap): stamp[key] = *step_dev, so that the
+ * untouched-row sweep can run inside the backward kernels (gtr_sweep slots of the
+ * readout / conv_bwd) and gtr_dp_tail sweeps only rows >= tail->sweep_from.          */
+int gtr_dp_union_stamp(const int32_t* keys_all, int64_t n, int num_items, int32_t* stamp, const int64_t* step_dev,
+                       gtr_stream_t stream);
+
 /* slot: [T][world] int2 {step, segment-start index} scratch (init to -1).          */
 int gtr_dp_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tail, const gtr_dp_layout* lay,
                 const float* recv, int32_t* slot, const gtr_adam* opt, gtr_stream_t stream);
