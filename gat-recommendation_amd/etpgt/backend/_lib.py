@@ -152,6 +152,9 @@ _SIGS = {
     "gtr_edge_hash_build": (C.c_int, [P, i64, P, i64, P]),
     "gtr_session_counts": (C.c_int, [P, P, i64, C.c_int, P, P, P]),
     "gtr_build_batch": (C.c_int, [P, P, i64, C.c_int, P, P, C.c_int, C.c_int, u32, P, P, P, P, P]),
+    "gtr_lap_build": (C.c_int, [P, P, C.c_int, P, P, P]),
+    "gtr_lap_plan": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P]),
+    "gtr_lap_spmm": (C.c_int, [P, P, C.c_int, C.c_int, P, i64, P, i64, P, P, P, f32, f32, P]),
     "gtr_topk_workspace_bytes": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_size_t)]),
     "gtr_score_topk": (C.c_int, [P, C.c_int, C.c_int, P, C.c_int, C.c_int, P, P, P, C.c_size_t, P]),
     "gtr_score_topk_masked": (C.c_int, [P, C.c_int, C.c_int, P, C.c_int, C.c_int, P, P, P, P, P, C.c_size_t, P]),

@@ -442,6 +442,26 @@ int gtr_build_batch(const gtr_sessions* ss, const uint64_t* slots, int64_t num_s
                     const gtr_batch* out, int32_t* scratch, int64_t* start, int32_t* status,
                     gtr_stream_t stream);
 
+/* ---- Laplacian positional-encoding precompute (etpgt.encodings.laplacian_gpu) ------
+ * Replaces the host eigsh of compute_laplacian_pe (etpgt/encodings/laplacian_pe.py:19-66:
+ * PyG get_laplacian(normalization="sym") + eigsh(k+1, which="SM"), reference
+ * scripts/train/train_etpgt.py's LapPE precompute) for a symmetric adjacency in CSR
+ * (ptr [n+1], col [nnz]):
+ *   gtr_lap_build writes the off-diagonal values of L = I - D^-1/2 A D^-1/2 (dis [n] =
+ *     deg^-1/2, val [nnz]; self loops 0; the unit diagonal is implicit).
+ *   gtr_lap_plan (HOST pointers) cuts the rows into an nnz-balanced work list: items
+ *     [n_items][4] = (row, e0, e1, part or -1), splits [n_splits][4] = (row, p0, p1, 0)
+ *     for rows longer than `chunk`; call with items = splits = NULL to get the counts.
+ *   gtr_lap_spmm computes Y = alpha * L X + beta * X for b <= 256 vectors (X, Y [n, b]
+ *     row-major, X != Y) from the plan (device copies) and a part [n_parts, b] scratch —
+ *     the block eigen-solver's operator; deterministic.                              */
+int gtr_lap_build(const int32_t* ptr, const int32_t* col, int n, float* dis, float* val, gtr_stream_t stream);
+int gtr_lap_plan(const int32_t* ptr, int n, int chunk, int32_t* items, int64_t* n_items, int32_t* splits,
+                 int64_t* n_splits, int64_t* n_parts);
+int gtr_lap_spmm(const int32_t* col, const float* val, int n, int b, const int32_t* items, int64_t n_items,
+                 const int32_t* splits, int64_t n_splits, float* part, const float* X, float* Y, float alpha,
+                 float beta, gtr_stream_t stream);
+
 /* Workgroups of gtr_readout_loss = the number of its loss / BatchNorm-sum partials
  * (gtr_tail.loss_nparts; the last layer's bn_gpart rows).                         */
 int gtr_readout_grid(int b_cap);

@@ -82,3 +82,37 @@ def test_status_codes_raise(libpath):
     assert rc != 0
     with pytest.raises(RuntimeError, match="bad arguments"):
         _lib.check(rc, "conv_fwd")
+
+
+def test_lap_plan_is_nnz_balanced(libpath):
+    """gtr_lap_plan (host-only): every nonzero lands in exactly one item of <= chunk
+    nonzeros, in row order; split rows list their consecutive partial slots."""
+    import numpy as np
+
+    from etpgt.backend import _lib
+
+    rng = np.random.default_rng(0)
+    deg = rng.integers(0, 40, 500)
+    deg[[3, 77, 499]] = [1000, 129, 128]  # hub rows, one just over / at the chunk
+    ptr = np.zeros(501, np.int32)
+    np.cumsum(deg, out=ptr[1:])
+    lib = _lib.lib()
+    ni, ns, npart = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    assert lib.gtr_lap_plan(ptr.ctypes.data, 500, 128, None, ctypes.byref(ni), None, ctypes.byref(ns),
+                            ctypes.byref(npart)) == 0
+    items = np.empty((ni.value, 4), np.int32)
+    splits = np.empty((ns.value, 4), np.int32)
+    assert lib.gtr_lap_plan(ptr.ctypes.data, 500, 128, items.ctypes.data, ctypes.byref(ni), splits.ctypes.data,
+                            ctypes.byref(ns), ctypes.byref(npart)) == 0
+    assert ns.value == 2 and npart.value == 8 + 2 and ni.value == 498 + 10
+    assert (items[:, 2] - items[:, 1] <= 128).all() and (items[:, 2] >= items[:, 1]).all()
+    assert np.array_equal(items[:, 1][1:], items[:, 2][:-1])  # contiguous cover of [0, nnz)
+    assert items[0, 1] == 0 and items[-1, 2] == ptr[-1]
+    assert np.array_equal(np.unique(items[:, 0]), np.arange(500))
+    assert splits[:, 0].tolist() == [3, 77] and splits[:, 1:3].tolist() == [[0, 8], [8, 10]]
+    split_items = items[items[:, 3] >= 0]
+    assert split_items[:, 3].tolist() == list(range(10))
+    assert (items[~np.isin(items[:, 0], [3, 77]), 3] == -1).all()
+    bad = np.array([0, 5, 3], np.int32)
+    assert lib.gtr_lap_plan(bad.ctypes.data, 2, 128, None, ctypes.byref(ni), None, ctypes.byref(ns),
+                            ctypes.byref(npart)) != 0
