@@ -55,7 +55,19 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def _claim_stdout():
+    """The bench line must be the only thing on stdout, but libraries write there at the
+    file-descriptor level (RCCL prints its version banner on every rank's communicator
+    init): fd 1 is pointed at stderr for the whole run and the JSON line goes to a saved
+    duplicate of the original stdout."""
+    sys.stdout.flush()
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    return fd
+
+
 def main():
+    json_fd = _claim_stdout()
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -71,6 +83,9 @@ def main():
     ap.add_argument("--sync-bn", action="store_true", help="BatchNorm statistics over every rank's batch")
     ap.add_argument("--lazy", type=int, default=None,
                     help="deferred zero-gradient AdamW of untouched table rows (1/0; default: per config)")
+    ap.add_argument("--lagged", type=int, default=None,
+                    help="lazy-table stamps with the previous step's untouched rows swept inside the chain "
+                         "(1/0; default: on for the data-parallel step)")
     ap.add_argument("--recall-steps", type=int, default=100,
                     help="Recall@10 parity leg: training steps of the HIP and oracle trainers (0 = skip)")
     ap.add_argument("--recall-sessions", type=int, default=2048, help="held-out sessions of the Recall@10 leg")
@@ -87,9 +102,15 @@ def main():
     share = os.environ.get("GTR_SHARE_DEVICE") == "1"
     backend = "gloo" if share else "nccl"
     dev_index = 0 if share else local
-    if world > 1:
+    # GTR_FORCE_PG=1: a process group even at world 1 (rehearses the RCCL exchange path
+    # on a one-GPU box: `--dp` then all-gathers over RCCL with one rank)
+    if world > 1 or os.environ.get("GTR_FORCE_PG") == "1":
         import torch.distributed as dist
 
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         torch.cuda.set_device(dev_index)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
@@ -110,9 +131,11 @@ def main():
 
     t0 = time.time()
     lazy = bool(args.lazy) if args.lazy is not None else bool(cfg.get("lazy", False))
+    dp_on = bool(args.dp or args.sync_bn or world > 1)
+    lagged = (bool(args.lagged) if args.lagged is not None else dp_on) and not lazy
     w = build_workload(args.config, args.batch_size, args.num_batches, dev, rank, use_graph=not args.no_graph,
                        data_parallel=True if (args.dp or args.sync_bn) else None, lazy=lazy,
-                       sync_bn=args.sync_bn and world > 1)
+                       sync_bn=args.sync_bn and world > 1, lagged=lagged)
     step, staged, batches, data, T, B, touched, st = (w[k] for k in ("step", "staged", "batches", "data", "T", "B",
                                                                    "touched", "stats"))
     log(f"data: T={T} sessions={data.num_sessions} edges={data.edge_keys.size} setup {time.time()-t0:.1f}s {st}")
@@ -204,6 +227,8 @@ def main():
                 "dp_exchange": step.dp is not None,
                 "hip_graph": not args.no_graph,
                 "lazy_table": lazy,
+                "lagged_sweep": lagged,
+                "graph_collectives": bool(step.dp is not None and step._graph_collectives()),
                 "sync_bn": bool(args.sync_bn and world > 1),
                 "gpu_ms_per_step_events": round(gpu_ms / args.steps, 4),
                 "final_loss": round(final_loss, 6),
@@ -233,13 +258,15 @@ def main():
             "gather_roofline": gather,
             "recall_parity": recall,
         }
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if world > 1:
         torch.distributed.destroy_process_group()
 
 
 def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, use_graph: bool = True,
-                   data_parallel: bool | None = None, lazy: bool = False, sync_bn: bool = False) -> dict:
+                   data_parallel: bool | None = None, lazy: bool = False, sync_bn: bool = False,
+                   lagged: bool = False) -> dict:
     """Synthetic RetailRocket-shaped data, the model of `config`, a bound fused step
     and `num_batches` packed batches pre-staged in HBM."""
     from etpgt.data.batch import Caps
@@ -265,7 +292,7 @@ def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, us
         model.laplacian_pe._cached_pe = random_pe_table(T, cfg["K"])
     model = model.to(dev).train()
     step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, loss=cfg["loss"], use_graph=use_graph,
-                          data_parallel=data_parallel, lazy=lazy, sync_bn=sync_bn)
+                          data_parallel=data_parallel, lazy=lazy, sync_bn=sync_bn, lagged=lagged)
     caps = Caps(max(b.num_nodes for b in batches), B, max(b.num_edges for b in batches), cfg["n_neg"])
     step._bind(caps)  # data parallel: the ranks agree on the largest capacities
     caps = step.caps

@@ -157,20 +157,26 @@ struct AdamStep {
 // blk of nblk streams float4s of rows [bounds[slot], bounds[slot+1]) whose stamp is not
 // the current step, SW_U float4 per thread in flight per tensor (one workgroup per CU
 // next to the layer kernels' LDS-heavy groups, so each thread keeps several in flight).
+// lag = 1: lazy-table stamps; rows behind the previous step are brought to it (one
+// zero-gradient update when one step behind, the consts chain otherwise) and stamped.
+// A row's float4s are consecutive lanes of one wave (D/4 <= 64 divides the wave), and
+// every lane reads the stamp before any lane of the row writes it.
 #define SW_U 4
 __device__ __forceinline__ void sweep_slice(const gtr_sweep& sw, int slot, int blk, int nblk) {
   __shared__ AdamStep s_sw_st;
   __shared__ int32_t s_sw_t;
   const int64_t r0 = sw.bounds[slot], r1 = sw.bounds[slot + 1];
   if (r1 <= r0) return;
+  const bool lag = sw.lag != 0;
   if (threadIdx.x == 0) {
-    const int64_t t = *sw.opt.step_dev + sw.opt.step_offset;
-    s_sw_st.init(sw.opt, t);
+    const int64_t t = *sw.opt.step_dev + sw.opt.step_offset - (lag ? 1 : 0);
+    if (t >= 1) s_sw_st.init(sw.opt, t);
     s_sw_t = (int32_t)t;
   }
   __syncthreads();
   const AdamStep st = s_sw_st;
-  const int32_t tcur = s_sw_t;
+  const int32_t tcur = s_sw_t;  // eager: the current step; lag: the step rows are brought to
+  if (lag && tcur < 1) return;
   int lg = 0;
   while ((1 << lg) < sw.dim / 4) ++lg;
   const int64_t v0 = r0 << lg, v1 = r1 << lg;
@@ -180,11 +186,13 @@ __device__ __forceinline__ void sweep_slice(const gtr_sweep& sw, int slot, int b
   float4* V = reinterpret_cast<float4*>(sw.v);
   for (int64_t i = v0 + (int64_t)blk * blockDim.x + threadIdx.x; i < v1; i += SW_U * stride) {
     bool on[SW_U];
+    int32_t old[SW_U];
     float4 p[SW_U], m[SW_U], q[SW_U];
 #pragma unroll
     for (int u = 0; u < SW_U; ++u) {
       const int64_t j = i + u * stride;
-      on[u] = j < v1 && sw.stamp[j >> lg] != tcur;
+      old[u] = j < v1 ? sw.stamp[j >> lg] : tcur;
+      on[u] = j < v1 && (lag ? old[u] < tcur : old[u] != tcur);
     }
 #pragma unroll
     for (int u = 0; u < SW_U; ++u) {
@@ -195,9 +203,21 @@ __device__ __forceinline__ void sweep_slice(const gtr_sweep& sw, int slot, int b
     for (int u = 0; u < SW_U; ++u) {
       const int64_t j = i + u * stride;
       if (on[u]) {
-        st.apply(p[u].x, m[u].x, q[u].x, 0.0f); st.apply(p[u].y, m[u].y, q[u].y, 0.0f);
-        st.apply(p[u].z, m[u].z, q[u].z, 0.0f); st.apply(p[u].w, m[u].w, q[u].w, 0.0f);
+        if (!lag || old[u] == tcur - 1) {
+          st.apply(p[u].x, m[u].x, q[u].x, 0.0f); st.apply(p[u].y, m[u].y, q[u].y, 0.0f);
+          st.apply(p[u].z, m[u].z, q[u].z, 0.0f); st.apply(p[u].w, m[u].w, q[u].w, 0.0f);
+        } else {  // more than one step behind: each missed step with its own scalars
+          AdamStep sc = st;
+          for (int tt = old[u] + 1; tt <= tcur; ++tt) {
+            const float2 c = reinterpret_cast<const float2*>(sw.consts)[tt];
+            sc.step_size = c.x;
+            sc.bc2_sqrt = c.y;
+            sc.apply(p[u].x, m[u].x, q[u].x, 0.0f); sc.apply(p[u].y, m[u].y, q[u].y, 0.0f);
+            sc.apply(p[u].z, m[u].z, q[u].z, 0.0f); sc.apply(p[u].w, m[u].w, q[u].w, 0.0f);
+          }
+        }
         P[j] = p[u]; M[j] = m[u]; V[j] = q[u];
+        if (lag && (j & ((1 << lg) - 1)) == 0) sw.stamp[j >> lg] = tcur;
       }
     }
   }

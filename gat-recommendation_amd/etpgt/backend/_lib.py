@@ -106,7 +106,7 @@ class GtrSessions(C.Structure):
 class GtrSweep(C.Structure):
     _fields_ = [
         ("table", P), ("m", P), ("v", P), ("stamp", P), ("opt", GtrAdam), ("bounds", i64 * (SWEEP_SLOTS + 1)),
-        ("dim", i32), ("blocks", i32),
+        ("dim", i32), ("blocks", i32), ("consts", P), ("lag", i32), ("pad", i32),
     ]
 
 

@@ -34,7 +34,7 @@ class FusedTrainStep:
                  weight_decay: float = 1e-5, decoupled: bool = True, loss: str = "bpr",
                  temperature: float = 1.0, alpha: float = 0.7, caps: Caps | None = None,
                  use_graph: bool = True, data_parallel: bool | None = None, process_group=None,
-                 lazy: bool = False, sync_bn: bool = False):
+                 lazy: bool = False, sync_bn: bool = False, lagged: bool = False):
         if loss not in ("bpr", "listwise", "dual", "sampled_softmax"):
             raise ValueError(f"Unknown loss type: {loss}")
         self.model = model
@@ -74,7 +74,12 @@ class FusedTrainStep:
         self.stamp = torch.zeros(T, dtype=torch.int32, device=self.dev)
         # deferred zero-gradient AdamW of untouched table rows (gtr_lazy in gtr.h):
         # bitwise-identical to the dense update, applied when a row is next read or on flush()
-        self.lazy = bool(lazy)
+        # lagged: lazy-table stamps, and the chain's launches sweep the PREVIOUS step's
+        # untouched rows (gtr_sweep.lag), so the sweep needs no knowledge of this step's
+        # touched rows -- in data parallel those are the ranks' union, known only after
+        # the exchange; rows the step reads are one step behind at most
+        self.lagged = bool(lagged) and not bool(lazy)
+        self.lazy = bool(lazy) or self.lagged
         self._host_steps = 0
         self._dirty = False
         self.lz = None
@@ -105,6 +110,8 @@ class FusedTrainStep:
         self.lz = lz
         if getattr(self, "tail", None) is not None:
             self.tail.lazy_consts = consts.data_ptr()
+        if getattr(self, "sweep", None) is not None and self.sweep.lag:
+            self.sweep.consts = consts.data_ptr()
         self.graph = self.graph_pe = self.graph_b = None  # captured pointers changed
 
     def flush(self):
@@ -170,7 +177,7 @@ class FusedTrainStep:
         # grids): the chain's 2L launches each sweep a slice of the table (gtr_sweep)
         self.sweep = None
         t.sweep_from = 0
-        chain = os.environ.get("GTR_CHAIN_SWEEP", "1") != "0" and not self.lazy
+        chain = os.environ.get("GTR_CHAIN_SWEEP", "1") != "0" and (not self.lazy or self.lagged)
         # slots: conv_fwd(l) -> l, readout -> L, conv_bwd(l) -> 2L - l; weighted by the
         # launches' measured slack (the readout is shorter than a layer kernel)
         wts = [1.0] * eng.L + [0.75] + [1.0] * eng.L
@@ -179,12 +186,12 @@ class FusedTrainStep:
         # data parallel: the union of the ranks' touched rows is known once the sorted keys
         # are all-gathered (early, overlapped with the forward), so only the launches after
         # the union stamp (readout, conv_bwd) can sweep
-        self.early_union = (self.data_parallel and chain and not self.sync_bn
+        self.early_union = (self.data_parallel and chain and not self.sync_bn and not self.lagged
                             and os.environ.get("GTR_DP_EARLY", "0") == "1")
         if self.early_union:
             wts = [0.0] * eng.L + wts[eng.L:]
         slots = len(wts)
-        if chain and (not self.data_parallel or self.early_union) and self.ws.g_cap <= 128 \
+        if chain and (not self.data_parallel or self.early_union or self.lagged) and self.ws.g_cap <= 128 \
                 and slots <= L.SWEEP_SLOTS:
             sw = L.GtrSweep()
             sw.table = eng.model.item_embedding.weight.data_ptr()
@@ -201,6 +208,8 @@ class FusedTrainStep:
             # 64 extra workgroups per launch measured best (C2 271.7k, C3 168.7k sessions/s;
             # more of them raise the latency-bound groups' load latency)
             sw.blocks = int(os.environ.get("GTR_SWEEP_BLOCKS", 64))
+            sw.lag = 1 if self.lagged else 0
+            sw.consts = self.lazy_consts.data_ptr() if self.lagged else None
             self.sweep = sw
             self.cfg.sweep = C.addressof(sw)
             t.sweep_from = eng.T
@@ -430,6 +439,30 @@ class FusedTrainStep:
         return [(begin, keys_start), (fwd, keys_wait), (rest, self.dp.exchange),
                 (lambda: self._launch_b(with_pe), None)]
 
+    def _graph_collectives(self) -> bool:
+        """RCCL collectives captured inside the step's hipGraph (one graph per step instead
+        of one per piece).  Only for the nccl (RCCL) backend -- gloo round-trips through
+        host memory -- and off with GTR_GRAPH_COLL=0."""
+        if self.dp is None or self.world <= 1 and os.environ.get("GTR_GRAPH_COLL") != "1":
+            return False
+        if os.environ.get("GTR_GRAPH_COLL", "1") == "0":
+            return False
+        import torch.distributed as dist
+
+        return dist.is_available() and dist.is_initialized() and dist.get_backend(self.group) == "nccl"
+
+    def _graph_pieces(self, with_pe: bool):
+        pieces = self._pieces(with_pe)
+        if len(pieces) == 1 or not self._graph_collectives():
+            return pieces
+
+        def whole():
+            for launch, coll in pieces:
+                launch()
+                if coll is not None:
+                    coll()
+        return [(whole, None)]
+
     def _launch(self, with_pe: bool):
         for launch, coll in self._pieces(with_pe):
             launch()
@@ -448,7 +481,7 @@ class FusedTrainStep:
     def capture(self, with_pe: bool = False):
         """Capture the step's pieces into hipGraphs (after one eager warm-up step): the
         whole step single-GPU; the pieces between collectives in DP mode."""
-        graphs = [(self._capture(launch), coll) for launch, coll in self._pieces(with_pe)]
+        graphs = [(self._capture(launch), coll) for launch, coll in self._graph_pieces(with_pe)]
         if with_pe:
             self.graph_pe = graphs
         else:

@@ -244,11 +244,19 @@ typedef struct gtr_sweep {
   float* table;
   float* m;
   float* v;
-  const int32_t* stamp;
+  int32_t* stamp;
   gtr_adam opt;       /* by value: the kernels copy it (opt.step_dev is a device pointer) */
   int64_t bounds[GTR_SWEEP_SLOTS + 1];
   int32_t dim;
   int32_t blocks;
+  /* lag = 1 (lazy-table stamps, "current through step s"): the launches of step t bring
+   * every row with stamp < t-1 forward to t-1 (the previous step's zero-gradient update,
+   * older steps from consts as gtr_lazy) and stamp it; the rows the step reads were
+   * brought forward by gtr_step_begin_lazy.  Used when the previous step's touched rows
+   * are only known after the kernels that sweep (data parallel: the ranks' union).      */
+  const float* consts;
+  int32_t lag;
+  int32_t pad;
 } gtr_sweep;
 
 #define GTR_SMALL_MAX_SEG 48

@@ -194,3 +194,99 @@ def test_sync_bn_two_ranks_equal_one_gpu_on_the_global_batch():
     for n, b in m.named_buffers():
         if "running" in n:
             assert_close_norm(torch.from_numpy(res[0][2][n]), b, rtol=1e-4, name=n)
+
+
+def _lagged_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        data = small_data()
+        T = data.table_rows
+        m1, _ = make_pair(T, D, H, K=0, seed=27)
+        m2 = copy.deepcopy(m1)
+        m1.train(); m2.train()
+        f1 = FusedTrainStep(m1, lr=1e-2, weight_decay=1e-2, loss="bpr")
+        f2 = FusedTrainStep(m2, lr=1e-2, weight_decay=1e-2, loss="bpr", lagged=True)
+        bl = batches(data, B, NNEG, 6 * world, seed=28)
+        for s in range(6):
+            l1 = float(f1(bl[s * world + rank].to("cuda")))
+            l2 = float(f2(bl[s * world + rank].to("cuda")))
+            assert l1 == l2, (s, l1, l2)
+        assert f2.sweep is not None and f2.sweep.lag == 1
+        f2.flush()
+        same = all(torch.equal(a, b) for a, b in zip(m1.parameters(), m2.parameters()))
+        same = same and torch.equal(f1.m_tab, f2.m_tab) and torch.equal(f1.v_tab, f2.v_tab)
+        q.put((rank, same, {n: p.detach().cpu().numpy().copy() for n, p in m2.named_parameters()}))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_lagged_sweep_two_ranks_bitwise_equals_eager_dp():
+    """Data parallel with the lagged sweep (each rank's chain sweeps the previous step's
+    untouched rows; the union's rows are updated by gtr_dp_tail): on 2 ranks sharing the
+    GPU it equals the eager data-parallel step bit for bit, and the replicas agree."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_lagged_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            rank, same, params = q.get(timeout=400)
+            res[rank] = (same, params)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert res[0][0] and res[1][0]
+    for k, v in res[0][1].items():
+        assert np.array_equal(v, res[1][1][k]), f"replicas diverged: {k}"
+
+
+def _rccl_worker(port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GTR_GRAPH_COLL="1")
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        data = small_data()
+        T = data.table_rows
+        m1, _ = make_pair(T, D, H, K=0, seed=29)
+        m2 = copy.deepcopy(m1)
+        m1.train(); m2.train()
+        f1 = FusedTrainStep(m1, lr=1e-2, weight_decay=1e-2, loss="bpr")
+        f2 = FusedTrainStep(m2, lr=1e-2, weight_decay=1e-2, loss="bpr", data_parallel=True, lagged=True)
+        out = []
+        for sb in batches(data, B, NNEG, 5, seed=30):
+            out.append((float(f1(sb.to("cuda"))), float(f2(sb.to("cuda")))))
+        f2.flush()
+        ok_graph = f2._graph_collectives() and len(f2.graph) == 1
+        diff = max(float((a - b).abs().max()) for a, b in zip(m1.parameters(), m2.parameters()))
+        q.put((out, ok_graph, diff))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_rccl_world1_graph_captured_collectives():
+    """The RCCL transport (nccl backend, one rank): the data-parallel step with its
+    all-gather captured inside the step's hipGraph and the lagged sweep equals the
+    single-GPU fused step."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
+    p.start()
+    try:
+        out, ok_graph, diff = q.get(timeout=300)
+    finally:
+        p.join(timeout=60)
+    assert p.exitcode == 0
+    assert ok_graph
+    for l1, l2 in out:
+        assert abs(l1 - l2) <= 1e-6 * max(1.0, abs(l1))
+    assert diff <= 1e-6

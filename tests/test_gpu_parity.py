@@ -269,7 +269,7 @@ def test_fused_steps_wave_readout_large_batch(monkeypatch):
     _fused_vs_reference(64, 2, 0, "listwise", "adamw", True, B=2100, steps=2)
 
 
-def _lazy_vs_eager(D, H, K, loss, opt, B, steps, dropout=0.1, use_graph=True, dp=None, cap=None):
+def _lazy_vs_eager(D, H, K, loss, opt, B, steps, dropout=0.1, use_graph=True, dp=None, cap=None, lagged=False):
     T = data().table_rows
     n = 5 if loss != "listwise" else 100
     m1, _ = make_pair(T, D, H, K=K, dropout=dropout, seed=7)
@@ -278,7 +278,7 @@ def _lazy_vs_eager(D, H, K, loss, opt, B, steps, dropout=0.1, use_graph=True, dp
     kw = dict(lr=1e-3, weight_decay=1e-2, decoupled=opt == "adamw", loss=loss, use_graph=use_graph,
               data_parallel=dp)
     f1 = FusedTrainStep(m1, **kw)
-    f2 = FusedTrainStep(m2, lazy=True, **kw)
+    f2 = FusedTrainStep(m2, lazy=not lagged, lagged=lagged, **kw)
     if cap is not None:
         f2._lazy_alloc(cap)
     for sb in batches(data(), B, n, steps, seed=13):
@@ -311,6 +311,26 @@ def test_lazy_table_large_batch_and_capacity_growth():
 def test_lazy_table_data_parallel_world1():
     """Data-parallel tail in lazy mode (catch-up of union rows in gtr_dp_tail)."""
     _lazy_vs_eager(64, 2, 0, "bpr", "adamw", B=32, steps=4, dp=True)
+
+
+@pytest.mark.parametrize("dp", [False, True])
+def test_lagged_sweep_bitwise_equals_dense_adamw(dp):
+    """Lagged sweep (gtr_sweep.lag): the chain's launches bring the previous step's
+    untouched rows forward; single GPU and the data-parallel step (world 1), 12 steps so
+    rows go untouched, get read again and get touched again."""
+    f2 = _lazy_vs_eager(64, 1, 0, "bpr", "adamw", B=32, steps=12, dp=dp, lagged=True)
+    assert f2.sweep is not None and f2.sweep.lag == 1
+    # after the flush every row is current through the last step
+    assert int(f2.stamp.min()) == f2.steps
+
+
+def test_lagged_sweep_consts_growth_and_listwise():
+    """Lagged mode with the consts table growing under it (capacity 4), D = 128 / 4 heads /
+    LapPE / listwise, and a large batch where the chain carries no sweep (g_cap > 128:
+    rows then fall further behind and are caught up on read)."""
+    _lazy_vs_eager(64, 1, 0, "bpr", "adamw", B=32, steps=10, cap=4, lagged=True)
+    _lazy_vs_eager(128, 4, 16, "listwise", "adam", B=32, steps=4, lagged=True)
+    _lazy_vs_eager(64, 2, 0, "bpr", "adamw", B=1400, steps=3, lagged=True)
 
 
 def test_lazy_table_flushes_before_eval_forward():
