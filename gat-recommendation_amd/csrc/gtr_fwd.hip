@@ -327,20 +327,45 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
       *reinterpret_cast<float4*>(XO + i * XS + j) = val;
     }
     __syncthreads();
+    // W fragments of tiles past the prefetched ones are double-buffered: tile ti+1's
+    // loads are issued before tile ti's MFMAs and stores (the compiler cannot hoist them
+    // over the qkvs stores itself), so only the first such tile waits on L2
+    constexpr int NT = NCT / CONV_WAVES;
+    constexpr bool DB = NT > PRE && D <= 128;  // D = 256: no registers to spare
+    float4 wnext[DB ? D / 16 : 1];
+    float bnext = 0.0f;
+    if constexpr (DB) {
+      const float* wrow = a.w_all + (size_t)((wave + PRE * CONV_WAVES) * 16 + lr) * D + lg * 4;
 #pragma unroll
-    for (int ti = 0; ti < NCT / CONV_WAVES; ++ti) {
+      for (int kb = 0; kb < D / 16; ++kb) wnext[kb] = *reinterpret_cast<const float4*>(wrow + kb * 16);
+      bnext = a.b_all[(wave + PRE * CONV_WAVES) * 16 + lr];
+    }
+#pragma unroll
+    for (int ti = 0; ti < NT; ++ti) {
       const int ct = wave + ti * CONV_WAVES;
       float4 wf[D / 16];
+      float bias;
       if (ti < PRE) {
 #pragma unroll
         for (int kb = 0; kb < D / 16; ++kb) wf[kb] = wpre[ti < PRE ? ti : 0][kb];
+        bias = a.b_all[ct * 16 + lr];
+      } else if constexpr (DB) {
+#pragma unroll
+        for (int kb = 0; kb < D / 16; ++kb) wf[kb] = wnext[kb];
+        bias = bnext;
+        if (ti + 1 < NT) {
+          const float* wrow = a.w_all + (size_t)((ct + CONV_WAVES) * 16 + lr) * D + lg * 4;
+#pragma unroll
+          for (int kb = 0; kb < D / 16; ++kb) wnext[kb] = *reinterpret_cast<const float4*>(wrow + kb * 16);
+          bnext = a.b_all[(ct + CONV_WAVES) * 16 + lr];
+        }
       } else {
         const float* wrow = a.w_all + (size_t)(ct * 16 + lr) * D + lg * 4;
 #pragma unroll
         for (int kb = 0; kb < D / 16; ++kb) wf[kb] = *reinterpret_cast<const float4*>(wrow + kb * 16);
+        bias = a.b_all[ct * 16 + lr];
       }
       const int col = ct * 16 + lr;
-      const float bias = a.b_all[col];
       const int which = col / D, cc = col - which * D;
       // LDS copies on the fast path: 0 = query -> QS[0], 1 = key -> KV[0], 2 = value -> KV[1], 3 = skip -> QS[1]
       float* ldst = nullptr;

@@ -189,14 +189,14 @@ __device__ __forceinline__ void sweep_body(int blk, int nblk, int64_t nvec, int 
   for (int64_t i = vbegin + (int64_t)blk * GTR_BLOCK + threadIdx.x; i < nvec; i += stride) {
     const int64_t row = i >> vpr_log2;
     if (stamp[row] == t) continue;
-    float4 p = table[i], mm = m[i], vv = v[i];
+    float4 p = sw_ld(table + i), mm = sw_ld(m + i), vv = sw_ld(v + i);  // streaming: spare L2
     st.apply(p.x, mm.x, vv.x, 0.0f);
     st.apply(p.y, mm.y, vv.y, 0.0f);
     st.apply(p.z, mm.z, vv.z, 0.0f);
     st.apply(p.w, mm.w, vv.w, 0.0f);
-    table[i] = p;
-    m[i] = mm;
-    v[i] = vv;
+    sw_st(table + i, p);
+    sw_st(m + i, mm);
+    sw_st(v + i, vv);
   }
 }
 
