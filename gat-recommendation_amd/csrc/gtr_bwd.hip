@@ -170,13 +170,16 @@ __device__ __forceinline__ void bwd_src_row(const ConvBwdK& a, int s, int sl, co
   store_vec<VPL>(a.dqkvs + (size_t)s * (4 * D) + 2 * D + d0, dv, act);
 }
 
-template <int D>
+template <int D, bool SPLIT>
 __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
   using G = LayerGeom<D>;
   constexpr int VPL = G::VPL, RMAX = G::RMAX, XS = G::XS, TPR = G::TPR, CH = G::CH;
   constexpr int NCT = D / 16;                                   // dX column tiles
   constexpr int CPW = NCT > CONV_WAVES ? NCT / CONV_WAVES : 1;  // column tiles per wave
   constexpr int WPC = NCT >= CONV_WAVES ? 1 : CONV_WAVES / NCT; // waves sharing a column tile
+  constexpr int ASB = 4 * D + 8;                                // LDS split dQKVS row stride (bf16)
+  constexpr int RTW = (RMAX / 16 + WPC - 1) / WPC;              // row tiles per wave
+  static_assert(!G::KV || RMAX * ASB <= G::B_RN, "split dQKVS rows must fit the K|V|Q|dA region");
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* Ks = sm + G::B_R;
   float* Vs = Ks + RMAX * XS;
@@ -270,7 +273,7 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
     // ---- (D1) BatchNorm backward, beta gate: TPR lanes per destination row, CH features each
     const bool live = prow < nrow;
     const int t = r0 + prow;
-    float gv[CH], sv[CH], agv[CH];
+    float gv[CH], sv[CH], agv[CH], dsv[CH];
     float dbeta = 0.0f, beta = 0.0f;
     if (live) {
       const size_t ro = (size_t)t * D + f0;
@@ -311,6 +314,7 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
           const float w1 = a.w_beta[j], w2 = a.w_beta[D + j], w3 = a.w_beta[2 * D + j];
           dag[q] = gv[c + q] * (1.0f - beta) + du * (w1 + w3);
           ds[q] = gv[c + q] * beta + du * (w2 - w3);
+          dsv[c + q] = ds[q];
         }
         *reinterpret_cast<float4*>(a.dqkvs + (size_t)t * (4 * D) + 3 * D + f0 + c) =
             make_float4(ds[0], ds[1], ds[2], ds[3]);
@@ -366,10 +370,10 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
     GTR_PH(a.layer, 2);
 
     // ---- (D4) dQ over in-edges, (D5) dK, dV over out-edges: TPR lanes per row
+    float dq[CH], dk[CH], dv[CH];
     if (live) {
       const int hd = f0 / C;
       const float isc = 1.0f / a.sqrt_c;
-      float dq[CH], dk[CH], dv[CH];
 #pragma unroll
       for (int c = 0; c < CH; ++c) { dq[c] = 0.0f; dk[c] = 0.0f; dv[c] = 0.0f; }
       const int e1 = iptr[prow + 1];
@@ -403,6 +407,26 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
         *reinterpret_cast<float4*>(drow + c) = make_float4(dq[c], dq[c + 1], dq[c + 2], dq[c + 3]);
         *reinterpret_cast<float4*>(drow + D + c) = make_float4(dk[c], dk[c + 1], dk[c + 2], dk[c + 3]);
         *reinterpret_cast<float4*>(drow + 2 * D + c) = make_float4(dv[c], dv[c + 1], dv[c + 2], dv[c + 3]);
+      }
+    }
+    if constexpr (SPLIT) {
+      // the group's dQKVS rows, split into bf16 hi | lo, over the K | V | Q | dA rows (dead
+      // from here on): the A operand of phase X, read from LDS by every wave
+      __syncthreads();
+      if (live) {
+        __bf16* ah = reinterpret_cast<__bf16*>(sm + G::B_R) + prow * ASB + f0;
+        __bf16* al = ah + RMAX * ASB;
+        const float* parts[4] = {dq, dk, dv, dsv};
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+#pragma unroll
+          for (int c = 0; c < CH; c += 4) {
+            bf16x4 h, l;
+            split4(make_float4(parts[p][c], parts[p][c + 1], parts[p][c + 2], parts[p][c + 3]), h, l);
+            *reinterpret_cast<bf16x4*>(ah + p * D + c) = h;
+            *reinterpret_cast<bf16x4*>(al + p * D + c) = l;
+          }
+        }
       }
     }
   } else {
@@ -449,7 +473,59 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
     const int ct = (WPC > 1 ? wave % NCT : wave) + c * CONV_WAVES;
     if (a.has_prev) { pm[c] = a.p_stats[ct * 16 + lr]; pr[c] = a.p_stats[D + ct * 16 + lr]; }
   }
-  for (int rt = r0 + rs * 16; rt < r1; rt += 16 * WPC) {
+  if constexpr (SPLIT) {
+    if (fast) {
+      // split-bf16 MFMA: A (dQKVS rows) hi | lo from LDS; each B fragment (8 K-values of
+      // one W_all column) is loaded and split once per wave and used for every row tile
+      const __bf16* AH = reinterpret_cast<const __bf16*>(sm + G::B_R);
+      const __bf16* AL = AH + RMAX * ASB;
+#pragma unroll
+      for (int c = 0; c < CPW; ++c) {
+        const int ct = (WPC > 1 ? wave % NCT : wave) + c * CONV_WAVES;
+        f32x4 acc[RTW];
+#pragma unroll
+        for (int r = 0; r < RTW; ++r) acc[r] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        const float* bcol = a.w_all + (size_t)(lg * 8) * D + ct * 16 + lr;
+#pragma unroll 2
+        for (int ks = 0; ks < D / 8; ++ks) {
+          const float* bp = bcol + (size_t)(ks * 32) * D;
+          bf16x8 bh, bl;
+          split8(make_float4(bp[0], bp[D], bp[2 * D], bp[3 * D]), make_float4(bp[4 * D], bp[5 * D], bp[6 * D], bp[7 * D]),
+                 bh, bl);
+#pragma unroll
+          for (int r = 0; r < RTW; ++r) {
+            const int tile = rs + r * WPC;
+            if (tile * 16 < nrow) {  // wave-uniform
+              const int off = (tile * 16 + lr) * ASB + ks * 32 + lg * 8;
+              acc[r] = mfma_split(*reinterpret_cast<const bf16x8*>(AH + off), *reinterpret_cast<const bf16x8*>(AL + off),
+                                  bh, bl, acc[r]);
+            }
+          }
+        }
+        const int col = ct * 16 + lr;
+#pragma unroll
+        for (int r = 0; r < RTW; ++r) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = r0 + (rs + r * WPC) * 16 + lg * 4 + i;
+            if (row < r1) {
+              const size_t o = (size_t)row * D + col;
+              const float dx = a.dy[o] + acc[r][i];
+              if (a.has_prev) {
+                const float d = dx * dr.mul(st_prev, (uint32_t)o);
+                a.p_dy[o] = d;
+                s1[c] += d;
+                s2[c] += d * ((a.p_out[o] - pm[c]) * pr[c]);
+              } else {
+                a.dx0[o] = dx;
+              }
+            }
+          }
+        }
+      }
+    }
+  }
+  for (int rt = r0 + rs * 16; !(SPLIT && fast) && rt < r1; rt += 16 * WPC) {
     const int ar = min(rt + lr, r1 - 1);  // clamp: rows past the group are computed, never stored
     const float* arow = a.dqkvs + (size_t)ar * (4 * D) + lg * 4;
 #pragma unroll
@@ -708,14 +784,15 @@ extern "C" int gtr_conv_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     }
   }
   hipStream_t s = (hipStream_t)stream;
-#define GTR_BWD(DD) set_lds_limit<DD>(k_conv_bwd<DD>, (size_t)LayerGeom<DD>::B_WORDS * 4); \
-  hipLaunchKernelGGL(k_conv_bwd<DD>, dim3(grid), dim3(CONV_BLOCK), \
+#define GTR_BWD(DD, SP) set_lds_limit<DD>(k_conv_bwd<DD, SP>, (size_t)LayerGeom<DD>::B_WORDS * 4); \
+  hipLaunchKernelGGL((k_conv_bwd<DD, SP>), dim3(grid), dim3(CONV_BLOCK), \
                                        (size_t)LayerGeom<DD>::B_WORDS * 4, s, k)
+  const bool sp = gemm_split() != 0;
   switch (D) {
-    case 32: GTR_BWD(32); break;
-    case 64: GTR_BWD(64); break;
-    case 128: GTR_BWD(128); break;
-    default: GTR_BWD(256); break;
+    case 32: if (sp) { GTR_BWD(32, true); } else { GTR_BWD(32, false); } break;
+    case 64: if (sp) { GTR_BWD(64, true); } else { GTR_BWD(64, false); } break;
+    case 128: if (sp) { GTR_BWD(128, true); } else { GTR_BWD(128, false); } break;
+    default: GTR_BWD(256, false); break;  // no LDS-staged rows at D = 256: f32 MFMA from L2
   }
 #undef GTR_BWD
   GTR_HIP_CHECK_LAUNCH();

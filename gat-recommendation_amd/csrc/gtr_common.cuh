@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/gtr.h"
 
@@ -232,6 +233,17 @@ __device__ __forceinline__ void sweep_slice(const gtr_sweep& sw, int slot, int b
       }
     }
   }
+}
+
+// GEMM arithmetic of the layer kernels (host side, read once): split-bf16 MFMA (default)
+// or exact f32-input MFMA (GTR_GEMM=f32).
+inline int gemm_split() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("GTR_GEMM");
+    v = (e && (e[0] == 'f' || e[0] == 'F')) ? 0 : 1;
+  }
+  return v;
 }
 
 }  // namespace gtr

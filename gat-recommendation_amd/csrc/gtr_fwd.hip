@@ -26,7 +26,7 @@ GTR_PH_DECL
 
 struct ConvFwdK {
   gtr_batch bt;
-  int H, C, first, train, layer, pe_k, cred, pad0;
+  int H, C, first, train, layer, pe_k, cred, split;  // split: split-bf16 projection GEMM
   float sqrt_c, bn_eps, bn_mom, scale;
   uint32_t seed, thresh;
   int drop_on, pad1;
@@ -163,7 +163,13 @@ __device__ __forceinline__ void attn_row(const ConvFwdK& a, int t, int tl, const
   if (lane == 0) a.gate[t] = beta;
 }
 
-template <int D>
+// Offset of float4 number kb of a lane's W-row fragment: f32 MFMA (k = kb*16 + lg*4 ..)
+// or split-bf16 MFMA (k-step kb/2 of 32, lane quad lg's 8 values, half kb&1).
+__device__ __forceinline__ int wfrag_off(int kb, int lg, int split) {
+  return split ? ((kb >> 1) * 32 + lg * 8 + (kb & 1) * 4) : (kb * 16 + lg * 4);
+}
+
+template <int D, bool SPLIT>
 __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
   using G = LayerGeom<D>;
   constexpr int VPL = G::VPL, RMAX = G::RMAX, XS = G::XS, KPE = G::KPE, TPR = G::TPR, CH = G::CH;
@@ -179,6 +185,8 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
   int* isrc = reinterpret_cast<int*>(sm + G::F_ISRC);
   int* edst = reinterpret_cast<int*>(sm + G::F_EDST);
   int* s_flag = reinterpret_cast<int*>(sm + G::F_FLAG);
+  __bf16* XH = reinterpret_cast<__bf16*>(sm + G::F_XH);
+  __bf16* XL = reinterpret_cast<__bf16*>(sm + G::F_XL);
 
   if ((int)blockIdx.x >= a.main_grid) {  // extra workgroups: untouched-row AdamW slice
     sweep_slice(a.sw, a.sw_slot, blockIdx.x - a.main_grid, gridDim.x - a.main_grid);
@@ -215,9 +223,10 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
   float4 wpre[PRE][D / 16];
 #pragma unroll
   for (int pi = 0; pi < PRE; ++pi) {
-    const float* wrow = a.w_all + (size_t)((wave + pi * CONV_WAVES) * 16 + lr) * D + lg * 4;
+    const float* wrow = a.w_all + (size_t)((wave + pi * CONV_WAVES) * 16 + lr) * D;
 #pragma unroll
-    for (int kb = 0; kb < D / 16; ++kb) wpre[pi][kb] = *reinterpret_cast<const float4*>(wrow + kb * 16);
+    for (int kb = 0; kb < D / 16; ++kb)
+      wpre[pi][kb] = *reinterpret_cast<const float4*>(wrow + wfrag_off(kb, lg, SPLIT));
   }
   // gate weights: the row-parallel fast path holds this thread's CH-feature chunk,
   // the wave-per-row general path VPL features per lane
@@ -325,6 +334,12 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
       }
       *reinterpret_cast<float4*>(a.xin + o) = val;
       *reinterpret_cast<float4*>(XO + i * XS + j) = val;
+      if constexpr (SPLIT) {
+        bf16x4 h, l;
+        split4(val, h, l);
+        *reinterpret_cast<bf16x4*>(XH + i * G::XSB + j) = h;
+        *reinterpret_cast<bf16x4*>(XL + i * G::XSB + j) = l;
+      }
     }
     __syncthreads();
     // W fragments of tiles past the prefetched ones are double-buffered: tile ti+1's
@@ -335,9 +350,10 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
     float4 wnext[DB ? D / 16 : 1];
     float bnext = 0.0f;
     if constexpr (DB) {
-      const float* wrow = a.w_all + (size_t)((wave + PRE * CONV_WAVES) * 16 + lr) * D + lg * 4;
+      const float* wrow = a.w_all + (size_t)((wave + PRE * CONV_WAVES) * 16 + lr) * D;
 #pragma unroll
-      for (int kb = 0; kb < D / 16; ++kb) wnext[kb] = *reinterpret_cast<const float4*>(wrow + kb * 16);
+      for (int kb = 0; kb < D / 16; ++kb)
+        wnext[kb] = *reinterpret_cast<const float4*>(wrow + wfrag_off(kb, lg, SPLIT));
       bnext = a.b_all[(wave + PRE * CONV_WAVES) * 16 + lr];
     }
 #pragma unroll
@@ -354,15 +370,17 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
         for (int kb = 0; kb < D / 16; ++kb) wf[kb] = wnext[kb];
         bias = bnext;
         if (ti + 1 < NT) {
-          const float* wrow = a.w_all + (size_t)((ct + CONV_WAVES) * 16 + lr) * D + lg * 4;
+          const float* wrow = a.w_all + (size_t)((ct + CONV_WAVES) * 16 + lr) * D;
 #pragma unroll
-          for (int kb = 0; kb < D / 16; ++kb) wnext[kb] = *reinterpret_cast<const float4*>(wrow + kb * 16);
+          for (int kb = 0; kb < D / 16; ++kb)
+            wnext[kb] = *reinterpret_cast<const float4*>(wrow + wfrag_off(kb, lg, SPLIT));
           bnext = a.b_all[(ct + CONV_WAVES) * 16 + lr];
         }
       } else {
-        const float* wrow = a.w_all + (size_t)(ct * 16 + lr) * D + lg * 4;
+        const float* wrow = a.w_all + (size_t)(ct * 16 + lr) * D;
 #pragma unroll
-        for (int kb = 0; kb < D / 16; ++kb) wf[kb] = *reinterpret_cast<const float4*>(wrow + kb * 16);
+        for (int kb = 0; kb < D / 16; ++kb)
+          wf[kb] = *reinterpret_cast<const float4*>(wrow + wfrag_off(kb, lg, SPLIT));
         bias = a.b_all[ct * 16 + lr];
       }
       const int col = ct * 16 + lr;
@@ -370,12 +388,26 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
       // LDS copies on the fast path: 0 = query -> QS[0], 1 = key -> KV[0], 2 = value -> KV[1], 3 = skip -> QS[1]
       float* ldst = nullptr;
       if (fast) ldst = (which == 0 ? QSs : which == 1 ? KVs : which == 2 ? KVs + RMAX * XS : QSs + RMAX * XS) + cc;
+      bf16x8 bh[D / 32], bl[D / 32];
+      if constexpr (SPLIT) {
+#pragma unroll
+        for (int ks = 0; ks < D / 32; ++ks) split8(wf[2 * ks], wf[2 * ks + 1], bh[ks], bl[ks]);
+      }
       for (int rt = 0; rt * 16 < m; ++rt) {
         f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
-        const float* xrow = XO + (rt * 16 + lr) * XS + lg * 4;
+        if constexpr (SPLIT) {
+          const __bf16* xh = XH + (rt * 16 + lr) * G::XSB + lg * 8;
+          const __bf16* xl = XL + (rt * 16 + lr) * G::XSB + lg * 8;
 #pragma unroll
-        for (int kb = 0; kb < D / 16; ++kb)
-          acc = mfma4(*reinterpret_cast<const float4*>(xrow + kb * 16), wf[kb], acc);
+          for (int ks = 0; ks < D / 32; ++ks)
+            acc = mfma_split(*reinterpret_cast<const bf16x8*>(xh + ks * 32),
+                             *reinterpret_cast<const bf16x8*>(xl + ks * 32), bh[ks], bl[ks], acc);
+        } else {
+          const float* xrow = XO + (rt * 16 + lr) * XS + lg * 4;
+#pragma unroll
+          for (int kb = 0; kb < D / 16; ++kb)
+            acc = mfma4(*reinterpret_cast<const float4*>(xrow + kb * 16), wf[kb], acc);
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int row = rt * 16 + lg * 4 + i;
@@ -1303,6 +1335,7 @@ extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   k.layer = l;
   k.pe_k = cfg->pe_k;
   k.cred = cfg->consumer_reduce;
+  k.split = gemm_split();
   k.sqrt_c = (float)sqrt((double)k.C);
   k.bn_eps = cfg->bn_eps;
   k.bn_mom = cfg->bn_momentum;
@@ -1337,13 +1370,16 @@ extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     grid += cfg->sweep->blocks;
   }
   hipStream_t s = (hipStream_t)stream;
-#define GTR_FWD(DD) set_lds_limit<DD>(k_conv_fwd<DD>, (size_t)LayerGeom<DD>::F_WORDS * 4); \
-  hipLaunchKernelGGL(k_conv_fwd<DD>, dim3(grid), dim3(CONV_BLOCK), (size_t)LayerGeom<DD>::F_WORDS * 4, s, k)
-  switch (cfg->dim) {
-    case 32: GTR_FWD(32); break;
-    case 64: GTR_FWD(64); break;
-    case 128: GTR_FWD(128); break;
-    default: GTR_FWD(256); break;
+#define GTR_FWD(DD, SP) set_lds_limit<DD>(k_conv_fwd<DD, SP>, (size_t)LayerGeom<DD>::F_WORDS * 4); \
+  hipLaunchKernelGGL((k_conv_fwd<DD, SP>), dim3(grid), dim3(CONV_BLOCK), (size_t)LayerGeom<DD>::F_WORDS * 4, s, k)
+  switch (cfg->dim * 2 + k.split) {
+    case 64: GTR_FWD(32, false); break;
+    case 65: GTR_FWD(32, true); break;
+    case 128: GTR_FWD(64, false); break;
+    case 129: GTR_FWD(64, true); break;
+    case 256: GTR_FWD(128, false); break;
+    case 257: GTR_FWD(128, true); break;
+    default: GTR_FWD(256, false); break;  // D = 256: f32 MFMA (no registers for the split fragments)
   }
 #undef GTR_FWD
   GTR_HIP_CHECK_LAUNCH();

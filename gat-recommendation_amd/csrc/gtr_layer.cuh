@@ -37,7 +37,10 @@ struct LayerGeom {
   static constexpr int F_ISRC = F_IPTR + RMAX + 4;            // [EMAX] local in_src
   static constexpr int F_EDST = F_ISRC + EMAX;                // [EMAX] local dst of each in-edge
   static constexpr int F_FLAG = F_EDST + EMAX;
-  static constexpr int F_WORDS = F_FLAG + 4;
+  static constexpr int XSB = D + 8;                           // padded bf16 row (16B aligned)
+  static constexpr int F_XH = F_FLAG + 4;                     // [RMAX][XSB] bf16 hi part of X rows
+  static constexpr int F_XL = F_XH + RMAX * XSB / 2;          // [RMAX][XSB] bf16 lo part (split GEMM)
+  static constexpr int F_WORDS = F_XL + RMAX * XSB / 2;
   // ---- backward LDS carve (4-byte words)
   static constexpr int B_RN = KV ? 4 * RMAX * XS : 0;
   static constexpr int B_R = 0;                               // [4][RMAX][XS] K | V | Q | dA rows
@@ -54,6 +57,32 @@ struct LayerGeom {
   static constexpr int B_FLAG = B_BNP + CONV_WAVES * 2 * D;
   static constexpr int B_WORDS = B_FLAG + 4;
 };
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// Split-bf16 GEMM operands: x = hi + lo with hi = bf16(x), lo = bf16(x - hi), so that
+// hi*hi' + hi*lo' + lo*hi' (three bf16 MFMAs, fp32 accumulation) carries ~16 bits of
+// each product (relative error ~2^-16) at 3/16 of the f32-input MFMA cycles.
+__device__ __forceinline__ void split4(const float4 v, bf16x4& h, bf16x4& l) {
+  h[0] = (__bf16)v.x; h[1] = (__bf16)v.y; h[2] = (__bf16)v.z; h[3] = (__bf16)v.w;
+  l[0] = (__bf16)(v.x - (float)h[0]); l[1] = (__bf16)(v.y - (float)h[1]);
+  l[2] = (__bf16)(v.z - (float)h[2]); l[3] = (__bf16)(v.w - (float)h[3]);
+}
+__device__ __forceinline__ void split8(const float4 a, const float4 b, bf16x8& h, bf16x8& l) {
+  bf16x4 ha, la, hb, lb;
+  split4(a, ha, la);
+  split4(b, hb, lb);
+  h = __builtin_shufflevector(ha, hb, 0, 1, 2, 3, 4, 5, 6, 7);
+  l = __builtin_shufflevector(la, lb, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+// acc += A*B for one 16x16x32 step from split operands (small terms first).
+__device__ __forceinline__ f32x4 mfma_split(const bf16x8 ah, const bf16x8 al, const bf16x8 bh, const bf16x8 bl,
+                                            f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, acc, 0, 0, 0);
+}
 
 // One 16x16 f32 MFMA tile-step over 4 k values held as float4 by each lane.
 __device__ __forceinline__ f32x4 mfma4(const float4 a, const float4 b, f32x4 acc) {

@@ -205,9 +205,10 @@ class FusedTrainStep:
                 if i < slots:
                     acc += wts[i]
             sw.dim = eng.D
-            # 64 extra workgroups per launch measured best (C2 271.7k, C3 168.7k sessions/s;
-            # more of them raise the latency-bound groups' load latency)
-            sw.blocks = int(os.environ.get("GTR_SWEEP_BLOCKS", 64))
+            # 128 extra workgroups per launch: with streaming sweep accesses and split-bf16
+            # GEMMs the slices, not the row groups, bounded each launch at 64 (C2 285k ->
+            # 323k, C3 174k -> 214k sessions/s; 96-160 within 1 %)
+            sw.blocks = int(os.environ.get("GTR_SWEEP_BLOCKS", 128))
             sw.lag = 1 if self.lagged else 0
             sw.consts = self.lazy_consts.data_ptr() if self.lagged else None
             self.sweep = sw
