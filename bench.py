@@ -77,6 +77,9 @@ def main():
     ap.add_argument("--num-batches", type=int, default=64, help="distinct pre-staged batches per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--resident", action="store_true",
+                    help="launch on the pre-staged batch images (one graph per image) instead of copying each "
+                         "into the step's blob")
     ap.add_argument("--dp", action="store_true", help="force the data-parallel step (exchange) even at N=1")
     ap.add_argument("--global-batch", type=int, default=None,
                     help="strong scaling: fixed global batch split over the ranks, SyncBN (1 GPU semantics)")
@@ -140,12 +143,23 @@ def main():
                                                                    "touched", "stats"))
     log(f"data: T={T} sessions={data.num_sessions} edges={data.edge_keys.size} setup {time.time()-t0:.1f}s {st}")
 
+    # default: each step copies its pre-staged batch image into the step's blob (one D2D
+    # copy, inside the timed step); --resident launches straight on the images instead
+    # (FusedTrainStep.bind_resident: one captured graph per image) -- measured equal
+    resident = args.resident
+    if resident:
+        step.bind_resident(staged)
+
     def one(i):
+        if resident:
+            return step.run_resident(i % len(staged))
         step.load_blob(staged[i % len(staged)])
         return step.run()
 
     for i in range(args.warmup):
         one(i)
+    if resident and not args.no_graph:
+        step.prepare_resident()  # no capture inside the timed region
     torch.cuda.synchronize(dev)
     if world > 1:
         torch.distributed.barrier()
@@ -226,6 +240,7 @@ def main():
                 "transport": "rccl" if backend == "nccl" else "gloo (shared-device rehearsal)",
                 "dp_exchange": step.dp is not None,
                 "hip_graph": not args.no_graph,
+                "batch_images": "resident, one graph per image" if args.resident else "copied per step (D2D)",
                 "lazy_table": lazy,
                 "lagged_sweep": lagged,
                 "graph_collectives": bool(step.dp is not None and step._graph_collectives()),

@@ -113,6 +113,7 @@ class FusedTrainStep:
         if getattr(self, "sweep", None) is not None and self.sweep.lag:
             self.sweep.consts = consts.data_ptr()
         self.graph = self.graph_pe = self.graph_b = None  # captured pointers changed
+        self.resident_graphs = None
 
     def flush(self):
         """Bring every table row up to the current step (lazy mode; no-op otherwise)."""
@@ -228,6 +229,8 @@ class FusedTrainStep:
         self.graph = None
         self.graph_pe = None
         self.graph_b = None
+        self.resident = None  # bind_resident: batch images bound to this workspace
+        self.resident_graphs = None
 
     def ensure_caps(self, batch: SessionBatch):
         N, B, E, n = batch.sizes()
@@ -275,10 +278,12 @@ class FusedTrainStep:
             self._bind(caps if self.caps is None else self.caps.grow(caps.n_cap, caps.b_cap, caps.e_cap, caps.n_neg))
         self.builder = builder
         self.graph = self.graph_pe = self.graph_b = None
+        self.resident_graphs = None
 
     def detach_builder(self):
         self.builder = None
         self.graph = self.graph_pe = self.graph_b = None
+        self.resident_graphs = None
 
     # ------------------------------------------------------------------ launches
     def _sync_alloc(self):
@@ -479,10 +484,76 @@ class FusedTrainStep:
         torch.cuda.current_stream(self.dev).wait_stream(s)
         return g
 
+    def bind_resident(self, blobs):
+        """Zero-copy steps over packed batch images already resident in HBM (the same
+        capacities as the step's own blob): each image gets its own batch struct and, on
+        first use, its own captured graph, so ``run_resident(i)`` launches straight on
+        image i instead of copying it into the step's blob first."""
+        if self.caps is None:
+            raise RuntimeError("bind the step's capacities first (load one batch)")
+        n = self.blob.numel()
+        for b in blobs:
+            if b.numel() != n or b.dtype != self.blob.dtype or b.device != self.blob.device:
+                raise ValueError("resident images must match the step's blob (size, dtype, device)")
+        self.resident = [(b, self.eng.batch_struct(self.caps, b, None)) for b in blobs]
+        self.resident_graphs = None
+
+    def _with_bs(self, bs, fn):
+        saved = self.bs
+        self.bs = bs
+        try:
+            return fn()
+        finally:
+            self.bs = saved
+
+    def prepare_resident(self):
+        """Capture every resident image's graph now (after at least one eager step), so
+        that no capture falls into a timed region."""
+        if self.resident is None:
+            raise RuntimeError("bind_resident first")
+        if self.resident_graphs is None:
+            self.resident_graphs = [None] * len(self.resident)
+        for i, (_, bs) in enumerate(self.resident):
+            if self.resident_graphs[i] is None:
+                self.resident_graphs[i] = self._with_bs(bs, lambda: self._capture_pieces(False))
+
+    def run_resident(self, i: int):
+        """One training step over resident image i (see bind_resident)."""
+        if self.resident is None:
+            raise RuntimeError("bind_resident first")
+        self.eng.check_intact()
+        if not self.model.training:
+            raise RuntimeError("FusedTrainStep requires model.train()")
+        if self.lazy:
+            if self._host_steps + 2 >= self.lz.cap:
+                self._lazy_alloc(2 * self.lz.cap)
+            self._host_steps += 1
+            self._dirty = True
+        bs = self.resident[i][1]
+        if not self.use_graph:
+            self._with_bs(bs, lambda: self._launch(False))
+            return self.ws.loss_out[0]
+        if self.resident_graphs is None:
+            self.resident_graphs = [None] * len(self.resident)
+        graphs = self.resident_graphs[i]
+        if graphs is None:
+            self._with_bs(bs, lambda: self._launch(False))  # eager step (first touch), then capture
+            torch.cuda.synchronize(self.dev)
+            self.resident_graphs[i] = self._with_bs(bs, lambda: self._capture_pieces(False))
+            return self.ws.loss_out[0]
+        for g, coll in graphs:
+            g.replay()
+            if coll is not None:
+                coll()
+        return self.ws.loss_out[0]
+
+    def _capture_pieces(self, with_pe: bool):
+        return [(self._capture(launch), coll) for launch, coll in self._graph_pieces(with_pe)]
+
     def capture(self, with_pe: bool = False):
         """Capture the step's pieces into hipGraphs (after one eager warm-up step): the
         whole step single-GPU; the pieces between collectives in DP mode."""
-        graphs = [(self._capture(launch), coll) for launch, coll in self._graph_pieces(with_pe)]
+        graphs = self._capture_pieces(with_pe)
         if with_pe:
             self.graph_pe = graphs
         else:
