@@ -243,6 +243,7 @@ def main():
                 "batch_images": "resident, one graph per image" if args.resident else "copied per step (D2D)",
                 "lazy_table": lazy,
                 "lagged_sweep": lagged,
+                "gemm": gemm_mode(D),
                 "graph_collectives": bool(step.dp is not None and step._graph_collectives()),
                 "sync_bn": bool(args.sync_bn and world > 1),
                 "gpu_ms_per_step_events": round(gpu_ms / args.steps, 4),
@@ -359,6 +360,14 @@ def measure_tail(step, iters) -> float:
         durs.append((e0, e1))
     torch.cuda.synchronize()
     return float(np.median([a.elapsed_time(b) for a, b in durs]))
+
+
+def gemm_mode(D: int) -> str:
+    """The layer GEMMs' arithmetic (gemm_split in csrc/gtr_common.cuh)."""
+    e = os.environ.get("GTR_GEMM", "").lower()
+    split = e.startswith("s") or (not e.startswith("f") and D >= 128 and D != 256)
+    return ("split-bf16 MFMA (hi/lo operands, 3 bf16 MFMAs, fp32 accumulate)" if split
+            else "f32-input MFMA (exact f32)")
 
 
 def step_bytes(step, cfg, T, N, B) -> float:

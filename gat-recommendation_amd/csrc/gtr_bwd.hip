@@ -787,7 +787,7 @@ extern "C" int gtr_conv_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
 #define GTR_BWD(DD, SP) set_lds_limit<DD>(k_conv_bwd<DD, SP>, (size_t)LayerGeom<DD>::B_WORDS * 4); \
   hipLaunchKernelGGL((k_conv_bwd<DD, SP>), dim3(grid), dim3(CONV_BLOCK), \
                                        (size_t)LayerGeom<DD>::B_WORDS * 4, s, k)
-  const bool sp = gemm_split() != 0;
+  const bool sp = gemm_split(D) != 0;
   switch (D) {
     case 32: if (sp) { GTR_BWD(32, true); } else { GTR_BWD(32, false); } break;
     case 64: if (sp) { GTR_BWD(64, true); } else { GTR_BWD(64, false); } break;

@@ -235,15 +235,14 @@ __device__ __forceinline__ void sweep_slice(const gtr_sweep& sw, int slot, int b
   }
 }
 
-// GEMM arithmetic of the layer kernels (host side, read once): split-bf16 MFMA (default)
-// or exact f32-input MFMA (GTR_GEMM=f32).
-inline int gemm_split() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("GTR_GEMM");
-    v = (e && (e[0] == 'f' || e[0] == 'F')) ? 0 : 1;
-  }
-  return v;
+// GEMM arithmetic of the layer kernels (host side): split-bf16 MFMA or exact f32-input
+// MFMA.  Default by width: D >= 128 split (the f32 MFMA cycles dominate the projection
+// and dX there: C3 +20 % sessions/s), D <= 64 exact f32 (+5 % only, and exact f32 keeps
+// C2's 100-step Recall@10 identical to the oracle's).  GTR_GEMM=split|f32 overrides.
+inline int gemm_split(int dim) {
+  const char* e = getenv("GTR_GEMM");  // read per launch: tests switch it within a process
+  const int v = !e ? -1 : (e[0] == 'f' || e[0] == 'F') ? 0 : (e[0] == 's' || e[0] == 'S') ? 1 : -1;
+  return v >= 0 ? v : (dim >= 128 ? 1 : 0);
 }
 
 }  // namespace gtr

@@ -1335,7 +1335,7 @@ extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   k.layer = l;
   k.pe_k = cfg->pe_k;
   k.cred = cfg->consumer_reduce;
-  k.split = gemm_split();
+  k.split = gemm_split(cfg->dim);
   k.sqrt_c = (float)sqrt((double)k.C);
   k.bn_eps = cfg->bn_eps;
   k.bn_mom = cfg->bn_momentum;

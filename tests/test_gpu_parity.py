@@ -369,3 +369,12 @@ def test_resident_images_equal_copied_blob():
         assert float(f1(bl[i].to("cuda"))) == float(f2.run_resident(i))
     for a, b in zip(m1.parameters(), m2.parameters()):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("gemm,D,H,K,loss", [("split", 64, 1, 0, "model_bpr"), ("f32", 128, 4, 16, "listwise"),
+                                             ("split", 32, 2, 0, "dual")])
+def test_train_grads_gemm_modes(gemm, D, H, K, loss, monkeypatch):
+    """The layer GEMMs in the mode the width does not default to (GTR_GEMM): split-bf16
+    at D <= 64, exact f32 at D = 128 -- gradients against the oracle at 2e-3."""
+    monkeypatch.setenv("GTR_GEMM", gemm)
+    test_train_grads(D, H, K, loss)
