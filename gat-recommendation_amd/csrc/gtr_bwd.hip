@@ -584,12 +584,7 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
   }
   if (a.cred) return;  // the next conv_bwd reduces the partials
   if (!arrive_last(a.p_cnt, (uint32_t)Gn, s_flag)) return;
-  for (int j = tid; j < 2 * D; j += CONV_BLOCK) {
-    float acc = 0.0f;
-#pragma unroll 4
-    for (int q = 0; q < Gn; ++q) acc += a.p_gpart[(size_t)q * 2 * D + j];
-    a.p_gsum[j] = acc;
-  }
+  block_sum_rows<CONV_BLOCK>(a.p_gpart, Gn, 2 * D, (size_t)2 * D, a.p_gsum, sm);  // LDS dead by now
   if (tid == 0) reset_counter(a.p_cnt);
 }
 
@@ -597,7 +592,7 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
 // weight gradients
 // ------------------------------------------------------------------------------------
 
-enum { WJ_MM = 0, WJ_GATE = 1 };
+enum { WJ_MM = 0, WJ_GATE = 1, WJ_COLSUM = 2 };
 
 struct WJob {
   int type, M1, M2, lda, ldb, tn, nt, blk0;
@@ -651,6 +646,16 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_wgrad(WgradK a) {
       acc += u * f;
     }
     J.outW[so + j] = acc;
+    return;
+  }
+
+  if (J.type == WJ_COLSUM) {  // bias gradient: column sums of A over this chunk's rows
+    const int j = tile * GTR_BLOCK + tid;
+    if (j >= J.M1) return;
+    float acc = 0.0f;
+#pragma unroll 8
+    for (int t = t0; t < t1; ++t) acc += J.A[(size_t)t * J.lda + j];
+    J.outB[so + j] = acc;
     return;
   }
 
@@ -807,7 +812,7 @@ extern "C" int gtr_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_l
     return GTR_E_ARG;
   }
   const int D = cfg->dim, Lc = cfg->num_layers;
-  if (2 * Lc + 1 > GTR_MAX_WJOBS) { set_error("gtr_wgrad: too many layers"); return GTR_E_ARG; }
+  if (3 * Lc + 1 > GTR_MAX_WJOBS) { set_error("gtr_wgrad: too many layers"); return GTR_E_ARG; }
   WgradK k{};
   k.hdr = bt->hdr;
   k.P = n_chunks;
@@ -820,10 +825,19 @@ extern "C" int gtr_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_l
     float* base = layer_slab[l];
     WJob& w = k.jobs[nj++];
     w.type = WJ_MM; w.M1 = 4 * D; w.M2 = D; w.lda = 4 * D; w.ldb = D;
-    w.tn = (D + 1 + 63) / 64; w.nt = ((4 * D + 63) / 64) * w.tn; w.blk0 = blocks;
+    // the bias rides as a ones-column in the last tile when it fits there (D = 32); for
+    // D a multiple of 64 it would need a tile column of its own (1/3 more tiles at
+    // D = 128), so it is a column-sum job instead
+    w.tn = (D + 63) / 64; w.nt = ((4 * D + 63) / 64) * w.tn; w.blk0 = blocks;
     w.A = L.dqkvs; w.B = L.xin; w.bidx = nullptr;
     w.outW = base; w.outB = base + (size_t)4 * D * D;
     blocks += w.nt * n_chunks;
+    if (D % 64 == 0) {
+      WJob& c = k.jobs[nj++];
+      c.type = WJ_COLSUM; c.M1 = 4 * D; c.lda = 4 * D; c.tn = 1; c.nt = (4 * D + GTR_BLOCK - 1) / GTR_BLOCK;
+      c.blk0 = blocks; c.A = L.dqkvs; c.outB = base + (size_t)4 * D * D;
+      blocks += c.nt * n_chunks;
+    }
     WJob& q = k.jobs[nj++];
     q.type = WJ_GATE; q.M1 = 1; q.M2 = 3 * D; q.lda = 4 * D; q.tn = 1; q.nt = (3 * D + GTR_BLOCK - 1) / GTR_BLOCK;
     q.blk0 = blocks; q.A = L.du; q.agg = L.agg; q.s = L.qkvs + 3 * D;

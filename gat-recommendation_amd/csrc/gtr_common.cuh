@@ -127,6 +127,42 @@ __device__ __forceinline__ void reset_counter(uint32_t* cnt) {
   __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Column sums of a [G][stride] partial array (columns [0, W)) with the whole block, in a
+// fixed order: slice sl of NSL = BLK / W sums rows sl, sl + NSL, ... with 8 loads in
+// flight, then the slices are combined through LDS (scr: >= BLK floats).  Used by the
+// last-arriving workgroup of a launch, where hundreds of partial rows (large batches)
+// summed by one thread per column were a serial chain of L2 round trips.
+template <int BLK>
+__device__ __forceinline__ void block_sum_rows(const float* p, int G, int W, size_t stride, float* out,
+                                               float* scr) {
+  const int tid = threadIdx.x;
+  if (W >= BLK) {
+    for (int j = tid; j < W; j += BLK) {
+      float acc = 0.0f;
+#pragma unroll 8
+      for (int q = 0; q < G; ++q) acc += p[(size_t)q * stride + j];
+      out[j] = acc;
+    }
+    __syncthreads();
+    return;
+  }
+  const int NSL = BLK / W;
+  const int j = tid % W, sl = tid / W;
+  if (sl < NSL) {
+    float acc = 0.0f;
+#pragma unroll 8
+    for (int q = sl; q < G; q += NSL) acc += p[(size_t)q * stride + j];
+    scr[sl * W + j] = acc;
+  }
+  __syncthreads();
+  if (tid < W) {
+    float t = 0.0f;
+    for (int q = 0; q < NSL; ++q) t += scr[q * W + tid];
+    out[tid] = t;
+  }
+  __syncthreads();
+}
+
 // torch.optim.AdamW / Adam single-tensor arithmetic (fp32 element ops; bias
 // corrections computed in double like the Python scalars of torch/optim/adamw.py).
 struct AdamStep {

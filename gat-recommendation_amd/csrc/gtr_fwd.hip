@@ -919,19 +919,12 @@ __global__ __launch_bounds__(RO_BLOCK) void k_readout(ReadoutK a) {
   GTR_PH(16, 3);
   if (!a.fin) return;  // loss summed by the step tail, BN sums reduced by the consuming conv_bwd
   if (!arrive_last(a.cnt, (uint32_t)a.main_grid, &s_flag)) return;
-  if (do_loss && tid == 0) {
-    float loss = 0.0f;
-    for (int q = 0; q < a.main_grid; ++q) loss += a.loss_part[(size_t)q * 2] + a.loss_part[(size_t)q * 2 + 1];
-    a.loss_out[0] = loss;
+  if (do_loss) {
+    __shared__ float s_pair[2];
+    block_sum_rows<RO_BLOCK>(a.loss_part, a.main_grid, 2, 2, s_pair, &s_red[0][0]);
+    if (tid == 0) a.loss_out[0] = s_pair[0] + s_pair[1];
   }
-  if (do_bwd) {
-    for (int j = tid; j < 2 * D; j += RO_BLOCK) {
-      float acc = 0.0f;
-#pragma unroll 4
-      for (int q = 0; q < a.main_grid; ++q) acc += a.gpart[(size_t)q * 2 * D + j];
-      a.gsum[j] = acc;
-    }
-  }
+  if (do_bwd) block_sum_rows<RO_BLOCK>(a.gpart, a.main_grid, 2 * D, (size_t)2 * D, a.gsum, &s_red[0][0]);
   if (tid == 0) reset_counter(a.cnt);
 }
 
@@ -1252,30 +1245,12 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
   }
   if (!a.fin) return;
   if (!arrive_last(a.cnt, (uint32_t)a.main_grid, &s_flag)) return;
-  if (do_loss && tid == 0) {
-    float loss = 0.0f;
-    for (int q = 0; q < a.main_grid; ++q) loss += a.loss_part[(size_t)q * 2] + a.loss_part[(size_t)q * 2 + 1];
-    a.loss_out[0] = loss;
+  if (do_loss) {
+    __shared__ float s_pair[2];
+    block_sum_rows<RW_BLOCK>(a.loss_part, a.main_grid, 2, 2, s_pair, s_scr);
+    if (tid == 0) a.loss_out[0] = s_pair[0] + s_pair[1];
   }
-  if (do_bwd) {
-    // NSL slices of the partials per column, summed in fixed order
-    constexpr int NSL = RW_BLOCK / (2 * D) >= 1 ? RW_BLOCK / (2 * D) : 1;
-    const int j = tid % (2 * D), sl = tid / (2 * D);
-    float acc = 0.0f;
-    if (sl < NSL) {
-#pragma unroll 8
-      for (int q = sl; q < a.main_grid; q += NSL) acc += a.gpart[(size_t)q * 2 * D + j];
-    }
-    __syncthreads();
-    float* red = s_scr;  // >= NSL * 2D floats (NSL * 2D <= RW_BLOCK)
-    if (sl < NSL) red[sl * 2 * D + j] = acc;
-    __syncthreads();
-    for (int jj = tid; jj < 2 * D; jj += RW_BLOCK) {
-      float t = 0.0f;
-      for (int q = 0; q < NSL; ++q) t += red[q * 2 * D + jj];
-      a.gsum[jj] = t;
-    }
-  }
+  if (do_bwd) block_sum_rows<RW_BLOCK>(a.gpart, a.main_grid, 2 * D, (size_t)2 * D, a.gsum, s_scr);
   if (tid == 0) reset_counter(a.cnt);
 }
 

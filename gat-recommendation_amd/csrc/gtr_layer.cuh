@@ -133,6 +133,7 @@ __device__ __forceinline__ void bn_stats_from_parts(const float* part, int G, fl
   float* s_mu = scr + 2 * NSL * D; // [D]
   if (sl < NSL) {
     float n = 0.0f, sum = 0.0f;
+#pragma unroll 8
     for (int q = sl; q < G; q += NSL) {
       const float* pp = part + (size_t)q * (1 + 2 * D);
       const float c = pp[0];
@@ -152,6 +153,7 @@ __device__ __forceinline__ void bn_stats_from_parts(const float* part, int G, fl
   if (sl < NSL) {
     const float mean = s_mu[j];
     float m2 = 0.0f;
+#pragma unroll 8
     for (int q = sl; q < G; q += NSL) {
       const float* pp = part + (size_t)q * (1 + 2 * D);
       const float d = pp[1 + j] - mean;
