@@ -108,7 +108,73 @@ __global__ __launch_bounds__(256) void k_spmm_split(const int4* splits, int64_t 
   }
 }
 
+// Gram matrices of the block eigen-solver, S^T S and S^T Y for tall-skinny S, Y [n, m]
+// (m <= 64), accumulated in fp64: workgroup p takes rows [p*rows, (p+1)*rows), stages
+// GRAM_TR rows of S and Y in LDS and each thread accumulates 16 entries of each 64x64
+// product (entry e = tid + 256k: row i = e / 64 is uniform across a wave, so the S[.][i]
+// read is a broadcast); k_gram_reduce sums the partials in workgroup order.
+#define GRAM_TR 32
+__global__ __launch_bounds__(256) void k_gram_part(const float* S, const float* Y, int n, int m, int rows,
+                                                   double* part) {
+  __shared__ float sS[GRAM_TR][64];
+  __shared__ float sY[GRAM_TR][64];
+  const int tid = threadIdx.x;
+  const int r0 = blockIdx.x * rows, r1 = min(n, r0 + rows);
+  double g[16], h[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) { g[k] = 0.0; h[k] = 0.0; }
+  for (int rb = r0; rb < r1; rb += GRAM_TR) {
+    for (int idx = tid; idx < GRAM_TR * 64; idx += 256) {
+      const int rr = idx >> 6, c = idx & 63, r = rb + rr;
+      const bool in = r < r1 && c < m;
+      sS[rr][c] = in ? S[(size_t)r * m + c] : 0.0f;
+      sY[rr][c] = in ? Y[(size_t)r * m + c] : 0.0f;
+    }
+    __syncthreads();
+    for (int rr = 0; rr < GRAM_TR; ++rr) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int e = tid + 256 * k;
+        const double si = (double)sS[rr][e >> 6];
+        g[k] += si * (double)sS[rr][e & 63];
+        h[k] += si * (double)sY[rr][e & 63];
+      }
+    }
+    __syncthreads();
+  }
+  double* out = part + (size_t)blockIdx.x * 8192;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    out[tid + 256 * k] = g[k];
+    out[4096 + tid + 256 * k] = h[k];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_gram_reduce(const double* part, int P, double* out) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= 8192) return;
+  double acc = 0.0;
+  for (int p = 0; p < P; ++p) acc += part[(size_t)p * 8192 + e];
+  out[e] = acc;
+}
+
 }  // namespace
+
+extern "C" int gtr_lap_gram(const float* S, const float* Y, int n, int m, double* part, int P, double* out,
+                            gtr_stream_t stream) {
+  if (!S || !Y || !part || !out || n <= 0 || m <= 0 || m > 64 || P <= 0) {
+    set_error("gtr_lap_gram: bad arguments (m <= 64, P >= 1)");
+    return GTR_E_ARG;
+  }
+  const int rows = (n + P - 1) / P;
+  const int grid = (n + rows - 1) / rows;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_gram_part, dim3(grid), dim3(256), 0, s, S, Y, n, m, rows, part);
+  GTR_HIP_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_gram_reduce, dim3(32), dim3(256), 0, s, part, grid, out);
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
 
 extern "C" int gtr_lap_build(const int32_t* ptr, const int32_t* col, int n, float* dis, float* val,
                              gtr_stream_t stream) {

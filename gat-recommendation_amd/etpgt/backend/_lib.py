@@ -155,6 +155,7 @@ _SIGS = {
     "gtr_lap_build": (C.c_int, [P, P, C.c_int, P, P, P]),
     "gtr_lap_plan": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P]),
     "gtr_lap_spmm": (C.c_int, [P, P, C.c_int, C.c_int, P, i64, P, i64, P, P, P, f32, f32, P]),
+    "gtr_lap_gram": (C.c_int, [P, P, C.c_int, C.c_int, P, C.c_int, P, P]),
     "gtr_topk_workspace_bytes": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_size_t)]),
     "gtr_score_topk": (C.c_int, [P, C.c_int, C.c_int, P, C.c_int, C.c_int, P, P, P, C.c_size_t, P]),
     "gtr_score_topk_masked": (C.c_int, [P, C.c_int, C.c_int, P, C.c_int, C.c_int, P, P, P, P, P, C.c_size_t, P]),

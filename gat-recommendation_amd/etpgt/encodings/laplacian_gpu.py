@@ -88,6 +88,22 @@ class LaplacianOperator:
     def _stream(self):
         return torch.cuda.current_stream(self.device).cuda_stream
 
+    GRAM_CHUNKS = 256
+
+    def gram(self, S: torch.Tensor, Y: torch.Tensor) -> np.ndarray:
+        """[2, m, m] fp64 host array (S^T S, S^T Y) for fp32 [n, m] blocks, m <= 64
+        (HIP kernel gtr_lap_gram: fp64 accumulation, fixed summation order)."""
+        m = S.shape[1]
+        if S.shape != Y.shape or S.shape[0] != self.n or m > 64:
+            raise ValueError("gram: S and Y must be [n, m <= 64]")
+        if getattr(self, "_gpart", None) is None:
+            self._gpart = torch.empty(self.GRAM_CHUNKS * 8192, dtype=torch.float64, device=self.device)
+            self._gout = torch.empty(8192, dtype=torch.float64, device=self.device)
+        S, Y = S.contiguous(), Y.contiguous()
+        L.check(L.lib().gtr_lap_gram(S.data_ptr(), Y.data_ptr(), self.n, m, self._gpart.data_ptr(),
+                                     self.GRAM_CHUNKS, self._gout.data_ptr(), self._stream()), "lap_gram")
+        return self._gout.view(2, 64, 64)[:, :m, :m].cpu().numpy()
+
     def _spmm(self, X: torch.Tensor, Y: torch.Tensor, alpha: float = 1.0, beta: float = 0.0):
         L.check(L.lib().gtr_lap_spmm(self.col.data_ptr(), self.val.data_ptr(), self.n, X.shape[1],
                                      self.items.data_ptr(), self.n_items, self.splits.data_ptr(), self.n_splits,
@@ -112,6 +128,11 @@ class LaplacianOperator:
         return Y
 
 
+def _gram_torch(S: torch.Tensor, Y: torch.Tensor) -> np.ndarray:
+    Sd = S.double()
+    return torch.stack([Sd.T @ Sd, Sd.T @ Y.double()]).cpu().numpy()
+
+
 def lobpcg_smallest(op: LaplacianOperator, nev: int, extra: int = 4, tol: float = 1e-5, maxiter: int = 2000,
                     seed: int = 0, drop: float = 1e-7):
     """The ``nev`` smallest eigenpairs of the symmetric operator (ascending).  Returns
@@ -130,7 +151,10 @@ def lobpcg_smallest(op: LaplacianOperator, nev: int, extra: int = 4, tol: float 
     g = torch.Generator(device="cpu").manual_seed(seed)
     X, _ = torch.linalg.qr(torch.randn(n, b, generator=g, dtype=torch.float32).to(dev))
     AX = op(X)
-    H = (X.T.double() @ AX.double()).cpu().numpy()
+    def gram(S, Y):  # the HIP Gram kernel takes blocks of <= 64 columns
+        return op.gram(S, Y) if hasattr(op, "gram") and S.shape[1] <= 64 else _gram_torch(S, Y)
+
+    H = gram(X, AX)[1]
     lam, Cm = np.linalg.eigh((H + H.T) / 2)
     Ct = torch.from_numpy(Cm).float().to(dev)
     X, AX = X @ Ct, AX @ Ct
@@ -140,8 +164,7 @@ def lobpcg_smallest(op: LaplacianOperator, nev: int, extra: int = 4, tol: float 
         R = AX - X * torch.from_numpy(lam[:b]).float().to(dev)
         S = torch.cat([X, R] if P is None else [X, R, P], dim=1)
         AS = op(S)
-        Sd = S.double()
-        GH = torch.stack([Sd.T @ Sd, Sd.T @ AS.double()]).cpu().numpy()
+        GH = gram(S, AS)
         G, H = GH[0], (GH[1] + GH[1].T) / 2
         dg = np.diag(G).copy()
         if np.sqrt(dg[b:b + nev].max()) < tol:

@@ -469,6 +469,11 @@ int gtr_lap_plan(const int32_t* ptr, int n, int chunk, int32_t* items, int64_t* 
 int gtr_lap_spmm(const int32_t* col, const float* val, int n, int b, const int32_t* items, int64_t n_items,
                  const int32_t* splits, int64_t n_splits, float* part, const float* X, float* Y, float alpha,
                  float beta, gtr_stream_t stream);
+/* The solver's Gram matrices: out [2][64][64] fp64 = S^T S | S^T Y for S, Y [n, m] fp32
+ * row-major, m <= 64 (entries past m are 0), accumulated in fp64 and summed in a fixed
+ * order; part: P * 8192 doubles of scratch (P row chunks).                           */
+int gtr_lap_gram(const float* S, const float* Y, int n, int m, double* part, int P, double* out,
+                 gtr_stream_t stream);
 
 /* Workgroups of gtr_readout_loss = the number of its loss / BatchNorm-sum partials
  * (gtr_tail.loss_nparts; the last layer's bn_gpart rows).                         */

@@ -129,3 +129,17 @@ def test_lappe_gpu_rejects_out_of_range():
     ei = torch.tensor([[0, 5], [5, 0]])
     with pytest.raises(IndexError):
         LaplacianOperator(ei, 4, "cuda")
+
+
+@pytest.mark.parametrize("n,m", [(1000, 1), (12345, 21), (3000, 63), (777, 64)])
+def test_gram_kernel_matches_fp64(n, m):
+    """gtr_lap_gram (the solver's S^T S | S^T Y in fp64) against numpy in fp64."""
+    ei = _graph(n, n, seed=1)
+    op = LaplacianOperator(ei, n, "cuda")
+    g = torch.Generator().manual_seed(m)
+    S = torch.randn(n, m, generator=g)
+    Y = torch.randn(n, m, generator=g)
+    GH = op.gram(S.cuda(), Y.cuda())
+    Sd, Yd = S.double().numpy(), Y.double().numpy()
+    np.testing.assert_allclose(GH[0], Sd.T @ Sd, rtol=1e-12, atol=1e-9)
+    np.testing.assert_allclose(GH[1], Sd.T @ Yd, rtol=1e-12, atol=1e-9)
