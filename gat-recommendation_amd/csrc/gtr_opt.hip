@@ -824,6 +824,17 @@ struct DpTailK {
   int vpr_log2, pad0;
 };
 
+// First slot of `key` in one rank's sorted contribution keys (sentinel-padded), or -1.
+__device__ __forceinline__ int dp_find(const float* keys_f, int m_cap, int key) {
+  const int32_t* kq = reinterpret_cast<const int32_t*>(keys_f);
+  int lo = 0, hi = m_cap;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (kq[mid] < key) lo = mid + 1; else hi = mid;
+  }
+  return (lo < m_cap && kq[lo] == key) ? lo : -1;
+}
+
 template <int D>
 __global__ __launch_bounds__(GTR_BLOCK) void k_dp_tail(DpTailK a) {
   constexpr int C4 = D / 4;
@@ -850,16 +861,28 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_dp_tail(DpTailK a) {
     const int32_t* keys = reinterpret_cast<const int32_t*>(a.recv + (size_t)r * a.lay.words + a.lay.keys_off);
     const int k = keys[i];
     if (k <= 0 || k >= a.T || (i > 0 && keys[i - 1] == k)) return;
-    const int2* sl = a.slot + (size_t)k * W;
-    for (int q = 0; q < r; ++q)
-      if (sl[q].x == t) return;
     float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int q = r; q < W; ++q) {
-      const int2 e = sl[q];
-      if (e.x != t) continue;
-      const float4 v = reinterpret_cast<const float4*>(a.recv + (size_t)q * a.lay.words + a.lay.rows_off +
-                                                       (size_t)e.y * D)[c];
-      g.x += v.x; g.y += v.y; g.z += v.z; g.w += v.w;
+    if (a.slot) {  // slot table from k_dp_stamp
+      const int2* sl = a.slot + (size_t)k * W;
+      for (int q = 0; q < r; ++q)
+        if (sl[q].x == t) return;
+      for (int q = r; q < W; ++q) {
+        const int2 e = sl[q];
+        if (e.x != t) continue;
+        const float4 v = reinterpret_cast<const float4*>(a.recv + (size_t)q * a.lay.words + a.lay.rows_off +
+                                                         (size_t)e.y * D)[c];
+        g.x += v.x; g.y += v.y; g.z += v.z; g.w += v.w;
+      }
+    } else {  // lazy stamps: no union pass; find the row in each rank's sorted keys
+      for (int q = 0; q < r; ++q)
+        if (dp_find(a.recv + (size_t)q * a.lay.words + a.lay.keys_off, a.lay.m_cap, k) >= 0) return;  // lower owner
+      for (int q = r; q < W; ++q) {
+        const int at = q == r ? i : dp_find(a.recv + (size_t)q * a.lay.words + a.lay.keys_off, a.lay.m_cap, k);
+        if (at < 0) continue;
+        const float4 v = reinterpret_cast<const float4*>(a.recv + (size_t)q * a.lay.words + a.lay.rows_off +
+                                                         (size_t)at * D)[c];
+        g.x += v.x; g.y += v.y; g.z += v.z; g.w += v.w;
+      }
     }
     g.x *= inv_w; g.y *= inv_w; g.z *= inv_w; g.w *= inv_w;
     const size_t base = (size_t)k * C4 + c;
@@ -1254,16 +1277,21 @@ int gtr_dp_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tai
   }
   hipStream_t s = (hipStream_t)stream;
   const int64_t slots = (int64_t)lay->world * lay->m_cap;
-  hipLaunchKernelGGL(k_dp_stamp, dim3((unsigned)((slots + GTR_BLOCK - 1) / GTR_BLOCK)), dim3(GTR_BLOCK), 0, s, *lay,
-                     num_items, recv, tail->lazy_consts ? nullptr : tail->stamp, reinterpret_cast<int2*>(slot),
-                     opt->step_dev, opt->step_offset);
-  GTR_HIP_CHECK_LAUNCH();
+  // eager: stamp the union (the tail's sweep skips it) and build the (row, rank) slot
+  // table; lazy stamps need neither -- each rank's sorted keys are binary-searched
+  const bool search = tail->lazy_consts != nullptr;
+  if (!search) {
+    hipLaunchKernelGGL(k_dp_stamp, dim3((unsigned)((slots + GTR_BLOCK - 1) / GTR_BLOCK)), dim3(GTR_BLOCK), 0, s,
+                       *lay, num_items, recv, tail->lazy_consts ? nullptr : tail->stamp,
+                       reinterpret_cast<int2*>(slot), opt->step_dev, opt->step_offset);
+    GTR_HIP_CHECK_LAUNCH();
+  }
   DpTailK k{};
   k.tl = *tail;
   k.lay = *lay;
   k.opt = *opt;
   k.recv = recv;
-  k.slot = reinterpret_cast<const int2*>(slot);
+  k.slot = search ? nullptr : reinterpret_cast<const int2*>(slot);
   k.T = num_items;
   k.nb_rows = (int)((slots * (dim / 4) + GTR_BLOCK - 1) / GTR_BLOCK);
   k.nb_small = (int)((lay->flat_total + 1 + GTR_BLOCK - 1) / GTR_BLOCK);
