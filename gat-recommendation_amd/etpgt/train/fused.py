@@ -548,7 +548,18 @@ class FusedTrainStep:
         return self.ws.loss_out[0]
 
     def _capture_pieces(self, with_pe: bool):
-        return [(self._capture(launch), coll) for launch, coll in self._graph_pieces(with_pe)]
+        try:
+            return [(self._capture(launch), coll) for launch, coll in self._graph_pieces(with_pe)]
+        except RuntimeError as e:
+            if not self._graph_collectives():
+                raise
+            # a transport that refuses capture: keep the collectives between graph pieces
+            import warnings
+
+            warnings.warn(f"capturing the collectives failed ({e}); falling back to one graph per piece")
+            torch.cuda.synchronize(self.dev)
+            os.environ["GTR_GRAPH_COLL"] = "0"
+            return [(self._capture(launch), coll) for launch, coll in self._graph_pieces(with_pe)]
 
     def capture(self, with_pe: bool = False):
         """Capture the step's pieces into hipGraphs (after one eager warm-up step): the
