@@ -197,7 +197,8 @@ def main():
     step_ms = gpu_ms / args.steps
     alg_bytes = step_bytes(step, cfg, T, st["nodes_per_session"] * B, B)
     achieved = alg_bytes / (step_ms * 1e-3) / 1e9
-    traffic, traffic_src = load_traffic(args.config) if step.dp is None else (None, None)
+    traffic, traffic_src = (load_traffic(args.config if B == cfg.get("batch", 32) else f"{args.config}_b{B}")
+                            if step.dp is None else (None, None))
     tail_ms = measure_tail(step, args.steps)
 
     cpu = None
