@@ -124,7 +124,8 @@ __device__ __forceinline__ void store_vec(float* p, const float (&x)[VPL], bool 
 // (deterministic).  scr: >= 2*BLK + D floats of LDS.  Call with the whole block.
 template <int D, int BLK>
 __device__ __forceinline__ void bn_stats_from_parts(const float* part, int G, float eps, float* s_mean,
-                                                    float* s_rstd, float* s_uvar, float* scr) {
+                                                    float* s_rstd, float* s_uvar, float* scr,
+                                                    size_t rstride = 1 + 2 * D, float* merged = nullptr) {
   constexpr int NSL = BLK / D >= 1 ? BLK / D : 1;
   const int tid = threadIdx.x;
   const int j = tid % D, sl = tid / D;
@@ -135,7 +136,7 @@ __device__ __forceinline__ void bn_stats_from_parts(const float* part, int G, fl
     float n = 0.0f, sum = 0.0f;
 #pragma unroll 8
     for (int q = sl; q < G; q += NSL) {
-      const float* pp = part + (size_t)q * (1 + 2 * D);
+      const float* pp = part + (size_t)q * rstride;
       const float c = pp[0];
       n += c;
       sum += c * pp[1 + j];
@@ -147,7 +148,7 @@ __device__ __forceinline__ void bn_stats_from_parts(const float* part, int G, fl
   if (tid < D) {
     float n = 0.0f, sum = 0.0f;
     for (int q = 0; q < NSL; ++q) { n += s_n[q * D + tid]; sum += s_sum[q * D + tid]; }
-    s_mu[tid] = sum / n;
+    s_mu[tid] = n > 0.0f ? sum / n : 0.0f;  // a bucket of empty groups merges to (0, 0, 0)
   }
   __syncthreads();
   if (sl < NSL) {
@@ -155,7 +156,7 @@ __device__ __forceinline__ void bn_stats_from_parts(const float* part, int G, fl
     float m2 = 0.0f;
 #pragma unroll 8
     for (int q = sl; q < G; q += NSL) {
-      const float* pp = part + (size_t)q * (1 + 2 * D);
+      const float* pp = part + (size_t)q * rstride;
       const float d = pp[1 + j] - mean;
       m2 += pp[1 + D + j] + pp[0] * d * d;
     }
@@ -165,13 +166,25 @@ __device__ __forceinline__ void bn_stats_from_parts(const float* part, int G, fl
   if (tid < D) {
     float n = 0.0f, m2 = 0.0f;
     for (int q = 0; q < NSL; ++q) { n += s_n[q * D + tid]; m2 += s_sum[q * D + tid]; }
-    const float var = m2 / n;
-    s_mean[tid] = s_mu[tid];
-    s_rstd[tid] = 1.0f / sqrtf(var + eps);
-    s_uvar[tid] = n > 1.0f ? m2 / (n - 1.0f) : var;
+    if (merged) {  // the G partials combined into one (count, mean, M2) row (may alias row 0)
+      merged[1 + tid] = s_mu[tid];
+      merged[1 + D + tid] = m2;
+      if (tid == 0) merged[0] = n;
+    } else {
+      const float var = m2 / n;
+      s_mean[tid] = s_mu[tid];
+      s_rstd[tid] = 1.0f / sqrtf(var + eps);
+      s_uvar[tid] = n > 1.0f ? m2 / (n - 1.0f) : var;
+    }
   }
   __syncthreads();
 }
+
+// Row groups whose partials one last-arriving workgroup combines; past that the groups
+// are bucketed: each bucket's last arriver merges its partials into the bucket's first
+// row, and the last bucket merger combines the bucket rows (two short reductions
+// instead of one pass over hundreds of partial rows).
+#define GTR_PART_BUCKET 32
 
 // Dynamic LDS above 64 KiB needs the per-kernel limit raised once (gfx950: 160 KiB per CU).
 template <int D, typename K>

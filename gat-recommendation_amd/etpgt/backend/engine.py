@@ -168,7 +168,7 @@ class Workspace:
                 agg=_f32(n, D, device=dev), gate=_f32(n, device=dev), out=_f32(n, D, device=dev),
                 bn_stats=_f32(2 * D, device=dev), bn_part=_f32(g, 1 + 2 * D, device=dev),
                 bn_gsum=_f32(2 * D, device=dev), bn_gpart=_f32(max(g, 256), 2 * D, device=dev),
-                cnt=_i32(4, dev), dy=_f32(n, D, device=dev), dqkvs=_f32(n, 4 * D, device=dev),
+                cnt=_i32(8 + 2 * ((g + 31) // 32), dev), dy=_f32(n, D, device=dev), dqkvs=_f32(n, 4 * D, device=dev),
                 du=_f32(n, device=dev), dlogit=_f32(e, H, device=dev), dagg=_f32(n, D, device=dev),
             )
             self.layers.append(t)

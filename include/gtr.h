@@ -138,7 +138,8 @@ typedef struct gtr_layer {
   float* bn_part;  /* [g_cap, 1+2D] forward partials                 */
   float* bn_gsum;  /* [2D] sum(dy), sum(dy*xhat)                     */
   float* bn_gpart; /* [max(g_cap, 256), 2D] backward partials         */
-  uint32_t* cnt;   /* [4] arrival counters (zero-initialised once)     */
+  uint32_t* cnt;   /* [4 + 2*ceil(groups/32)] arrival counters (zero-initialised once;
+                      past 32 row groups the partials are merged per bucket of 32)   */
   float* dy;       /* [n_cap, D]  grad wrt BN(out)+x_{l-1} (pre dropout) */
   float* dqkvs;    /* [n_cap, 4D]                                    */
   float* du;       /* [n_cap]     grad wrt gate logit                 */
