@@ -41,7 +41,10 @@ class Caps:
     def R(self) -> int:
         """Row-group width of the layer kernels: a workgroup owns every session whose
         first node lies in [g*R, (g+1)*R)."""
-        return 16 if self.n_cap <= 8192 else (32 if self.n_cap <= 65536 else 64)
+        # a group's rows are R plus the tail of its last session, and the LDS fast path of
+        # the layer kernels takes <= 32 rows at D = 128 (RMAX): R = 32 sent nearly every
+        # group of a large batch down the global-memory path
+        return 16 if self.n_cap <= 65536 else 32
 
     @property
     def g_cap(self) -> int:
