@@ -95,7 +95,8 @@ def main():
     ap.add_argument("--e2e-steps", type=int, default=200,
                     help="end-to-end leg: steps with the batch built on the device inside the step (0 = skip)")
     ap.add_argument("--gather-batch", type=int, default=8192,
-                    help="embedding-gather roofline leg: C3 shape (d=128, 100 negatives) at this batch (0 = skip)")
+                    help="embedding-gather roofline legs: C5 (512 MB table, HBM) and C3 (42 MB, Infinity Cache) "
+                         "shapes (d=128, 100 negatives) at this batch (0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -195,10 +196,10 @@ def main():
     # sweep rides in the layer kernels, so the step is the unit that streams the table
     D = cfg["D"]
     step_ms = gpu_ms / args.steps
-    alg_bytes = step_bytes(step, cfg, T, st["nodes_per_session"] * B, B)
+    alg_bytes = step_bytes(step, cfg, T, st["nodes_per_session"] * B, B, touched, lazy)
     achieved = alg_bytes / (step_ms * 1e-3) / 1e9
-    traffic, traffic_src = (load_traffic(args.config if B == cfg.get("batch", 32) else f"{args.config}_b{B}")
-                            if step.dp is None else (None, None))
+    traffic, traffic_src = (load_traffic(args.config if B == cfg.get("batch", 32) else f"{args.config}_b{B}",
+                                         lazy) if step.dp is None else (None, None))
     tail_ms = measure_tail(step, args.steps)
 
     cpu = None
@@ -207,9 +208,10 @@ def main():
     e2e = None
     if rank == 0 and world == 1 and args.e2e_steps > 0:
         e2e = e2e_probe(cfg, data, dev, B, args.e2e_steps)
-    gather = None
+    gather = gather_c = None
     if rank == 0 and world == 1 and args.gather_batch > 0:
-        gather = gather_probe(dev, args.gather_batch)
+        gather = gather_probe(dev, args.gather_batch, "c5")
+        gather_c = gather_probe(dev, args.gather_batch, "c3")
     recall = None
     if rank == 0 and world == 1 and args.recall_steps > 0:
         recall = recall_parity(cfg, data, T, dev, args.recall_steps, args.recall_sessions)
@@ -227,6 +229,7 @@ def main():
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "fp32",
+            "gemm_precision": gemm_mode(D),
             "data": ("synthetic Yoochoose-scale" if cfg.get("scale") else "synthetic RetailRocket-shaped")
                     + " sessions/graph (seed 42), random-init weights",
             "config": {
@@ -264,8 +267,11 @@ def main():
                 "traffic_unit": "HBM bytes per step (PMC FETCH_SIZE x2 + WRITE_SIZE, summed over the step's kernels)",
                 "traffic_source": traffic_src,
                 "alg_bytes_per_launch": int(alg_bytes),
-                "alg_bytes_terms": "24*T*D table p/m/v + 4*T stamps + gathered rows/ids + 36*4*N*D per layer "
-                                   "+ small params (24 + 4*P slab partials per element)",
+                "alg_bytes_terms": ("(24*D + 4) per touched row (lazy table: no untouched-row sweep)" if lazy
+                                    else "24*T*D table p/m/v + 4*T stamps")
+                                   + " + gathered rows/ids + 36*4*N*D per layer + small params (24 + 4*P slab partials "
+                                     "per element)",
+                "touched_rows_per_step": round(touched, 1),
                 "avg_launch_ms": round(step_ms, 5),
                 "tail_kernel": {"name": "k_dp_tail" if step.dp is not None else "k_step_tail",
                                 "avg_launch_ms": round(tail_ms, 5)},
@@ -273,6 +279,7 @@ def main():
             "cpu_baseline": cpu,
             "end_to_end": e2e,
             "gather_roofline": gather,
+            "gather_roofline_infinity_cache": gather_c,
             "recall_parity": recall,
         }
         sys.stdout.flush()
@@ -320,19 +327,24 @@ def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, us
                 caps=caps, model=model)
 
 
-def load_traffic(config: str):
+def load_traffic(config: str, lazy: bool = False):
     """HBM bytes per training step from the newest committed PMC summary
-    (profiles/rNN/<config>_pmc.json: scripts/gpu_pmc.sh = two rocprofv3 --pmc passes,
+    (profiles/rNN/<config>_pmc.json, scripts/gpu/profile.sh: two rocprofv3 --pmc passes,
     FETCH_SIZE doubled per the gfx950 note + WRITE_SIZE, summed over the step's kernels
-    by scripts/pmc_parse.py)."""
+    by scripts/pmc_parse.py).  Only a profile of THESE kernel sources counts (its
+    ``_source_hash`` must equal the tree's); otherwise traffic is null."""
     import glob
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"{config}_pmc.json")))
+    from etpgt.backend._lib import source_hash
+
+    name = f"{config}_lazy" if lazy and not config.startswith("c5") else config
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"{name}_pmc.json")))
     if not files:
         return None, None
     with open(files[-1]) as f:
-        rec = json.load(f).get("_per_step")
-    if not rec:
+        d = json.load(f)
+    rec = d.get("_per_step")
+    if not rec or d.get("_source_hash") != source_hash():
         return None, None
     return float(rec["hbm_bytes_per_step"]), os.path.relpath(files[-1], ROOT)
 
@@ -366,19 +378,22 @@ def measure_tail(step, iters) -> float:
 def gemm_mode(D: int) -> str:
     """The layer GEMMs' arithmetic (gemm_split in csrc/gtr_common.cuh)."""
     e = os.environ.get("GTR_GEMM", "").lower()
-    split = e.startswith("s") or (not e.startswith("f") and D >= 128 and D != 256)
+    split = e.startswith("s")  # opt-in only (csrc/gtr_common.cuh gemm_split)
     return ("split-bf16 MFMA (hi/lo operands, 3 bf16 MFMAs, fp32 accumulate)" if split
             else "f32-input MFMA (exact f32)")
 
 
-def step_bytes(step, cfg, T, N, B) -> float:
+def step_bytes(step, cfg, T, N, B, touched: float, lazy: bool) -> float:
     """Algorithmic HBM bytes of one training step (each distinct tensor
     read or written once): the table AdamW (p, m, v read + write = 24 B per element; no
-    dense gradient) + touched-row stamps; the gathered node / PE / scoring rows and
-    their ids; layer activations (12 forward + 24 backward D-vectors per node and
-    layer, §8d); the small parameters (p, m, v + one read of each split-K partial)."""
+    dense gradient) + the stamps; the gathered node / PE / scoring rows and their ids;
+    layer activations (12 forward + 24 backward D-vectors per node and layer, §8d); the
+    small parameters (p, m, v + one read of each split-K partial).  The lazy table
+    (gtr_lazy) does not sweep the untouched rows: its table term is the touched rows
+    only (catch-up and update of a row = one read + write of p, m, v, 24 B per element)
+    plus their stamps."""
     D, K, n = cfg["D"], cfg["K"], cfg["n_neg"]
-    table = 24.0 * T * D + 4.0 * T
+    table = (24.0 * D + 4.0) * (touched if lazy else T)
     gather = 4.0 * N * D + 4.0 * N * K + 4.0 * B * (1 + n) * D + 4.0 * (N + B * (1 + n))
     acts = step.eng.L * 36 * 4.0 * N * D
     small = step.eng.flat.layout.total * (24.0 + 4.0 * step.ws.P)
@@ -449,19 +464,23 @@ def e2e_probe(cfg, data, dev, B, steps):
     }
 
 
-def gather_probe(dev, B, nbatch=2, steps=20):
+def gather_probe(dev, B, config="c5", nbatch=2, steps=20):
     """North-star embedding-gather target: the sampled-scoring gather at
-    d=128, n=100 negatives, large batch (C3 model).  The dominant gather kernel is the
-    readout/scoring kernel (wave per session at this size): per launch it reads B*(1+n)
-    table rows + ids, the last layer's out/xin node rows, writes se, dy and the score
+    d=128, n=100 negatives, large batch.  The dominant gather kernel is the readout /
+    scoring kernel (wave per session at this size): per launch it reads B*(1+n) table
+    rows + ids, the last layer's out/xin node rows, writes se, dy and the score
     coefficients.  Its average launch time is measured with HIP events around re-launches
     of that kernel (FWD|LOSS|BWD, the same work as inside the step) on the step's stream;
-    the full-step rate at this batch is reported beside it."""
+    the full-step rate at this batch is reported beside it.
+
+    ``config="c5"`` gathers from the 1M x 128 table (512 MB: larger than the 256 MB
+    Infinity Cache, so the rows come from HBM -- the honest number for the target);
+    ``"c3"`` from the 82k x 128 table (42 MB, Infinity-Cache resident)."""
     from etpgt.backend import _lib as L
 
-    cfg = CONFIGS["c3"]
-    w = build_workload("c3", B, nbatch, dev, 0, use_graph=True)
-    step, staged, batches = w["step"], w["staged"], w["batches"]
+    cfg = CONFIGS[config]
+    w = build_workload(config, B, nbatch, dev, 0, use_graph=True, lazy=bool(cfg.get("lazy", False)))
+    step, staged, batches, T = w["step"], w["staged"], w["batches"], w["T"]
     for i in range(3):
         step.load_blob(staged[i % nbatch])
         step.run()
@@ -489,19 +508,16 @@ def gather_probe(dev, B, nbatch=2, steps=20):
     rows = 4.0 * Bl * (1 + n) * D
     alg = rows + 4.0 * Bl * (1 + n) + 4.0 * (Bl + 1) + 3 * 4.0 * N * D + 4.0 * Bl * D + 4.0 * Bl * (1 + n)
     ach = alg / (ms * 1e-3) / 1e9
-    traffic, src = None, None
-    import glob
-
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"c3_b{B}_pmc.json")))
-    if files:
-        with open(files[-1]) as f:
-            rec = json.load(f).get("k_readout_wave")
-        if rec:
-            traffic, src = round(float(rec["hbm_bytes_per_launch"])), os.path.relpath(files[-1], ROOT)
+    traffic, src = load_kernel_traffic(f"{config}_b{B}" if B != cfg.get("batch", 32) else config, "k_readout_wave")
+    table_mb = T * D * 4 / 1e6
+    step.flush()
+    del w, step
+    torch.cuda.empty_cache()
     return {
         "bound": "hbm",
         "kernel": "k_readout_wave (mean readout + sampled scoring gather + listwise loss fwd/bwd)",
-        "workload": f"C3 model (d=128, 4 heads, LapPE), listwise with {n} negatives, B={Bl}, N={N} nodes",
+        "workload": f"{config.upper()} model (d=128, 4 heads, LapPE), listwise with {n} negatives, B={Bl}, N={N} nodes, "
+                    f"table {T} x {D} fp32 ({table_mb:.0f} MB)",
         "achieved": round(ach, 1),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
@@ -513,8 +529,27 @@ def gather_probe(dev, B, nbatch=2, steps=20):
         "scoring_row_bytes_per_launch": int(rows),
         "avg_launch_ms": round(ms, 5),
         "step_sessions_per_s": round(Bl / step_s, 1),
-        "note": "42 MB table sits in the 256 MB Infinity Cache; rows are algorithmic bytes",
+        "note": ("table larger than the 256 MB Infinity Cache: scoring rows are served from HBM" if table_mb > 256
+                 else "table sits in the 256 MB Infinity Cache: rows are algorithmic bytes, not HBM bytes"),
     }
+
+
+def load_kernel_traffic(name: str, kernel: str):
+    """Per-launch HBM bytes of one kernel from profiles/rNN/<name>_pmc.json, if that
+    profile was taken on these kernel sources."""
+    import glob
+
+    from etpgt.backend._lib import source_hash
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"{name}_pmc.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    rec = d.get(kernel)
+    if not rec or d.get("_source_hash") != source_hash():
+        return None, None
+    return round(float(rec["hbm_bytes_per_launch"])), os.path.relpath(files[-1], ROOT)
 
 
 def recall_parity(cfg, data, T, dev, steps, n_val, B=32):
@@ -581,6 +616,26 @@ def recall_parity(cfg, data, T, dev, steps, n_val, B=32):
     return out
 
 
+def _cpu_threads(step_fn, trial_s: float = 2.0) -> int:
+    """The faster of os.cpu_count() and the affinity-set size, by median step time."""
+    cands = sorted({os.cpu_count() or 1, len(os.sched_getaffinity(0))}, reverse=True)
+    if len(cands) == 1:
+        return cands[0]
+    best, best_t = cands[0], float("inf")
+    for th in cands:
+        torch.set_num_threads(th)
+        step_fn()
+        ts, end = [], time.perf_counter() + trial_s
+        while time.perf_counter() < end or len(ts) < 3:
+            t = time.perf_counter()
+            step_fn()
+            ts.append(time.perf_counter() - t)
+        med = float(np.median(ts))
+        if med < best_t:
+            best, best_t = th, med
+    return best
+
+
 def cpu_baseline(cfg, batches, T, seconds):
     """The reference CPU path (oracle restatement: PyG TransformerConv semantics,
     Python-loop mean readout, loss, torch AdamW) on the host cores, bounded sample."""
@@ -589,8 +644,6 @@ def cpu_baseline(cfg, batches, T, seconds):
 
     from etpgt.data.synthetic import random_pe_table
 
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
     torch.manual_seed(42)
     ref = R.ref_create_graph_transformer_optimized(T, embedding_dim=cfg["D"], hidden_dim=cfg["D"], num_layers=2,
                                                    num_heads=cfg["H"], dropout=0.1, use_laplacian_pe=cfg["K"] > 0,
@@ -600,6 +653,10 @@ def cpu_baseline(cfg, batches, T, seconds):
     ref.train()
     opt = torch.optim.AdamW(ref.parameters(), lr=1e-3, weight_decay=1e-5)
     rbs = [R.ref_batch_from(b) for b in batches]
+    # threads: every host core (os.cpu_count()) unless the cores this process
+    # may run on (its affinity set, e.g. a box's CPU share) train faster; short trial of each
+    threads = _cpu_threads(lambda: R.ref_train_step(ref, rbs[0], opt, cfg["loss"]))
+    torch.set_num_threads(threads)
     for i in range(3):
         R.ref_train_step(ref, rbs[i % len(rbs)], opt, cfg["loss"])
     times = []
@@ -625,6 +682,7 @@ def cpu_baseline(cfg, batches, T, seconds):
         "value": round(B / med, 1),
         "unit": "sessions/s",
         "cores": threads,
+        "host_cpus": os.cpu_count(),
         "kind": "port",
         "sample": f"{len(times)} training steps of B={B} ({len(times)*B} sessions, median step {med*1e3:.2f} ms) "
                   f"on the same pre-staged batches; oracle/etpgt_ref.py restatement, torch CPU, {cpu_model}",

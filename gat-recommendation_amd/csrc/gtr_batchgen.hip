@@ -27,6 +27,7 @@ using namespace gtr;
 
 #define BB_WAVES 4
 #define BB_BLOCK (64 * BB_WAVES)
+#define BB_NEG_ROUNDS (1u << 20)  // rejection rounds before a session is declared unsatisfiable
 #define BB_SCAN_BLOCK 1024
 #define BB_BMAX 16384  // sessions per batch (k_bb_scan keeps node_ptr in LDS)
 #define EMPTY_KEY 0xFFFFFFFFFFFFFFFFull
@@ -76,7 +77,7 @@ struct BBK {
   const uint64_t* slots;        // edge hash
   uint64_t mask;
   int32_t* scratch;             // [2 * b_cap]: edge offset, node offset per session
-  int32_t* status;              // [1]: 1 if the batch exceeded the capacities
+  int32_t* status;              // [2]: this batch's code (1 over capacity, 2 negatives unsatisfiable), sticky OR
   int32_t B, T, max_len, R, S, seed;
 };
 
@@ -215,6 +216,7 @@ __global__ __launch_bounds__(BB_SCAN_BLOCK) void k_bb_scan(BBK a) {
     hdr[0] = over ? 0 : N; hdr[1] = over ? 0 : B; hdr[2] = over ? 0 : E; hdr[3] = bt.n_neg;
     hdr[4] = over ? 0 : G; hdr[5] = R; hdr[6] = 0; hdr[7] = 0;
     a.status[0] = over ? 1 : 0;
+    if (over) a.status[1] |= 1;  // sticky over the batches built since the host cleared it
     *a.start = cur;
     *a.cursor = cur + B;
   }
@@ -311,17 +313,26 @@ __global__ __launch_bounds__(BB_BLOCK) void k_bb_write(BBK a) {
     }
   }
   if (lane == 0) const_cast<int32_t*>(bt.target)[b] = tgt;
-  // negatives: uniform in [1, T) rejecting the session's clicks, 64 candidates a round
+  // negatives: uniform in [1, T) rejecting the session's clicks, 64 candidates a round,
+  // rejected for as long as it takes (dataloader.py:107-124 loops until it has n).  Only a
+  // session holding (nearly) every catalog item could exhaust BB_NEG_ROUNDS rounds; the
+  // wave then stops (no GPU hang where the reference would spin forever) and flags
+  // status 2, which the host turns into an error.
   const int n = bt.n_neg;
   int32_t* negs = const_cast<int32_t*>(bt.negatives) + (size_t)b * n;
   int filled = 0;
   for (uint32_t round = 0; filled < n; ++round) {
+    if (round == BB_NEG_ROUNDS) {
+      if (lane == 0) {
+        __hip_atomic_store(a.status, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_or(a.status + 1, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      break;
+    }
     const uint32_t h = mix3((uint32_t)a.seed, (uint32_t)pos, round * 64u + (uint32_t)lane);
     const int cand = 1 + (int)(h % (uint32_t)(a.T - 1));
     bool seen = false;
-    if (round < 64) {
-      for (int i = 0; i < len; ++i) seen |= s_clk[w][i] == cand;
-    }
+    for (int i = 0; i < len; ++i) seen |= s_clk[w][i] == cand;
     const unsigned long long ok = __ballot(!seen);
     const int rk = __popcll(ok & ((1ull << lane) - 1ull));
     if (!seen && filled + rk < n) negs[filled + rk] = cand;

@@ -572,8 +572,7 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
     const int bk = g / GTR_PART_BUCKET, b0 = bk * GTR_PART_BUCKET;
     if (!arrive_last(a.cnt + 4 + 2 * bk, (uint32_t)min(GTR_PART_BUCKET, Gn - b0), s_flag)) return;
     float* row0 = a.bn_part + (size_t)b0 * PW;
-    bn_stats_from_parts<D, CONV_BLOCK>(row0, min(GTR_PART_BUCKET, Gn - b0), a.bn_eps, s_bn, s_bn + D, XO, red,
-                                       PW, row0);
+    bn_merge_parts<D, CONV_BLOCK>(row0, min(GTR_PART_BUCKET, Gn - b0), red, PW, row0);
     if (tid == 0) reset_counter(a.cnt + 4 + 2 * bk);
     if (!arrive_last(a.cnt, (uint32_t)nbk, s_flag)) return;
     bn_stats_from_parts<D, CONV_BLOCK>(a.bn_part, nbk, a.bn_eps, s_bn, s_bn + D, XO, red,

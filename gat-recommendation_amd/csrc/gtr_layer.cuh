@@ -118,14 +118,24 @@ __device__ __forceinline__ void store_vec(float* p, const float (&x)[VPL], bool 
   }
 }
 
-// Consumer-side BatchNorm statistics: combine G per-group (count, mean, M2) partials
-// (layout [G][1+2D]) into mean / rstd / unbiased var.  BLK/D slices of the groups are
-// folded in parallel (Chan's parallel-variance formula), then combined in fixed order
-// (deterministic).  scr: >= 2*BLK + D floats of LDS.  Call with the whole block.
+// Combine G per-group (count, mean, M2) partials (rows `rstride` floats apart) in
+// fixed order (deterministic): BLK/D slices of the groups are folded in parallel (Chan's
+// parallel-variance formula), then the slices are combined.  Two uses, one helper each
+// below, so that the modes cannot be mixed at a call site:
+//   bn_stats_from_parts  -> mean / rstd / unbiased var in LDS (s_mean, s_rstd, s_uvar);
+//   bn_merge_parts       -> ONE merged (count, mean, M2) row written to `merged`, which
+//                           may alias the first partial row (every read of the partials
+//                           completes before the internal __syncthreads that precedes
+//                           the write); s_mean / s_rstd / s_uvar are not written.
+// After a forward with more than GTR_PART_BUCKET row groups (the last-arriver mode,
+// consumer_reduce = 0), gtr_layer.bn_part row b*GTR_PART_BUCKET therefore holds bucket
+// b's MERGED row, not group b*GTR_PART_BUCKET's partial: nothing may re-read bn_part
+// as per-group partials after such a forward.
+// scr: >= 2*BLK + D floats of LDS.  Call with the whole block.
 template <int D, int BLK>
-__device__ __forceinline__ void bn_stats_from_parts(const float* part, int G, float eps, float* s_mean,
-                                                    float* s_rstd, float* s_uvar, float* scr,
-                                                    size_t rstride = 1 + 2 * D, float* merged = nullptr) {
+__device__ __forceinline__ void bn_fold_parts_(const float* part, int G, float eps, float* s_mean,
+                                               float* s_rstd, float* s_uvar, float* scr, size_t rstride,
+                                               float* merged) {
   constexpr int NSL = BLK / D >= 1 ? BLK / D : 1;
   const int tid = threadIdx.x;
   const int j = tid % D, sl = tid / D;
@@ -178,6 +188,19 @@ __device__ __forceinline__ void bn_stats_from_parts(const float* part, int G, fl
     }
   }
   __syncthreads();
+}
+
+template <int D, int BLK>
+__device__ __forceinline__ void bn_stats_from_parts(const float* part, int G, float eps, float* s_mean,
+                                                    float* s_rstd, float* s_uvar, float* scr,
+                                                    size_t rstride = 1 + 2 * D) {
+  bn_fold_parts_<D, BLK>(part, G, eps, s_mean, s_rstd, s_uvar, scr, rstride, nullptr);
+}
+
+template <int D, int BLK>
+__device__ __forceinline__ void bn_merge_parts(const float* part, int G, float* scr, size_t rstride,
+                                               float* merged) {
+  bn_fold_parts_<D, BLK>(part, G, 0.0f, nullptr, nullptr, nullptr, scr, rstride, merged);
 }
 
 // Row groups whose partials one last-arriving workgroup combines; past that the groups

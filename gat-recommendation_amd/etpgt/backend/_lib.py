@@ -88,6 +88,7 @@ class GtrTail(C.Structure):
 
 
 SWEEP_SLOTS = 8
+ABI_VERSION = 2  # GTR_ABI_VERSION of include/gtr.h
 
 
 class GtrLazy(C.Structure):
@@ -185,10 +186,26 @@ def lib():
             fn = getattr(h, name)
             fn.restype = res
             fn.argtypes = args
-        if h.gtr_abi_version() != 1:
+        if h.gtr_abi_version() != ABI_VERSION:
             raise RuntimeError("libgtr_hip.so ABI version mismatch")
         _lib = h
     return _lib
+
+
+def source_hash() -> str:
+    """Hash of the library's sources (csrc/*.hip, *.cuh, include/gtr.h).  Profiles
+    record it, so a measurement taken on other kernels is recognisable as stale."""
+    import glob
+    import hashlib
+
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(PKG_ROOT, "csrc", "*.hip")) + glob.glob(os.path.join(PKG_ROOT, "csrc", "*.cuh"))
+                   + [os.path.join(os.path.dirname(PKG_ROOT), "include", "gtr.h")])
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def check(status: int, what: str = "") -> None:

@@ -389,6 +389,12 @@ class Engine:
 
     # ------------------------------------------------------------------ batches
     def prepare(self, batch) -> tuple[Caps, torch.Tensor, torch.Tensor | None]:
+        from etpgt.data.gpu_batch import DeviceBatch
+
+        if isinstance(batch, DeviceBatch):  # built on the device: ids checked by the builder
+            if batch.blob.device != self.device:
+                raise ValueError("device-built batch lives on another device than the model")
+            return batch.caps, batch.blob, None
         if not isinstance(batch, SessionBatch):
             batch = SessionBatch(batch.x, batch.edge_index, getattr(batch, "batch", None),
                                  getattr(batch, "target_item", None), getattr(batch, "negative_items", None),

@@ -298,3 +298,27 @@ def collate_sessions(items: list[dict]) -> SessionBatch:
         torch.from_numpy(np.concatenate(ng)) if ng else None,
         num_graphs=len(items),
     )
+
+
+class Data:
+    """PyG ``torch_geometric.data.Data`` duck type for the graph-level call sites that
+    need one (``LaplacianPECached.precompute(Data(edge_index=..., num_nodes=...))``,
+    reference train_baseline.py:236-243): keyword attributes, ``num_nodes`` inferred
+    from ``x`` or ``edge_index`` when not given."""
+
+    def __init__(self, x=None, edge_index=None, num_nodes: int | None = None, **kwargs):
+        self.x = x
+        self.edge_index = edge_index
+        self._num_nodes = num_nodes
+        for k, v in kwargs.items():
+            setattr(self, k, v)
+
+    @property
+    def num_nodes(self) -> int:
+        if self._num_nodes is not None:
+            return int(self._num_nodes)
+        if self.x is not None:
+            return int(self.x.shape[0])
+        if self.edge_index is not None and self.edge_index.numel():
+            return int(self.edge_index.max()) + 1
+        return 0

@@ -98,7 +98,9 @@ class GpuBatchBuilder:
         dev = store.device
         self.cursor = torch.zeros(1, dtype=torch.int64, device=dev)
         self.start = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.status = torch.zeros(1, dtype=torch.int32, device=dev)
+        # [this batch's code, sticky OR since the last check_status()] (gtr_build_batch)
+        self.status = torch.zeros(2, dtype=torch.int32, device=dev)
+        self.pos = 0  # host mirror of the device cursor
         self.scratch = None
         self.order_h = np.arange(store.S, dtype=np.int64)
         self.order_d = torch.from_numpy(self.order_h.astype(np.int32)).to(dev)
@@ -111,6 +113,7 @@ class GpuBatchBuilder:
         self.order_h = o
         self.order_d = torch.from_numpy(o.astype(np.int32)).to(self.store.device)
         self.cursor.fill_(int(position))
+        self.pos = int(position)
 
     def batch_sizes(self, num_batches: int, position: int = 0) -> tuple[np.ndarray, np.ndarray]:
         """(N, E) of the next ``num_batches`` batches from ``position`` (host, from the counts)."""
@@ -125,24 +128,104 @@ class GpuBatchBuilder:
         N, E = self.batch_sizes(num_batches, position)
         return Caps.bucket(int(N.max()), self.B, max(int(E.max()), 1), self.n_neg)
 
-    def launch(self, bs: L.GtrBatch, caps: Caps, stream: int) -> None:
-        """Build the next batch into the batch image ``bs`` (capacities ``caps``)."""
+    def launch(self, bs: L.GtrBatch, caps: Caps, stream: int, B: int | None = None) -> None:
+        """Build the next batch (``B`` sessions, default the builder's batch size) into the
+        batch image ``bs`` (capacities ``caps``)."""
+        B = self.B if B is None else int(B)
+        if not 0 < B <= caps.b_cap:
+            raise ValueError(f"batch of {B} sessions does not fit b_cap {caps.b_cap}")
         if self.scratch is None or self.scratch.numel() < 2 * caps.b_cap:
             self.scratch = torch.zeros(2 * caps.b_cap, dtype=torch.int32, device=self.store.device)
         st = self.store
         L.check(L.lib().gtr_build_batch(C.byref(st.ss), st.slots.data_ptr(), st.num_slots, st.max_len,
-                                        self.order_d.data_ptr(), self.cursor.data_ptr(), self.B, caps.R,
+                                        self.order_d.data_ptr(), self.cursor.data_ptr(), B, caps.R,
                                         self.seed, C.byref(bs), self.scratch.data_ptr(), self.start.data_ptr(),
                                         self.status.data_ptr(), stream), "build_batch")
+        self.pos += B
 
-    def build(self, caps: Caps | None = None) -> tuple[Caps, torch.Tensor]:
+    def check_status(self) -> None:
+        """Raise if any batch built since the last check failed (host sync)."""
+        code = int(self.status[1].item())
+        self.status.zero_()
+        if code & 2:
+            raise RuntimeError("negative sampling: a session holds (nearly) every catalog item, so no "
+                               "negative outside it exists (the reference would loop forever)")
+        if code & 1:
+            raise RuntimeError("GPU batch exceeded its capacities")
+
+    def build(self, caps: Caps | None = None, B: int | None = None) -> tuple[Caps, torch.Tensor]:
         """Build the next batch into a fresh blob (eager; tests and tools)."""
         from etpgt.backend.engine import Engine
 
-        caps = caps or self.plan_caps(1, int(self.cursor.item()))
+        B = self.B if B is None else int(B)
+        if caps is None:
+            N, E = self._sizes_at(self.pos, B)
+            caps = Caps.bucket(N, B, max(E, 1), self.n_neg)
         blob = torch.zeros(blob_layout(caps)["_total"], dtype=torch.int32, device=self.store.device)
         bs = Engine.batch_struct(caps, blob)
-        self.launch(bs, caps, torch.cuda.current_stream(self.store.device).cuda_stream)
-        if int(self.status.item()) != 0:
-            raise RuntimeError("GPU batch exceeded its capacities")
+        self.launch(bs, caps, torch.cuda.current_stream(self.store.device).cuda_stream, B)
+        self.check_status()
         return caps, blob
+
+    def _sizes_at(self, position: int, B: int) -> tuple[int, int]:
+        sess = self.order_h[(position + np.arange(B)) % self.order_h.size]
+        return int(self.store.nodes[sess].sum()), int(self.store.edges[sess].sum())
+
+    def build_device_batch(self, B: int | None = None) -> "DeviceBatch":
+        """The next batch as a PyG-Batch-like object whose index arrays live in HBM."""
+        B = self.B if B is None else int(B)
+        N, _ = self._sizes_at(self.pos, B)
+        caps, blob = self.build(None, B)
+        return DeviceBatch(caps, blob, N, B, self.n_neg)
+
+
+class DeviceBatch:
+    """A batch built on the device (``GpuBatchBuilder``): the packed image plus the PyG
+    ``Batch`` fields the model / Trainer read (``x``, ``target_item``,
+    ``negative_items``, ``num_graphs``), as views into the image (int32 -> int64)."""
+
+    laplacian_pe = None
+
+    def __init__(self, caps: Caps, blob: torch.Tensor, num_nodes: int, num_graphs: int, n_neg: int):
+        self.caps, self.blob = caps, blob
+        self._N, self._B, self._n = int(num_nodes), int(num_graphs), int(n_neg)
+        self._lay = blob_layout(caps)
+
+    def _view(self, name: str, count: int) -> torch.Tensor:
+        o, _ = self._lay[name]
+        return self.blob[o: o + count].long()
+
+    @property
+    def num_graphs(self) -> int:
+        return self._B
+
+    @property
+    def num_nodes(self) -> int:
+        return self._N
+
+    @property
+    def x(self) -> torch.Tensor:
+        return self._view("node_item", self._N)
+
+    @property
+    def target_item(self) -> torch.Tensor:
+        return self._view("target", self._B)
+
+    @property
+    def negative_items(self) -> torch.Tensor:
+        return self._view("negatives", self._B * self._n)
+
+    @property
+    def ptr(self) -> torch.Tensor:
+        return self._view("node_ptr", self._B + 1)
+
+    @property
+    def batch(self) -> torch.Tensor:
+        p = self.ptr
+        return torch.repeat_interleave(torch.arange(self._B, device=p.device), p[1:] - p[:-1])
+
+    def to(self, device, non_blocking: bool = False) -> "DeviceBatch":
+        d = torch.device(device)
+        if d.type != self.blob.device.type or (d.index is not None and d.index != self.blob.device.index):
+            raise ValueError("a device-built batch stays on the device it was built on")
+        return self

@@ -101,11 +101,23 @@ class Recommender:
             raise ValueError("session_items must not be empty.")
         batch = self._build_session_graph(request.session_items)
         se = self.model(batch.to(self.device))  # [1, hidden_dim]
-        excl = sorted(set(int(v) for v in request.session_items) | {0})
-        if request.k > self.num_items - len(excl):
+        excl = sorted(set(int(v) for v in request.session_items if 0 <= int(v) < self.num_items) | {0})
+        k = int(request.k)
+        if k > self.num_items:
             raise RuntimeError("selected index k out of range")
-        idx, sc = score_topk(se, self.item_embeddings, int(request.k), exclude=[excl])
-        return [int(v) for v in idx[0].tolist()], [float(v) for v in sc[0].tolist()]
+        # the reference scores excluded items -inf and takes torch.topk over all T, so a k
+        # past the unmasked count (validation clamps k to num_items - 1 only) returns the
+        # masked ids after every finite score.  torch.topk leaves the order among equal
+        # -inf scores unspecified; they come back here in ascending id order.
+        live = min(k, self.num_items - len(excl))
+        idx, sc = (score_topk(se, self.item_embeddings, live, exclude=[excl]) if live > 0
+                   else (torch.empty(1, 0, dtype=torch.int64), torch.empty(1, 0)))
+        ids = [int(v) for v in idx[0].tolist()]
+        scores = [float(v) for v in sc[0].tolist()]
+        if k > live:
+            ids += excl[: k - live]
+            scores += [float("-inf")] * (k - live)
+        return ids, scores
 
     def health(self) -> dict:
         return {

@@ -117,7 +117,73 @@ def collate_fn(batch: list[dict]) -> SessionBatch:
 
 def create_dataloader(sessions_path: Path | str, graph_edges_path: Path | str, batch_size: int = 32,
                       num_negatives: int = 5, max_session_length: int = 50, shuffle: bool = True,
-                      num_workers: int = 0) -> torch.utils.data.DataLoader:
+                      num_workers: int = 0, device_builder: bool = False, device: str = "cuda",
+                      seed: int = 0):
+    """dataloader.py:205-241.  ``device_builder=True`` returns a ``DeviceSessionLoader``:
+    the same epochs (order, batch sizes, last partial batch) built on the GPU
+    (etpgt.data.gpu_batch) instead of host workers; ``Trainer`` then captures the build
+    inside the fused step."""
     ds = SessionDataset(sessions_path, graph_edges_path, num_negatives, max_session_length)
+    if device_builder:
+        return DeviceSessionLoader(ds, batch_size, num_negatives, shuffle=shuffle, device=device, seed=seed)
     return torch.utils.data.DataLoader(ds, batch_size=batch_size, shuffle=shuffle, num_workers=num_workers,
                                        collate_fn=collate_fn)
+
+
+class DeviceSessionLoader:
+    """The epochs of ``DataLoader(SessionDataset, batch_size, shuffle, collate_fn)`` with
+    every batch built on the GPU.
+
+    * Order: ``shuffle=True`` draws each epoch's permutation exactly as the DataLoader's
+      ``RandomSampler`` does (a generator seeded from the global torch RNG, then
+      ``torch.randperm``), so a run seeded like the reference visits sessions in the
+      reference's order; ``shuffle=False`` walks session-id order.
+    * Batches: ``len(loader)`` = ceil(S / batch_size), the last one partial
+      (``drop_last=False``).
+    * Per session: the reference's example (last ``max_session_length`` clicks, target,
+      sorted unique context, induced directed edges) bit for bit; negatives uniform in
+      [1, T) rejecting the session's clicks, from the device's counter-based stream keyed
+      by (seed, epoch * S + position) instead of ``torch.randint`` (same distribution,
+      fresh every epoch).
+    Iterating yields ``DeviceBatch`` objects (PyG-Batch-like views of HBM images) for any
+    consumer; ``Trainer``'s fused step instead attaches ``builder`` and builds inside its
+    captured graph."""
+
+    def __init__(self, dataset: SessionDataset, batch_size: int, num_negatives: int, shuffle: bool = True,
+                 device: str = "cuda", seed: int = 0):
+        from etpgt.data.gpu_batch import GpuBatchBuilder, GpuSessionStore
+
+        self.dataset = dataset
+        self.batch_size = int(batch_size)
+        self.shuffle = bool(shuffle)
+        self.store = GpuSessionStore.from_dataset(dataset, device)
+        self.builder = GpuBatchBuilder(self.store, self.batch_size, num_negatives, seed=seed)
+        self.epoch = -1
+        self.order = None
+
+    def __len__(self) -> int:
+        return -(-len(self.dataset) // self.batch_size)
+
+    def batch_sizes(self) -> list[int]:
+        S, B = len(self.dataset), self.batch_size
+        return [min(B, S - i * B) for i in range(len(self))]
+
+    def _epoch_order(self) -> np.ndarray:
+        n = len(self.dataset)
+        if not self.shuffle:
+            return np.arange(n, dtype=np.int64)
+        seed = int(torch.empty((), dtype=torch.int64).random_().item())  # RandomSampler.__iter__
+        g = torch.Generator()
+        g.manual_seed(seed)
+        return torch.randperm(n, generator=g).numpy().astype(np.int64)
+
+    def start_epoch(self) -> None:
+        """Draw the next epoch's order and put the builder at its start."""
+        self.epoch += 1
+        self.order = self._epoch_order()
+        self.builder.set_epoch_order(self.order, position=self.epoch * len(self.dataset))
+
+    def __iter__(self):
+        self.start_epoch()
+        for b in self.batch_sizes():
+            yield self.builder.build_device_batch(b)

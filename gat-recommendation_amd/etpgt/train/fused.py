@@ -59,6 +59,7 @@ class FusedTrainStep:
             raise ValueError("sync_bn needs the data-parallel step")
         self.dp = None
         self.graph_b = None
+        self._coll_capture_refused = False  # set once if the transport refuses stream capture
         eng = self.eng
         T, D = eng.T, eng.D
         self.adam = L.GtrAdam()
@@ -89,6 +90,7 @@ class FusedTrainStep:
         self.caps = None
         self.graph = None
         self.builder = None
+        self._builder_B = None  # sessions of the device-built batch (None: the builder's B)
         if caps is not None:
             self._bind(caps)
 
@@ -321,7 +323,7 @@ class FusedTrainStep:
         eng = self.eng
         lib = L.lib()
         if self.builder is not None:
-            self.builder.launch(bs, self.caps, st)
+            self.builder.launch(bs, self.caps, st, self._builder_B)
         if self.lazy:
             L.check(lib.gtr_step_begin_lazy(C.byref(bs), eng.T, eng.D, self.keys.data_ptr(), self.vals.data_ptr(),
                                             self.skeys.data_ptr(), self.svals.data_ptr(), self.stamp.data_ptr(),
@@ -451,7 +453,7 @@ class FusedTrainStep:
         host memory -- and off with GTR_GRAPH_COLL=0."""
         if self.dp is None or self.world <= 1 and os.environ.get("GTR_GRAPH_COLL") != "1":
             return False
-        if os.environ.get("GTR_GRAPH_COLL", "1") == "0":
+        if os.environ.get("GTR_GRAPH_COLL", "1") == "0" or self._coll_capture_refused:
             return False
         import torch.distributed as dist
 
@@ -548,18 +550,39 @@ class FusedTrainStep:
         return self.ws.loss_out[0]
 
     def _capture_pieces(self, with_pe: bool):
-        try:
+        if not self._graph_collectives():
             return [(self._capture(launch), coll) for launch, coll in self._graph_pieces(with_pe)]
+        graphs, err = None, None
+        try:
+            graphs = [(self._capture(launch), coll) for launch, coll in self._graph_pieces(with_pe)]
         except RuntimeError as e:
-            if not self._graph_collectives():
+            if "captur" not in str(e).lower():
                 raise
-            # a transport that refuses capture: keep the collectives between graph pieces
+            err = e
+            torch.cuda.synchronize(self.dev)
+        # a transport that refuses stream capture: keep the collectives between graph pieces,
+        # for this step object only -- and on every rank, so the ranks agree first (every
+        # rank reaches this all-reduce whether its own capture succeeded or not)
+        if self._ranks_agree_refused(err is not None):
             import warnings
 
-            warnings.warn(f"capturing the collectives failed ({e}); falling back to one graph per piece")
-            torch.cuda.synchronize(self.dev)
-            os.environ["GTR_GRAPH_COLL"] = "0"
-            return [(self._capture(launch), coll) for launch, coll in self._graph_pieces(with_pe)]
+            self._coll_capture_refused = True
+            warnings.warn(f"capturing the collectives failed ({err or 'on another rank'}); "
+                          "falling back to one graph per piece")
+            graphs = [(self._capture(launch), coll) for launch, coll in self._graph_pieces(with_pe)]
+        return graphs
+
+    def _ranks_agree_refused(self, refused: bool) -> bool:
+        """True if any rank's capture of the collectives was refused (MAX all-reduce,
+        outside any capture)."""
+        import torch.distributed as dist
+
+        if not (dist.is_available() and dist.is_initialized()) or self.world <= 1:
+            return refused
+        dev = self.dev if dist.get_backend(self.group) != "gloo" else "cpu"
+        t = torch.tensor([int(refused)], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return bool(t.item())
 
     def capture(self, with_pe: bool = False):
         """Capture the step's pieces into hipGraphs (after one eager warm-up step): the
@@ -571,7 +594,20 @@ class FusedTrainStep:
             self.graph = graphs
         return graphs
 
-    def run(self, with_pe: bool = False):
+    def run_partial(self, B: int):
+        """One step whose device-built batch holds ``B`` sessions instead of the builder's
+        batch size (the last, partial batch of an epoch, as a DataLoader with
+        drop_last=False yields it): launched eagerly, the captured graph keeps the full
+        batch size."""
+        if self.builder is None:
+            raise RuntimeError("run_partial needs a device batch builder (attach_builder)")
+        self._builder_B = int(B)
+        try:
+            return self.run(eager=True)
+        finally:
+            self._builder_B = None
+
+    def run(self, with_pe: bool = False, eager: bool = False):
         """One training step over the batch currently in the device blob."""
         self.eng.check_intact()
         if not self.model.training:
@@ -581,7 +617,7 @@ class FusedTrainStep:
                 self._lazy_alloc(2 * self.lz.cap)
             self._host_steps += 1
             self._dirty = True
-        if self.use_graph:
+        if self.use_graph and not eager:
             graphs = self.graph_pe if with_pe else self.graph
             if graphs is None:
                 self._launch(with_pe)  # eager warm-up (first touch of every code path)

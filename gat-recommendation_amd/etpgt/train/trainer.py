@@ -97,9 +97,34 @@ class Trainer:
             self._fused.export_optimizer_state(self.optimizer)
 
     # ------------------------------------------------------------------ loops
+    def _train_epoch_device_batches(self, fused) -> float:
+        """One epoch of a ``DeviceSessionLoader`` through the fused step: the batch build
+        runs inside the captured step (no host work per batch); the partial last batch is
+        launched eagerly."""
+        loader = self.train_loader
+        loader.start_epoch()
+        sizes = loader.batch_sizes()
+        bld = loader.builder
+        if fused.builder is not bld:
+            fused.attach_builder(bld, num_batches=len(sizes))
+        else:  # capacities for this epoch's order (rebinds only if they grew)
+            caps = bld.plan_caps(len(sizes), bld.pos)
+            if not fused.caps.fits(caps.n_cap, caps.b_cap, caps.e_cap, caps.n_neg):
+                fused.attach_builder(bld, num_batches=len(sizes))
+        total = torch.zeros((), dtype=torch.float64, device=self.device)
+        for b in sizes:
+            loss = fused.run() if b == loader.batch_size else fused.run_partial(b)
+            total += loss
+        bld.check_status()
+        return float(total.item()) / max(len(sizes), 1)
+
     def train_epoch(self) -> float:
         self.model.train()
         fused = self._fused_step()
+        from etpgt.train.dataloader import DeviceSessionLoader
+
+        if fused is not None and isinstance(self.train_loader, DeviceSessionLoader):
+            return self._train_epoch_device_batches(fused)
         total = torch.zeros((), dtype=torch.float64, device=self.device)
         num_batches = 0
         for batch in self.train_loader:

@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GTR_ABI_VERSION 1
+#define GTR_ABI_VERSION 2 /* 2: gtr_layer.cnt holds 4 + 2*ceil(groups/32) counters */
 
 #define GTR_OK 0
 #define GTR_E_ARG 1001      /* bad argument / unsupported shape */
@@ -135,7 +135,10 @@ typedef struct gtr_layer {
   float* gate;     /* [n_cap]     beta gate                         */
   float* out;      /* [n_cap, D]  conv output (pre BatchNorm)        */
   float* bn_stats; /* [2D] batch mean, rstd                         */
-  float* bn_part;  /* [g_cap, 1+2D] forward partials                 */
+  float* bn_part;  /* [g_cap, 1+2D] forward (count, mean, M2) partials per row group.
+                      consumer_reduce = 0 with > 32 row groups: the forward's bucket
+                      mergers overwrite row 32*b with bucket b's merged row, so after
+                      such a forward bn_part is NOT per-group partials any more      */
   float* bn_gsum;  /* [2D] sum(dy), sum(dy*xhat)                     */
   float* bn_gpart; /* [max(g_cap, 256), 2D] backward partials         */
   uint32_t* cnt;   /* [4 + 2*ceil(groups/32)] arrival counters (zero-initialised once;
@@ -444,7 +447,10 @@ int gtr_session_counts(const gtr_sessions* ss, const uint64_t* slots, int64_t nu
                        int32_t* nodes, int32_t* edges, gtr_stream_t stream);
 /* One batch of the B sessions order[(*cursor + b) % S] into *out (device blob arrays;
  * hdr sizes live), then *cursor += B.  scratch: [2 * b_cap] int32; start: [1] int64;
- * status[0] = 1 (and an empty header) if the batch exceeds out's capacities.
+ * status [2]: status[0] = this batch's code -- 1 (and an empty header) if the batch exceeds
+ * out's capacities, 2 if a session leaves no item to sample negatives from (it holds
+ * nearly the whole catalog: the reference would reject forever); status[1] |= each code
+ * (sticky until the caller clears it).
  * row_group = the layer kernels' R for out's n_cap.  B <= 16384, max_len <= 64.        */
 int gtr_build_batch(const gtr_sessions* ss, const uint64_t* slots, int64_t num_slots, int max_len,
                     const int32_t* order, int64_t* cursor, int B, int row_group, uint32_t seed,

@@ -51,11 +51,15 @@ def negatives(seed: int, pos: int, clicks: np.ndarray, n: int, T: int) -> np.nda
     seen = set(int(v) for v in clicks)
     out = []
     rnd = 0
-    while len(out) < n:
+    if len(seen & set(range(1, T))) == T - 1:  # nothing to find: the device builder gives up
+        raise RuntimeError("negative sampling: the session covers the whole catalog")
+    while len(out) < n:  # rejection until n are found (dataloader.py:107-124)
+        if rnd == 1 << 20:
+            raise RuntimeError("negative sampling: the session covers (nearly) the whole catalog")
         h = mix3(seed, pos, rnd * 64 + np.arange(64, dtype=np.uint64))
         cand = 1 + (h % np.uint64(T - 1)).astype(np.int64)
         for c in cand:
-            if rnd >= 64 or int(c) not in seen:
+            if int(c) not in seen:
                 out.append(int(c))
                 if len(out) == n:
                     break

@@ -90,7 +90,11 @@ class RefTransformerConv(nn.Module):
         src, dst = edge_index[0], edge_index[1]  # flow source_to_target
         alpha = (q[dst] * k[src]).sum(dim=-1) / math.sqrt(C)  # [E, H]
         alpha = pyg_softmax(alpha, dst, N)
-        alpha = F.dropout(alpha, p=self.dropout, training=self.training)
+        mask = getattr(self, "attn_mask", None)
+        if mask is not None and self.training:  # injected mask (hip_dropout_masks), else torch's RNG
+            alpha = alpha * mask
+        else:
+            alpha = F.dropout(alpha, p=self.dropout, training=self.training)
         msg = v[src] * alpha.view(-1, H, 1)
         out = torch.zeros((N, H, C), dtype=x.dtype).index_add(0, dst, msg)
         out = out.view(-1, H * C)
@@ -276,9 +280,15 @@ class RefGraphTransformer(nn.Module):
                 r = x
                 x = ffn(x) + r
         else:
-            for conv, bn in zip(self.convs, self.batch_norms):
+            masks = getattr(self, "drop_masks", None) if self.training else None
+            for l, (conv, bn) in enumerate(zip(self.convs, self.batch_norms)):
                 r = x
-                x = self.dropout_layer(bn(conv(x, edge_index)) + r)
+                if masks is not None:
+                    conv.attn_mask = masks["attn"][l]
+                    x = (bn(conv(x, edge_index)) + r) * masks["out"][l]
+                    conv.attn_mask = None
+                else:
+                    x = self.dropout_layer(bn(conv(x, edge_index)) + r)
         return self.readout(x, batch.batch)
 
     def get_item_embeddings(self) -> torch.Tensor:
@@ -301,6 +311,67 @@ def ref_create_graph_transformer_optimized(num_items, **kw) -> RefGraphTransform
     )
     d.update(kw)
     return RefGraphTransformer(num_items, **d)
+
+
+# --------------------------------------------------------------------------------------
+# The HIP path's dropout stream, restated so that the oracle can apply the SAME masks
+# (value-level parity at p > 0; torch's CPU generator cannot be reproduced on the device)
+# --------------------------------------------------------------------------------------
+
+_M32 = np.uint64(0xFFFFFFFF)
+
+
+def _u32(x):
+    return np.asarray(x, np.uint64) & _M32
+
+
+def hip_mix3(a, b, c) -> np.ndarray:
+    """gtr_common.cuh ``mix3`` (32-bit wrap-around arithmetic) over numpy arrays."""
+    a, b, c = _u32(a), _u32(b), _u32(c)
+    h = (a * np.uint64(0x9E3779B1)) & _M32
+    h ^= (b + np.uint64(0x7F4A7C15) + ((h << np.uint64(6)) & _M32) + (h >> np.uint64(2))) & _M32
+    h = (h * np.uint64(0x85EBCA77)) & _M32
+    h ^= (c * np.uint64(0xC2B2AE3D)) & _M32
+    h ^= h >> np.uint64(16)
+    h = (h * np.uint64(0x7FEB352D)) & _M32
+    h ^= h >> np.uint64(15)
+    h = (h * np.uint64(0x846CA68B)) & _M32
+    h ^= h >> np.uint64(16)
+    return h
+
+
+def hip_drop_stream(kind: int, layer: int, ctr: int) -> int:
+    """gtr_common.cuh ``drop_stream``: kind 0 = attention probabilities of a layer,
+    kind 1 = the layer's output (BN + residual)."""
+    return int(((kind << 28) ^ (layer << 20) ^ ((ctr * 0x632BE5AB) & 0xFFFFFFFF)) & 0xFFFFFFFF)
+
+
+def hip_dropout_masks(seed: int, ctr: int, p: float, num_layers: int, edge_index, num_nodes: int, dim: int,
+                      heads: int) -> dict:
+    """The masks (0 or 1/(1-p)) the HIP step applies at dropout ``p`` with stream counter
+    ``ctr``: {"attn": [L] x [E, H] in edge_index order, "out": [L] x [N, D]}.
+
+    Element indices follow the kernels: attention (edge, head) pairs are numbered in the
+    packed batch's destination order (a stable sort of edge_index by destination,
+    etpgt/data/batch.py build_csr) as e*H + h; output elements as row*D + j.  Keep iff
+    mix3(seed, stream, idx) >= uint32(p * 2^32) (p as the fp32 config value)."""
+    pf = float(np.float32(p))
+    thresh = np.uint64(int(pf * 4294967296.0))
+    scale = float(np.float32(1.0 / (1.0 - pf)))
+    dst = np.asarray(edge_index[1], np.int64)
+    E = dst.shape[0]
+    order = np.argsort(dst, kind="stable")
+    pos = np.empty(E, np.int64)
+    pos[order] = np.arange(E)
+    idx_attn = pos[:, None] * heads + np.arange(heads)[None, :]
+    idx_out = np.arange(num_nodes * dim, dtype=np.int64).reshape(num_nodes, dim)
+    out = {"attn": [], "out": []}
+    for l in range(num_layers):
+        ha = hip_mix3(seed, hip_drop_stream(0, l, ctr), idx_attn)
+        ho = hip_mix3(seed, hip_drop_stream(1, l, ctr), idx_out)
+        out["attn"].append(torch.from_numpy(np.where(ha >= thresh, scale, 0.0).astype(np.float32)))
+        out["out"].append(torch.from_numpy(np.where(ho >= thresh, scale, 0.0).astype(np.float32)))
+    return out
 
 
 # --------------------------------------------------------------------------------------

@@ -4,6 +4,7 @@ passes (counter_collection.csv), with the gfx950 correction of
 /opt/skills/guides/MI355X_MICROARCH.md §HBM: FETCH_SIZE reports half the bytes of a
 wide streaming read -> doubled.  Prints JSON {kernel: {...}}."""
 import csv
+import os
 import re
 import glob
 import json
@@ -53,6 +54,12 @@ def main():
         tot = sum(v["hbm_bytes_per_launch"] * v["dispatches"] for k, v in out.items()
                   if k.startswith("k_") or k.startswith("__amd_rocclr_copyBuffer"))
         out["_per_step"] = {"steps": steps, "hbm_bytes_per_step": tot / steps}
+    # the kernels these counters belong to: bench.py ignores a profile whose sources differ
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "gat-recommendation_amd"))
+    from etpgt.backend._lib import source_hash
+
+    out["_source_hash"] = source_hash()
     print(json.dumps(out, indent=1))
 
 

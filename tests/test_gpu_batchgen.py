@@ -108,3 +108,27 @@ def test_fused_step_with_device_builder_equals_host_batches(use_graph):
         l2 = float(f2(collate_sessions(ex)))
         assert l1 == l2, (k, l1, l2)
     assert torch.equal(m1.item_embedding.weight, m2.item_embedding.weight)
+
+
+def test_negatives_reject_until_found_and_unsatisfiable_session_raises():
+    """Negative sampling rejects session items for as long as it takes
+    (dataloader.py:107-124), beyond the 64 rounds of the earlier builder: a session holding
+    all but one catalog item gets that item n times, exactly as the oracle restatement.
+    A session holding every item has no negative at all -- the reference would spin
+    forever; the builder stops and the host raises."""
+    T = 8  # items 1..7
+    ptr = np.array([0, 7, 14])
+    items = np.array([1, 2, 3, 4, 5, 6, 2, 1, 2, 3, 4, 5, 6, 7])  # session 1 holds all of 1..7
+    keys = np.array([1 * T + 2, 2 * T + 3])
+    store = GpuSessionStore(ptr, items, keys, T, "cuda")
+    bld = GpuBatchBuilder(store, 1, 6, seed=4)
+    bld.set_epoch_order(np.array([0, 1]))
+    caps = bld.plan_caps(1, 0)
+    _, blob = bld.build(caps)
+    ex = BR.build_batch(ptr, items, keys, T, np.array([0, 1]), 0, 1, 50, 6, 4)
+    assert ex[0]["negative_items"].tolist() == [7] * 6
+    assert np.array_equal(blob.cpu().numpy(), collate_sessions(ex).packed(caps)[1])
+    with pytest.raises(RuntimeError, match="negative sampling"):
+        bld.build(caps)
+    with pytest.raises(RuntimeError, match="negative sampling"):
+        BR.build_batch(ptr, items, keys, T, np.array([0, 1]), 1, 1, 50, 6, 4)

@@ -293,3 +293,58 @@ def test_dp_rccl_world1_graph_captured_collectives():
     for l1, l2 in out:
         assert abs(l1 - l2) <= 1e-6 * max(1.0, abs(l1))
     assert diff <= 1e-6
+
+
+def _refuse_worker(port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GTR_GRAPH_COLL="1")
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        data = small_data()
+        T = data.table_rows
+        m1, _ = make_pair(T, D, H, K=0, seed=31)
+        m2 = copy.deepcopy(m1)
+        m1.train(); m2.train()
+        f1 = FusedTrainStep(m1, lr=1e-2, weight_decay=1e-2, loss="bpr", data_parallel=True, lagged=True)
+        f2 = FusedTrainStep(m2, lr=1e-2, weight_decay=1e-2, loss="bpr", data_parallel=True, lagged=True)
+        real = f2._capture
+        calls = {"n": 0}
+
+        def refuse_once(fn):
+            calls["n"] += 1
+            if calls["n"] == 1:
+                raise RuntimeError("operation not permitted when stream is capturing")
+            return real(fn)
+
+        f2._capture = refuse_once
+        out = []
+        for sb in batches(data, B, NNEG, 4, seed=32):
+            out.append((float(f1(sb.to("cuda"))), float(f2(sb.to("cuda")))))
+        f1.flush(); f2.flush()
+        same = all(torch.equal(a, b) for a, b in zip(m1.parameters(), m2.parameters()))
+        q.put((out, same, f2._coll_capture_refused, len(f2.graph), f1._graph_collectives(),
+               os.environ.get("GTR_GRAPH_COLL")))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_collective_capture_refusal_falls_back_per_instance():
+    """A transport that refuses stream capture of the collectives: that step object falls
+    back to one graph per piece (same numbers), without touching the environment or any
+    other step object in the process."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_refuse_worker, args=(_free_port(), q))
+    p.start()
+    try:
+        out, same, refused, pieces, other_captures, env = q.get(timeout=300)
+    finally:
+        p.join(timeout=60)
+    assert p.exitcode == 0
+    assert refused and pieces == 2
+    assert other_captures and env == "1"
+    assert same
+    for l1, l2 in out:
+        assert l1 == l2

@@ -225,3 +225,28 @@ def test_recommender_matches_oracle(tmp_path):
             assert float(top.values[9] - top.values[10]) <= 1e-4 * float(top.values.abs().max())
         assert not set(ids) & (seen | {0})
         np.testing.assert_allclose(scores, sc[ids].numpy(), rtol=1e-3, atol=1e-5)
+
+
+def test_recommender_k_past_the_unmasked_items(tmp_path):
+    """A validated request near the catalog size (validation.py:89 clamps k to
+    num_items - 1 only): the reference's torch.topk returns every finite score and then
+    the masked ids at -inf; so does the Recommender (masked ids in ascending order)."""
+    import pandas as pd
+
+    from etpgt.serving import Recommender, ValidatedRequest
+
+    T = 12
+    m, _ = make_pair(T, 32, 2, K=4, seed=24)
+    torch.save({"epoch": 0, "model_state_dict": m.state_dict()}, tmp_path / "ck.pt")
+    pd.DataFrame({"item_i": [1, 2, 3, 5], "item_j": [2, 3, 5, 5]}).to_csv(tmp_path / "edges.csv", index=False)
+    rec = Recommender(tmp_path / "ck.pt", tmp_path / "edges.csv", device="cuda")
+    session = [3, 1, 5, 2]
+    ids, scores = rec.recommend(ValidatedRequest(session, T - 1))
+    live = T - len(set(session) | {0})
+    assert len(ids) == T - 1 and len(set(ids)) == T - 1
+    assert set(ids[:live]) == set(range(T)) - set(session) - {0}
+    assert all(np.isfinite(scores[:live])) and scores[:live] == sorted(scores[:live], reverse=True)
+    assert ids[live:] == sorted(set(session) | {0})[: T - 1 - live]
+    assert all(s == float("-inf") for s in scores[live:])
+    short, _ = rec.recommend(ValidatedRequest(session, live))
+    assert short == ids[:live]

@@ -371,10 +371,10 @@ def test_resident_images_equal_copied_blob():
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("gemm,D,H,K,loss", [("split", 64, 1, 0, "model_bpr"), ("f32", 128, 4, 16, "listwise"),
-                                             ("split", 32, 2, 0, "dual")])
+@pytest.mark.parametrize("gemm,D,H,K,loss", [("split", 64, 1, 0, "model_bpr"), ("split", 128, 4, 16, "listwise"),
+                                             ("split", 32, 2, 0, "dual"), ("f32", 128, 4, 16, "listwise")])
 def test_train_grads_gemm_modes(gemm, D, H, K, loss, monkeypatch):
-    """The layer GEMMs in the mode the width does not default to (GTR_GEMM): split-bf16
-    at D <= 64, exact f32 at D = 128 -- gradients against the oracle at 2e-3."""
+    """The layer GEMMs in the opt-in split-bf16 mode (GTR_GEMM=split) and forced exact f32:
+    single-step gradients against the oracle at 2e-3."""
     monkeypatch.setenv("GTR_GEMM", gemm)
     test_train_grads(D, H, K, loss)

@@ -137,3 +137,38 @@ def test_cached_pe_raises_without_precompute():
     m = R.RefLaplacianPECached(k=2, embedding_dim=16)
     with pytest.raises(RuntimeError, match="not precomputed"):
         m(torch.tensor([0, 1]))
+
+
+def test_hip_dropout_mask_restatement_keep_rate_and_scale():
+    """The oracle's restatement of the HIP dropout stream (used for value-level parity at
+    p = 0.1): keep rate 1 - p within 3 sigma, kept entries scaled by fp32 1/(1 - p),
+    streams of different layers / kinds / counters independent, attention masks indexed
+    in destination order."""
+    import numpy as np
+    import torch
+
+    import etpgt_ref as R
+
+    p, N, D, H = 0.1, 4000, 64, 4
+    ei = np.stack([np.arange(3000) % N, (np.arange(3000) * 7) % N])
+    m1 = R.hip_dropout_masks(123456789, 5, p, 2, ei, N, D, H)
+    m2 = R.hip_dropout_masks(123456789, 6, p, 2, ei, N, D, H)
+    scale = float(np.float32(1.0 / (1.0 - np.float32(p))))
+    for k in ("attn", "out"):
+        for l in range(2):
+            m = m1[k][l].numpy()
+            kept = m > 0
+            n = m.size
+            assert abs(kept.mean() - (1 - p)) <= 3 * np.sqrt(p * (1 - p) / n)
+            assert np.all(m[kept] == np.float32(scale))
+        # layers and counters draw different masks
+        assert not torch.equal(m1[k][0], m1[k][1])
+        assert not torch.equal(m1[k][0], m2[k][0])
+    assert not torch.equal(m1["attn"][0][:, 0], m1["out"][0][:3000, 0])
+    # attention element index = (destination-order position) * H + head
+    dst = ei[1]
+    order = np.argsort(dst, kind="stable")
+    e = int(order[17])  # the edge at destination-order position 17
+    want = R.hip_mix3(123456789, R.hip_drop_stream(0, 1, 5), np.array([17 * H + 2]))[0]
+    thresh = int(float(np.float32(p)) * 4294967296.0)
+    assert (m1["attn"][1][e, 2].item() > 0) == (int(want) >= thresh)
