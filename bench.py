@@ -94,6 +94,9 @@ def main():
     ap.add_argument("--recall-sessions", type=int, default=2048, help="held-out sessions of the Recall@10 leg")
     ap.add_argument("--e2e-steps", type=int, default=200,
                     help="end-to-end leg: steps with the batch built on the device inside the step (0 = skip)")
+    ap.add_argument("--tail-probe", type=int, default=1,
+                    help="re-launch the step tail alone to time it (0 = skip; PMC passes skip it so that the "
+                         "per-step kernel counts stay exact)")
     ap.add_argument("--gather-batch", type=int, default=8192,
                     help="embedding-gather roofline legs: C5 (512 MB table, HBM) and C3 (42 MB, Infinity Cache) "
                          "shapes (d=128, 100 negatives) at this batch (0 = skip)")
@@ -200,7 +203,7 @@ def main():
     achieved = alg_bytes / (step_ms * 1e-3) / 1e9
     traffic, traffic_src = (load_traffic(args.config if B == cfg.get("batch", 32) else f"{args.config}_b{B}",
                                          lazy) if step.dp is None else (None, None))
-    tail_ms = measure_tail(step, args.steps)
+    tail_ms = measure_tail(step, args.steps) if args.tail_probe else None
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -274,7 +277,7 @@ def main():
                 "touched_rows_per_step": round(touched, 1),
                 "avg_launch_ms": round(step_ms, 5),
                 "tail_kernel": {"name": "k_dp_tail" if step.dp is not None else "k_step_tail",
-                                "avg_launch_ms": round(tail_ms, 5)},
+                                "avg_launch_ms": None if tail_ms is None else round(tail_ms, 5)},
             },
             "cpu_baseline": cpu,
             "end_to_end": e2e,

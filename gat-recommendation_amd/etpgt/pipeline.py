@@ -3,12 +3,20 @@
 BASELINE.json configs[0] — "graph_transformer_optimized on 1k-node synthetic graph,
 CPU reference path, 100 sessions, 3 epochs (run_full_pipeline.py plumbing)":
 
-* ``generate_synthetic_events``   scripts/data/00_generate_synthetic_data.py:24-139
-  (Zipf(1.5) item popularity, session length U[3, 20], 70 % new item / 30 % re-view,
-  exponential 5-minute gaps capped at 30 minutes, view / addtocart / transaction mix);
-  one visitor per session, so ``session_id`` = the visitor's index.
-* ``build_co_event_graph``        scripts/data/04_build_graph.py:23-88 (pairs within
-  +-5 steps of a session, canonical item_i <= item_j, count / last_ts).
+* ``generate_synthetic_events``   scripts/data/00_generate_synthetic_data.py:24-139,
+  reproduced bit for bit: the same draws, in the same order, from the streams the
+  reference seeds with ``set_seed`` (Python ``random`` and numpy's legacy global
+  generator; here private instances seeded the same way, so the caller's global state is
+  untouched): Zipf(1.5) item popularity, session length U[3, 20], 70 % new item /
+  30 % re-view of a viewed item, exponential 5-minute gaps capped at 30 minutes,
+  view / addtocart / transaction mix, then the timestamp sort.
+* ``sessionize_events``           scripts/data/02_sessionize.py:25-81 (30-minute
+  inactivity gap per visitor, sessions of >= 3 events, ``sess_<n>`` ids).
+* ``build_co_event_graph``        scripts/data/04_build_graph.py:23-127 (pairs within
+  +-5 steps of a session, canonical item_i <= item_j, count / last_ts, most frequent
+  first; the event-pair histogram column is not kept: nothing on the hot path reads it).
+* ``create_test_subset``          run_full_pipeline.py:34-82 (first ``num_sessions``
+  sessions, graph edges among their items).
 * ``create_batch_from_sessions``  run_full_pipeline.py:85-179 (first ``batch_size``
   sessions, timestamp order, context = all but the last event, sorted unique context
   items as nodes, induced co-event edges in BOTH directions, self loops when a session
@@ -18,7 +26,11 @@ CPU reference path, 100 sessions, 3 epochs (run_full_pipeline.py plumbing)":
 * ``test_model_with_real_data``   run_full_pipeline.py:182-270 (Adam(lr=1e-3), the
   listwise loss on ``model.item_embedding``, ``num_epochs`` steps on the one batch).
 
-The model runs on the HIP path (libgtr_hip): there is no CPU fallback here.
+Pandas sorts use the reference's calls (default, non-stable quicksort), so ties come
+out in the same order.  tests/golden/c1_data.npz holds the reference scripts' own
+output for seed 42 (oracle/gen_golden.py), which these functions reproduce exactly
+(tests/test_host.py).  The model runs on the HIP path (libgtr_hip): there is no CPU
+fallback here.
 """
 
 from __future__ import annotations
@@ -34,66 +46,89 @@ import torch
 from etpgt.data.batch import SessionBatch, collate_sessions
 from etpgt.train.losses import create_loss_function
 
+SESSION_GAP_MS = 30 * 60 * 1000  # 02_sessionize.py:20-22
+MIN_SESSION_LENGTH = 3
+CO_EVENT_WINDOW = 5  # 04_build_graph.py:21
+_EVENT_PROBS = (  # (in cart, viewed before, new item)
+    {"view": 0.3, "addtocart": 0.2, "transaction": 0.5},
+    {"view": 0.6, "addtocart": 0.35, "transaction": 0.05},
+    {"view": 0.85, "addtocart": 0.13, "transaction": 0.02},
+)
 
-def generate_synthetic_events(num_sessions: int = 100, num_items: int = 1000, min_session_length: int = 3,
+
+def generate_synthetic_events(num_sessions: int = 10000, num_items: int = 5000, min_session_length: int = 3,
                               max_session_length: int = 20, start_date: str = "2024-01-01",
                               duration_days: int = 90, seed: int = 42) -> pd.DataFrame:
-    """Synthetic RetailRocket-like events with a ``session_id`` column (one session per
-    visitor), sorted by timestamp."""
-    rng = np.random.default_rng(seed)
-    prng = random.Random(seed)
-    pop = rng.zipf(1.5, num_items).astype(np.float64)
-    pop /= pop.sum()
+    """Synthetic RetailRocket-like events (timestamp, visitorid, event, itemid,
+    transactionid), sorted by timestamp; one visitor per generated session."""
+    py = random.Random(seed)              # == random.seed(seed)
+    npr = np.random.RandomState(seed)     # == np.random.seed(seed)
+    pop = npr.zipf(1.5, num_items)
+    pop = pop / pop.sum()
     start_ts = int(datetime.strptime(start_date, "%Y-%m-%d").timestamp() * 1000)
-    end_ts = start_ts + duration_days * 24 * 3600 * 1000
+    end_ts = start_ts + duration_days * 24 * 60 * 60 * 1000
     rows = []
     for s in range(num_sessions):
-        length = prng.randint(min_session_length, max_session_length)
-        ts = prng.randint(start_ts, end_ts - 3_600_000)
-        viewed, cart = [], set()
+        length = py.randint(min_session_length, max_session_length)
+        ts = py.randint(start_ts, end_ts - 3600000)
+        viewed, cart = set(), set()
         for e in range(length):
             if e > 0:
-                ts += min(int(rng.exponential(300)), 1800) * 1000
-            if e == 0 or prng.random() < 0.7 or not viewed:
-                item = int(rng.choice(num_items, p=pop))
+                ts += min(int(npr.exponential(300)), 1800) * 1000
+            if e == 0 or py.random() < 0.7:
+                item = int(npr.choice(num_items, p=pop))
+            elif viewed:
+                item = int(py.choice(list(viewed)))
             else:
-                item = prng.choice(viewed)
-            if item in cart:
-                probs = (0.3, 0.2, 0.5)
-            elif item in viewed:
-                probs = (0.6, 0.35, 0.05)
-            else:
-                probs = (0.85, 0.13, 0.02)
-            ev = prng.choices(("view", "addtocart", "transaction"), weights=probs)[0]
-            if item not in viewed:
-                viewed.append(item)
+                item = int(npr.choice(num_items, p=pop))
+            probs = _EVENT_PROBS[0] if item in cart else _EVENT_PROBS[1] if item in viewed else _EVENT_PROBS[2]
+            ev = py.choices(list(probs.keys()), weights=list(probs.values()))[0]
+            viewed.add(item)
             if ev == "addtocart":
                 cart.add(item)
             rows.append({"timestamp": ts, "visitorid": f"visitor_{s}", "event": ev, "itemid": item,
-                         "transactionid": f"txn_{s}_{e}" if ev == "transaction" else None, "session_id": s})
-    return pd.DataFrame(rows).sort_values("timestamp", kind="stable").reset_index(drop=True)
+                         "transactionid": f"txn_{s}_{e}" if ev == "transaction" else None})
+    return pd.DataFrame(rows).sort_values("timestamp").reset_index(drop=True)
 
 
-def build_co_event_graph(sessions_df: pd.DataFrame, window: int = 5) -> pd.DataFrame:
+def sessionize_events(events_df: pd.DataFrame, gap_ms: int = SESSION_GAP_MS,
+                      min_length: int = MIN_SESSION_LENGTH) -> pd.DataFrame:
+    """Sessions by visitor and inactivity gap, with a ``session_id`` column."""
+    df = events_df.sort_values(["visitorid", "timestamp"]).reset_index(drop=True)
+    gap = df.groupby("visitorid")["timestamp"].diff()
+    df["session_id"] = "sess_" + (gap.isna() | (gap > gap_ms)).cumsum().astype(str)
+    size = df.groupby("session_id").size()
+    return df[df["session_id"].isin(size[size >= min_length].index)].copy()
+
+
+def build_co_event_graph(sessions_df: pd.DataFrame, window: int = CO_EVENT_WINDOW) -> pd.DataFrame:
     """Co-event edges (item_i <= item_j, count, last_ts), most frequent first."""
     edges: dict[tuple[int, int], list[int]] = {}
-    for _, g in sessions_df.groupby("session_id", sort=True):
-        ev = g.sort_values("timestamp", kind="stable")
+    for _, g in sessions_df.groupby("session_id"):
+        ev = g.sort_values("timestamp").reset_index(drop=True)
         items = ev["itemid"].tolist()
         tss = ev["timestamp"].tolist()
         for i in range(len(items)):
             for j in range(i + 1, min(i + window + 1, len(items))):
-                a, b = items[i], items[j]
-                ts = tss[i]
+                a, b, ts = items[i], items[j], tss[i]
                 if a > b:
-                    a, b = b, a
-                    ts = tss[j]
+                    a, b, ts = b, a, tss[j]
                 rec = edges.setdefault((a, b), [0, 0])
                 rec[0] += 1
                 rec[1] = max(rec[1], ts)
     df = pd.DataFrame([{"item_i": a, "item_j": b, "count": c, "last_ts": t} for (a, b), (c, t) in edges.items()],
                       columns=["item_i", "item_j", "count", "last_ts"])
-    return df.sort_values("count", ascending=False, kind="stable").reset_index(drop=True)
+    return df.sort_values("count", ascending=False).reset_index(drop=True)
+
+
+def create_test_subset(sessions_df: pd.DataFrame, graph_df: pd.DataFrame,
+                       num_sessions: int = 100) -> tuple[pd.DataFrame, pd.DataFrame]:
+    """The first ``num_sessions`` sessions (file order) and the graph edges among their
+    items (run_full_pipeline.py:34-82, in memory)."""
+    keep = sessions_df["session_id"].unique()[:num_sessions]
+    sub = sessions_df[sessions_df["session_id"].isin(keep)]
+    items = set(sub["itemid"].unique())
+    return sub, graph_df[graph_df["item_i"].isin(items) & graph_df["item_j"].isin(items)]
 
 
 def create_batch_from_sessions(sessions_df: pd.DataFrame, graph_df: pd.DataFrame, batch_size: int = 8,
@@ -107,7 +142,7 @@ def create_batch_from_sessions(sessions_df: pd.DataFrame, graph_df: pd.DataFrame
     gj = graph_df["item_j"].to_numpy()
     examples = []
     for sid in session_ids:
-        sd = sessions_df[sessions_df["session_id"] == sid].sort_values("timestamp", kind="stable")
+        sd = sessions_df[sessions_df["session_id"] == sid].sort_values("timestamp")
         items = sd["itemid"].to_numpy()
         if len(items) < 2:
             continue

@@ -9,6 +9,8 @@ bytecode writing disabled so nothing lands in the read-only tree:
 * ``etpgt/train/losses.py`` -> BPR / Listwise / Dual / SampledSoftmax
 * ``etpgt/utils/metrics.py``-> compute_recall_at_k / compute_ndcg_at_k
 * ``etpgt/train/trainer.py``-> Trainer.train_epoch / Trainer.evaluate (the step loop)
+* ``scripts/data/00_generate_synthetic_data.py``, ``02_sessionize.py``,
+  ``04_build_graph.py`` -> config C1's events, sessions and co-event graph
 
 PyG (``torch_geometric``) is not installed here, so the model's TransformerConv
 arithmetic inside the trainer fixture is the oracle restatement
@@ -231,6 +233,38 @@ def gen_trainer(ref_trainer, ref_losses, out):
     np.savez(os.path.join(out, "trainer.npz"), **res)
 
 
+def gen_c1(ref_root, out):
+    """BASELINE.json configs[0] inputs from the reference's own data scripts, imported by
+    path: scripts/data/00_generate_synthetic_data.py (seed 42, 100 sessions, 1k items),
+    02_sessionize.py (30-minute gap, >= 3 events) and 04_build_graph.py (+-5 window).
+    The temporal split (03) is skipped: it keeps ~70 of the 100 sessions, while C1 names
+    100 (run_full_pipeline.py's 100-session subset of them is all of them).  Events,
+    sessions and graph edges go to tests/golden/c1_data.npz (strings as category codes)."""
+    gen = load_by_path("ref_gen00", os.path.join(ref_root, "scripts/data/00_generate_synthetic_data.py"))
+    ses = load_by_path("ref_ses02", os.path.join(ref_root, "scripts/data/02_sessionize.py"))
+    grf = load_by_path("ref_grf04", os.path.join(ref_root, "scripts/data/04_build_graph.py"))
+    ev = gen.generate_synthetic_events(num_sessions=100, num_items=1000, seed=42)
+    sd = ses.sessionize_events(ev)
+    edges, _ = grf.build_co_event_graph(sd)
+    code = {"view": 0, "addtocart": 1, "transaction": 2}
+    res = {
+        "ev_timestamp": ev["timestamp"].to_numpy(np.int64),
+        "ev_visitor": ev["visitorid"].str.replace("visitor_", "").astype(np.int64).to_numpy(),
+        "ev_event": ev["event"].map(code).to_numpy(np.int64),
+        "ev_itemid": ev["itemid"].to_numpy(np.int64),
+        "ev_txn": ev["transactionid"].notna().to_numpy(),
+        "sd_timestamp": sd["timestamp"].to_numpy(np.int64),
+        "sd_itemid": sd["itemid"].to_numpy(np.int64),
+        "sd_session": sd["session_id"].str.replace("sess_", "").astype(np.int64).to_numpy(),
+        "sd_index": sd.index.to_numpy(np.int64),
+        "g_item_i": edges["item_i"].to_numpy(np.int64),
+        "g_item_j": edges["item_j"].to_numpy(np.int64),
+        "g_count": edges["count"].to_numpy(np.int64),
+        "g_last_ts": edges["last_ts"].to_numpy(np.int64),
+    }
+    np.savez_compressed(os.path.join(out, "c1_data.npz"), **res)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -247,6 +281,7 @@ def main():
     gen_losses(ref_base, ref_losses, a.out)
     gen_metrics(ref_metrics, a.out)
     gen_trainer(ref_trainer, ref_losses, a.out)
+    gen_c1(a.ref, a.out)
     for f in sorted(os.listdir(a.out)):
         print(f, os.path.getsize(os.path.join(a.out, f)))
 

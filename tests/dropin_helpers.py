@@ -42,3 +42,15 @@ REFERENCE_IMPORTS = {
                     "set_seed", "get_logger"],
     "etpgt.utils.io": ["load_config", "save_json", "load_json"],
 }
+
+
+def c1_inputs():
+    """Config C1's data chain: the reference's scripts/data 00 -> 02 -> 04 as restated by
+    etpgt.pipeline (pinned to their own output by tests/golden/c1_data.npz), then
+    run_full_pipeline.py's 100-session subset: (events, sessions, graph, (subset, graph))."""
+    from etpgt.pipeline import build_co_event_graph, create_test_subset, generate_synthetic_events, sessionize_events
+
+    ev = generate_synthetic_events(num_sessions=100, num_items=1000, seed=42)
+    sd = sessionize_events(ev)
+    g = build_co_event_graph(sd)
+    return ev, sd, g, create_test_subset(sd, g, num_sessions=100)

@@ -1,5 +1,6 @@
 """Config C1 (BASELINE.json configs[0]): the reference's run_full_pipeline.py quick path
-— 100 synthetic sessions over a 1k-item catalogue, the 16-session bidirectional batch,
+— 100 synthetic sessions over a 1k-item catalogue (the reference generator's own output,
+pinned by tests/golden/c1_data.npz), the 16-session bidirectional batch,
 graph_transformer_optimized (d=64, 2 heads, 2 layers, no LapPE), listwise loss,
 Adam(1e-3), 3 epochs — on the HIP model against the same plumbing on the oracle.
 
@@ -24,9 +25,12 @@ CFG = {"embedding_dim": 64, "hidden_dim": 64, "num_layers": 2, "num_heads": 2, "
 
 
 def _c1_batch():
-    ev = P.generate_synthetic_events(num_sessions=100, num_items=1000, seed=42)
-    g = P.build_co_event_graph(ev)
-    return P.create_batch_from_sessions(ev, g, batch_size=16, num_negatives=5)
+    """The reference's own C1 data (scripts/data 00 -> 02 -> 04, pinned by
+    tests/golden/c1_data.npz) -> run_full_pipeline.py's 16-session batch."""
+    from dropin_helpers import c1_inputs
+
+    _, _, _, (sub, g) = c1_inputs()
+    return P.create_batch_from_sessions(sub, g, batch_size=16, num_negatives=5)
 
 
 def test_c1_pipeline_matches_oracle():

@@ -243,27 +243,50 @@ def test_metrics_and_seed():
     assert compute_ndcg_at_k(p, torch.tensor([1, 9, 20]), 5) == pytest.approx(0.4769, abs=1e-4)
 
 
-def test_c1_pipeline_batch_semantics():
-    """run_full_pipeline.py:85-179 batch construction: sorted unique context items as
-    nodes, induced co-event edges in both directions (self loops if none), the first
-    n catalogue items outside the session as negatives, remapped ids."""
-    from etpgt.pipeline import build_co_event_graph, create_batch_from_sessions, generate_synthetic_events
+def test_c1_data_chain_matches_reference_scripts(golden_dir):
+    """etpgt.pipeline reproduces the reference's own scripts/data/00 -> 02 -> 04 output
+    (tests/golden/c1_data.npz, oracle/gen_golden.py gen_c1) exactly: events, sessions
+    and the co-event graph, integer for integer and in the same row order."""
+    from dropin_helpers import c1_inputs
 
-    ev = generate_synthetic_events(num_sessions=100, num_items=1000, seed=42)
-    assert ev["session_id"].nunique() == 100
-    lens = ev.groupby("session_id").size()
+    gd = np.load(os.path.join(golden_dir, "c1_data.npz"))
+    ev, sd, g, _ = c1_inputs()
+    code = {"view": 0, "addtocart": 1, "transaction": 2}
+    assert np.array_equal(ev["timestamp"].to_numpy(np.int64), gd["ev_timestamp"])
+    assert np.array_equal(ev["visitorid"].str.replace("visitor_", "").astype(np.int64).to_numpy(), gd["ev_visitor"])
+    assert np.array_equal(ev["event"].map(code).to_numpy(np.int64), gd["ev_event"])
+    assert np.array_equal(ev["itemid"].to_numpy(np.int64), gd["ev_itemid"])
+    assert np.array_equal(ev["transactionid"].notna().to_numpy(), gd["ev_txn"])
+    assert np.array_equal(sd["timestamp"].to_numpy(np.int64), gd["sd_timestamp"])
+    assert np.array_equal(sd["itemid"].to_numpy(np.int64), gd["sd_itemid"])
+    assert np.array_equal(sd["session_id"].str.replace("sess_", "").astype(np.int64).to_numpy(), gd["sd_session"])
+    assert np.array_equal(sd.index.to_numpy(np.int64), gd["sd_index"])
+    for k in ("item_i", "item_j", "count", "last_ts"):
+        assert np.array_equal(g[k].to_numpy(np.int64), gd[f"g_{k}"]), k
+
+
+def test_c1_pipeline_batch_semantics():
+    """run_full_pipeline.py:85-179 batch construction on C1's pinned data: sorted unique
+    context items as nodes, induced co-event edges in both directions (self loops if
+    none), the first n catalogue items outside the session as negatives, remapped ids."""
+    from dropin_helpers import c1_inputs
+
+    from etpgt.pipeline import create_batch_from_sessions
+
+    _, _, _, (sub, gsub) = c1_inputs()
+    assert sub["session_id"].nunique() == 100
+    lens = sub.groupby("session_id").size()
     assert lens.min() >= 3 and lens.max() <= 20
-    g = build_co_event_graph(ev)
-    assert bool((g["item_i"] <= g["item_j"]).all()) and bool((g["count"] >= 1).all())
-    batch, T = create_batch_from_sessions(ev, g, batch_size=16, num_negatives=5)
-    assert T == ev["itemid"].nunique()
+    assert bool((gsub["item_i"] <= gsub["item_j"]).all()) and bool((gsub["count"] >= 1).all())
+    batch, T = create_batch_from_sessions(sub, gsub, batch_size=16, num_negatives=5)
+    assert T == sub["itemid"].nunique()
     assert batch.num_graphs == 16 and tuple(batch.negative_items.shape) == (16, 5)
     ptr = batch.ptr.numpy()
     ei = batch.edge_index.numpy()
-    items = sorted(ev["itemid"].unique())
+    items = sorted(sub["itemid"].unique())
     idx = {it: k for k, it in enumerate(items)}
-    for b, sid in enumerate(ev["session_id"].unique()[:16]):
-        sd = ev[ev["session_id"] == sid].sort_values("timestamp", kind="stable")["itemid"].to_numpy()
+    for b, sid in enumerate(sub["session_id"].unique()[:16]):
+        sd = sub[sub["session_id"] == sid].sort_values("timestamp")["itemid"].to_numpy()
         x = batch.x.numpy()[ptr[b]:ptr[b + 1]]
         assert x.tolist() == sorted({idx[i] for i in sd[:-1]})
         assert int(batch.target_item[b]) == idx[sd[-1]]
