@@ -205,19 +205,25 @@ def main():
                                          lazy) if step.dp is None else (None, None))
     tail_ms = measure_tail(step, args.steps) if args.tail_probe else None
 
+    log(f"timed: {value:.1f} sessions/s, {ms_per_step:.4f} ms/step")
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(cfg, batches, T, args.cpu_seconds)
+        log(f"cpu baseline: {cpu['value']} sessions/s")
     e2e = None
     if rank == 0 and world == 1 and args.e2e_steps > 0:
         e2e = e2e_probe(cfg, data, dev, B, args.e2e_steps)
+        log(f"end to end: {e2e['device_batch_build_sessions_per_s']} sessions/s")
     gather = gather_c = None
     if rank == 0 and world == 1 and args.gather_batch > 0:
         gather = gather_probe(dev, args.gather_batch, "c5")
+        log(f"gather roofline (C5 table): frac {gather['frac']}")
         gather_c = gather_probe(dev, args.gather_batch, "c3")
+        log(f"gather roofline (C3 table): frac {gather_c['frac']}")
     recall = None
     if rank == 0 and world == 1 and args.recall_steps > 0:
         recall = recall_parity(cfg, data, T, dev, args.recall_steps, args.recall_sessions)
+        log(f"recall parity: {recall['gpu']} vs {recall['oracle']}")
 
     if rank == 0:
         out = {
@@ -619,24 +625,29 @@ def recall_parity(cfg, data, T, dev, steps, n_val, B=32):
     return out
 
 
-def _cpu_threads(step_fn, trial_s: float = 2.0) -> int:
-    """The faster of os.cpu_count() and the affinity-set size, by median step time."""
-    cands = sorted({os.cpu_count() or 1, len(os.sched_getaffinity(0))}, reverse=True)
-    if len(cands) == 1:
-        return cands[0]
-    best, best_t = cands[0], float("inf")
-    for th in cands:
-        torch.set_num_threads(th)
-        step_fn()
-        ts, end = [], time.perf_counter() + trial_s
-        while time.perf_counter() < end or len(ts) < 3:
-            t = time.perf_counter()
-            step_fn()
-            ts.append(time.perf_counter() - t)
-        med = float(np.median(ts))
-        if med < best_t:
-            best, best_t = th, med
-    return best
+def _cpu_share() -> tuple[int, str]:
+    """Threads for the CPU baseline: the CPU share this process may actually use.  On the
+    GPU box ``os.cpu_count()`` reports the whole machine while a cgroup quota grants this
+    job a slice of it (16 CPUs per GPU); oversubscribing the quota with one thread per
+    machine core stalls torch's OpenMP pool, so the quota (or the affinity set, whichever
+    is smaller) is the honest core count."""
+    share, why = os.cpu_count() or 1, "os.cpu_count()"
+    try:
+        aff = len(os.sched_getaffinity(0))
+        if aff < share:
+            share, why = aff, "sched_getaffinity"
+    except (AttributeError, OSError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(per)))
+            if quota < share:
+                share, why = quota, "cgroup cpu.max quota"
+    except (OSError, ValueError):
+        pass
+    return share, why
 
 
 def cpu_baseline(cfg, batches, T, seconds):
@@ -656,10 +667,9 @@ def cpu_baseline(cfg, batches, T, seconds):
     ref.train()
     opt = torch.optim.AdamW(ref.parameters(), lr=1e-3, weight_decay=1e-5)
     rbs = [R.ref_batch_from(b) for b in batches]
-    # threads: every host core (os.cpu_count()) unless the cores this process
-    # may run on (its affinity set, e.g. a box's CPU share) train faster; short trial of each
-    threads = _cpu_threads(lambda: R.ref_train_step(ref, rbs[0], opt, cfg["loss"]))
+    threads, why = _cpu_share()
     torch.set_num_threads(threads)
+    log(f"cpu baseline: {threads} threads ({why}; host reports {os.cpu_count()} CPUs)")
     for i in range(3):
         R.ref_train_step(ref, rbs[i % len(rbs)], opt, cfg["loss"])
     times = []
@@ -685,6 +695,7 @@ def cpu_baseline(cfg, batches, T, seconds):
         "value": round(B / med, 1),
         "unit": "sessions/s",
         "cores": threads,
+        "cores_source": why,
         "host_cpus": os.cpu_count(),
         "kind": "port",
         "sample": f"{len(times)} training steps of B={B} ({len(times)*B} sessions, median step {med*1e3:.2f} ms) "
