@@ -67,9 +67,9 @@ def test_struct_layouts_match_header():
             decl = decl.strip()
             if not decl:
                 continue
-            parts = decl.replace("*", " ").split()
+            parts = [t for t in decl.replace("*", " ").split() if t not in ("struct", "const")]
             # "int32_t n_cap, b_cap, e_cap" declares several fields
-            tail = " ".join(parts[1:]) if parts[0] != "const" else " ".join(parts[2:])
+            tail = " ".join(parts[1:])
             names += [n.split("[")[0].strip() for n in tail.split(",") if n.strip()]  # arrays: name only
         assert [f[0] for f in py._fields_] == names, cname
 
