@@ -84,6 +84,9 @@ def main():
     ap.add_argument("--global-batch", type=int, default=None,
                     help="strong scaling: fixed global batch split over the ranks, SyncBN (1 GPU semantics)")
     ap.add_argument("--sync-bn", action="store_true", help="BatchNorm statistics over every rank's batch")
+    ap.add_argument("--shard-table", action="store_true",
+                    help="row-sharded item table + AdamW state (rank p owns rows r %% P == p), rows and row "
+                         "gradients by all-to-all (etpgt.train.sharded)")
     ap.add_argument("--lazy", type=int, default=None,
                     help="deferred zero-gradient AdamW of untouched table rows (1/0; default: per config)")
     ap.add_argument("--lagged", type=int, default=None,
@@ -139,10 +142,13 @@ def main():
     t0 = time.time()
     lazy = bool(args.lazy) if args.lazy is not None else bool(cfg.get("lazy", False))
     dp_on = bool(args.dp or args.sync_bn or world > 1)
-    lagged = (bool(args.lagged) if args.lagged is not None else dp_on) and not lazy
+    shard = bool(args.shard_table)
+    if shard:
+        lazy = False  # the shards keep their own lazy stamps
+    lagged = (bool(args.lagged) if args.lagged is not None else dp_on) and not lazy and not shard
     w = build_workload(args.config, args.batch_size, args.num_batches, dev, rank, use_graph=not args.no_graph,
                        data_parallel=True if (args.dp or args.sync_bn) else None, lazy=lazy,
-                       sync_bn=args.sync_bn and world > 1, lagged=lagged)
+                       sync_bn=args.sync_bn and world > 1, lagged=lagged, shard_table=shard)
     step, staged, batches, data, T, B, touched, st = (w[k] for k in ("step", "staged", "batches", "data", "T", "B",
                                                                    "touched", "stats"))
     log(f"data: T={T} sessions={data.num_sessions} edges={data.edge_keys.size} setup {time.time()-t0:.1f}s {st}")
@@ -184,7 +190,7 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(loss)
-    step.flush()  # lazy table: bring every row to the last step before reading it
+    step.sync_table()  # lazy table: rows brought to the last step; sharded: gathered from the shards
     replicas_identical = None
     if world > 1:  # data parallel: every rank must hold the same parameters
         chk = torch.stack([step.model.item_embedding.weight.double().sum(), step.eng.flat.flat.double().sum()])
@@ -199,11 +205,13 @@ def main():
     # sweep rides in the layer kernels, so the step is the unit that streams the table
     D = cfg["D"]
     step_ms = gpu_ms / args.steps
-    alg_bytes = step_bytes(step, cfg, T, st["nodes_per_session"] * B, B, touched, lazy)
+    alg_bytes = step_bytes(step, cfg, T, st["nodes_per_session"] * B, B, touched, lazy or shard)
+    if shard:  # fetched rows written by the owner, gradient rows written + read by the owner
+        alg_bytes += 3 * 4.0 * touched * D
     achieved = alg_bytes / (step_ms * 1e-3) / 1e9
     traffic, traffic_src = (load_traffic(args.config if B == cfg.get("batch", 32) else f"{args.config}_b{B}",
-                                         lazy) if step.dp is None else (None, None))
-    tail_ms = measure_tail(step, args.steps) if args.tail_probe else None
+                                         lazy) if step.dp is None and not shard else (None, None))
+    tail_ms = measure_tail(step, args.steps) if args.tail_probe and not shard else None
 
     log(f"timed: {value:.1f} sessions/s, {ms_per_step:.4f} ms/step")
     cpu = None
@@ -249,15 +257,16 @@ def main():
                 "graph_edges": int(data.edge_keys.size),
                 "nodes_per_session": round(st["nodes_per_session"], 3),
                 "edges_per_session": round(st["edges_per_session"], 3),
-                "parallelism": f"dp{world}",
+                "parallelism": f"dp{world}" + ("+rowshard" if shard else ""),
                 "transport": "rccl" if backend == "nccl" else "gloo (shared-device rehearsal)",
-                "dp_exchange": step.dp is not None,
+                "dp_exchange": ("row-sharded table: all-to-all of row ids, rows and row gradients "
+                                f"({step.shard.volume()})") if shard else step.dp is not None,
                 "hip_graph": not args.no_graph,
                 "batch_images": "resident, one graph per image" if args.resident else "copied per step (D2D)",
                 "lazy_table": lazy,
                 "lagged_sweep": lagged,
                 "gemm": gemm_mode(D),
-                "graph_collectives": bool(step.dp is not None and step._graph_collectives()),
+                "graph_collectives": bool((step.dp is not None or shard) and step._graph_collectives()),
                 "sync_bn": bool(args.sync_bn and world > 1),
                 "gpu_ms_per_step_events": round(gpu_ms / args.steps, 4),
                 "final_loss": round(final_loss, 6),
@@ -299,7 +308,7 @@ def main():
 
 def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, use_graph: bool = True,
                    data_parallel: bool | None = None, lazy: bool = False, sync_bn: bool = False,
-                   lagged: bool = False) -> dict:
+                   lagged: bool = False, shard_table: bool = False) -> dict:
     """Synthetic RetailRocket-shaped data, the model of `config`, a bound fused step
     and `num_batches` packed batches pre-staged in HBM."""
     from etpgt.data.batch import Caps
@@ -325,7 +334,8 @@ def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, us
         model.laplacian_pe._cached_pe = random_pe_table(T, cfg["K"])
     model = model.to(dev).train()
     step = FusedTrainStep(model, lr=1e-3, weight_decay=1e-5, loss=cfg["loss"], use_graph=use_graph,
-                          data_parallel=data_parallel, lazy=lazy, sync_bn=sync_bn, lagged=lagged)
+                          data_parallel=data_parallel, lazy=lazy, sync_bn=sync_bn, lagged=lagged,
+                          shard_table=shard_table)
     caps = Caps(max(b.num_nodes for b in batches), B, max(b.num_edges for b in batches), cfg["n_neg"])
     step._bind(caps)  # data parallel: the ranks agree on the largest capacities
     caps = step.caps

@@ -1,0 +1,520 @@
+// gtr_shard.hip — row-sharded item table for the multi-GPU step (SURVEY.md §8e ii).
+//
+// The reference keeps one dense nn.Embedding(T, d) (base.py:36) updated by a dense AdamW
+// (train_baseline.py:252-256).  Across P ranks the table and its AdamW moments are
+// row-sharded: global row r lives on rank r % P as local row r / P (cyclic ownership
+// spreads the Zipf-hot items over every owner).  One step per rank:
+//
+//   gtr_step_begin   (sorted contribution list of the rank's batch, global keys)
+//   gtr_shard_route  unique requested rows per owner -> send_ids [P][cap]; the batch's
+//                    ids remapped to "compact" rows q*cap + 1 + j of the fetched-row buffer
+//   all-to-all ids   (RCCL)
+//   gtr_shard_serve  owner: requested rows brought up to step t-1 (lazy zero-gradient
+//                    AdamW, bitwise the dense update) -> send_rows [P][cap][D]
+//   all-to-all rows  == the "halo" fetch of source embeddings at layer 0
+//   forward / loss / backward on the compact rows (unchanged layer kernels)
+//   gtr_shard_pack   per requested row the summed table-gradient row -> send_grads
+//                    [P][cap][D] (the rank's contributions in sorted order, as the
+//                    single-GPU tail sums them) + the small-parameter gradient and loss
+//   all-to-all grads + all-gather of the small packs
+//   gtr_shard_update owner: every requested row's gradient summed over the requesting
+//                    ranks in rank order / P, AdamW at step t (the same arithmetic as
+//                    gtr_dp_tail); small parameters from the gathered packs.
+//
+// Slot 0 of every peer block carries the block's count; capacities are fixed so that the
+// collectives and kernels replay from one captured hipGraph.  A block that would overflow
+// its capacity sets status[0] (sticky in status[1]); the host checks it.
+
+#include "gtr_rows.cuh"
+
+namespace {
+
+using namespace gtr;
+
+#define RB_THREADS 256
+#define RB_ROUNDS 4
+#define RB_SLOTS (RB_THREADS * RB_ROUNDS)
+#define SH_MAXP 16
+
+struct RouteK {
+  gtr_batch bt;
+  const int32_t* skeys;
+  const int32_t* svals;
+  int32_t* send_ids;
+  int32_t* ckeys;
+  int32_t* node_item_c;
+  int32_t* target_c;
+  int32_t* negatives_c;
+  const float* pe_tab;
+  float* node_pe;
+  int32_t* bcnt;    // [nblk][P] first-occurrence counts per owner, then exclusive offsets
+  int32_t* status;
+  int T, P, cap, pe_k, m_cap, nblk;
+};
+
+__device__ __forceinline__ bool slot_info(const RouteK& a, int i, int& key, int& owner, bool& first) {
+  key = i < a.m_cap ? a.skeys[i] : a.T;
+  const bool valid = key >= 0 && key < a.T;
+  owner = valid ? key % a.P : 0;
+  first = valid && (i == 0 || a.skeys[i - 1] != key);
+  return valid;
+}
+
+// Pass 1: first occurrences (segment starts of the sorted list) per owner and block.
+__global__ __launch_bounds__(RB_THREADS) void k_route_count(RouteK a) {
+  __shared__ int s_cnt[SH_MAXP];
+  if (threadIdx.x < SH_MAXP) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  for (int r = 0; r < RB_ROUNDS; ++r) {
+    const int i = blockIdx.x * RB_SLOTS + r * RB_THREADS + threadIdx.x;
+    int key, q;
+    bool first;
+    slot_info(a, i, key, q, first);
+    if (first) atomicAdd(&s_cnt[q], 1);  // integer counts: order-independent
+  }
+  __syncthreads();
+  if (threadIdx.x < a.P) a.bcnt[(size_t)blockIdx.x * a.P + threadIdx.x] = s_cnt[threadIdx.x];
+}
+
+// Pass 2 (one workgroup): exclusive offsets of every block per owner, the owners' totals
+// into the count slots, overflow status.
+__global__ __launch_bounds__(RB_THREADS) void k_route_scan(RouteK a) {
+  __shared__ int s_part[RB_THREADS][SH_MAXP];
+  const int tid = threadIdx.x;
+  const int per = (a.nblk + RB_THREADS - 1) / RB_THREADS;
+  const int b0 = min(a.nblk, tid * per), b1 = min(a.nblk, b0 + per);
+  for (int q = 0; q < a.P; ++q) {
+    int s = 0;
+    for (int b = b0; b < b1; ++b) s += a.bcnt[(size_t)b * a.P + q];
+    s_part[tid][q] = s;
+  }
+  __syncthreads();
+  if (tid < a.P) {  // scan over the threads' chunks for owner q
+    int run = 0;
+    for (int t = 0; t < RB_THREADS; ++t) {
+      const int v = s_part[t][tid];
+      s_part[t][tid] = run;
+      run += v;
+    }
+    const int lim = a.cap - 1;
+    a.send_ids[(size_t)tid * a.cap] = min(run, lim);
+    if (run > lim) {
+      a.status[0] = 1;
+      atomicOr(a.status + 1, 1);
+    }
+  }
+  __syncthreads();
+  for (int q = 0; q < a.P; ++q) {
+    int run = s_part[tid][q];
+    for (int b = b0; b < b1; ++b) {
+      const int v = a.bcnt[(size_t)b * a.P + q];
+      a.bcnt[(size_t)b * a.P + q] = run;
+      run += v;
+    }
+  }
+}
+
+// Pass 3: inclusive first-occurrence rank of each slot among its owner's rows (slot
+// order), compact row q*cap + rank, owner lists, remapped batch ids (+ PE rows).
+__global__ __launch_bounds__(RB_THREADS) void k_route_write(RouteK a) {
+  __shared__ int s_run[SH_MAXP];
+  __shared__ int s_wt[RB_THREADS / 64][SH_MAXP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < a.P) s_run[tid] = a.bcnt[(size_t)blockIdx.x * a.P + tid];
+  __syncthreads();
+  const unsigned long long le = lane == 63 ? ~0ull : ((1ull << (lane + 1)) - 1ull);
+  for (int r = 0; r < RB_ROUNDS; ++r) {
+    const int i = blockIdx.x * RB_SLOTS + r * RB_THREADS + tid;
+    int key, q;
+    bool first;
+    const bool valid = slot_info(a, i, key, q, first);
+    int mine = 0;
+    for (int o = 0; o < a.P; ++o) {
+      const unsigned long long bal = __ballot(first && q == o);
+      if (lane == 0) s_wt[wave][o] = __popcll(bal);
+      if (q == o) mine = __popcll(bal & le);
+    }
+    __syncthreads();
+    int base = s_run[q];
+    for (int w = 0; w < wave; ++w) base += s_wt[w][q];
+    if (valid) {
+      const int incl = base + mine;  // first occurrences of owner q in [0, i]
+      int compact = q * a.cap + incl;
+      if (incl > a.cap - 1) {
+        compact = q * a.cap;  // in bounds; the step is flagged invalid
+        a.status[0] = 1;
+        atomicOr(a.status + 1, 1);
+      } else if (first) {
+        a.send_ids[compact] = key;
+      }
+      a.ckeys[i] = compact;
+      const int s = a.svals[i];
+      const gtr_batch& bt = a.bt;
+      if (s < bt.n_cap) {
+        a.node_item_c[s] = compact;
+        if (a.node_pe)
+          for (int k = 0; k < a.pe_k; ++k) a.node_pe[(size_t)s * a.pe_k + k] = a.pe_tab[(size_t)key * a.pe_k + k];
+      } else if (s < bt.n_cap + bt.b_cap) {
+        a.target_c[s - bt.n_cap] = compact;
+      } else {
+        a.negatives_c[s - bt.n_cap - bt.b_cap] = compact;
+      }
+    } else if (i < a.m_cap) {
+      a.ckeys[i] = -1;
+    }
+    __syncthreads();
+    if (tid < a.P) {
+      int t = 0;
+      for (int w = 0; w < RB_THREADS / 64; ++w) t += s_wt[w][tid];
+      s_run[tid] += t;
+    }
+    __syncthreads();
+  }
+}
+
+// Owner side, step t: claim each requested local row (first claimer gets the old stamp)
+// and bring it to step t-1 with the zero-gradient update of every missed step (the
+// consts chain of the lazy table, bitwise the dense sweep).  16 lanes per entry.
+__device__ __forceinline__ void shard_claim_row(int local, const gtr_shard& sh, int32_t t, int gl, int gbase) {
+  int old = 0;
+  const bool ok = local >= 0 && local < sh.local_rows;
+  if (gl == 0 && ok) old = atomicExch(sh.stamp + local, t - 1);
+  old = __shfl(old, gbase);
+  if (!ok || old >= t - 1) return;
+  const int C4 = sh.dim / 4;
+  float4* P = reinterpret_cast<float4*>(sh.table) + (size_t)local * C4;
+  float4* M = reinterpret_cast<float4*>(sh.m) + (size_t)local * C4;
+  float4* V = reinterpret_cast<float4*>(sh.v) + (size_t)local * C4;
+  for (int c = gl; c < C4; c += 16) {
+    float4 p = P[c], m = M[c], v = V[c];
+    catch_up4(p, m, v, old, t - 1, sh.opt, sh.consts);
+    P[c] = p; M[c] = m; V[c] = v;
+  }
+}
+
+__device__ __forceinline__ int peer_count(const int32_t* ids, int r, int cap) {
+  const int c = ids[(size_t)r * cap];
+  return c < 0 ? 0 : (c > cap - 1 ? cap - 1 : c);
+}
+
+__global__ __launch_bounds__(GTR_BLOCK) void k_shard_claim(gtr_shard sh, const int32_t* recv_ids,
+                                                           const int64_t* step_dev) {
+  const int64_t gid = (int64_t)blockIdx.x * GTR_BLOCK + threadIdx.x;
+  const int64_t e = gid / 16;
+  const int r = (int)(e / sh.cap), j = (int)(e - (int64_t)r * sh.cap);
+  int local = -1;
+  if (r < sh.world && j >= 1 && j <= peer_count(recv_ids, r, sh.cap)) local = recv_ids[e] / sh.world;
+  shard_claim_row(local, sh, (int32_t)(*step_dev + sh.opt.step_offset), threadIdx.x & 15, (threadIdx.x & 63) & ~15);
+}
+
+template <int D>
+__global__ __launch_bounds__(GTR_BLOCK) void k_shard_copy(gtr_shard sh, const int32_t* recv_ids, float* send_rows) {
+  constexpr int C4 = D / 4;
+  const int64_t gid = (int64_t)blockIdx.x * GTR_BLOCK + threadIdx.x;
+  const int64_t e = gid / C4;
+  const int c = (int)(gid - e * C4);
+  const int r = (int)(e / sh.cap), j = (int)(e - (int64_t)r * sh.cap);
+  if (r >= sh.world || j < 1 || j > peer_count(recv_ids, r, sh.cap)) return;
+  const int local = recv_ids[e] / sh.world;
+  reinterpret_cast<float4*>(send_rows)[e * C4 + c] = reinterpret_cast<const float4*>(sh.table)[(size_t)local * C4 + c];
+}
+
+struct PackK {
+  gtr_batch bt;
+  gtr_tail tl;
+  const int32_t* ckeys;
+  float* send_grads;
+  float* small_pack;
+  int T, nb_rows, nseg, m_cap;
+  gtr_segment segs[GTR_SMALL_MAX_SEG];
+};
+
+// Requester side: the summed gradient row of every requested row (segment of the sorted
+// contribution list, summed in slot order like the single-GPU tail) -> its compact slot;
+// then the summed small-parameter gradient and the local loss -> small_pack.
+template <int D>
+__global__ __launch_bounds__(GTR_BLOCK) void k_shard_pack(PackK a) {
+  constexpr int C4 = D / 4, NG = GTR_BLOCK / C4;
+  __shared__ float s_acc[GTR_BLOCK];
+  const int tid = threadIdx.x, lane = tid & 63;
+  if ((int)blockIdx.x < a.nb_rows) {
+    const int grp = tid / C4, gl = tid % C4, gb = grp * C4 % 64;
+    const int i = blockIdx.x * NG + grp;
+    const int key = i < a.m_cap ? a.tl.skeys[i] : a.T;
+    const bool start = key >= 0 && key < a.T && (i == 0 || a.tl.skeys[i - 1] != key);
+    // segment end: the group's lanes probe C4 slots per round (ballot inside the wave)
+    int e = i + 1;
+    bool more = start;
+    while (__ballot(more) != 0ull) {  // wave-uniform loop; groups of the wave step together
+      const int k = e + gl;
+      const bool same = more && k < a.m_cap && a.tl.skeys[k] == key;
+      const unsigned long long bal = __ballot(!same && more) >> gb;
+      const unsigned long long gm = C4 == 64 ? ~0ull : ((1ull << C4) - 1ull);
+      if (more) {
+        const unsigned long long stop = bal & gm;
+        if (stop) { e += __ffsll((long long)stop) - 1; more = false; }
+        else e += C4;
+      }
+    }
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (start && key > 0)  // padding_idx = 0: no gradient (the owner still applies g = 0)
+      g = piece_sum<D>(a.bt, a.tl.svals, i, e, a.tl.dx0, a.tl.se, a.tl.coef_tgt, a.tl.coef_neg, gl, gb);
+    if (start) {
+      const int ck = a.ckeys[i];
+      if (ck >= 0) reinterpret_cast<float4*>(a.send_grads)[(size_t)ck * C4 + gl] = g;
+    }
+    (void)lane;
+    return;
+  }
+  const int sb = blockIdx.x - a.nb_rows;
+  const AdamStep unused{};
+  small_body((int64_t)sb * GTR_BLOCK + tid, a.segs, a.nseg, nullptr, nullptr, nullptr, a.small_pack, unused);
+  if (sb == 0) {  // local loss after the flat gradient
+    float acc = 0.0f;
+    if (a.tl.loss_part)
+      for (int q = tid; q < a.tl.loss_nparts; q += GTR_BLOCK)
+        acc += a.tl.loss_part[(size_t)q * 2] + a.tl.loss_part[(size_t)q * 2 + 1];
+    s_acc[tid] = acc;
+    __syncthreads();
+    if (tid == 0) {
+      float t = 0.0f;
+      if (a.tl.loss_part) {
+        for (int q = 0; q < GTR_BLOCK; ++q) t += s_acc[q];
+      } else {
+        t = a.tl.loss_out[0];
+      }
+      a.small_pack[a.tl.flat_total] = t;
+    }
+  }
+}
+
+// Position of `key` among peer r's requested ids (ascending, slots 1..count), or -1.
+__device__ __forceinline__ int peer_find(const int32_t* ids, int r, int cap, int key) {
+  const int32_t* p = ids + (size_t)r * cap + 1;
+  int lo = 0, hi = peer_count(ids, r, cap);
+  const int n = hi;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (p[mid] < key) lo = mid + 1; else hi = mid;
+  }
+  return (lo < n && p[lo] == key) ? lo + 1 : -1;
+}
+
+struct UpdateK {
+  gtr_shard sh;
+  gtr_tail tl;
+  const int32_t* recv_ids;
+  const float* recv_grads;
+  const float* small_all;
+  int64_t small_words;
+  int nb_rows, pad0;
+};
+
+template <int D>
+__global__ __launch_bounds__(GTR_BLOCK) void k_shard_update(UpdateK a) {
+  constexpr int C4 = D / 4;
+  __shared__ AdamStep s_st;
+  __shared__ int32_t s_t;
+  const int tid = threadIdx.x;
+  const gtr_shard& sh = a.sh;
+  if (tid == 0) {
+    const int64_t t = *sh.opt.step_dev + sh.opt.step_offset;
+    s_st.init(sh.opt, t);
+    s_t = (int32_t)t;
+    if (blockIdx.x == 0 && t < sh.consts_cap) lazy_consts_for(sh.opt, t, sh.consts);
+  }
+  __syncthreads();
+  const AdamStep st = s_st;
+  const int32_t t = s_t;
+  const int W = sh.world;
+  const float inv_w = 1.0f / (float)W;
+  if ((int)blockIdx.x < a.nb_rows) {
+    const int64_t gid = (int64_t)blockIdx.x * GTR_BLOCK + tid;
+    const int64_t e = gid / C4;
+    const int c = (int)(gid - e * C4);
+    const int r = (int)(e / sh.cap), j = (int)(e - (int64_t)r * sh.cap);
+    if (r >= W || j < 1 || j > peer_count(a.recv_ids, r, sh.cap)) return;
+    const int key = a.recv_ids[e];
+    for (int q = 0; q < r; ++q)
+      if (peer_find(a.recv_ids, q, sh.cap, key) >= 0) return;  // a lower rank leads this row
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int q = r; q < W; ++q) {
+      const int at = q == r ? j : peer_find(a.recv_ids, q, sh.cap, key);
+      if (at < 0) continue;
+      const float4 v = reinterpret_cast<const float4*>(a.recv_grads)[((size_t)q * sh.cap + at) * C4 + c];
+      g.x += v.x; g.y += v.y; g.z += v.z; g.w += v.w;
+    }
+    g.x *= inv_w; g.y *= inv_w; g.z *= inv_w; g.w *= inv_w;
+    const int local = key / W;
+    const size_t base = (size_t)local * C4 + c;
+    float4 pv = reinterpret_cast<const float4*>(sh.table)[base];
+    float4 mv = reinterpret_cast<const float4*>(sh.m)[base];
+    float4 vv = reinterpret_cast<const float4*>(sh.v)[base];
+    st.apply(pv.x, mv.x, vv.x, g.x);
+    st.apply(pv.y, mv.y, vv.y, g.y);
+    st.apply(pv.z, mv.z, vv.z, g.z);
+    st.apply(pv.w, mv.w, vv.w, g.w);
+    reinterpret_cast<float4*>(sh.table)[base] = pv;
+    reinterpret_cast<float4*>(sh.m)[base] = mv;
+    reinterpret_cast<float4*>(sh.v)[base] = vv;
+    if (c == 0) sh.stamp[local] = t;
+    return;
+  }
+  const int64_t e = (int64_t)(blockIdx.x - a.nb_rows) * GTR_BLOCK + tid;
+  const int64_t F = a.tl.flat_total;
+  if (e < F) {
+    float g = 0.0f;
+    for (int q = 0; q < W; ++q) g += a.small_all[(size_t)q * a.small_words + e];
+    g *= inv_w;
+    float pv = a.tl.flat[e], mv = a.tl.flat_m[e], vv = a.tl.flat_v[e];
+    st.apply(pv, mv, vv, g);
+    a.tl.flat[e] = pv;
+    a.tl.flat_m[e] = mv;
+    a.tl.flat_v[e] = vv;
+  } else if (e == F && a.tl.loss_out) {
+    float l = 0.0f;
+    for (int q = 0; q < W; ++q) l += a.small_all[(size_t)q * a.small_words + F];
+    a.tl.loss_out[0] = l * inv_w;
+  }
+}
+
+bool shard_ok(const gtr_shard* s) {
+  return s && s->world >= 1 && s->world <= SH_MAXP && s->rank >= 0 && s->rank < s->world && s->cap >= 2 &&
+         s->num_items > 0 && s->local_rows == (s->num_items - s->rank + s->world - 1) / s->world &&
+         (s->dim == 32 || s->dim == 64 || s->dim == 128 || s->dim == 256) && s->table && s->m && s->v && s->stamp &&
+         s->consts && s->consts_cap > 0 && s->status && s->opt.step_dev;
+}
+
+}  // namespace
+
+extern "C" {
+
+int gtr_shard_route_scratch(int m_cap, int world, size_t* bytes) {
+  if (!bytes || m_cap <= 0 || world < 1 || world > SH_MAXP) {
+    set_error("gtr_shard_route_scratch: bad arguments");
+    return GTR_E_ARG;
+  }
+  *bytes = (size_t)((m_cap + RB_SLOTS - 1) / RB_SLOTS) * world * sizeof(int32_t);
+  return GTR_OK;
+}
+
+int gtr_shard_route(const gtr_batch* bt, const int32_t* skeys, const int32_t* svals, const gtr_shard* sh,
+                    int32_t* send_ids, int32_t* ckeys, int32_t* node_item_c, int32_t* target_c, int32_t* negatives_c,
+                    const float* pe_tab, int pe_k, float* node_pe, void* scratch, size_t scratch_bytes,
+                    gtr_stream_t stream) {
+  if (!bt || !skeys || !svals || !shard_ok(sh) || !send_ids || !ckeys || !node_item_c || !target_c || !negatives_c ||
+      !scratch || (node_pe && (!pe_tab || pe_k <= 0))) {
+    set_error("gtr_shard_route: bad arguments");
+    return GTR_E_ARG;
+  }
+  RouteK k{};
+  k.bt = *bt;
+  k.skeys = skeys; k.svals = svals; k.send_ids = send_ids; k.ckeys = ckeys;
+  k.node_item_c = node_item_c; k.target_c = target_c; k.negatives_c = negatives_c;
+  k.pe_tab = pe_tab; k.node_pe = node_pe; k.pe_k = node_pe ? pe_k : 0;
+  k.status = sh->status;
+  k.T = sh->num_items; k.P = sh->world; k.cap = sh->cap;
+  k.m_cap = bt->n_cap + bt->b_cap * (1 + bt->n_neg);
+  k.nblk = (k.m_cap + RB_SLOTS - 1) / RB_SLOTS;
+  if (scratch_bytes < (size_t)k.nblk * k.P * sizeof(int32_t)) {
+    set_error("gtr_shard_route: scratch of %zu bytes < %zu", scratch_bytes, (size_t)k.nblk * k.P * sizeof(int32_t));
+    return GTR_E_ARG;
+  }
+  k.bcnt = static_cast<int32_t*>(scratch);
+  hipStream_t s = (hipStream_t)stream;
+  (void)hipMemsetAsync(sh->status, 0, sizeof(int32_t), s);
+  hipLaunchKernelGGL(k_route_count, dim3(k.nblk), dim3(RB_THREADS), 0, s, k);
+  GTR_HIP_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(RB_THREADS), 0, s, k);
+  GTR_HIP_CHECK_LAUNCH();
+  hipLaunchKernelGGL(k_route_write, dim3(k.nblk), dim3(RB_THREADS), 0, s, k);
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+int gtr_shard_serve(const gtr_shard* sh, const int32_t* recv_ids, float* send_rows, gtr_stream_t stream) {
+  if (!shard_ok(sh) || !recv_ids || !send_rows) {
+    set_error("gtr_shard_serve: bad arguments");
+    return GTR_E_ARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t entries = (int64_t)sh->world * sh->cap;
+  hipLaunchKernelGGL(k_shard_claim, dim3((unsigned)((entries * 16 + GTR_BLOCK - 1) / GTR_BLOCK)), dim3(GTR_BLOCK), 0,
+                     s, *sh, recv_ids, sh->opt.step_dev);
+  GTR_HIP_CHECK_LAUNCH();
+  const int64_t threads = entries * (sh->dim / 4);
+  const dim3 grid((unsigned)((threads + GTR_BLOCK - 1) / GTR_BLOCK));
+  switch (sh->dim) {
+    case 32: hipLaunchKernelGGL(k_shard_copy<32>, grid, dim3(GTR_BLOCK), 0, s, *sh, recv_ids, send_rows); break;
+    case 64: hipLaunchKernelGGL(k_shard_copy<64>, grid, dim3(GTR_BLOCK), 0, s, *sh, recv_ids, send_rows); break;
+    case 128: hipLaunchKernelGGL(k_shard_copy<128>, grid, dim3(GTR_BLOCK), 0, s, *sh, recv_ids, send_rows); break;
+    default: hipLaunchKernelGGL(k_shard_copy<256>, grid, dim3(GTR_BLOCK), 0, s, *sh, recv_ids, send_rows); break;
+  }
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+int gtr_shard_pack(const gtr_batch* bt, const gtr_shard* sh, const gtr_tail* tail, const int32_t* ckeys,
+                   const gtr_segment* segs, int nseg, float* send_grads, float* small_pack, gtr_stream_t stream) {
+  if (!bt || !shard_ok(sh) || !tail || !ckeys || !send_grads || !small_pack || nseg < 0 ||
+      nseg > GTR_SMALL_MAX_SEG || (nseg > 0 && !segs) || !tail->skeys || !tail->svals || !tail->dx0 || !tail->se ||
+      !tail->coef_tgt || !tail->coef_neg || (!tail->loss_part && !tail->loss_out)) {
+    set_error("gtr_shard_pack: bad arguments");
+    return GTR_E_ARG;
+  }
+  PackK k{};
+  k.bt = *bt;
+  k.tl = *tail;
+  k.ckeys = ckeys;
+  k.send_grads = send_grads;
+  k.small_pack = small_pack;
+  k.T = sh->num_items;
+  k.m_cap = bt->n_cap + bt->b_cap * (1 + bt->n_neg);
+  const int NG = GTR_BLOCK / (sh->dim / 4);
+  k.nb_rows = (k.m_cap + NG - 1) / NG;
+  k.nseg = nseg;
+  for (int i = 0; i < nseg; ++i) k.segs[i] = segs[i];
+  int nb_small = (int)((tail->flat_total + GTR_BLOCK - 1) / GTR_BLOCK);
+  if (nb_small == 0) nb_small = 1;
+  const dim3 grid(k.nb_rows + nb_small);
+  hipStream_t s = (hipStream_t)stream;
+  switch (sh->dim) {
+    case 32: hipLaunchKernelGGL(k_shard_pack<32>, grid, dim3(GTR_BLOCK), 0, s, k); break;
+    case 64: hipLaunchKernelGGL(k_shard_pack<64>, grid, dim3(GTR_BLOCK), 0, s, k); break;
+    case 128: hipLaunchKernelGGL(k_shard_pack<128>, grid, dim3(GTR_BLOCK), 0, s, k); break;
+    default: hipLaunchKernelGGL(k_shard_pack<256>, grid, dim3(GTR_BLOCK), 0, s, k); break;
+  }
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+int gtr_shard_update(const gtr_shard* sh, const gtr_tail* tail, const int32_t* recv_ids, const float* recv_grads,
+                     const float* small_all, int64_t small_words, gtr_stream_t stream) {
+  if (!shard_ok(sh) || !tail || !recv_ids || !recv_grads || !small_all || small_words < tail->flat_total + 1 ||
+      (tail->flat_total > 0 && (!tail->flat || !tail->flat_m || !tail->flat_v))) {
+    set_error("gtr_shard_update: bad arguments");
+    return GTR_E_ARG;
+  }
+  UpdateK k{};
+  k.sh = *sh;
+  k.tl = *tail;
+  k.recv_ids = recv_ids;
+  k.recv_grads = recv_grads;
+  k.small_all = small_all;
+  k.small_words = small_words;
+  const int64_t entries = (int64_t)sh->world * sh->cap;
+  k.nb_rows = (int)((entries * (sh->dim / 4) + GTR_BLOCK - 1) / GTR_BLOCK);
+  const int nb_small = (int)((tail->flat_total + 1 + GTR_BLOCK - 1) / GTR_BLOCK);
+  const dim3 grid(k.nb_rows + nb_small);
+  hipStream_t s = (hipStream_t)stream;
+  switch (sh->dim) {
+    case 32: hipLaunchKernelGGL(k_shard_update<32>, grid, dim3(GTR_BLOCK), 0, s, k); break;
+    case 64: hipLaunchKernelGGL(k_shard_update<64>, grid, dim3(GTR_BLOCK), 0, s, k); break;
+    case 128: hipLaunchKernelGGL(k_shard_update<128>, grid, dim3(GTR_BLOCK), 0, s, k); break;
+    default: hipLaunchKernelGGL(k_shard_update<256>, grid, dim3(GTR_BLOCK), 0, s, k); break;
+  }
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+}  // extern "C"

@@ -118,6 +118,14 @@ class GtrDpLayout(C.Structure):
     ]
 
 
+class GtrShard(C.Structure):
+    _fields_ = [
+        ("num_items", i32), ("world", i32), ("rank", i32), ("cap", i32), ("local_rows", i32), ("dim", i32),
+        ("table", P), ("m", P), ("v", P), ("stamp", P), ("consts", P), ("consts_cap", i32), ("pad", i32),
+        ("status", P), ("opt", GtrAdam),
+    ]
+
+
 GTR_LOSS = {"none": 0, "bpr": 1, "listwise": 2, "sampled_softmax": 2, "dual": 3}
 RO_FWD, RO_LOSS, RO_BWD = 1, 2, 4
 SMALL_MAX_SEG = 48
@@ -157,6 +165,11 @@ _SIGS = {
     "gtr_lap_plan": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P]),
     "gtr_lap_spmm": (C.c_int, [P, P, C.c_int, C.c_int, P, i64, P, i64, P, P, P, f32, f32, P]),
     "gtr_lap_gram": (C.c_int, [P, P, C.c_int, C.c_int, P, C.c_int, P, P]),
+    "gtr_shard_route_scratch": (C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_size_t)]),
+    "gtr_shard_route": (C.c_int, [P, P, P, P, P, P, P, P, P, P, C.c_int, P, P, C.c_size_t, P]),
+    "gtr_shard_serve": (C.c_int, [P, P, P, P]),
+    "gtr_shard_pack": (C.c_int, [P, P, P, P, P, C.c_int, P, P, P]),
+    "gtr_shard_update": (C.c_int, [P, P, P, P, P, i64, P]),
     "gtr_topk_workspace_bytes": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_size_t)]),
     "gtr_score_topk": (C.c_int, [P, C.c_int, C.c_int, P, C.c_int, C.c_int, P, P, P, C.c_size_t, P]),
     "gtr_score_topk_masked": (C.c_int, [P, C.c_int, C.c_int, P, C.c_int, C.c_int, P, P, P, P, P, C.c_size_t, P]),

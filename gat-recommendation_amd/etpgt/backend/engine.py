@@ -278,10 +278,12 @@ class Engine:
         cfg.consumer_reduce = int(cred) if cred is not None else (1 if ws.g_cap <= 64 else 0)
         return cfg
 
-    def fill_embed(self):
+    def fill_embed(self, table: int | None = None):
+        """Layer-0 inputs; ``table``: another row buffer standing in for the item table
+        (the fetched rows of the row-sharded step, indexed by the batch's compact ids)."""
         m = self.model
         e = self.embed
-        e.table = m.item_embedding.weight.data_ptr()
+        e.table = m.item_embedding.weight.data_ptr() if table is None else table
         if self.K > 0:
             pe = m.laplacian_pe._cached_pe
             e.pe_tab = None if pe is None else pe.data_ptr()
@@ -316,7 +318,7 @@ class Engine:
             L.check(lib.gtr_conv_fwd(C.byref(cfg), C.byref(bs), C.byref(emb), ws.structs, l, st), "conv_fwd")
         self.run_head(ws, cfg, bs, flags, loss_kind, temperature, alpha)
 
-    def run_head(self, ws, cfg, bs, flags, loss_kind=0, temperature=1.0, alpha=0.7, dse_out=False):
+    def run_head(self, ws, cfg, bs, flags, loss_kind=0, temperature=1.0, alpha=0.7, dse_out=False, table=None):
         h = ws.head
         h.flags = flags
         h.loss_kind = loss_kind
@@ -330,8 +332,9 @@ class Engine:
         h.loss_part = ws.loss_part.data_ptr()
         h.loss_out = ws.loss_out.data_ptr()
         h.cnt = ws.head_cnt.data_ptr()
-        L.check(L.lib().gtr_readout_loss(C.byref(cfg), C.byref(bs), self.model.item_embedding.weight.data_ptr(),
-                                         ws.structs, C.byref(h), self.stream()), "readout_loss")
+        tab = self.model.item_embedding.weight.data_ptr() if table is None else table
+        L.check(L.lib().gtr_readout_loss(C.byref(cfg), C.byref(bs), tab, ws.structs, C.byref(h), self.stream()),
+                "readout_loss")
 
     def _wgrad(self, ws, cfg, bs, l0, l1, st):
         pe_tab = None

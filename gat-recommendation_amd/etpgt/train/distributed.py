@@ -95,6 +95,21 @@ def all_gather_packs(recv: torch.Tensor, pack: torch.Tensor, group=None) -> None
         dist.all_gather_into_tensor(recv.view(-1), pack.reshape(-1), group=group)
 
 
+def all_to_all(recv: torch.Tensor, send: torch.Tensor, group=None) -> None:
+    """recv[p] <- rank p's send[my rank] for equal blocks along dim 0 (one collective).
+    RCCL on device tensors; a gloo group round-trips through host memory; without an
+    initialised process group (one rank) the block is copied."""
+    if not (dist.is_available() and dist.is_initialized()):
+        recv.copy_(send)
+        return
+    if dist.get_backend(group) == "gloo":
+        host = torch.empty(send.shape, dtype=send.dtype)
+        dist.all_to_all_single(host, send.detach().cpu(), group=group)
+        recv.copy_(host)
+    else:
+        dist.all_to_all_single(recv, send, group=group)
+
+
 class _Done:
     def wait(self):
         return None

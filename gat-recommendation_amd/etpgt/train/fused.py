@@ -34,7 +34,7 @@ class FusedTrainStep:
                  weight_decay: float = 1e-5, decoupled: bool = True, loss: str = "bpr",
                  temperature: float = 1.0, alpha: float = 0.7, caps: Caps | None = None,
                  use_graph: bool = True, data_parallel: bool | None = None, process_group=None,
-                 lazy: bool = False, sync_bn: bool = False, lagged: bool = False):
+                 lazy: bool = False, sync_bn: bool = False, lagged: bool = False, shard_table: bool = False):
         if loss not in ("bpr", "listwise", "dual", "sampled_softmax"):
             raise ValueError(f"Unknown loss type: {loss}")
         self.model = model
@@ -51,7 +51,13 @@ class FusedTrainStep:
 
         self.group = process_group
         self.rank, self.world = world_info(process_group)
+        # row-sharded item table (etpgt.train.sharded, SURVEY.md §8e ii): rank p owns the rows
+        # r % P == p and their AdamW state; rows travel by all-to-all
+        self.shard_table = bool(shard_table)
+        if self.shard_table and (lazy or lagged):
+            raise ValueError("the row-sharded table keeps its own lazy stamps (no lazy/lagged option)")
         self.data_parallel = (self.world > 1) if data_parallel is None else bool(data_parallel)
+        self.data_parallel = self.data_parallel or self.shard_table
         # SyncBN: BatchNorm statistics over every rank's batch (all-gathered partials per
         # BatchNorm), so N ranks train exactly like one GPU on the concatenated batch
         self.sync_bn = bool(sync_bn)
@@ -68,11 +74,12 @@ class FusedTrainStep:
         self.step_dev = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self.adam.step_dev = self.step_dev.data_ptr()
         self.adam.step_offset = 0  # kernels after gtr_step_begin see the current step
-        self.m_tab = torch.zeros(T, D, dtype=torch.float32, device=self.dev)
-        self.v_tab = torch.zeros(T, D, dtype=torch.float32, device=self.dev)
+        tab_rows = 1 if self.shard_table else T  # sharded: the moments live in the shards
+        self.m_tab = torch.zeros(tab_rows, D, dtype=torch.float32, device=self.dev)
+        self.v_tab = torch.zeros(tab_rows, D, dtype=torch.float32, device=self.dev)
         self.m_flat = torch.zeros_like(eng.flat.flat)
         self.v_flat = torch.zeros_like(eng.flat.flat)
-        self.stamp = torch.zeros(T, dtype=torch.int32, device=self.dev)
+        self.stamp = torch.zeros(tab_rows, dtype=torch.int32, device=self.dev)
         # deferred zero-gradient AdamW of untouched table rows (gtr_lazy in gtr.h):
         # bitwise-identical to the dense update, applied when a row is next read or on flush()
         # lagged: lazy-table stamps, and the chain's launches sweep the PREVIOUS step's
@@ -87,6 +94,13 @@ class FusedTrainStep:
         if self.lazy:
             self._lazy_alloc(1 << 16)
             model.__dict__["_lazy_sync"] = self.flush  # forward / predict / state_dict bring rows up to date
+        self.shard_state = None
+        self.shard = None
+        if self.shard_table:
+            from etpgt.train.sharded import ShardState
+
+            self.shard_state = ShardState(self, process_group)
+            model.__dict__["_lazy_sync"] = self._shard_guard
         self.caps = None
         self.graph = None
         self.builder = None
@@ -222,7 +236,12 @@ class FusedTrainStep:
         self.carry = torch.zeros(max(nc, 4), dtype=torch.float32, device=self.dev) if nc > 0 else None
         t.carry = self.carry.data_ptr() if self.carry is not None else None
         self.tail = t
-        if self.data_parallel:
+        if self.shard_table:
+            from etpgt.train.sharded import ShardExchange
+
+            self.dp = None
+            self.shard = ShardExchange(self, self.shard_state)
+        elif self.data_parallel:
             from etpgt.train.distributed import DpExchange
 
             self.dp = DpExchange(self, self.group)
@@ -363,6 +382,8 @@ class FusedTrainStep:
         """The step as (launches, collective-after) pieces: one piece single-GPU; the
         halves around the gradient all-gather in DP mode; with SyncBN also a cut after
         every producer of BatchNorm partials (all-gather of the partials)."""
+        if self.shard is not None:
+            return self._shard_pieces(with_pe)
         if self.dp is None:
             def whole():
                 self._launch_a(with_pe)
@@ -408,6 +429,82 @@ class FusedTrainStep:
         pieces.append((lambda: self._launch_b(with_pe), None))
         return pieces
 
+    def _shard_pieces(self, with_pe: bool):
+        """Row-sharded table: begin + route | A2A ids | serve | A2A rows | forward, loss,
+        backward (SyncBN: cut after every BatchNorm partial producer) + pack | A2A grads +
+        all-gather of the small packs | owner update (etpgt.train.sharded)."""
+        eng, ws, cfg, sh = self.eng, self.ws, self.cfg, self.shard
+        bs = self.bs_pe if with_pe else self.bs
+        bc = sh.compact(with_pe)
+        lib = L.lib()
+        Lc = eng.L
+        tab = sh.table_ptr()
+
+        def st():
+            return torch.cuda.current_stream(self.dev).cuda_stream
+
+        def begin_route():
+            if self.builder is not None:
+                self.builder.launch(bs, self.caps, st(), self._builder_B)
+            L.check(lib.gtr_step_begin(C.byref(bs), eng.T, self.keys.data_ptr(), self.vals.data_ptr(),
+                                       self.skeys.data_ptr(), self.svals.data_ptr(), None, self.step_dev.data_ptr(),
+                                       eng.rng_ctr.data_ptr(), self.sort_tmp.data_ptr(), self.sort_tmp.numel(), st()),
+                    "step_begin")
+            sh.route(bs, st())
+
+        def fwd(l):
+            L.check(lib.gtr_conv_fwd(C.byref(cfg), C.byref(bc), C.byref(eng.fill_embed(tab)), ws.structs, l, st()),
+                    "conv_fwd")
+
+        def head():
+            eng.run_head(ws, cfg, bc, L.RO_FWD | L.RO_LOSS | L.RO_BWD, self.loss_kind, self.temperature, self.alpha,
+                         table=tab)
+
+        def bwd(l):
+            L.check(lib.gtr_conv_bwd(C.byref(cfg), C.byref(bc), ws.structs, l, ws.dx0.data_ptr(), st()), "conv_bwd")
+            if l == 0:
+                eng._wgrad(ws, cfg, bc, 0, Lc, st())
+                sh.pack(bs, st())
+
+        pieces = [(begin_route, sh.exchange_ids), (lambda: sh.serve(st()), sh.exchange_rows)]
+        if not self.sync_bn:
+            def middle():
+                for l in range(Lc):
+                    fwd(l)
+                head()
+                for l in range(Lc - 1, -1, -1):
+                    bwd(l)
+            pieces.append((middle, sh.exchange_grads))
+        else:
+            for l in range(Lc):
+                pieces.append(((lambda l=l: fwd(l)), (lambda l=l: self._gather_fwd(l))))
+            pieces.append((head, lambda: self._gather_bwd(Lc - 1)))
+            for l in range(Lc - 1, 0, -1):
+                pieces.append(((lambda l=l: bwd(l)), (lambda l=l: self._gather_bwd(l - 1))))
+            pieces.append(((lambda: bwd(0)), sh.exchange_grads))
+        pieces.append((lambda: sh.update(st()), None))
+        return pieces
+
+    def _shard_guard(self):
+        """Model hook (forward / predict / state_dict): the item table of a sharded step
+        lives in the ranks' shards; reading the model's copy needs sync_table() first."""
+        if self.shard_state is not None and self.shard_state.stale:
+            raise RuntimeError("the item table is row-sharded across the ranks: call "
+                               "FusedTrainStep.sync_table() on every rank before reading the model")
+
+    def sync_table(self):
+        """Collective (every rank): bring the shards to the current step and write the full
+        table into the model's item_embedding.weight (and the moments into m_tab / v_tab)."""
+        if self.shard_state is None:
+            self.flush()
+            return
+        self.shard_state.check_status(block=True)
+        tab, m, v = self.shard_state.gather_table()
+        with torch.no_grad():
+            self.model.item_embedding.weight.data.copy_(tab)
+        self.m_tab, self.v_tab = m, v
+        self.shard_state.stale = False
+
     def _early_pieces(self, with_pe: bool):
         """DP with the early union: begin | all-gather the sorted keys (async, overlapped
         with the forward) | forward | wait + union stamp + readout + backward (carrying the
@@ -451,7 +548,7 @@ class FusedTrainStep:
         """RCCL collectives captured inside the step's hipGraph (one graph per step instead
         of one per piece).  Only for the nccl (RCCL) backend -- gloo round-trips through
         host memory -- and off with GTR_GRAPH_COLL=0."""
-        if self.dp is None or self.world <= 1 and os.environ.get("GTR_GRAPH_COLL") != "1":
+        if (self.dp is None and self.shard is None) or self.world <= 1 and os.environ.get("GTR_GRAPH_COLL") != "1":
             return False
         if os.environ.get("GTR_GRAPH_COLL", "1") == "0" or self._coll_capture_refused:
             return False
@@ -493,6 +590,8 @@ class FusedTrainStep:
         image i instead of copying it into the step's blob first."""
         if self.caps is None:
             raise RuntimeError("bind the step's capacities first (load one batch)")
+        if self.shard is not None:
+            raise NotImplementedError("resident batch images are not supported with the row-sharded table")
         n = self.blob.numel()
         for b in blobs:
             if b.numel() != n or b.dtype != self.blob.dtype or b.device != self.blob.device:
@@ -612,6 +711,12 @@ class FusedTrainStep:
         self.eng.check_intact()
         if not self.model.training:
             raise RuntimeError("FusedTrainStep requires model.train()")
+        if self.shard_state is not None:
+            self._host_steps += 1
+            if self.shard_state.ensure_steps(self._host_steps):
+                self.graph = self.graph_pe = self.graph_b = None  # consts moved: recapture
+                self.resident_graphs = None
+            self.shard_state.check_status()
         if self.lazy:
             if self._host_steps + 2 >= self.lz.cap:
                 self._lazy_alloc(2 * self.lz.cap)
@@ -647,7 +752,10 @@ class FusedTrainStep:
         return int(self.step_dev.item())
 
     def export_optimizer_state(self, optimizer: torch.optim.Optimizer):
-        """Write exp_avg / exp_avg_sq / step into a torch Adam(W) optimizer's state."""
+        """Write exp_avg / exp_avg_sq / step into a torch Adam(W) optimizer's state
+        (row-sharded table: collective, gathers the shards first)."""
+        if self.shard_state is not None:
+            self.sync_table()
         self.flush()
         t = torch.tensor(float(self.steps))
         tab = self.model.item_embedding.weight

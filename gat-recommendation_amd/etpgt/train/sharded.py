@@ -1,0 +1,247 @@
+"""Row-sharded item table for the multi-GPU step (SURVEY.md §8e ii).
+
+The reference trains one dense ``nn.Embedding(T, d)`` (``etpgt/model/base.py:36``) with a
+dense AdamW (``scripts/train/train_baseline.py:252-256``); it has no multi-GPU path.  In
+the data-parallel step of ``etpgt.train.distributed`` every rank keeps the whole table
+and its moments and receives every rank's touched rows.  Here the table, ``exp_avg``,
+``exp_avg_sq`` and the lazy-table stamps are row-sharded instead: global row ``r`` lives
+on rank ``r % P`` as local row ``r // P`` (cyclic: Zipf-hot items spread over every
+owner).  Per step (``include/gtr.h``, ``gtr_shard_*``):
+
+    begin     sorted contribution list of the rank's own batch (global row ids)
+    route     unique rows per owner -> send_ids[P][cap]; the batch's ids -> compact rows
+    A2A ids   RCCL all-to-all
+    serve     owners bring the requested rows to step t-1 (bitwise the dense zero-gradient
+              AdamW) -> send_rows[P][cap][D]
+    A2A rows  == the layer-0 halo fetch of source embeddings
+    forward / loss / backward / weight gradients on the compact rows (unchanged kernels)
+    pack      summed gradient row per requested row -> send_grads; small-parameter
+              gradient + loss -> small_pack
+    A2A grads + all-gather of the small packs
+    update    owners: rank-ordered sum / P + AdamW (the arithmetic of gtr_dp_tail), stamps;
+              every rank: the small parameters from the gathered packs
+
+Per rank and step the table traffic is the rows its batch touches plus the rows it owns
+that any rank touched, instead of every rank's touched rows (all-gather) or the whole
+table (dense sweep).  Results are bit-identical to the replicated data-parallel step
+with the lazy table (same per-rank sums, same rank-ordered averaging, same catch-up).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+
+import torch
+
+from etpgt.backend import _lib as L
+from etpgt.train.distributed import all_gather_packs, all_to_all, world_info
+
+
+def shard_capacity(m_cap: int, num_items: int, world: int, slack: float | None = None) -> int:
+    """Slots per peer block (count slot included).  A requester asks one owner for at
+    most min(m_cap, rows the owner holds) distinct rows; under cyclic ownership the
+    distinct ids of a batch split evenly, so the block is sized at ``slack`` x the even
+    share (the all-to-alls move whole blocks) unless the exact bound is smaller.  A batch
+    that overflows a block is flagged (``status``) and raises on the host."""
+    if slack is None:
+        slack = float(os.environ.get("GTR_SHARD_SLACK", "1.5"))
+    exact = min(m_cap, (num_items + world - 1) // world)
+    even = max(64, int(math.ceil(slack * m_cap / world)) + 64)
+    return 1 + min(exact, even)
+
+
+class ShardState:
+    """This rank's rows of the item table and their AdamW / lazy-table state."""
+
+    def __init__(self, step, group=None):
+        self.step = step
+        self.group = group
+        self.rank, self.world = world_info(group)
+        if self.world > 16:
+            raise ValueError("the row-sharded table supports at most 16 ranks")
+        eng = step.eng
+        T, D, P, p = eng.T, eng.D, self.world, self.rank
+        dev = step.dev
+        self.T, self.D = T, D
+        self.local_rows = (T - p + P - 1) // P
+        self.rows_max = (T + P - 1) // P
+        w = eng.model.item_embedding.weight.data
+        self.table = w[p::P].contiguous().clone()  # [local_rows, D]
+        self.m = torch.zeros_like(self.table)
+        self.v = torch.zeros_like(self.table)
+        self.stamp = torch.zeros(self.local_rows, dtype=torch.int32, device=dev)
+        self.status = torch.zeros(4, dtype=torch.int32, device=dev)
+        self.status_host = torch.zeros(4, dtype=torch.int32).pin_memory()
+        self._status_event = None
+        self.consts = None
+        self.stale = False  # the model's item_embedding.weight lags the shards
+        self.s = L.GtrShard()
+        self._alloc_consts(1 << 12)
+
+    def _alloc_consts(self, cap: int):
+        c = torch.zeros(cap, 2, dtype=torch.float32, device=self.step.dev)
+        if self.consts is not None:
+            k = min(cap, self.consts.shape[0])
+            c[:k].copy_(self.consts[:k])
+        self.consts = c
+        self._fill()
+
+    def _fill(self):
+        s = self.s
+        s.num_items, s.world, s.rank, s.local_rows, s.dim = self.T, self.world, self.rank, self.local_rows, self.D
+        s.table, s.m, s.v, s.stamp = (self.table.data_ptr(), self.m.data_ptr(), self.v.data_ptr(),
+                                      self.stamp.data_ptr())
+        s.consts, s.consts_cap = self.consts.data_ptr(), self.consts.shape[0]
+        s.status = self.status.data_ptr()
+        s.opt = self.step.adam
+
+    def ensure_steps(self, steps: int) -> bool:
+        """Grow the per-step scalar table before step ``steps``; True if pointers moved."""
+        if steps + 2 < self.consts.shape[0]:
+            return False
+        self._alloc_consts(2 * self.consts.shape[0])
+        return True
+
+    def check_status(self, block: bool = False):
+        """Raise if any step since the last check overflowed an exchange block (the
+        status word is copied asynchronously after each step and read one step later)."""
+        if self._status_event is not None and (block or self._status_event.query()):
+            self._status_event.synchronize()
+            if int(self.status_host[1]) != 0:
+                raise RuntimeError("row-sharded table: a batch requested more rows from one owner than the "
+                                   "exchange capacity holds (raise GTR_SHARD_SLACK)")
+            self._status_event = None
+        if self._status_event is None:
+            self.status_host.copy_(self.status, non_blocking=True)
+            self._status_event = torch.cuda.Event()
+            self._status_event.record()
+
+    # ---------------------------------------------------------------- the full table
+    def flush(self):
+        """Bring every local row to the current step (lazy zero-gradient updates)."""
+        st = self.step
+        lz = L.GtrLazy()
+        lz.consts, lz.cap = self.consts.data_ptr(), self.consts.shape[0]
+        lz.table, lz.m, lz.v, lz.opt = self.table.data_ptr(), self.m.data_ptr(), self.v.data_ptr(), st.adam
+        L.check(L.lib().gtr_lazy_flush(self.local_rows, self.D, self.stamp.data_ptr(), st.step_dev.data_ptr(),
+                                       C.byref(lz), torch.cuda.current_stream(st.dev).cuda_stream), "lazy_flush")
+
+    def _gather(self, local: torch.Tensor) -> torch.Tensor:
+        P, D = self.world, self.D
+        pad = torch.zeros(self.rows_max, D, dtype=local.dtype, device=local.device)
+        pad[: self.local_rows].copy_(local)
+        allr = torch.zeros(P, self.rows_max * D, dtype=local.dtype, device=local.device)
+        all_gather_packs(allr, pad.view(-1), self.group)
+        return allr.view(P, self.rows_max, D).transpose(0, 1).reshape(self.rows_max * P, D)[: self.T]
+
+    def gather_table(self):
+        """Collective: the full [T, D] table (and its moments) on every rank."""
+        self.flush()
+        return self._gather(self.table), self._gather(self.m), self._gather(self.v)
+
+    def sync_model(self):
+        """Collective: write the full table into the model's item_embedding.weight."""
+        tab, _, _ = self.gather_table()
+        with torch.no_grad():
+            self.step.eng.model.item_embedding.weight.data.copy_(tab)
+        self.stale = False
+
+
+class ShardExchange:
+    """Per-capacity exchange buffers and launches of the sharded step."""
+
+    def __init__(self, step, state: ShardState):
+        self.step, self.state = step, state
+        eng, caps, dev = step.eng, step.caps, step.dev
+        P, D = state.world, eng.D
+        self.m_cap = caps.n_cap + caps.b_cap * (1 + caps.n_neg)
+        self.cap = shard_capacity(self.m_cap, eng.T, P)
+        state.s.cap = self.cap
+        slots = P * self.cap
+        i32 = dict(dtype=torch.int32, device=dev)
+        f32 = dict(dtype=torch.float32, device=dev)
+        self.send_ids = torch.zeros(slots, **i32)
+        self.recv_ids = torch.zeros(slots, **i32)
+        self.send_rows = torch.zeros(slots, D, **f32)
+        self.recv_rows = torch.zeros(slots, D, **f32)  # the compact "table" the layer kernels read
+        self.send_grads = torch.zeros(slots, D, **f32)
+        self.recv_grads = torch.zeros(slots, D, **f32)
+        self.ckeys = torch.zeros(self.m_cap, **i32)
+        self.node_item_c = torch.zeros(caps.n_cap, **i32)
+        self.target_c = torch.zeros(caps.b_cap, **i32)
+        self.negatives_c = torch.zeros(max(1, caps.b_cap * caps.n_neg), **i32)
+        self.node_pe_c = torch.zeros(caps.n_cap, eng.K, **f32) if eng.K > 0 else None
+        nb = C.c_size_t(0)
+        L.check(L.lib().gtr_shard_route_scratch(self.m_cap, P, C.byref(nb)), "shard_route_scratch")
+        self.scratch = torch.zeros(max(int(nb.value), 16), dtype=torch.uint8, device=dev)
+        F = eng.flat.layout.total
+        self.small_words = (F + 1 + 3) & ~3
+        self.small_pack = torch.zeros(self.small_words, **f32)
+        self.small_all = torch.zeros(P, self.small_words, **f32)
+        self.bs_c = self._compact(step.bs)
+        self.bs_c_pe = self._compact(step.bs_pe) if step.bs_pe is not None else None
+
+    def _compact(self, bs):
+        """The batch struct the layer kernels read: ids -> compact rows; PE per node."""
+        c = L.GtrBatch()
+        C.memmove(C.byref(c), C.byref(bs), C.sizeof(bs))
+        c.node_item, c.target, c.negatives = (self.node_item_c.data_ptr(), self.target_c.data_ptr(),
+                                              self.negatives_c.data_ptr())
+        if bs.node_pe is None and self.node_pe_c is not None:
+            c.node_pe = self.node_pe_c.data_ptr()
+        return c
+
+    def table_ptr(self) -> int:
+        return self.recv_rows.data_ptr()
+
+    def compact(self, with_pe: bool):
+        return self.bs_c_pe if with_pe else self.bs_c
+
+    # ---------------------------------------------------------------- launches
+    def route(self, bs, stream):
+        st, eng = self.step, self.step.eng
+        pe_tab, node_pe = None, None
+        if self.node_pe_c is not None and bs.node_pe is None:
+            pe = eng.model.laplacian_pe._cached_pe
+            if pe is None:
+                raise RuntimeError("Laplacian PE not precomputed. Call precompute() first.")
+            pe_tab, node_pe = pe.data_ptr(), self.node_pe_c.data_ptr()
+        L.check(L.lib().gtr_shard_route(C.byref(bs), st.skeys.data_ptr(), st.svals.data_ptr(), C.byref(self.state.s),
+                                        self.send_ids.data_ptr(), self.ckeys.data_ptr(), self.node_item_c.data_ptr(),
+                                        self.target_c.data_ptr(), self.negatives_c.data_ptr(), pe_tab, eng.K, node_pe,
+                                        self.scratch.data_ptr(), self.scratch.numel(), stream), "shard_route")
+
+    def exchange_ids(self):
+        all_to_all(self.recv_ids, self.send_ids, self.state.group)
+
+    def serve(self, stream):
+        L.check(L.lib().gtr_shard_serve(C.byref(self.state.s), self.recv_ids.data_ptr(), self.send_rows.data_ptr(),
+                                        stream), "shard_serve")
+
+    def exchange_rows(self):
+        all_to_all(self.recv_rows, self.send_rows, self.state.group)
+
+    def pack(self, bs, stream):
+        st = self.step
+        L.check(L.lib().gtr_shard_pack(C.byref(bs), C.byref(self.state.s), C.byref(st.tail), self.ckeys.data_ptr(),
+                                       st.segs, st.nseg, self.send_grads.data_ptr(), self.small_pack.data_ptr(),
+                                       stream), "shard_pack")
+
+    def exchange_grads(self):
+        all_to_all(self.recv_grads, self.send_grads, self.state.group)
+        all_gather_packs(self.small_all, self.small_pack, self.state.group)
+
+    def update(self, stream):
+        st = self.step
+        L.check(L.lib().gtr_shard_update(C.byref(self.state.s), C.byref(st.tail), self.recv_ids.data_ptr(),
+                                         self.recv_grads.data_ptr(), self.small_all.data_ptr(), self.small_words,
+                                         stream), "shard_update")
+        self.state.stale = True
+
+    def volume(self) -> dict:
+        """Bytes each rank sends per step over the collectives (fixed-size blocks)."""
+        P, D = self.state.world, self.step.eng.D
+        return {"ids": 4 * P * self.cap, "rows": 4 * P * self.cap * D, "grads": 4 * P * self.cap * D,
+                "small": 4 * self.small_words * P, "cap": self.cap}

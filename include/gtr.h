@@ -403,6 +403,60 @@ int gtr_dp_union_stamp(const int32_t* keys_all, int64_t n, int num_items, int32_
 int gtr_dp_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tail, const gtr_dp_layout* lay,
                 const float* recv, int32_t* slot, const gtr_adam* opt, gtr_stream_t stream);
 
+/* ---- row-sharded item table (etpgt.train.sharded; SURVEY.md §8e ii) ---------------
+ * Replaces, across P ranks, the one dense nn.Embedding(T, d) of base.py:36 and its dense
+ * AdamW state (train_baseline.py:252-256): global row r lives on rank r % P as local row
+ * r / P, with its exp_avg / exp_avg_sq and a lazy-table stamp (gtr_lazy semantics: the
+ * step through which the row is current).  Exchange buffers are [P][cap] blocks whose
+ * slot 0 holds the block's count; "compact" row q*cap + 1 + j of a requester's fetched
+ * rows is the j-th (ascending) row it requested from owner q.  A step:
+ *   gtr_step_begin (global keys, stamp NULL) -> gtr_shard_route -> all-to-all send_ids
+ *   -> gtr_shard_serve -> all-to-all send_rows -> forward/backward on the compact batch
+ *   (table = fetched rows) -> gtr_shard_pack -> all-to-all send_grads + all-gather of
+ *   small_pack -> gtr_shard_update.                                                   */
+typedef struct gtr_shard {
+  int32_t num_items;   /* T (global rows)                                       */
+  int32_t world;       /* P (<= 16)                                             */
+  int32_t rank;
+  int32_t cap;         /* slots per peer block, the count slot included        */
+  int32_t local_rows;  /* (T - rank + P - 1) / P                                */
+  int32_t dim;
+  float* table;        /* [local_rows, D] this rank's rows, exp_avg, exp_avg_sq */
+  float* m;
+  float* v;
+  int32_t* stamp;      /* [local_rows] step through which the row is current   */
+  float* consts;       /* [consts_cap][2] per-step AdamW scalars (gtr_lazy)     */
+  int32_t consts_cap;
+  int32_t pad;
+  int32_t* status;     /* [2]: [0] this step overflowed a block, [1] sticky     */
+  gtr_adam opt;        /* by value; step_offset 0 (runs after gtr_step_begin)   */
+} gtr_shard;
+
+/* Bytes of route scratch at contribution capacity m_cap.                            */
+int gtr_shard_route_scratch(int m_cap, int world, size_t* bytes);
+/* Requester: from the sorted contribution list (skeys / svals of gtr_step_begin), the
+ * unique rows per owner -> send_ids [P][cap]; ckeys [m_cap] = compact row of each sorted
+ * slot (-1: unused); the batch's node / target / negative ids as compact rows (the
+ * arrays of the batch the layer kernels then read); node_pe [n_cap][pe_k] = pe_tab rows
+ * of the nodes when given (LapPE: the layer kernels read node_pe, not pe_tab[id]).     */
+int gtr_shard_route(const gtr_batch* bt, const int32_t* skeys, const int32_t* svals, const gtr_shard* sh,
+                    int32_t* send_ids, int32_t* ckeys, int32_t* node_item_c, int32_t* target_c, int32_t* negatives_c,
+                    const float* pe_tab, int pe_k, float* node_pe, void* scratch, size_t scratch_bytes,
+                    gtr_stream_t stream);
+/* Owner: the rows every peer requested (recv_ids = the all-to-all of send_ids), brought
+ * to step t-1, into send_rows [P][cap][D] (row j of block r = recv_ids[r][j]).       */
+int gtr_shard_serve(const gtr_shard* sh, const int32_t* recv_ids, float* send_rows, gtr_stream_t stream);
+/* Requester: summed table-gradient row of every requested row -> send_grads [P][cap][D]
+ * at its compact slot; summed small-parameter gradient [flat_total] + local loss ->
+ * small_pack [flat_total + 1].                                                        */
+int gtr_shard_pack(const gtr_batch* bt, const gtr_shard* sh, const gtr_tail* tail, const int32_t* ckeys,
+                   const gtr_segment* segs, int nseg, float* send_grads, float* small_pack, gtr_stream_t stream);
+/* Owner: AdamW at step t of every requested row with the rank-averaged gradient (peers
+ * summed in rank order), stamps t, consts[t]; small parameters from small_all
+ * [P][small_words] (rank-averaged) and the rank-averaged loss -> tail->loss_out.      */
+int gtr_shard_update(const gtr_shard* sh, const gtr_tail* tail, const int32_t* recv_ids, const float* recv_grads,
+                     const float* small_all, int64_t small_words, gtr_stream_t stream);
+
 /* ---- evaluation: full-catalog scoring + top-k (etpgt.model.base.predict) ---------
  * Replaces base.py:59-78 (scores = se @ item_embedding.weight.T; torch.topk(scores, k))
  * as called by Trainer.evaluate (trainer.py:138-173) for Recall@K / NDCG@K.

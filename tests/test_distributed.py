@@ -157,3 +157,94 @@ def test_dp_layout_is_aligned_and_packed():
         s = lay.struct()
         assert (s.flat_total, s.loss_off, s.keys_off, s.rows_off, s.words, s.m_cap, s.world) == (
             F, lay.loss_off, lay.keys_off, lay.rows_off, lay.words, m, w)
+
+
+# ---- row-sharded table protocol (etpgt.train.sharded) on CPU ------------------------------
+def _route_reference(keys: torch.Tensor, T: int, P: int, cap: int) -> torch.Tensor:
+    """send_ids [P][cap] of gtr_shard_route: the distinct rows of a batch per owner r % P,
+    ascending, count in slot 0."""
+    out = torch.zeros(P, cap, dtype=torch.int32)
+    u = torch.unique(keys[(keys >= 0) & (keys < T)])
+    for q in range(P):
+        mine = u[u % P == q]
+        assert mine.numel() <= cap - 1
+        out[q, 0] = mine.numel()
+        out[q, 1 : 1 + mine.numel()] = mine.to(torch.int32)
+    return out
+
+
+def _shard_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from etpgt.train.distributed import all_to_all
+    from etpgt.train.sharded import shard_capacity
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        model = _model()
+        sb = _batches(world)[rank]
+        _grads(model, sb)
+        tab_grad = model.item_embedding.weight.grad
+        keys = torch.cat([sb.x.reshape(-1), sb.target_item.reshape(-1), sb.negative_items.reshape(-1)])
+        m_cap = torch.tensor([keys.numel()])
+        dist.all_reduce(m_cap, op=dist.ReduceOp.MAX)  # the ranks bind equal capacities (FusedTrainStep._agree)
+        cap = shard_capacity(int(m_cap), T, world)
+        send_ids = _route_reference(keys, T, world, cap)
+        recv_ids = torch.zeros_like(send_ids)
+        all_to_all(recv_ids, send_ids)
+        # requester: the summed gradient row of each requested row, at its slot
+        send_g = torch.zeros(world, cap, D)
+        for o in range(world):
+            for j in range(1, int(send_ids[o, 0]) + 1):
+                send_g[o, j] = tab_grad[int(send_ids[o, j])]
+        recv_g = torch.zeros_like(send_g)
+        all_to_all(recv_g, send_g)
+        # owner: rank-ordered sum / P of every requested row it owns
+        got = {}
+        for r in range(world):
+            for j in range(1, int(recv_ids[r, 0]) + 1):
+                k = int(recv_ids[r, j])
+                assert k % world == rank
+                got[k] = got.get(k, torch.zeros(D)) + recv_g[r, j]
+        q.put((rank, {k: (v / world).numpy() for k, v in got.items()}, tab_grad.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_protocol_routes_rows_to_owners_and_averages():
+    """gloo world 2: the all-to-all route of requested rows to their owners (r % P) and the
+    owners' rank-ordered average equal the dense averaged table gradient on every touched
+    row, each row updated by exactly one owner."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            rank, got, g = q.get(timeout=300)
+            res[rank] = (got, g)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    dense = (torch.from_numpy(res[0][1]) + torch.from_numpy(res[1][1])) / world
+    touched = set(res[0][0]) | set(res[1][0])
+    assert not (set(res[0][0]) & set(res[1][0]))
+    assert touched == set(int(i) for i in torch.nonzero(dense.abs().sum(1)).reshape(-1)) - {0} | (touched & {0})
+    for rank in range(world):
+        for k, v in res[rank][0].items():
+            torch.testing.assert_close(torch.from_numpy(v), dense[k], rtol=1e-6, atol=1e-7)
+
+
+def test_shard_capacity_bounds():
+    from etpgt.train.sharded import shard_capacity
+
+    assert shard_capacity(1000, 300, 2) == 1 + 150            # exact bound: the owner's 150 rows
+    assert shard_capacity(100, 10**6, 8) == 1 + 19 + 64       # 1.5 x the even share + 64 ...
+    assert shard_capacity(40, 10**6, 8) == 1 + 40             # ... never above the batch's rows
+    assert shard_capacity(107_000, 10**6, 8, slack=1.5) == 1 + 20_063 + 64  # 1.5 x the even share
