@@ -291,7 +291,8 @@ def main():
                                      "per element)",
                 "touched_rows_per_step": round(touched, 1),
                 "avg_launch_ms": round(step_ms, 5),
-                "tail_kernel": {"name": "k_dp_tail" if step.dp is not None else "k_step_tail",
+                "tail_kernel": {"name": ("k_dp_tail" if step.dp is not None else
+                                         "k_step_tail_wgrad" if getattr(step, "tail_wgrad", False) else "k_step_tail"),
                                 "avg_launch_ms": None if tail_ms is None else round(tail_ms, 5)},
             },
             "cpu_baseline": cpu,
@@ -372,22 +373,13 @@ def measure_tail(step, iters) -> float:
     """Average duration (ms) of the step-tail kernel (AdamW over every item-table row
     + small parameters), bracketed by HIP events on the stream it is launched on.
     Re-launches the last step's tail: a valid optimizer update on that step's gradients."""
-    from etpgt.backend import _lib as L
-    import ctypes as C
-
-    lib = L.lib()
-    eng = step.eng
     main = torch.cuda.current_stream()
     durs = []
     n = max(10, min(iters, 200))
     for _ in range(n):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(main)
-        if step.dp is not None:  # data parallel: the rank-averaged tail (k_dp_stamp + k_dp_tail)
-            step.dp.launch_tail(step.bs, main.cuda_stream)
-        else:
-            L.check(lib.gtr_step_tail(C.byref(step.bs), eng.T, eng.D, C.byref(step.tail), step.segs, step.nseg,
-                                      C.byref(step.adam), main.cuda_stream), "step_tail")
+        step._launch_b(False)  # the step's own tail: dp tail, tail with weight gradients, or plain
         e1.record(main)
         durs.append((e0, e1))
     torch.cuda.synchronize()

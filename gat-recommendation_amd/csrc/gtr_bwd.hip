@@ -10,6 +10,7 @@
 //   gradients as deterministic per-chunk partial slabs (summed by the optimizer).
 
 #include "gtr_layer.cuh"
+#include "gtr_wgrad.cuh"
 
 namespace {
 
@@ -603,33 +604,7 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
 // weight gradients
 // ------------------------------------------------------------------------------------
 
-enum { WJ_MM = 0, WJ_GATE = 1, WJ_COLSUM = 2 };
-
-struct WJob {
-  int type, M1, M2, lda, ldb, tn, nt, blk0;
-  const float* A;
-  const float* B;
-  const int32_t* bidx;
-  const float* agg;
-  const float* s;   // skip rows (qkvs + 3D), row stride lda
-  float* outW;
-  float* outB;
-};
-
-#define GTR_MAX_WJOBS 16
-
-struct WgradK {
-  const int32_t* hdr;
-  int P, njobs, D, pad0;
-  int64_t stride;
-  WJob jobs[GTR_MAX_WJOBS];
-};
-
 __global__ __launch_bounds__(GTR_BLOCK) void k_wgrad(WgradK a) {
-  constexpr int TK = 32;  // node rows staged per round
-  __shared__ __attribute__((aligned(16))) float As[TK][64];
-  __shared__ __attribute__((aligned(16))) float Bs[TK][64];
-  const int tid = threadIdx.x;
   const int blk = blockIdx.x;
   int jid = 0;
   while (jid + 1 < a.njobs && blk >= a.jobs[jid + 1].blk0) ++jid;
@@ -641,94 +616,10 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_wgrad(WgradK a) {
   const int t0 = p * per;
   const int t1 = min(N, t0 + per);
   const int64_t so = (int64_t)p * a.stride;
-
-  if (J.type == WJ_GATE) {
-    const int D = a.D;
-    const int j = tile * GTR_BLOCK + tid;
-    if (j >= 3 * D) return;
-    float acc = 0.0f;
-#pragma unroll 4
-    for (int t = t0; t < t1; ++t) {
-      const float u = J.A[t];
-      float f;
-      if (j < D) f = J.agg[(size_t)t * D + j];
-      else if (j < 2 * D) f = J.s[(size_t)t * J.lda + (j - D)];
-      else f = J.agg[(size_t)t * D + (j - 2 * D)] - J.s[(size_t)t * J.lda + (j - 2 * D)];
-      acc += u * f;
-    }
-    J.outW[so + j] = acc;
-    return;
-  }
-
-  if (J.type == WJ_COLSUM) {  // bias gradient: column sums of A over this chunk's rows
-    const int j = tile * GTR_BLOCK + tid;
-    if (j >= J.M1) return;
-    float acc = 0.0f;
-#pragma unroll 8
-    for (int t = t0; t < t1; ++t) acc += J.A[(size_t)t * J.lda + j];
-    J.outB[so + j] = acc;
-    return;
-  }
-
-  const int tm = tile / J.tn, tq = tile - tm * J.tn;
-  const int m0 = tm * 64, n0 = tq * 64;
-  const int ty = tid >> 4, tx = tid & 15;
-  float acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) acc[i][k] = 0.0f;
-  for (int tb = t0; tb < t1; tb += TK) {
-    float av[TK * 64 / GTR_BLOCK], bv[TK * 64 / GTR_BLOCK];
-#pragma unroll
-    for (int q = 0; q < TK * 64 / GTR_BLOCK; ++q) {
-      const int idx = tid + q * GTR_BLOCK;
-      const int i = idx >> 6, c = idx & 63;
-      const int t = tb + i;
-      av[q] = 0.0f;
-      bv[q] = 0.0f;
-      if (t < t1) {
-        if (m0 + c < J.M1) av[q] = J.A[(size_t)t * J.lda + m0 + c];
-        const int col = n0 + c;
-        if (col < J.M2) {
-          const float* brow = J.bidx ? J.B + (size_t)J.bidx[t] * J.ldb : J.B + (size_t)t * J.ldb;
-          bv[q] = brow[col];
-        } else if (col == J.M2) {
-          bv[q] = 1.0f;
-        }
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < TK * 64 / GTR_BLOCK; ++q) {
-      const int idx = tid + q * GTR_BLOCK;
-      As[idx >> 6][idx & 63] = av[q];
-      Bs[idx >> 6][idx & 63] = bv[q];
-    }
-    __syncthreads();
-#pragma unroll 8
-    for (int k = 0; k < TK; ++k) {
-      const float4 a4 = *reinterpret_cast<const float4*>(&As[k][ty * 4]);
-      const float4 b4 = *reinterpret_cast<const float4*>(&Bs[k][tx * 4]);
-      const float ar[4] = {a4.x, a4.y, a4.z, a4.w};
-      const float br[4] = {b4.x, b4.y, b4.z, b4.w};
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) acc[i][q] += ar[i] * br[q];
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + ty * 4 + i;
-    if (m >= J.M1) continue;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int nn = n0 + tx * 4 + q;
-      if (nn < J.M2) J.outW[so + (int64_t)m * J.M2 + nn] = acc[i][q];
-      else if (nn == J.M2) J.outB[so + m] = acc[i][q];
-    }
-  }
+  wgrad_tile(J, tile, t0, t1, a.D, [&](int which, int64_t idx, float v) {
+    if (which == 0) J.outW[so + idx] = v;
+    else J.outB[so + idx] = v;
+  });
 }
 
 }  // namespace
@@ -831,42 +722,9 @@ extern "C" int gtr_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_l
   k.stride = slab_stride;
   if (l_begin < 0 || l_end > Lc || l_begin > l_end) { set_error("gtr_wgrad: bad layer range"); return GTR_E_ARG; }
   int nj = 0, blocks = 0;
-  for (int l = l_begin; l < l_end; ++l) {
-    const gtr_layer& L = layers[l];
-    float* base = layer_slab[l];
-    WJob& w = k.jobs[nj++];
-    w.type = WJ_MM; w.M1 = 4 * D; w.M2 = D; w.lda = 4 * D; w.ldb = D;
-    // the bias rides as a ones-column in the last tile when it fits there (D = 32); for
-    // D a multiple of 64 it would need a tile column of its own (1/3 more tiles at
-    // D = 128), so it is a column-sum job instead
-    w.tn = (D + 63) / 64; w.nt = ((4 * D + 63) / 64) * w.tn; w.blk0 = blocks;
-    w.A = L.dqkvs; w.B = L.xin; w.bidx = nullptr;
-    w.outW = base; w.outB = base + (size_t)4 * D * D;
-    blocks += w.nt * n_chunks;
-    if (D % 64 == 0) {
-      WJob& c = k.jobs[nj++];
-      c.type = WJ_COLSUM; c.M1 = 4 * D; c.lda = 4 * D; c.tn = 1; c.nt = (4 * D + GTR_BLOCK - 1) / GTR_BLOCK;
-      c.blk0 = blocks; c.A = L.dqkvs; c.outB = base + (size_t)4 * D * D;
-      blocks += c.nt * n_chunks;
-    }
-    WJob& q = k.jobs[nj++];
-    q.type = WJ_GATE; q.M1 = 1; q.M2 = 3 * D; q.lda = 4 * D; q.tn = 1; q.nt = (3 * D + GTR_BLOCK - 1) / GTR_BLOCK;
-    q.blk0 = blocks; q.A = L.du; q.agg = L.agg; q.s = L.qkvs + 3 * D;
-    q.outW = base + (size_t)4 * D * D + 4 * D;
-    blocks += q.nt * n_chunks;
-  }
-  if (cfg->pe_k > 0 && pe_slab && l_begin == 0) {
-    if (!dx0 || (!pe_tab && !bt->node_pe)) { set_error("gtr_wgrad: PE gradient needs dx0 and PE rows"); return GTR_E_ARG; }
-    const int K = cfg->pe_k;
-    WJob& w = k.jobs[nj++];
-    w.type = WJ_MM; w.M1 = D; w.M2 = K; w.lda = D; w.ldb = K;
-    w.tn = (K + 1 + 63) / 64; w.nt = ((D + 63) / 64) * w.tn; w.blk0 = blocks;
-    w.A = dx0;
-    if (bt->node_pe) { w.B = bt->node_pe; w.bidx = nullptr; }
-    else { w.B = pe_tab; w.bidx = bt->node_item; }
-    w.outW = pe_slab; w.outB = pe_slab + (size_t)D * K;
-    blocks += w.nt * n_chunks;
-  }
+  const int rc = build_wjobs(cfg, bt, layers, dx0, pe_tab, layer_slab, pe_slab, nullptr, nullptr, n_chunks, l_begin,
+                             l_end, k.jobs, nj, blocks);
+  if (rc) return rc;
   k.njobs = nj;
   if (nj == 0 || blocks == 0) return GTR_OK;
   hipStream_t s = (hipStream_t)stream;

@@ -12,11 +12,13 @@
 //   * gtr_adamw_small: every other parameter (flat buffer, partial slabs summed).
 
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <cstdarg>
 #include <cstdio>
 
 #include "gtr_rows.cuh"
+#include "gtr_wgrad.cuh"
 
 namespace gtr {
 
@@ -241,6 +243,7 @@ __device__ __forceinline__ void lazy_claim_row(int key, int T, int D, int32_t t,
 #define GTR_BEGIN_WAVES (GTR_BEGIN_BLOCK / 64)
 #define GTR_BEGIN_MCAP 8192
 #define GTR_BEGIN_KEY_LIMIT (1 << 19)
+#define GTR_TAILW_NCAP 512  // node-row capacity up to which the tail computes the weight gradients
 
 // Rank sort: composite keys (row << 13 | slot) are unique, so the stable order by row
 // is the plain order of the composites and slot j goes to rank #{composites < c_j}.
@@ -550,6 +553,97 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_step_tail(TailK a) {
              reinterpret_cast<float4*>(a.tl.table_v), st, a.vbegin);
 }
 
+// ---- small batches: the weight gradients inside the tail ------------------------------
+// Workgroups: [touched rows | weight-gradient tiles (gtr_wgrad.cuh jobs, one chunk over
+// all node rows) + their AdamW | BatchNorm gamma / beta segments (bn_gsum) + the loss |
+// untouched rows].  Replaces k_wgrad + the tail's slab sums for batches whose whole
+// weight-gradient reduction is a few row rounds (n_cap <= GTR_TAILW_NCAP): one launch less
+// on the step's dependency chain, bitwise the result of k_wgrad with one chunk.
+#define GTR_TAILW_SEGS 16
+struct TailWK {
+  gtr_batch bt;
+  gtr_tail tl;
+  gtr_adam opt;
+  int T, nb_rows, nb_wg, nb_small, nb_sweep, njobs, D, nseg;
+  int64_t vbegin, nvec;
+  int vpr_log2, small_total;
+  gtr_segment segs[GTR_TAILW_SEGS];
+  WJob jobs[GTR_MAX_WJOBS];
+};
+
+template <int D>
+__global__ __launch_bounds__(GTR_BLOCK) void k_step_tail_wgrad(TailWK a) {
+  __shared__ AdamStep s_st;
+  __shared__ int32_t s_t;
+  __shared__ float s_acc[GTR_BLOCK];
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    const int64_t t = *a.opt.step_dev + a.opt.step_offset;
+    s_st.init(a.opt, t);
+    s_t = (int32_t)t;
+  }
+  __syncthreads();
+  const AdamStep st = s_st;
+  int blk = blockIdx.x;
+  if (blk < a.nb_rows) {
+    rows_body<D>(blk * GTR_BLOCK + tid, a.bt, a.T, a.tl.skeys, a.tl.svals, a.tl.dx0, a.tl.se, a.tl.coef_tgt,
+                 a.tl.coef_neg, a.tl.table, a.tl.table_m, a.tl.table_v, nullptr, st,
+                 a.tl.lazy_consts ? a.tl.stamp : nullptr, s_t);
+    return;
+  }
+  blk -= a.nb_rows;
+  if (blk < a.nb_wg) {
+    int jid = 0;
+    while (jid + 1 < a.njobs && blk >= a.jobs[jid + 1].blk0) ++jid;
+    const WJob& J = a.jobs[jid];
+    float* P = a.tl.flat;
+    float* M = a.tl.flat_m;
+    float* V = a.tl.flat_v;
+    wgrad_tile(J, blk - J.blk0, 0, a.bt.hdr[0], a.D, [&](int which, int64_t idx, float g) {
+      const int64_t e = (which == 0 ? J.fW : J.fB) + idx;
+      float pv = P[e], mv = M[e], vv = V[e];
+      st.apply(pv, mv, vv, g);
+      P[e] = pv;
+      M[e] = mv;
+      V[e] = vv;
+    });
+    return;
+  }
+  blk -= a.nb_wg;
+  if (blk < a.nb_small) {
+    int64_t i = (int64_t)blk * GTR_BLOCK + tid;  // index into the concatenated segments
+    if (i < a.small_total) {
+      int sg = 0;
+      while (i >= a.segs[sg].len) { i -= a.segs[sg].len; ++sg; }
+      const gtr_segment& S = a.segs[sg];
+      float g = 0.0f;
+      for (int p = 0; p < S.nparts; ++p) g += S.src[(int64_t)p * S.pstride + i];
+      const int64_t e = S.begin + i;
+      float pv = a.tl.flat[e], mv = a.tl.flat_m[e], vv = a.tl.flat_v[e];
+      st.apply(pv, mv, vv, g);
+      a.tl.flat[e] = pv;
+      a.tl.flat_m[e] = mv;
+      a.tl.flat_v[e] = vv;
+    }
+    if (blk == 0 && a.tl.loss_part) {  // loss of the step: the readout's partials, fixed order
+      float acc = 0.0f;
+      for (int q = tid; q < a.tl.loss_nparts; q += GTR_BLOCK)
+        acc += a.tl.loss_part[(size_t)q * 2] + a.tl.loss_part[(size_t)q * 2 + 1];
+      s_acc[tid] = acc;
+      __syncthreads();
+      if (tid == 0) {
+        float t = 0.0f;
+        for (int q = 0; q < GTR_BLOCK; ++q) t += s_acc[q];
+        a.tl.loss_out[0] = t;
+      }
+    }
+    return;
+  }
+  blk -= a.nb_small;
+  sweep_body(blk, a.nb_sweep, a.nvec, a.vpr_log2, a.tl.stamp, s_t, reinterpret_cast<float4*>(a.tl.table),
+             reinterpret_cast<float4*>(a.tl.table_m), reinterpret_cast<float4*>(a.tl.table_v), st, a.vbegin);
+}
+
 template <int D>
 __global__ __launch_bounds__(GTR_BLOCK) void k_scatter_rows(gtr_batch bt, int mode, const float* src,
                                                             const float* coef_tgt, const float* coef_neg,
@@ -835,6 +929,25 @@ int key_bits(int T) {
 
 bool dim_ok(int D) { return D == 32 || D == 64 || D == 128 || D == 256; }
 
+// Stable (key, slot) radix sort of the contribution list.  rocPRIM's default config runs
+// a block sort + merge passes below 1M items (~20 launches at m_cap ~ 855k); the Onesweep
+// config (merge-sort limit 0) runs one histogram launch and one launch per radix digit of
+// the key bits.  Both are stable, so they sort identically.  GTR_SORT=onesweep selects
+// it.  The
+// workspace query and the sort MUST use the same config (gtr_contrib_sort checks it).
+using OnesweepConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                  rocprim::default_config, 0>;
+bool sort_onesweep() {
+  const char* e = getenv("GTR_SORT");
+  return e && (e[0] == 'o' || e[0] == 'O');
+}
+hipError_t sort_pairs(void* tmp, size_t& bytes, const int32_t* keys, int32_t* skeys, const int32_t* vals,
+                      int32_t* svals, int n, int bits, hipStream_t s) {
+  if (sort_onesweep())
+    return rocprim::radix_sort_pairs<OnesweepConfig>(tmp, bytes, keys, skeys, vals, svals, (size_t)n, 0, bits, s);
+  return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, keys, skeys, vals, svals, n, 0, bits, s);
+}
+
 }  // namespace
 
 extern "C" {
@@ -899,9 +1012,8 @@ int gtr_contrib_prep(const gtr_batch* bt, int num_items, int32_t* keys, int32_t*
 int gtr_contrib_sort_bytes(int m_cap, int num_items, size_t* bytes) {
   if (!bytes || m_cap <= 0) { set_error("gtr_contrib_sort_bytes: bad arguments"); return GTR_E_ARG; }
   size_t b = 0;
-  hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, b, (const int32_t*)nullptr, (int32_t*)nullptr,
-                                                     (const int32_t*)nullptr, (int32_t*)nullptr, m_cap, 0,
-                                                     key_bits(num_items));
+  hipError_t e = sort_pairs(nullptr, b, (const int32_t*)nullptr, (int32_t*)nullptr, (const int32_t*)nullptr,
+                            (int32_t*)nullptr, m_cap, key_bits(num_items), nullptr);
   if (e != hipSuccess) { set_error("gtr_contrib_sort_bytes: %s", hipGetErrorString(e)); return (int)e; }
   *bytes = b;
   return GTR_OK;
@@ -909,9 +1021,18 @@ int gtr_contrib_sort_bytes(int m_cap, int num_items, size_t* bytes) {
 
 int gtr_contrib_sort(const int32_t* keys, const int32_t* vals, int32_t* skeys, int32_t* svals, int m_cap,
                      int num_items, void* tmp, size_t tmp_bytes, gtr_stream_t stream) {
+  // The temporary storage must be sized by the SAME algorithm and key width as this call
+  // (gtr_contrib_sort_bytes): round 1's rocPRIM Onesweep trial faulted (illegal address)
+  // because its workspace was still sized for hipCUB's merge-sort path, which needs less.
+  size_t need = 0;
+  if (gtr_contrib_sort_bytes(m_cap, num_items, &need) != GTR_OK) return GTR_E_ARG;
+  if (!keys || !vals || !skeys || !svals || !tmp || tmp_bytes < need) {
+    set_error("gtr_contrib_sort: workspace of %zu bytes < %zu needed (m_cap %d, T %d)", tmp_bytes, need, m_cap,
+              num_items);
+    return GTR_E_ARG;
+  }
   size_t b = tmp_bytes;
-  hipError_t e = hipcub::DeviceRadixSort::SortPairs(tmp, b, keys, skeys, vals, svals, m_cap, 0, key_bits(num_items),
-                                                     (hipStream_t)stream);
+  hipError_t e = sort_pairs(tmp, b, keys, skeys, vals, svals, m_cap, key_bits(num_items), (hipStream_t)stream);
   if (e != hipSuccess) { set_error("gtr_contrib_sort: %s", hipGetErrorString(e)); return (int)e; }
   return GTR_OK;
 }
@@ -1123,6 +1244,66 @@ int gtr_step_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* t
     case 64: hipLaunchKernelGGL(k_step_tail<64>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
     case 128: hipLaunchKernelGGL(k_step_tail<128>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
     default: hipLaunchKernelGGL(k_step_tail<256>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+  }
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+int gtr_step_tail_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, const float* pe_tab,
+                        const int64_t* layer_flat, const int64_t* pe_flat, int num_items, const gtr_tail* tail,
+                        const gtr_segment* segs, int nseg, const gtr_adam* opt, gtr_stream_t stream) {
+  if (!cfg || !bt || !layers || !layer_flat || !tail || !opt || !opt->step_dev || num_items <= 0 || nseg < 0 ||
+      nseg > GTR_TAILW_SEGS || (nseg > 0 && !segs) || !dim_ok(cfg->dim) || 3 * cfg->num_layers + 1 > GTR_MAX_WJOBS) {
+    set_error("gtr_step_tail_wgrad: bad arguments");
+    return GTR_E_ARG;
+  }
+  const gtr_tail& t = *tail;
+  const int D = cfg->dim;
+  const int m_cap = bt->n_cap + bt->b_cap * (1 + bt->n_neg);
+  if (m_cap > GTR_BEGIN_MCAP || bt->n_cap > GTR_TAILW_NCAP) {
+    set_error("gtr_step_tail_wgrad: batch too large (m_cap %d > %d or n_cap %d > %d): use gtr_wgrad + gtr_step_tail",
+              m_cap, GTR_BEGIN_MCAP, bt->n_cap, GTR_TAILW_NCAP);
+    return GTR_E_ARG;
+  }
+  if (!t.skeys || !t.svals || !t.dx0 || !t.se || !t.coef_tgt || !t.coef_neg || !t.table || !t.table_m ||
+      !t.table_v || !t.stamp || !t.flat || !t.flat_m || !t.flat_v || (t.loss_part && (!t.loss_out || t.loss_nparts < 0))) {
+    set_error("gtr_step_tail_wgrad: missing buffers");
+    return GTR_E_ARG;
+  }
+  TailWK k{};
+  k.bt = *bt;
+  k.tl = t;
+  k.opt = *opt;
+  k.T = num_items;
+  k.D = D;
+  int nj = 0, wblocks = 0;
+  const int rc = build_wjobs(cfg, bt, layers, t.dx0, pe_tab, nullptr, nullptr, layer_flat, pe_flat, 1, 0,
+                             cfg->num_layers, k.jobs, nj, wblocks);
+  if (rc) return rc;
+  k.njobs = nj;
+  k.nb_wg = wblocks;
+  k.nb_rows = (int)(((int64_t)m_cap * (D / 4) + GTR_BLOCK - 1) / GTR_BLOCK);
+  int64_t tot = 0;
+  for (int i = 0; i < nseg; ++i) { k.segs[i] = segs[i]; tot += segs[i].len; }
+  k.nseg = nseg;
+  k.small_total = (int)tot;
+  k.nb_small = (int)((tot + GTR_BLOCK - 1) / GTR_BLOCK);
+  if (k.nb_small == 0 && t.loss_part) k.nb_small = 1;
+  k.nvec = (int64_t)num_items * D / 4;
+  k.vpr_log2 = 0;
+  while ((1 << k.vpr_log2) < D / 4) ++k.vpr_log2;
+  const int64_t from = t.lazy_consts ? num_items
+                                      : (t.sweep_from < 0 ? 0 : (t.sweep_from > num_items ? num_items : t.sweep_from));
+  k.vbegin = from * (D / 4);
+  const int64_t sw = (k.nvec - k.vbegin + GTR_BLOCK - 1) / GTR_BLOCK;
+  k.nb_sweep = (int)(sw > 2048 ? 2048 : sw);
+  const int grid = k.nb_rows + k.nb_wg + k.nb_small + k.nb_sweep;
+  hipStream_t s = (hipStream_t)stream;
+  switch (D) {
+    case 32: hipLaunchKernelGGL(k_step_tail_wgrad<32>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    case 64: hipLaunchKernelGGL(k_step_tail_wgrad<64>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    case 128: hipLaunchKernelGGL(k_step_tail_wgrad<128>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    default: hipLaunchKernelGGL(k_step_tail_wgrad<256>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
   }
   GTR_HIP_CHECK_LAUNCH();
   return GTR_OK;

@@ -154,6 +154,7 @@ _SIGS = {
     "gtr_dp_union_stamp": (C.c_int, [P, i64, C.c_int, P, P, P]),
     "gtr_step_begin": (C.c_int, [P, C.c_int, P, P, P, P, P, P, P, P, C.c_size_t, P]),
     "gtr_step_tail": (C.c_int, [P, C.c_int, C.c_int, P, P, C.c_int, P, P]),
+    "gtr_step_tail_wgrad": (C.c_int, [P, P, P, P, P, P, C.c_int, P, P, C.c_int, P, P]),
     "gtr_step_begin_lazy": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P, P, P, C.c_size_t, P, P]),
     "gtr_lazy_flush": (C.c_int, [C.c_int, C.c_int, P, P, P, P]),
     "gtr_tail_carry_floats": (C.c_int, [C.c_int, C.c_int]),

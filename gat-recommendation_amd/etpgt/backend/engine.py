@@ -241,8 +241,14 @@ class Engine:
     def choose_R(self, caps: Caps) -> int:
         return caps.R
 
+    TAILW_NCAP = 512  # GTR_TAILW_NCAP (csrc/gtr_opt.hip)
+
     def choose_P(self, caps: Caps) -> int:
-        # split-K of the weight gradients: <= 32 node rows per workgroup, <= 64 slabs
+        # split-K of the weight gradients: <= 32 node rows per workgroup, <= 64 slabs; small
+        # batches use ONE chunk, the reduction the fused tail (gtr_step_tail_wgrad) computes
+        # in-launch, so every path (fused, data parallel, eager) sums the same way
+        if caps.n_cap <= self.TAILW_NCAP:
+            return 1
         return max(1, min(64, (caps.n_cap + 31) // 32))
 
     def workspace(self, caps: Caps, fresh: bool = False) -> Workspace:
@@ -344,18 +350,22 @@ class Engine:
                                   None if ws.pe_slab is None else ws.pe_slab.data_ptr(), ws.P,
                                   self.flat.layout.slab_stride, l0, l1, st), "wgrad")
 
-    def run_backward(self, ws: Workspace, cfg: L.GtrConfig, bs: L.GtrBatch, side: torch.cuda.Stream | None = None):
+    def run_backward(self, ws: Workspace, cfg: L.GtrConfig, bs: L.GtrBatch, side: torch.cuda.Stream | None = None,
+                     wgrad: bool = True):
         """conv_bwd(L-1..0) + weight-gradient slabs; expects layers[L-1].dy / bn_gsum.
         With ``side``, layer l >= 1 weight gradients run on that stream concurrently
-        with conv_bwd(l-1..0); the caller must join ``side`` before reading slabs."""
+        with conv_bwd(l-1..0); the caller must join ``side`` before reading slabs.
+        ``wgrad=False``: the weight gradients are left to the fused tail."""
         lib = L.lib()
         main = torch.cuda.current_stream(self.device)
         st = main.cuda_stream
         for l in range(self.L - 1, -1, -1):
             L.check(lib.gtr_conv_bwd(C.byref(cfg), C.byref(bs), ws.structs, l, ws.dx0.data_ptr(), st), "conv_bwd")
-            if side is not None and l >= 1:
+            if wgrad and side is not None and l >= 1:
                 side.wait_stream(main)
                 self._wgrad(ws, cfg, bs, l, l + 1, side.cuda_stream)
+        if not wgrad:
+            return
         if side is not None:
             self._wgrad(ws, cfg, bs, 0, 1, st)
         else:

@@ -247,6 +247,20 @@ class FusedTrainStep:
             self.dp = DpExchange(self, self.group)
         if self.sync_bn:
             self._sync_alloc()
+        # small batches: the weight gradients ride in the tail launch (gtr_step_tail_wgrad)
+        self.tail_wgrad = (self.dp is None and self.shard is None and m_cap <= 8192
+                           and caps.n_cap <= eng.TAILW_NCAP and os.environ.get("GTR_TAILW", "0") == "1")
+        if self.tail_wgrad:
+            lay = eng.flat.layout
+            gb = [i for i in range(self.nseg)
+                  if any(self.segs[i].begin == lay.seg(f"{l}.{n}").begin for l in range(eng.L) for n in ("gamma", "beta"))]
+            self.segs_gb = (L.GtrSegment * max(1, len(gb)))()
+            for j, i in enumerate(gb):
+                self.segs_gb[j] = self.segs[i]
+            self.nseg_gb = len(gb)
+            self.layer_flat = (C.c_int64 * (3 * eng.L))(*[lay.seg(f"{l}.{n}").begin for l in range(eng.L)
+                                                          for n in ("w_all", "b_all", "w_beta")])
+            self.pe_flat = (C.c_int64 * 2)(lay.seg("pe.w").begin, lay.seg("pe.b").begin) if eng.K > 0 else None
         self.graph = None
         self.graph_pe = None
         self.graph_b = None
@@ -363,7 +377,7 @@ class FusedTrainStep:
         st = torch.cuda.current_stream(self.dev).cuda_stream
         self._begin(bs, st)
         eng.run_forward(ws, cfg, bs, L.RO_FWD | L.RO_LOSS | L.RO_BWD, self.loss_kind, self.temperature, self.alpha)
-        eng.run_backward(ws, cfg, bs)
+        eng.run_backward(ws, cfg, bs, wgrad=not self.tail_wgrad)
         if self.dp is not None:
             self.dp.launch_pack(bs, st)
 
@@ -374,6 +388,12 @@ class FusedTrainStep:
         st = torch.cuda.current_stream(self.dev).cuda_stream
         if self.dp is not None:
             self.dp.launch_tail(bs, st)
+        elif self.tail_wgrad:
+            pe = self.model.laplacian_pe._cached_pe if eng.K > 0 else None
+            L.check(L.lib().gtr_step_tail_wgrad(C.byref(self.cfg), C.byref(bs), self.ws.structs,
+                                                None if pe is None else pe.data_ptr(), self.layer_flat,
+                                                self.pe_flat, eng.T, C.byref(self.tail), self.segs_gb,
+                                                self.nseg_gb, C.byref(self.adam), st), "step_tail_wgrad")
         else:
             L.check(L.lib().gtr_step_tail(C.byref(bs), eng.T, eng.D, C.byref(self.tail), self.segs, self.nseg,
                                           C.byref(self.adam), st), "step_tail")

@@ -374,6 +374,17 @@ int gtr_tail_carry_floats(int m_cap, int dim);
 int gtr_step_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tail,
                   const gtr_segment* segs, int nseg, const gtr_adam* opt, gtr_stream_t stream);
 
+/* Small batches (n_cap <= 512, m_cap <= 8192): gtr_step_tail with the weight gradients of
+ * gtr_wgrad (one row chunk) computed inside the same launch and applied by AdamW directly,
+ * one launch less on the step's chain (trainer.py:123-127: backward + optimizer.step()).
+ * layer_flat [L][3] = element offsets into tail->flat of each layer's w_all / b_all /
+ * w_beta; pe_flat [2] = offsets of the LapPE projection weight / bias (NULL without
+ * LapPE); segs = the remaining dense segments (BatchNorm gamma / beta from bn_gsum,
+ * <= 16).  Bitwise equal to gtr_wgrad(n_chunks = 1) + gtr_step_tail.                    */
+int gtr_step_tail_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, const float* pe_tab,
+                        const int64_t* layer_flat, const int64_t* pe_flat, int num_items, const gtr_tail* tail,
+                        const gtr_segment* segs, int nseg, const gtr_adam* opt, gtr_stream_t stream);
+
 /* ---- data-parallel step (one process per GPU; etpgt.train.distributed) --------
  * Each rank packs its gradients into `pack` (words per rank = layout.words):
  *   [0, flat_total)          summed small-parameter gradient (flat layout)

@@ -5,8 +5,8 @@ gradients returned by all-to-all.  The arithmetic is the replicated data-paralle
 with the lazy table (same per-rank segment sums, rank-ordered averaging, the same
 zero-gradient catch-up), so the tests ask for bit equality:
   * one rank: the sharded step == the single-GPU fused step with the lazy table;
-  * two ranks sharing the GPU (gloo transport): == the replicated data-parallel step, with
-    and without SyncBN, with LapPE, and the replicas agree;
+  * two and four ranks sharing the GPU (gloo transport): == the replicated data-parallel
+    step, with and without SyncBN, with LapPE, and the replicas agree;
   * a batch that overflows an exchange block is reported, not silently trained on."""
 
 from __future__ import annotations
@@ -90,14 +90,14 @@ def _free_port() -> int:
     return port
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, ncases):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import torch.distributed as dist
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         out = []
-        for (D, H, K, loss, steps, B), sync in zip(CASES, (False, True)):
+        for (D, H, K, loss, steps, B), sync in list(zip(CASES, (False, True)))[:ncases]:
             data = small_data()
             T = data.table_rows
             m1, _ = make_pair(T, D, H, K=K, seed=45)
@@ -125,15 +125,15 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_shard_two_ranks_bitwise_equals_replicated_dp():
-    """2 ranks sharing the GPU over gloo: the sharded step equals the replicated
-    data-parallel step (lazy table) bit for bit -- BPR at D=64, and listwise at D=128 /
-    4 heads / LapPE with SyncBN -- and the gathered tables agree across ranks."""
-    world = 2
+@pytest.mark.parametrize("world,ncases", [(2, 2), (4, 1)])
+def test_shard_ranks_bitwise_equal_replicated_dp(world, ncases):
+    """2 (4) ranks sharing the GPU over gloo: the sharded step equals the replicated
+    data-parallel step (lazy table) bit for bit -- BPR at D=64, and (2 ranks) listwise at
+    D=128 / 4 heads / LapPE with SyncBN -- and the gathered tables agree across ranks."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, ncases)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -145,10 +145,11 @@ def test_shard_two_ranks_bitwise_equals_replicated_dp():
         for p in procs:
             p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs)
-    for case in range(len(CASES)):
+    for case in range(ncases):
         for r in range(world):
             same_loss, same, bad, _, vol = res[r][case]
             assert same_loss, (case, r)
             assert same, (case, r, bad)
-        for k, v in res[0][case][3].items():
-            assert np.array_equal(v, res[1][case][3][k]), f"replicas diverged: {k}"
+        for r in range(1, world):
+            for k, v in res[0][case][3].items():
+                assert np.array_equal(v, res[r][case][3][k]), f"replicas diverged: {k}"
