@@ -53,6 +53,8 @@ struct ConvBwdK {
   int sync, nparts_bwd, nparts_fwd, pad_s;  // SyncBN: every rank's partials (this layer)
   const float* gpart_all;
   const float* part_all;
+  uint32_t ctr_add;
+  int xpack;            // XCD-packed roles (role_block)
 };
 
 // Destination-row backward: BatchNorm backward, beta gate, softmax backward, dQ, dS.
@@ -198,15 +200,16 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
   float* s_bnp = sm + G::B_BNP;
   int* s_flag = reinterpret_cast<int*>(sm + G::B_FLAG);
 
-  if ((int)blockIdx.x >= a.main_grid) {  // extra workgroups: untouched-row AdamW slice
-    sweep_slice(a.sw, a.sw_slot, blockIdx.x - a.main_grid, gridDim.x - a.main_grid);
+  const int rb = role_block(a.main_grid, a.xpack);
+  if (rb >= a.main_grid) {  // extra workgroups: untouched-row AdamW slice
+    sweep_slice(a.sw, a.sw_slot, rb - a.main_grid, gridDim.x - a.main_grid);
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   GTR_PH(a.layer, 0);
   const int Gn = a.bt.hdr[4];
   int N = a.bt.hdr[0];
-  const int g = blockIdx.x;
+  const int g = rb;
   if (g >= Gn) {
     if (a.sync && a.has_prev)  // SyncBN: an empty group's backward partial is zero
       for (int j = threadIdx.x; j < 2 * D; j += CONV_BLOCK) a.p_gpart[(size_t)g * 2 * D + j] = 0.0f;
@@ -226,7 +229,7 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
   const int H = a.H, C = a.C;
   const int ne = e_hi - e_lo;
   const bool fast = G::KV && nrow <= RMAX && ne <= G::EMAX && ne * H <= G::EH && H <= 8 && C >= CH;
-  const uint32_t ctr = a.rng_ctr ? *a.rng_ctr : 0u;
+  const uint32_t ctr = a.rng_ctr ? *a.rng_ctr + a.ctr_add : 0u;
   const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
   const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
   const float invN = 1.0f / (float)N;
@@ -355,16 +358,28 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
     __syncthreads();
 
     // ---- (D3) softmax backward per (destination, head): dlogit = alpha * (da - sum alpha*da)
-    for (int idx = tid; idx < nrow * H; idx += CONV_BLOCK) {
-      const int i = idx / H, h = idx - i * H;
-      const int e0 = iptr[i], e1 = iptr[i + 1];
-      float sdot = 0.0f;
-      for (int e = e0; e < e1; ++e) sdot += AL[e * H + h] * DL[e * H + h];
-      for (int e = e0; e < e1; ++e) {
-        const int k = e * H + h;
-        const float al = AL[k];
-        DL[k] = al * (DL[k] - sdot);
-        AL[k] = al * dr.mul(st_attn, (uint32_t)((e + e_lo) * H + h));
+    //      GL lanes per (row, head), edges strided over the lanes, sum by shuffles
+    {
+      const int pairs = nrow * H;
+      const int GL = pair_lanes(pairs, CONV_BLOCK);
+      for (int base = 0; base < pairs; base += CONV_BLOCK / GL) {
+        const int pidx = base + tid / GL, gl = tid & (GL - 1);
+        int h = 0, e0 = 0, e1 = 0;
+        if (pidx < pairs) {
+          const int i = pidx / H;
+          h = pidx - i * H;
+          e0 = iptr[i];
+          e1 = iptr[i + 1];
+        }
+        float sdot = 0.0f;
+        for (int e = e0 + gl; e < e1; e += GL) sdot += AL[e * H + h] * DL[e * H + h];
+        sdot = group_sum(sdot, GL);
+        for (int e = e0 + gl; e < e1; e += GL) {
+          const int k = e * H + h;
+          const float al = AL[k];
+          DL[k] = al * (DL[k] - sdot);
+          AL[k] = al * dr.mul(st_attn, (uint32_t)((e + e_lo) * H + h));
+        }
       }
     }
     __syncthreads();
@@ -660,6 +675,7 @@ extern "C" int gtr_conv_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   k.scale = k.drop_on ? (float)(1.0 / (1.0 - p)) : 1.0f;
   k.seed = cfg->seed;
   k.rng_ctr = cfg->rng_ctr;
+  k.ctr_add = (uint32_t)cfg->ctr_add;
   k.dy = L.dy; k.out = L.out; k.stats = L.bn_stats; k.gsum = L.bn_gsum; k.gpart = L.bn_gpart; k.gamma = L.bn_gamma;
   k.qkvs = L.qkvs; k.alpha = L.alpha; k.agg = L.agg; k.gate = L.gate; k.w_all = L.w_all; k.w_beta = L.w_beta;
   k.dqkvs = L.dqkvs; k.du = L.du; k.dlogit = L.dlogit; k.dagg = L.dagg;
@@ -690,6 +706,7 @@ extern "C" int gtr_conv_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
       grid += cfg->sweep->blocks;
     }
   }
+  k.xpack = xcd_pack(k.main_grid, grid);
   hipStream_t s = (hipStream_t)stream;
 #define GTR_BWD(DD, SP) set_lds_limit<DD>(k_conv_bwd<DD, SP>, (size_t)LayerGeom<DD>::B_WORDS * 4); \
   hipLaunchKernelGGL((k_conv_bwd<DD, SP>), dim3(grid), dim3(CONV_BLOCK), \

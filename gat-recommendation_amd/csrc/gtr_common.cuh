@@ -34,6 +34,21 @@ __device__ __forceinline__ float group_sum(float x, int gl) {
   return x;
 }
 
+// Max inside aligned groups of `gl` lanes (gl a power of two <= 64).
+__device__ __forceinline__ float group_max(float x, int gl) {
+  for (int o = 1; o < gl; o <<= 1) x = fmaxf(x, __shfl_xor(x, o));
+  return x;
+}
+
+// Lanes per (destination row, head) pair of a row group's segmented softmax passes: the
+// widest power of two <= 64 that keeps every pair of the group in one round of `blk`
+// threads (the in-edges of a pair are strided over its lanes, reduced by shuffles).
+__device__ __forceinline__ int pair_lanes(int pairs, int blk) {
+  int gl = 64;
+  while (gl > 1 && gl * pairs > blk) gl >>= 1;
+  return gl;
+}
+
 // Counter-based dropout stream: one 32-bit hash per (seed, stream, element).
 __device__ __forceinline__ uint32_t mix3(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t h = a * 0x9E3779B1u;
@@ -99,6 +114,20 @@ __device__ __forceinline__ void group_rows(const int32_t* node_ptr, int B, int R
   const int s1 = wave_lower_bound(node_ptr, B, (g + 1) * R);
   r0 = node_ptr[s0];
   r1 = node_ptr[s1];
+}
+
+// XCD-packed block roles (speed only, never correctness): hardware blocks b and b + 8
+// share an XCD under the round-robin dispatch, so with `pack` the launch's M main
+// workgroups (row groups / readout sessions) run on blocks 0, 8, 16, ...: they then share
+// one XCD's L2 for the layer's weights (fetched once, not once per XCD) and for the rows
+// they exchange; the extra workgroups (sweep slices, fused begin) take the other blocks.
+// Returns the ROLE index: [0, M) main, [M, gridDim.x) extra.  Host: pack only when
+// 8 * (M - 1) < gridDim.x (gtr::xcd_pack).
+__device__ __forceinline__ int role_block(int M, int pack) {
+  const int b = blockIdx.x;
+  if (!pack) return b;
+  if ((b & 7) == 0 && (b >> 3) < M) return b >> 3;
+  return M + b - min(M, (b + 7) >> 3);
 }
 
 // Last-arriver election across the workgroups of one launch (placement independent:
@@ -276,6 +305,12 @@ __device__ __forceinline__ void sweep_slice(const gtr_sweep& sw, int slot, int b
 // each product; after a few AdamW steps that moved a few parameters per million past the
 // north star's elementwise 1e-3 bar against the fp32 oracle on the full C3 / C5 tables
 // (tests/test_gpu_fullsize.py), so it is not the default at any width.
+inline int xcd_pack(int main_blocks, int grid) {
+  const char* e = getenv("GTR_XCD_PACK");
+  if (e && e[0] == '0') return 0;
+  return main_blocks > 0 && 8 * (main_blocks - 1) < grid ? 1 : 0;
+}
+
 inline int gemm_split(int dim) {
   (void)dim;
   const char* e = getenv("GTR_GEMM");  // read per launch: tests switch it within a process
@@ -288,7 +323,7 @@ inline int gemm_split(int dim) {
 // kernels, s_memrealtime (100 MHz) taken by thread 0; read back by gtr_dbg_*_phases.
 #define GTR_PH_KERNELS 32
 #define GTR_PH_GROUPS 1024
-#define GTR_PH_SLOTS 8
+#define GTR_PH_SLOTS 16
 #ifdef GTR_PHASE_TIMING
 #define GTR_PH_DECL static __device__ unsigned long long g_ph[GTR_PH_KERNELS][GTR_PH_GROUPS][GTR_PH_SLOTS];
 #define GTR_PH(kid, k)                                                                               \

@@ -17,6 +17,7 @@
 //   the last BatchNorm's backward partial sums.
 
 #include "gtr_layer.cuh"
+#include "gtr_rows.cuh"
 
 namespace {
 
@@ -63,6 +64,10 @@ struct ConvFwdK {
   int sw_slot, main_grid;
   int sync, p_nparts;   // SyncBN: previous layer's partials of every rank (p_part_all, p_nparts)
   const float* p_part_all;
+  uint32_t ctr_add;     // dropout counter read as *rng_ctr + ctr_add (1 with a fused begin)
+  int nbeg;             // fused step begin (layer 0): roles [main_grid, main_grid + nbeg)
+  gtr_begin beg;
+  int xpack, pad_x;     // XCD-packed roles (role_block)
 };
 
 // Block prologue shared by k_conv_fwd (previous layer) and k_readout (last layer):
@@ -73,7 +78,7 @@ struct ConvFwdK {
 template <int D, int BLK>
 __device__ __forceinline__ void prev_bn_stats(int train, int cred, int G, const float* part, float* stats,
                                               float* rmean, float* rvar, int64_t* nbt, float eps, float mom,
-                                              float* s_mean, float* s_rstd, float* s_uvar, float* scr) {
+                                              float* s_mean, float* s_rstd, float* s_uvar, float* scr, bool lead) {
   if (!train) {
     for (int j = threadIdx.x; j < D; j += BLK) {
       s_mean[j] = rmean[j];
@@ -81,7 +86,7 @@ __device__ __forceinline__ void prev_bn_stats(int train, int cred, int G, const 
     }
   } else if (cred) {
     bn_stats_from_parts<D, BLK>(part, G, eps, s_mean, s_rstd, s_uvar, scr);
-    if (blockIdx.x == 0) {
+    if (lead) {
       for (int j = threadIdx.x; j < D; j += BLK) {
         stats[j] = s_mean[j];
         stats[D + j] = s_rstd[j];
@@ -163,6 +168,50 @@ __device__ __forceinline__ void attn_row(const ConvFwdK& a, int t, int tl, const
   if (lane == 0) a.gate[t] = beta;
 }
 
+// gtr_step_begin's work run by extra workgroups of conv_fwd(layer 0) (gtr_begin): each of
+// them stages every (row << 13 | slot) composite in LDS and ranks 64 slots, its 8 waves
+// counting over slices (the rank sort of k_step_begin with 512 threads); workgroup 0 also
+// stamps the touched rows and advances the step counter.  The dropout counter is left
+// to the tail: the row groups of this very launch read it (gtr_config.ctr_add).
+__device__ __forceinline__ void begin_slice(const gtr_batch& bt, const gtr_begin& g, int blk, uint32_t* ck) {
+  int* part = reinterpret_cast<int*>(ck + GTR_BEGIN_MCAP);  // [CONV_WAVES][64]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
+  const int m4 = (m_cap + 3) & ~3;
+  const int N = bt.hdr[0], B = bt.hdr[1];
+  const bool lead = blk == 0;
+  const int32_t tnew = lead ? (int32_t)(*g.step_dev + 1) : 0;
+  for (int j = tid; j < m4; j += CONV_BLOCK) {
+    uint32_t c = 0xFFFFFFFFu;
+    if (j < m_cap) {
+      const int key = contrib_key(bt, g.num_items, j, N, B);
+      c = ((uint32_t)key << 13) | (uint32_t)j;
+      if (lead && g.stamp && key > 0 && key < g.num_items) g.stamp[key] = tnew;
+    }
+    ck[j] = c;
+  }
+  __syncthreads();
+  const int j = blk * 64 + lane;
+  const uint32_t mine = j < m_cap ? ck[j] : 0u;
+  const int S = ((m4 / CONV_WAVES) + 4) & ~3;
+  const int i0 = wave * S, i1 = min(m4, i0 + S);
+  int rank = 0;
+  for (int i = i0; i < i1; i += 4) {
+    const uint4 q = *reinterpret_cast<const uint4*>(ck + i);
+    rank += (q.x < mine) + (q.y < mine) + (q.z < mine) + (q.w < mine);
+  }
+  part[wave * 64 + lane] = rank;
+  __syncthreads();
+  if (wave == 0 && j < m_cap) {
+    int r = 0;
+#pragma unroll
+    for (int w = 0; w < CONV_WAVES; ++w) r += part[w * 64 + lane];
+    g.skeys[r] = (int32_t)(mine >> 13);
+    g.svals[r] = (int32_t)(mine & 0x1FFFu);
+  }
+  if (lead && tid == 0) *g.step_dev = tnew;
+}
+
 // Offset of float4 number kb of a lane's W-row fragment: f32 MFMA (k = kb*16 + lg*4 ..)
 // or split-bf16 MFMA (k-step kb/2 of 32, lane quad lg's 8 values, half kb&1).
 __device__ __forceinline__ int wfrag_off(int kb, int lg, int split) {
@@ -172,6 +221,7 @@ __device__ __forceinline__ int wfrag_off(int kb, int lg, int split) {
 template <int D, bool SPLIT>
 __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
   using G = LayerGeom<D>;
+  static_assert(G::F_WORDS >= GTR_BEGIN_MCAP + CONV_WAVES * 64, "LDS carve too small for the fused begin");
   constexpr int VPL = G::VPL, RMAX = G::RMAX, XS = G::XS, KPE = G::KPE, TPR = G::TPR, CH = G::CH;
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* XO = sm + G::F_XO;
@@ -188,15 +238,20 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
   __bf16* XH = reinterpret_cast<__bf16*>(sm + G::F_XH);
   __bf16* XL = reinterpret_cast<__bf16*>(sm + G::F_XL);
 
-  if ((int)blockIdx.x >= a.main_grid) {  // extra workgroups: untouched-row AdamW slice
-    sweep_slice(a.sw, a.sw_slot, blockIdx.x - a.main_grid, gridDim.x - a.main_grid);
+  const int rb = role_block(a.main_grid, a.xpack);
+  if (rb >= a.main_grid + a.nbeg) {  // extra workgroups: untouched-row AdamW slice
+    sweep_slice(a.sw, a.sw_slot, rb - a.main_grid - a.nbeg, gridDim.x - a.main_grid - a.nbeg);
+    return;
+  }
+  if (rb >= a.main_grid) {  // fused step begin (layer 0)
+    begin_slice(a.bt, a.beg, rb - a.main_grid, reinterpret_cast<uint32_t*>(sm));
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   GTR_PH(a.layer, 0);
   GTR_PH_CLK(a.layer, 6);
   const int Gn = a.bt.hdr[4];
-  const int g = blockIdx.x;
+  const int g = rb;
   if (g >= Gn) {
     if (a.sync && a.train)  // SyncBN: an empty group contributes a zero-count partial
       for (int j = threadIdx.x; j < 1 + 2 * D; j += CONV_BLOCK) a.bn_part[(size_t)g * (1 + 2 * D) + j] = 0.0f;
@@ -209,7 +264,8 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
   // fast path: the group's rows, edges and (edge, head) logits fit the LDS carve and
   // every thread's CH-feature chunk lies inside one head
   const bool fast = G::KV && nrow <= RMAX && ne <= G::EMAX && ne * a.H <= G::EH && a.H <= 8 && a.C >= CH;
-  const uint32_t ctr = a.rng_ctr ? *a.rng_ctr : 0u;
+  if (fast) GTR_PH(a.layer, 10);
+  const uint32_t ctr = a.rng_ctr ? *a.rng_ctr + a.ctr_add : 0u;
   const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
   const bool pe_lds = a.first && a.pe_k > 0 && a.pe_k <= KPE;
   const int lr = lane & 15, lg = lane >> 4;
@@ -253,7 +309,7 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
   if (!a.first) {
     prev_bn_stats<D, CONV_BLOCK>(a.train, a.cred, a.sync ? a.p_nparts : Gn, a.sync ? a.p_part_all : a.p_part,
                                  a.p_stats, a.p_rmean, a.p_rvar, a.p_nbt, a.bn_eps,
-                                 a.bn_mom, s_bn, s_bn + D, XO, LOG);
+                                 a.bn_mom, s_bn, s_bn + D, XO, LOG, g == 0);
   }
   if (fast) {
     for (int i = tid; i <= nrow; i += CONV_BLOCK) iptr[i] = a.bt.in_ptr[r0 + i] - e_lo;
@@ -342,6 +398,7 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
       }
     }
     __syncthreads();
+    GTR_PH(a.layer, 11);
     // W fragments of tiles past the prefetched ones are double-buffered: tile ti+1's
     // loads are issued before tile ti's MFMAs and stores (the compiler cannot hoist them
     // over the qkvs stores itself), so only the first such tile waits on L2
@@ -453,34 +510,52 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
       if (idx < nit && idx == it * SPL) LOG[it] = dot / a.sqrt_c;
     }
     __syncthreads();
+    GTR_PH(a.layer, 5);
     // (S) softmax over each destination's in-edges per head (PyG softmax: exp(l - max) /
-    //     (sum + 1e-16)); alpha -> HBM for backward, alpha * dropout mask -> LDS
-    for (int idx = tid; idx < nrow * H; idx += CONV_BLOCK) {
-      const int i = idx / H, h = idx - i * H;
-      const int e0 = iptr[i], e1 = iptr[i + 1];
-      float m = -INFINITY;
-      for (int e = e0; e < e1; ++e) m = fmaxf(m, LOG[e * H + h]);
-      float z = 0.0f;
-      for (int e = e0; e < e1; ++e) z += expf(LOG[e * H + h] - m);
-      const float zd = z + 1e-16f;
-      for (int e = e0; e < e1; ++e) {
-        const int eg = (e + e_lo) * H + h;
-        const float al = expf(LOG[e * H + h] - m) / zd;
-        a.alpha[eg] = al;
-        LOG[e * H + h] = al * dr.mul(st_attn, (uint32_t)eg);
+    //     (sum + 1e-16)); alpha -> HBM for backward, alpha * dropout mask -> LDS.  GL lanes
+    //     per (row, head): edges strided over the lanes, max and sum by shuffles (a serial
+    //     walk per row made the group's busiest destination the phase's critical path)
+    {
+      const int pairs = nrow * H;
+      const int GL = pair_lanes(pairs, CONV_BLOCK);
+      for (int base = 0; base < pairs; base += CONV_BLOCK / GL) {
+        const int pidx = base + tid / GL, gl = tid & (GL - 1);
+        int h = 0, e0 = 0, e1 = 0;
+        if (pidx < pairs) {
+          const int i = pidx / H;
+          h = pidx - i * H;
+          e0 = iptr[i];
+          e1 = iptr[i + 1];
+        }
+        float m = -INFINITY;
+        for (int e = e0 + gl; e < e1; e += GL) m = fmaxf(m, LOG[e * H + h]);
+        m = group_max(m, GL);
+        float z = 0.0f;
+        for (int e = e0 + gl; e < e1; e += GL) z += expf(LOG[e * H + h] - m);
+        const float zd = group_sum(z, GL) + 1e-16f;
+        for (int e = e0 + gl; e < e1; e += GL) {
+          const int eg = (e + e_lo) * H + h;
+          const float al = expf(LOG[e * H + h] - m) / zd;
+          a.alpha[eg] = al;
+          LOG[e * H + h] = al * dr.mul(st_attn, (uint32_t)eg);
+        }
       }
     }
     __syncthreads();
-    // (G) aggregation + beta gate: TPR lanes per row, CH features each
+    GTR_PH(a.layer, 8);
+    // (G) aggregation + beta gate: TPR lanes per row, CH features each (the in-edge walk
+    //     can be split ES ways over further lanes, partials summed by shuffles)
+    const int ES = 1;  // edge splits measured slower at C2 (1.04 -> 1.32 us): the shuffles cost more than the walk
+    const int grow = tid / (TPR * ES), es = (tid / TPR) & (ES - 1);
     float ag[CH], sv[CH];
     float u = 0.0f;
-    const bool live = prow < nrow;
+    const bool live = grow < nrow;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) ag[c] = 0.0f;
     if (live) {
       const int hd = f0 / C;
-#pragma unroll
-      for (int c = 0; c < CH; ++c) ag[c] = 0.0f;
-      const int e1 = iptr[prow + 1];
-      for (int e = iptr[prow]; e < e1; ++e) {
+      const int e1 = iptr[grow + 1];
+      for (int e = iptr[grow] + es; e < e1; e += ES) {
         const float ad = LOG[e * H + hd];
         const float* vr = KVs + RMAX * XS + isrc[e] * XS + f0;
 #pragma unroll
@@ -489,7 +564,13 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
           ag[c] += ad * v.x; ag[c + 1] += ad * v.y; ag[c + 2] += ad * v.z; ag[c + 3] += ad * v.w;
         }
       }
-      const float* srow = QSs + RMAX * XS + prow * XS + f0;
+    }
+    for (int o = TPR; o < TPR * ES; o <<= 1) {
+#pragma unroll
+      for (int c = 0; c < CH; ++c) ag[c] += __shfl_xor(ag[c], o);
+    }
+    if (live) {
+      const float* srow = QSs + RMAX * XS + grow * XS + f0;
 #pragma unroll
       for (int c = 0; c < CH; c += 4) {
         const float4 v = *reinterpret_cast<const float4*>(srow + c);
@@ -500,9 +581,9 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
     }
 #pragma unroll
     for (int o = 1; o < TPR; o <<= 1) u += __shfl_xor(u, o);
-    if (live) {
+    if (live && es == 0) {
       const float beta = 1.0f / (1.0f + expf(-u));
-      const size_t ro = (size_t)(r0 + prow) * D + f0;
+      const size_t ro = (size_t)(r0 + grow) * D + f0;
 #pragma unroll
       for (int c = 0; c < CH; c += 4) {
         float4 o4;
@@ -512,9 +593,9 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
         o4.w = beta * sv[c + 3] + (1.0f - beta) * ag[c + 3];
         *reinterpret_cast<float4*>(a.agg + ro + c) = make_float4(ag[c], ag[c + 1], ag[c + 2], ag[c + 3]);
         *reinterpret_cast<float4*>(a.out + ro + c) = o4;
-        *reinterpret_cast<float4*>(XO + prow * XS + f0 + c) = o4;
+        *reinterpret_cast<float4*>(XO + grow * XS + f0 + c) = o4;
       }
-      if (pchunk == 0) a.gate[r0 + prow] = beta;
+      if (pchunk == 0) a.gate[r0 + grow] = beta;
     }
   } else {
     for (int t = r0 + wave; t < r1; t += CONV_WAVES)
@@ -625,6 +706,8 @@ struct ReadoutK {
   int sw_slot, main_grid;
   int sync, nparts;     // SyncBN: the last layer's partials of every rank (part_all, nparts)
   const float* part_all;
+  uint32_t ctr_add;
+  int xpack;            // XCD-packed roles (role_block)
 };
 
 // Block per session (grid-strided): RO_WAVES waves split the session's node rows and
@@ -646,8 +729,9 @@ __global__ __launch_bounds__(RO_BLOCK) void k_readout(ReadoutK a) {
   __shared__ float s_red[RO_WAVES][2 * D];
   __shared__ float s_loss[RO_WAVES][2];
   __shared__ int s_flag;
-  if ((int)blockIdx.x >= a.main_grid) {  // extra workgroups: untouched-row AdamW slice
-    sweep_slice(a.sw, a.sw_slot, blockIdx.x - a.main_grid, gridDim.x - a.main_grid);
+  const int rb = role_block(a.main_grid, a.xpack);
+  if (rb >= a.main_grid) {  // extra workgroups: untouched-row AdamW slice
+    sweep_slice(a.sw, a.sw_slot, rb - a.main_grid, gridDim.x - a.main_grid);
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -656,7 +740,7 @@ __global__ __launch_bounds__(RO_BLOCK) void k_readout(ReadoutK a) {
   const int n = a.bt.n_neg;
   const int d0 = lane * VPL;
   const bool act = d0 < D;
-  const uint32_t ctr = a.rng_ctr ? *a.rng_ctr : 0u;
+  const uint32_t ctr = a.rng_ctr ? *a.rng_ctr + a.ctr_add : 0u;
   const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
   const uint32_t st = drop_stream(1, (uint32_t)a.L1, ctr);
   const bool do_fwd = a.flags & GTR_RO_FWD, do_loss = a.flags & GTR_RO_LOSS, do_bwd = a.flags & GTR_RO_BWD;
@@ -672,7 +756,7 @@ __global__ __launch_bounds__(RO_BLOCK) void k_readout(ReadoutK a) {
   if (do_fwd) {
     prev_bn_stats<D, RO_BLOCK>(a.train, a.cred, a.sync ? a.nparts : a.bt.hdr[4], a.sync ? a.part_all : a.part,
                                a.stats, a.rmean, a.rvar, a.nbt, a.bn_eps,
-                               a.bn_mom, s_bn, s_bn + D, s_bn + 2 * D, s_scr);
+                               a.bn_mom, s_bn, s_bn + D, s_bn + 2 * D, s_scr, rb == 0);
   } else if (do_bwd) {
     for (int j = tid; j < D; j += RO_BLOCK) { s_bn[j] = a.stats[j]; s_bn[D + j] = a.stats[D + j]; }
   }
@@ -692,7 +776,7 @@ __global__ __launch_bounds__(RO_BLOCK) void k_readout(ReadoutK a) {
   for (int v = 0; v < VPL; ++v) { gs[v] = 0.0f; gx[v] = 0.0f; }
   float lw_sum = 0.0f, bpr_sum = 0.0f;
 
-  for (int b = blockIdx.x; b < B; b += a.main_grid) {
+  for (int b = rb; b < B; b += a.main_grid) {
     const int n0 = a.bt.node_ptr[b], n1 = a.bt.node_ptr[b + 1];
     const float cnt = (float)(n1 - n0);
     const int* negs = a.bt.negatives + (size_t)b * n;
@@ -920,13 +1004,13 @@ __global__ __launch_bounds__(RO_BLOCK) void k_readout(ReadoutK a) {
   if (do_loss && tid < 2) {
     float acc = 0.0f;
     for (int w = 0; w < RO_WAVES; ++w) acc += s_loss[w][tid];
-    a.loss_part[(size_t)blockIdx.x * 2 + tid] = acc;
+    a.loss_part[(size_t)rb * 2 + tid] = acc;
   }
   if (do_bwd) {
     for (int j = tid; j < 2 * D; j += RO_BLOCK) {
       float acc = 0.0f;
       for (int w = 0; w < RO_WAVES; ++w) acc += s_red[w][j];
-      a.gpart[(size_t)blockIdx.x * 2 * D + j] = acc;
+      a.gpart[(size_t)rb * 2 * D + j] = acc;
     }
   }
   GTR_PH(16, 3);
@@ -1058,8 +1142,9 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
   __shared__ float s_loss[RW_WAVES][2];
   __shared__ float s_sc[RW_WAVES][RW_NMAX];  // raw listwise scores of the wave's session
   __shared__ int s_flag;
-  if ((int)blockIdx.x >= a.main_grid) {  // extra workgroups: untouched-row AdamW slice
-    sweep_slice(a.sw, a.sw_slot, blockIdx.x - a.main_grid, gridDim.x - a.main_grid);
+  const int rb = role_block(a.main_grid, a.xpack);
+  if (rb >= a.main_grid) {  // extra workgroups: untouched-row AdamW slice
+    sweep_slice(a.sw, a.sw_slot, rb - a.main_grid, gridDim.x - a.main_grid);
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1067,7 +1152,7 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
   const bool lead = (lane & 15) == 0;
   const int B = a.bt.hdr[1];
   const int n = a.bt.n_neg;
-  const uint32_t ctr = a.rng_ctr ? *a.rng_ctr : 0u;
+  const uint32_t ctr = a.rng_ctr ? *a.rng_ctr + a.ctr_add : 0u;
   const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
   const uint32_t st = drop_stream(1, (uint32_t)a.L1, ctr);
   const bool do_fwd = a.flags & GTR_RO_FWD, do_loss = a.flags & GTR_RO_LOSS, do_bwd = a.flags & GTR_RO_BWD;
@@ -1082,7 +1167,7 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
   if (do_fwd) {
     prev_bn_stats<D, RW_BLOCK>(a.train, a.cred, a.sync ? a.nparts : a.bt.hdr[4], a.sync ? a.part_all : a.part,
                                a.stats, a.rmean, a.rvar, a.nbt, a.bn_eps,
-                               a.bn_mom, s_bn, s_bn + D, s_bn + 2 * D, s_scr);
+                               a.bn_mom, s_bn, s_bn + D, s_bn + 2 * D, s_scr, rb == 0);
   } else if (do_bwd) {
     for (int j = tid; j < D; j += RW_BLOCK) { s_bn[j] = a.stats[j]; s_bn[D + j] = a.stats[D + j]; }
   }
@@ -1094,7 +1179,7 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
   float lw_sum = 0.0f, bpr_sum = 0.0f;
 
 #pragma unroll 1
-  for (int b = blockIdx.x * RW_WAVES + wave; b < B; b += a.main_grid * RW_WAVES) {
+  for (int b = rb * RW_WAVES + wave; b < B; b += a.main_grid * RW_WAVES) {
     const int n0 = a.bt.node_ptr[b], n1 = a.bt.node_ptr[b + 1];
     const float cnt = (float)(n1 - n0);
     const int* negs = a.bt.negatives + (size_t)b * n;
@@ -1247,13 +1332,13 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
   if (do_loss && tid < 2) {
     float acc = 0.0f;
     for (int w = 0; w < RW_WAVES; ++w) acc += s_loss[w][tid];
-    a.loss_part[(size_t)blockIdx.x * 2 + tid] = acc;
+    a.loss_part[(size_t)rb * 2 + tid] = acc;
   }
   if (do_bwd) {
     for (int j = tid; j < 2 * D; j += RW_BLOCK) {
       float acc = 0.0f;
       for (int w = 0; w < RW_WAVES; ++w) acc += s_red[w][j];
-      a.gpart[(size_t)blockIdx.x * 2 * D + j] = acc;
+      a.gpart[(size_t)rb * 2 * D + j] = acc;
     }
   }
   if (!a.fin) return;
@@ -1330,6 +1415,7 @@ extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   drop_params(cfg, k.thresh, k.scale, k.drop_on);
   k.seed = cfg->seed;
   k.rng_ctr = cfg->rng_ctr;
+  k.ctr_add = (uint32_t)cfg->ctr_add;
   k.sync = cfg->sync_bn;
   if (cfg->sync_bn && !cfg->consumer_reduce) { set_error("gtr_conv_fwd: sync_bn needs consumer_reduce"); return GTR_E_ARG; }
   if (l == 0) {
@@ -1352,11 +1438,28 @@ extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   int grid = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;
   if (grid <= 0) return GTR_OK;
   k.main_grid = grid;
+  if (l == 0 && cfg->begin) {
+    const gtr_begin& g = *cfg->begin;
+    const int m_cap = bt->n_cap + bt->b_cap * (1 + bt->n_neg);
+    if (!g.skeys || !g.svals || !g.step_dev || g.num_items <= 0 || g.num_items >= GTR_BEGIN_KEY_LIMIT ||
+        m_cap > GTR_BEGIN_MCAP || bt->n_neg <= 0) {
+      set_error("gtr_conv_fwd: fused begin needs skeys/svals/step_dev, m_cap <= %d and T < 2^19", GTR_BEGIN_MCAP);
+      return GTR_E_ARG;
+    }
+    if (cfg->sweep && cfg->sweep->bounds[1] > cfg->sweep->bounds[0]) {
+      set_error("gtr_conv_fwd: a fused begin stamps the rows the layer-0 sweep slice would read: slot 0 must be empty");
+      return GTR_E_ARG;
+    }
+    k.beg = g;
+    k.nbeg = (m_cap + 63) / 64;
+    grid += k.nbeg;
+  }
   if (cfg->sweep && l < GTR_SWEEP_SLOTS && cfg->sweep->bounds[l + 1] > cfg->sweep->bounds[l]) {
     k.sw = *cfg->sweep;
     k.sw_slot = l;
     grid += cfg->sweep->blocks;
   }
+  k.xpack = xcd_pack(k.main_grid, grid);
   hipStream_t s = (hipStream_t)stream;
 #define GTR_FWD(DD, SP) set_lds_limit<DD>(k_conv_fwd<DD, SP>, (size_t)LayerGeom<DD>::F_WORDS * 4); \
   hipLaunchKernelGGL((k_conv_fwd<DD, SP>), dim3(grid), dim3(CONV_BLOCK), (size_t)LayerGeom<DD>::F_WORDS * 4, s, k)
@@ -1405,6 +1508,7 @@ extern "C" int gtr_readout_loss(const gtr_config* cfg, const gtr_batch* bt, cons
   drop_params(cfg, k.thresh, k.scale, k.drop_on);
   k.seed = cfg->seed;
   k.rng_ctr = cfg->rng_ctr;
+  k.ctr_add = (uint32_t)cfg->ctr_add;
   k.table = table;
   k.out = L.out; k.xin = L.xin; k.stats = L.bn_stats; k.part = L.bn_part; k.gamma = L.bn_gamma; k.beta = L.bn_beta;
   k.rmean = L.bn_rmean; k.rvar = L.bn_rvar; k.nbt = L.bn_nbt;
@@ -1427,6 +1531,7 @@ extern "C" int gtr_readout_loss(const gtr_config* cfg, const gtr_batch* bt, cons
     k.sw_slot = cfg->num_layers;
     grid += cfg->sweep->blocks;
   }
+  k.xpack = xcd_pack(k.main_grid, grid);
   hipStream_t s = (hipStream_t)stream;
   if (bt->b_cap >= ro_wave_min_b() && cfg->dim <= 128) {
     switch (cfg->dim) {

@@ -57,22 +57,6 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_adamw_small(SmallK a) {
   small_body(e, a.segs, a.nseg, a.param, a.m, a.v, a.grad_out, st);
 }
 
-// Contribution key of slot j (sentinel T for unused slots), see gtr_contrib_prep.
-__device__ __forceinline__ int contrib_key(const gtr_batch& bt, int T, int j, int N, int B) {
-  int key = T;
-  if (j < bt.n_cap) {
-    if (j < N) key = bt.node_item[j];
-  } else if (j < bt.n_cap + bt.b_cap) {
-    const int b = j - bt.n_cap;
-    if (b < B) key = bt.target[b];
-  } else {
-    const int q = j - bt.n_cap - bt.b_cap;
-    if (q / bt.n_neg < B) key = bt.negatives[q];
-  }
-  if (key < 0 || key > T) key = T;
-  return key;
-}
-
 __global__ __launch_bounds__(GTR_BLOCK) void k_contrib_prep(gtr_batch bt, int T, int32_t* keys, int32_t* vals,
                                                             int32_t* stamp, const int64_t* step_dev) {
   const int j = blockIdx.x * GTR_BLOCK + threadIdx.x;
@@ -241,8 +225,6 @@ __device__ __forceinline__ void lazy_claim_row(int key, int T, int D, int32_t t,
 // ---- fused step: begin (counters, stamps, sorted contribution list) -------------------
 #define GTR_BEGIN_BLOCK 1024
 #define GTR_BEGIN_WAVES (GTR_BEGIN_BLOCK / 64)
-#define GTR_BEGIN_MCAP 8192
-#define GTR_BEGIN_KEY_LIMIT (1 << 19)
 #define GTR_TAILW_NCAP 512  // node-row capacity up to which the tail computes the weight gradients
 
 // Rank sort: composite keys (row << 13 | slot) are unique, so the stable order by row
@@ -521,6 +503,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_step_tail(TailK a) {
   __syncthreads();
   const AdamStep st = s_st;
   const int blk = blockIdx.x;
+  if (blk == 0 && tid == 0 && a.tl.rng_inc) *a.tl.rng_inc += 1;  // fused begin: the step's dropout counter
   if (blk < a.nb_rows && a.windowed) {
     window_rows<D>(blk, a.bt, a.T, a.tl, st, a.tl.lazy_consts ? a.tl.stamp : nullptr, s_t);
     return;
@@ -585,6 +568,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_step_tail_wgrad(TailWK a) {
   __syncthreads();
   const AdamStep st = s_st;
   int blk = blockIdx.x;
+  if (blk == 0 && tid == 0 && a.tl.rng_inc) *a.tl.rng_inc += 1;  // fused begin: the step's dropout counter
   if (blk < a.nb_rows) {
     rows_body<D>(blk * GTR_BLOCK + tid, a.bt, a.T, a.tl.skeys, a.tl.svals, a.tl.dx0, a.tl.se, a.tl.coef_tgt,
                  a.tl.coef_neg, a.tl.table, a.tl.table_m, a.tl.table_v, nullptr, st,

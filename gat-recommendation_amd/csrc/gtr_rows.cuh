@@ -8,6 +8,25 @@
 
 namespace gtr {
 
+#define GTR_BEGIN_MCAP 8192            // contributions ranked in LDS by the one-launch begin
+#define GTR_BEGIN_KEY_LIMIT (1 << 19)  // rows a (row << 13 | slot) composite key can hold
+
+// Contribution key of slot j (sentinel T for unused slots), see gtr_contrib_prep.
+__device__ __forceinline__ int contrib_key(const gtr_batch& bt, int T, int j, int N, int B) {
+  int key = T;
+  if (j < bt.n_cap) {
+    if (j < N) key = bt.node_item[j];
+  } else if (j < bt.n_cap + bt.b_cap) {
+    const int b = j - bt.n_cap;
+    if (b < B) key = bt.target[b];
+  } else {
+    const int q = j - bt.n_cap - bt.b_cap;
+    if (q / bt.n_neg < B) key = bt.negatives[q];
+  }
+  if (key < 0 || key > T) key = T;
+  return key;
+}
+
 // Small parameters: element e of the flat buffer; its segment's gradient partials summed.
 __device__ __forceinline__ void small_body(int64_t e, const gtr_segment* segs, int nseg, float* param, float* m,
                                            float* v, float* grad_out, const AdamStep& st) {

@@ -37,8 +37,12 @@ class GtrConfig(C.Structure):
         ("num_items", i32), ("dim", i32), ("heads", i32), ("pe_k", i32), ("num_layers", i32),
         ("row_group", i32), ("training", i32), ("dropout", f32), ("bn_eps", f32),
         ("bn_momentum", f32), ("seed", u32), ("rng_ctr", P), ("consumer_reduce", i32), ("sync_bn", i32),
-        ("sweep", P),
+        ("sweep", P), ("begin", P), ("ctr_add", i32), ("pad_cfg", i32),
     ]
+
+
+class GtrBegin(C.Structure):
+    _fields_ = [("skeys", P), ("svals", P), ("stamp", P), ("step_dev", P), ("num_items", i32), ("pad", i32)]
 
 
 class GtrLayer(C.Structure):
@@ -83,12 +87,12 @@ class GtrTail(C.Structure):
         ("table", P), ("table_m", P), ("table_v", P), ("stamp", P),
         ("flat", P), ("flat_m", P), ("flat_v", P), ("flat_total", i64),
         ("loss_part", P), ("loss_out", P), ("loss_nparts", i32), ("pad0", i32), ("carry", P),
-        ("sweep_from", i64), ("lazy_consts", P),
+        ("sweep_from", i64), ("lazy_consts", P), ("rng_inc", P),
     ]
 
 
 SWEEP_SLOTS = 8
-ABI_VERSION = 2  # GTR_ABI_VERSION of include/gtr.h
+ABI_VERSION = 3  # GTR_ABI_VERSION of include/gtr.h
 
 
 class GtrLazy(C.Structure):

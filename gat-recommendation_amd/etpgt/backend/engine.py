@@ -244,11 +244,8 @@ class Engine:
     TAILW_NCAP = 512  # GTR_TAILW_NCAP (csrc/gtr_opt.hip)
 
     def choose_P(self, caps: Caps) -> int:
-        # split-K of the weight gradients: <= 32 node rows per workgroup, <= 64 slabs; small
-        # batches use ONE chunk, the reduction the fused tail (gtr_step_tail_wgrad) computes
-        # in-launch, so every path (fused, data parallel, eager) sums the same way
-        if caps.n_cap <= self.TAILW_NCAP:
-            return 1
+        # split-K of the weight gradients: <= 32 node rows per workgroup, <= 64 slabs (one
+        # chunk over ~110 rows made k_wgrad 2x slower at C2: measured 0.105 -> 0.119 ms/step)
         return max(1, min(64, (caps.n_cap + 31) // 32))
 
     def workspace(self, caps: Caps, fresh: bool = False) -> Workspace:

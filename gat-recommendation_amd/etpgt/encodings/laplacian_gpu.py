@@ -16,11 +16,20 @@ pairs; P carries the search direction.  b = k + 1 + ``extra`` guard vectors spee
 
 Scope: the solver needs a symmetric adjacency (every i -> j with its j -> i) -- then L
 is symmetric and its eigenvectors are well defined.  The reference's training script
-feeds one-directional edges, which makes L non-symmetric; eigsh on such a matrix has
-no well-defined answer to reproduce, so that input is refused here (use the host
-``compute_laplacian_pe``, which keeps the reference's behaviour).  As with eigsh,
-eigenvectors of repeated eigenvalues (e.g. one zero eigenvalue per connected
-component) are only defined up to a rotation inside their eigenspace.
+(train_baseline.py:236-242) feeds the graph CSV's one-directional edges item_i -> item_j
+(item_i < item_j once self loops are dropped) with num_nodes = num_items.  Then
+D^-1/2 A D^-1/2 is strictly upper triangular, so L = I - D^-1/2 A D^-1/2 is UNIT upper
+triangular: every eigenvalue is exactly 1 and L is defective.  ``eigsh`` (symmetric
+Lanczos) on it returns Ritz pairs of a symmetry it assumes, not eigenpairs: on such
+inputs its values lie in (-0.1, 1), its residuals ||L v - lambda v|| are 0.2-0.6, and two
+calls give different vectors (ARPACK's random start; tests/test_host.py pins all three).
+There is no answer to reproduce.  ``directed="reject"`` (default) raises on such input
+(the host ``compute_laplacian_pe`` keeps the reference's behaviour);
+``directed="symmetrize"`` takes the PE of the undirected graph (PyG ``to_undirected``:
+each edge in both directions, duplicates merged), the well-defined spectrum the
+positional encoding is meant to carry.  As with eigsh, eigenvectors of repeated
+eigenvalues (e.g. one zero eigenvalue per connected component) are only defined up to a
+rotation inside their eigenspace.
 """
 
 from __future__ import annotations
@@ -33,17 +42,32 @@ import torch
 from etpgt.backend import _lib as L
 
 
-def _csr(edge_index, n: int):
+def to_undirected(edge_index, n: int) -> np.ndarray:
+    """PyG ``to_undirected`` without edge attributes: every edge in both directions,
+    duplicates merged, sorted by (row, col); [2, E'] int64."""
+    ei = edge_index.detach().cpu().numpy() if isinstance(edge_index, torch.Tensor) else np.asarray(edge_index)
+    row, col = ei[0].astype(np.int64), ei[1].astype(np.int64)
+    key = np.unique(np.concatenate([row * n + col, col * n + row]))
+    return np.stack([key // n, key % n])
+
+
+def _csr(edge_index, n: int, directed: str = "reject"):
+    if directed not in ("reject", "symmetrize"):
+        raise ValueError("directed must be 'reject' or 'symmetrize'")
     ei = edge_index.detach().cpu().numpy() if isinstance(edge_index, torch.Tensor) else np.asarray(edge_index)
     row, col = ei[0].astype(np.int64), ei[1].astype(np.int64)
     if row.size and (min(row.min(), col.min()) < 0 or max(row.max(), col.max()) >= n):
         raise IndexError("edge_index outside [0, num_nodes)")
+    if directed == "symmetrize":
+        row, col = to_undirected(np.stack([row, col]), n)
     keep = row != col
     r, c = row[keep], col[keep]
     if not np.array_equal(np.sort(r * n + c), np.sort(c * n + r)):
         raise NotImplementedError(
             "the GPU LapPE solver needs a symmetric adjacency (each i->j with its j->i); the reference's "
-            "one-directional edge list gives a non-symmetric Laplacian -- use compute_laplacian_pe (host eigsh)")
+            "one-directional edge list gives a unit upper-triangular (non-symmetric) Laplacian whose eigsh output "
+            "is not an eigen-decomposition -- pass directed='symmetrize' for the undirected graph's PE, or use "
+            "compute_laplacian_pe (host eigsh) for the reference's behaviour")
     order = np.argsort(row, kind="stable")
     ptr = np.zeros(n + 1, np.int64)
     np.cumsum(np.bincount(row, minlength=n), out=ptr[1:])
@@ -56,14 +80,14 @@ class LaplacianOperator:
     """X -> L X for [n, b] blocks by the HIP SpMM (gtr_lap_spmm) over an nnz-balanced
     work list (gtr_lap_plan: rows longer than ``chunk`` nonzeros are split)."""
 
-    def __init__(self, edge_index, num_nodes: int, device="cuda", chunk: int = 128):
+    def __init__(self, edge_index, num_nodes: int, device="cuda", chunk: int = 128, directed: str = "reject"):
         self.n = int(num_nodes)
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise ValueError("LaplacianOperator runs on the GPU (HIP kernels); got device %s" % self.device)
         if self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
-        ptr, col = _csr(edge_index, self.n)
+        ptr, col = _csr(edge_index, self.n, directed)
         self.nnz = int(col.size)
         lib = L.lib()
         ni, ns, npart = C.c_int64(), C.c_int64(), C.c_int64()
@@ -184,10 +208,12 @@ def lobpcg_smallest(op: LaplacianOperator, nev: int, extra: int = 4, tol: float 
 
 
 def compute_laplacian_pe_gpu(edge_index, num_nodes: int, k: int = 16, device="cuda", tol: float = 1e-5,
-                             maxiter: int = 2000, extra: int = 4, seed: int = 0) -> torch.Tensor:
+                             maxiter: int = 2000, extra: int = 4, seed: int = 0,
+                             directed: str = "reject") -> torch.Tensor:
     """``compute_laplacian_pe`` (laplacian_pe.py:19-66) for a symmetric graph on the GPU:
     the k+1 smallest eigenvectors of the sym-normalised Laplacian, the first dropped,
-    abs, fp32 [num_nodes, k] on ``device``."""
-    op = LaplacianOperator(edge_index, num_nodes, device)
+    abs, fp32 [num_nodes, k] on ``device``.  ``directed="symmetrize"``: one-directional
+    input (the reference training script's) is made undirected first (module doc)."""
+    op = LaplacianOperator(edge_index, num_nodes, device, directed=directed)
     _, vecs, _ = lobpcg_smallest(op, k + 1, extra=extra, tol=tol, maxiter=maxiter, seed=seed)
     return vecs[:, 1:k + 1].abs().contiguous()

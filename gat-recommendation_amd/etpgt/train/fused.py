@@ -200,6 +200,13 @@ class FusedTrainStep:
         wts = [1.0] * eng.L + [0.75] + [1.0] * eng.L
         if os.environ.get("GTR_SWEEP_WTS"):  # experiments: comma-separated slot weights
             wts = [float(x) for x in os.environ["GTR_SWEEP_WTS"].split(",")]
+        # single-GPU small batches: gtr_step_begin's work runs as extra workgroups of
+        # conv_fwd(0) (gtr_begin) -- one launch less; that launch stamps the touched rows,
+        # so it carries no sweep slice
+        self.begin_fused = (not self.data_parallel and not self.lazy and m_cap <= 8192 and eng.T < (1 << 19)
+                            and os.environ.get("GTR_BEGIN_FUSED", "0") == "1")
+        if self.begin_fused:
+            wts[0] = 0.0
         # data parallel: the union of the ranks' touched rows is known once the sorted keys
         # are all-gathered (early, overlapped with the forward), so only the launches after
         # the union stamp (readout, conv_bwd) can sweep
@@ -235,6 +242,15 @@ class FusedTrainStep:
         nc = int(L.lib().gtr_tail_carry_floats(m_cap, eng.D))
         self.carry = torch.zeros(max(nc, 4), dtype=torch.float32, device=self.dev) if nc > 0 else None
         t.carry = self.carry.data_ptr() if self.carry is not None else None
+        self.cfg.begin, self.cfg.ctr_add, t.rng_inc = None, 0, None
+        if self.begin_fused:
+            bg = L.GtrBegin()
+            bg.skeys, bg.svals, bg.stamp = self.skeys.data_ptr(), self.svals.data_ptr(), self.stamp.data_ptr()
+            bg.step_dev, bg.num_items = self.step_dev.data_ptr(), eng.T
+            self.begin_st = bg
+            self.cfg.begin = C.addressof(bg)
+            self.cfg.ctr_add = 1  # the tail advances the dropout counter at the end of the step
+            t.rng_inc = eng.rng_ctr.data_ptr()
         self.tail = t
         if self.shard_table:
             from etpgt.train.sharded import ShardExchange
@@ -357,6 +373,8 @@ class FusedTrainStep:
         lib = L.lib()
         if self.builder is not None:
             self.builder.launch(bs, self.caps, st, self._builder_B)
+        if self.begin_fused:  # runs inside conv_fwd(0)
+            return
         if self.lazy:
             L.check(lib.gtr_step_begin_lazy(C.byref(bs), eng.T, eng.D, self.keys.data_ptr(), self.vals.data_ptr(),
                                             self.skeys.data_ptr(), self.svals.data_ptr(), self.stamp.data_ptr(),

@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GTR_ABI_VERSION 2 /* 2: gtr_layer.cnt holds 4 + 2*ceil(groups/32) counters */
+#define GTR_ABI_VERSION 3 /* 3: gtr_config.begin / ctr_add, gtr_tail.rng_inc (begin fused into conv_fwd(0)) */
 
 #define GTR_OK 0
 #define GTR_E_ARG 1001      /* bad argument / unsupported shape */
@@ -89,6 +89,20 @@ typedef struct gtr_batch {
 
 typedef struct gtr_sweep gtr_sweep;
 
+/* gtr_step_begin's work (stamps of the touched rows, *step_dev += 1, the rank-sorted
+ * contribution list) run by extra workgroups of gtr_conv_fwd(layer 0) instead of a launch
+ * of its own (gtr_config.begin; m_cap <= 8192, num_items < 2^19).  The dropout counter is
+ * then NOT advanced there: every kernel of the step reads *rng_ctr + gtr_config.ctr_add
+ * (1) and the step tail advances it at its end (gtr_tail.rng_inc).                      */
+typedef struct gtr_begin {
+  int32_t* skeys;
+  int32_t* svals;
+  int32_t* stamp;      /* or NULL */
+  int64_t* step_dev;
+  int32_t num_items;
+  int32_t pad;
+} gtr_begin;
+
 typedef struct gtr_config {
   int32_t num_items;  /* T: table rows                          */
   int32_t dim;        /* D = embedding_dim = hidden_dim          */
@@ -112,6 +126,9 @@ typedef struct gtr_config {
                               and producers zero the partial rows of their empty groups */
   const gtr_sweep* sweep;  /* optional (fused single-GPU step): untouched-row AdamW
                               slices run by extra workgroups of the layer kernels */
+  const gtr_begin* begin;  /* optional: gtr_conv_fwd(layer 0) also runs the step begin */
+  int32_t ctr_add;         /* added to *rng_ctr by every kernel (1 with a fused begin)    */
+  int32_t pad_cfg;
 } gtr_config;
 
 
@@ -361,6 +378,7 @@ typedef struct gtr_tail {
   int64_t sweep_from;     /* untouched rows below this were updated during the chain (gtr_sweep) */
   const float* lazy_consts; /* lazy mode (gtr_lazy.consts): no untouched-row sweep; touched rows
                                are stamped with the step; the dp tail catches rows up first */
+  uint32_t* rng_inc;        /* optional: += 1 at the end of the tail (fused begin, gtr_begin) */
 } gtr_tail;
 
 /* Floats of gtr_tail.carry needed at contribution capacity m_cap (0: not used).      */

@@ -1,0 +1,13 @@
+#!/bin/bash
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+LEAN="--cpu-seconds 0 --gather-batch 0 --recall-steps 0 --e2e-steps 0 --steps 400 --warmup 30"
+GTR_XCD_PACK=0 GTR_LIB=gat-recommendation_amd/build/timing/libgtr_hip.so timeout -k 10 300 python3 scripts/dbg_phases.py c2 > gpurun_out/ph.txt 2> gpurun_out/ph.err || { tail -5 gpurun_out/ph.err; exit 1; }
+cat gpurun_out/ph.txt
+for round in 1 2; do
+for E in "GTR_BEGIN_FUSED=0" "GTR_BEGIN_FUSED=1" "GTR_BEGIN_FUSED=1 GTR_SWEEP_BLOCKS=96"; do
+  env $E timeout -k 10 300 python3 bench.py --config c2 $LEAN > gpurun_out/v.json 2>> gpurun_out/v.err || exit 1
+  python3 -c "import json;d=json.load(open('gpurun_out/v.json'));print('c2 $E', d['value'], d['ms_per_step'], d['roofline']['tail_kernel'])"
+done
+done

@@ -1,0 +1,20 @@
+#!/bin/bash
+# Full GPU suite, fine phase stamps (no packing: the stamps index hardware blocks), and
+# A/B of the XCD-packed roles and the fused begin on C2 / C3.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+mkdir -p gpurun_out
+XFLAG= bash scripts/gpu/tests.sh "" ab5 || exit 1
+GTR_XCD_PACK=0 GTR_LIB=gat-recommendation_amd/build/timing/libgtr_hip.so timeout -k 10 300 python3 scripts/dbg_phases.py c2 > gpurun_out/ph.txt 2> gpurun_out/ph.err || { tail -5 gpurun_out/ph.err; exit 1; }
+cat gpurun_out/ph.txt
+LEAN="--cpu-seconds 0 --gather-batch 0 --recall-steps 0 --e2e-steps 0 --steps 400 --warmup 30"
+for round in 1 2; do
+for E in "GTR_XCD_PACK=0" "GTR_XCD_PACK=1" "GTR_XCD_PACK=1 GTR_BEGIN_FUSED=1"; do
+  env $E timeout -k 10 300 python3 bench.py --config c2 $LEAN > gpurun_out/v.json 2>> gpurun_out/v.err || exit 1
+  python3 -c "import json;d=json.load(open('gpurun_out/v.json'));print('c2 $E', d['value'], d['ms_per_step'])"
+done
+done
+for E in "GTR_XCD_PACK=0" "GTR_XCD_PACK=1 GTR_BEGIN_FUSED=1"; do
+  env $E timeout -k 10 300 python3 bench.py --config c3 $LEAN > gpurun_out/v.json 2>> gpurun_out/v.err || exit 1
+  python3 -c "import json;d=json.load(open('gpurun_out/v.json'));print('c3 $E', d['value'], d['ms_per_step'])"
+done

@@ -125,6 +125,40 @@ def test_lappe_gpu_rejects_one_directional_edges():
         compute_laplacian_pe_gpu(ei, num_nodes=4, k=2)
 
 
+def _one_directional(n, m, seed):
+    """The reference training script's LapPE input (train_baseline.py:236-242): the graph
+    CSV's canonical edges item_i -> item_j with item_i <= item_j, self loops included."""
+    rng = np.random.default_rng(seed)
+    i, j = rng.integers(0, n, m), rng.integers(0, n, m)
+    return torch.from_numpy(np.stack([np.minimum(i, j), np.maximum(i, j)]).astype(np.int64))
+
+
+@pytest.mark.parametrize("n,m,k", [(4, 6, 2), (1500, 9000, 16)])
+def test_lappe_gpu_symmetrizes_the_reference_input(n, m, k):
+    """directed='symmetrize': the reference's one-directional input gives the PE of its
+    undirected graph (PyG to_undirected), checked against the oracle restatement on the
+    symmetrized edges (eigenvalues vs dense eigh, well-separated columns, the span)."""
+    from etpgt.encodings.laplacian_gpu import to_undirected
+
+    ei = _one_directional(n, m, seed=n) if n > 4 else torch.tensor([[0, 0, 1, 1, 2, 2], [1, 2, 2, 3, 3, 2]])
+    und = torch.from_numpy(to_undirected(ei, n))
+    Lm = R.ref_sym_laplacian(und.numpy(), n)
+    lam_all, vec_all = np.linalg.eigh(Lm.toarray().astype(np.float64))
+    pe = compute_laplacian_pe_gpu(ei, n, k=k, tol=1e-5, directed="symmetrize").cpu().numpy()
+    assert pe.shape == (n, k) and (pe >= 0).all()
+    want = R.ref_compute_laplacian_pe(und, n, k=k).numpy()
+    lam_ctx = np.concatenate([lam_all[: k + 2], [np.inf]])
+    checked = _check_columns(pe, want, lam_ctx)
+    assert checked >= 1
+    op = LaplacianOperator(ei, n, "cuda", directed="symmetrize")
+    lam, X, _ = lobpcg_smallest(op, k + 1, tol=1e-5)
+    np.testing.assert_allclose(lam, lam_all[: k + 1], atol=1e-5)
+    if lam_all[k + 1] - lam_all[k] > 1e-3:
+        Xn = X.cpu().numpy().astype(np.float64)
+        Vr = vec_all[:, : k + 1]
+        assert np.abs(Xn @ Xn.T - Vr @ Vr.T).max() < 1e-3
+
+
 def test_lappe_gpu_rejects_out_of_range():
     ei = torch.tensor([[0, 5], [5, 0]])
     with pytest.raises(IndexError):

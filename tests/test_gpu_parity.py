@@ -174,7 +174,14 @@ def test_fused_steps_large_batch():
     _fused_vs_reference(64, 2, 0, "bpr", "adamw", True, B=1400, steps=2)
 
 
-def _fused_vs_reference(D, H, K, loss, opt, use_graph, B, steps):
+def test_fused_steps_large_batch_c3_shape():
+    """The C3 / C5 layer shape (D = 128, 4 heads, LapPE k = 16, listwise) at a batch whose
+    node capacity passes 8192 rows: row groups of R = 16 rows (hundreds of groups), the
+    bucketed last-arriver merges of the forward (count, mean, M2) and backward sums."""
+    _fused_vs_reference(128, 4, 16, "listwise", "adamw", True, B=2400, steps=2, expect_ncap=8192)
+
+
+def _fused_vs_reference(D, H, K, loss, opt, use_graph, B, steps, expect_ncap=0):
     T = data().table_rows
     n = 5 if loss != "listwise" else 100
     m, ref = make_pair(T, D, H, K=K, seed=4)
@@ -192,6 +199,8 @@ def _fused_vs_reference(D, H, K, loss, opt, use_graph, B, steps):
         losses.append(float(fused(sb.to("cuda"))))
         rlosses.append(float(R.ref_train_step(ref, ref_batch(sb), ropt, loss)))
     np.testing.assert_allclose(losses, rlosses, rtol=2e-3)
+    if expect_ncap:
+        assert fused.caps.n_cap > expect_ncap and fused.ws.R == 16, (fused.caps, fused.ws.R)
     hp = dict(m.named_parameters())
     for name, p in ref.named_parameters():
         if name.endswith("lin_key.bias"):

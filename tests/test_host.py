@@ -369,3 +369,28 @@ def test_train_baseline_counterpart_cli_plumbing(tmp_path):
         tb.main(base[:1] + ["gat"] + base[2:] + ["--device", "cpu"])
     with pytest.raises(RuntimeError, match="HIP path only"):
         tb.main(base + ["--device", "cpu"])
+
+
+def test_reference_directed_lappe_input_has_no_eigen_answer():
+    """The reference training script's LapPE input (train_baseline.py:236-242: the graph
+    CSV's item_i -> item_j with item_i <= item_j, num_nodes = num_items) gives a unit
+    upper-triangular Laplacian: its spectrum is exactly {1}, and eigsh(k+1, 'SM') -- the
+    reference's compute_laplacian_pe -- returns Ritz pairs that are not eigenpairs.  This
+    pins why the GPU solver refuses that input or symmetrizes it
+    (etpgt/encodings/laplacian_gpu.py)."""
+    import numpy as np
+    import scipy.sparse as sp
+    from scipy.sparse.linalg import eigsh
+
+    import oracle.etpgt_ref as R
+
+    rng = np.random.default_rng(7)
+    n, m = 1500, 9000
+    i, j = rng.integers(0, n, m), rng.integers(0, n, m)
+    ei = np.stack([np.minimum(i, j), np.maximum(i, j)])
+    L = R.ref_sym_laplacian(ei, n)
+    assert sp.tril(L, -1).count_nonzero() == 0 and np.allclose(L.diagonal(), 1.0)  # unit upper triangular
+    w, v = eigsh(L.astype(np.float64), k=17, which="SM")
+    res = np.linalg.norm(L @ v - v * w, axis=0)
+    assert np.abs(w - 1.0).max() > 0.1  # the "eigenvalues" are not the spectrum {1}
+    assert res.min() > 0.05             # and the vectors are not eigenvectors
