@@ -204,7 +204,7 @@ class FusedTrainStep:
         # conv_fwd(0) (gtr_begin) -- one launch less; that launch stamps the touched rows,
         # so it carries no sweep slice
         self.begin_fused = (not self.data_parallel and not self.lazy and m_cap <= 8192 and eng.T < (1 << 19)
-                            and os.environ.get("GTR_BEGIN_FUSED", "0") == "1")
+                            and os.environ.get("GTR_BEGIN_FUSED", "1") != "0")
         if self.begin_fused:
             wts[0] = 0.0
         # data parallel: the union of the ranks' touched rows is known once the sorted keys

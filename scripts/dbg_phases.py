@@ -20,13 +20,19 @@ import bench  # noqa: E402
 from etpgt.backend import _lib as L  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"
+# XCD-packed roles (GTR_XCD_PACK, default on): row group g runs on hardware block 8g
+stride = 8 if os.environ.get("GTR_XCD_PACK", "1") != "0" else 1
 dev = torch.device("cuda", 0)
 w = bench.build_workload(cfg, 32, 16, dev)
 step, staged = w["step"], w["staged"]
 h = L.lib()
-h.gtr_dbg_fwd_phases.restype = C.c_int
-h.gtr_dbg_fwd_phases.argtypes = [C.c_void_p, C.c_size_t]
+for fn in ("gtr_dbg_fwd_phases", "gtr_dbg_bwd_phases"):
+    getattr(h, fn).restype = C.c_int
+    getattr(h, fn).argtypes = [C.c_void_p, C.c_size_t]
 ph = np.zeros((32, 1024, 16), np.uint64)
+pb = np.zeros((32, 1024, 16), np.uint64)
+bnames = ["stage", "dst", "src", "dX"]
+bacc = {0: [], 1: []}
 order = [0, 10, 1, 11, 2, 5, 8, 3, 4]
 names = ["ranges", "staged", "rows", "proj", "logits", "softmax", "agg+gate", "bnpart"]
 acc = {0: [], 1: []}
@@ -37,11 +43,18 @@ for i in range(40):
     if i < 5:
         continue
     assert h.gtr_dbg_fwd_phases(ph.ctypes.data, ph.nbytes) == 0
+    assert h.gtr_dbg_bwd_phases(pb.ctypes.data, pb.nbytes) == 0
     G = int(staged[i % len(staged)][4].item())
     for l in (0, 1):
-        a = ph[l, :G][:, order].astype(np.int64)
+        a = ph[l, : G * stride : stride][:, order].astype(np.int64)
         ok = (a > 0).all(axis=1)
         acc[l].append(np.median(np.diff(a[ok], axis=1), axis=0) * 10e-3)
+        b = pb[l, : G * stride : stride][:, :5].astype(np.int64)
+        okb = (b > 0).all(axis=1)
+        bacc[l].append(np.median(np.diff(b[okb], axis=1), axis=0) * 10e-3)
 for l in (0, 1):
     m = np.median(np.stack(acc[l]), axis=0)
     print(f"conv_fwd L{l}: " + " ".join(f"{n}={v:.2f}" for n, v in zip(names, m)) + f"  total={m.sum():.2f} us")
+for l in (1, 0):
+    m = np.median(np.stack(bacc[l]), axis=0)
+    print(f"conv_bwd L{l}: " + " ".join(f"{n}={v:.2f}" for n, v in zip(bnames, m)) + f"  total={m.sum():.2f} us")
