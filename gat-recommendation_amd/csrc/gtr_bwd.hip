@@ -703,7 +703,7 @@ extern "C" int gtr_conv_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     if (cfg->sweep && slot < GTR_SWEEP_SLOTS && cfg->sweep->bounds[slot + 1] > cfg->sweep->bounds[slot]) {
       k.sw = *cfg->sweep;
       k.sw_slot = slot;
-      grid += cfg->sweep->blocks;
+      grid += sweep_blocks(cfg->sweep, grid);
     }
   }
   k.xpack = xcd_pack(k.main_grid, grid);

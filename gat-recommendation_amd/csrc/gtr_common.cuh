@@ -305,6 +305,20 @@ __device__ __forceinline__ void sweep_slice(const gtr_sweep& sw, int slot, int b
 // each product; after a few AdamW steps that moved a few parameters per million past the
 // north star's elementwise 1e-3 bar against the fp32 oracle on the full C3 / C5 tables
 // (tests/test_gpu_fullsize.py), so it is not the default at any width.
+// Sweep workgroups appended to a launch with `grid_main` other workgroups: gtr_sweep.blocks,
+// or (blocks <= 0) enough to fill the chip's CUs exactly -- every workgroup on a CU of its
+// own, and the main workgroups packable onto one XCD (xcd_pack) -- at least 64.
+inline int sweep_blocks(const gtr_sweep* sw, int grid_main) {
+  if (sw->blocks > 0) return sw->blocks;
+  static int cus = 0;
+  if (cus <= 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  return cus - grid_main > 64 ? cus - grid_main : 64;
+}
+
 inline int xcd_pack(int main_blocks, int grid) {
   const char* e = getenv("GTR_XCD_PACK");
   if (e && e[0] == '0') return 0;

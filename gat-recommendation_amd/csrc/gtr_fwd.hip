@@ -1457,7 +1457,7 @@ extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   if (cfg->sweep && l < GTR_SWEEP_SLOTS && cfg->sweep->bounds[l + 1] > cfg->sweep->bounds[l]) {
     k.sw = *cfg->sweep;
     k.sw_slot = l;
-    grid += cfg->sweep->blocks;
+    grid += sweep_blocks(cfg->sweep, grid);
   }
   k.xpack = xcd_pack(k.main_grid, grid);
   hipStream_t s = (hipStream_t)stream;
@@ -1529,7 +1529,7 @@ extern "C" int gtr_readout_loss(const gtr_config* cfg, const gtr_batch* bt, cons
       cfg->sweep->bounds[cfg->num_layers + 1] > cfg->sweep->bounds[cfg->num_layers]) {
     k.sw = *cfg->sweep;
     k.sw_slot = cfg->num_layers;
-    grid += cfg->sweep->blocks;
+    grid += sweep_blocks(cfg->sweep, grid);
   }
   k.xpack = xcd_pack(k.main_grid, grid);
   hipStream_t s = (hipStream_t)stream;

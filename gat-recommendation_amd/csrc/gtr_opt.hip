@@ -913,21 +913,196 @@ int key_bits(int T) {
 
 bool dim_ok(int D) { return D == 32 || D == 64 || D == 128 || D == 256; }
 
-// Stable (key, slot) radix sort of the contribution list.  rocPRIM's default config runs
-// a block sort + merge passes below 1M items (~20 launches at m_cap ~ 855k); the Onesweep
-// config (merge-sort limit 0) runs one histogram launch and one launch per radix digit of
-// the key bits.  Both are stable, so they sort identically.  GTR_SORT=onesweep selects
-// it.  The
-// workspace query and the sort MUST use the same config (gtr_contrib_sort checks it).
+// ---- contribution sort (large batches): own LSD radix, 10-bit digits -------------------
+// keys < 2^20 (T <= 1M + 1) sort in two passes of three launches each: per-tile digit
+// histograms (tile = 4096 items) and digit totals, the scatter offsets of every (tile,
+// digit) from them (16 workgroups), then a stable scatter.  Inside a tile items are ranked in 16 rounds of 256 (the
+// original order): a round's items of equal digit are matched by 10 ballots within the
+// wave, waves of the round are offset by per-(wave, digit) counts in LDS, rounds by a
+// running count per digit -- no atomics on the ranks, so the sort is stable and
+// deterministic, equal to any stable sort of the (key, slot) pairs.
+#define RS_BITS 10
+#define RS_RADIX (1 << RS_BITS)
+#define RS_THREADS 256
+#define RS_ROUNDS 16
+#define RS_TILE (RS_THREADS * RS_ROUNDS)
+
+__global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const int32_t* keys, int n, int shift, int32_t* hist,
+                                                       int32_t* tot) {
+  __shared__ int h[RS_RADIX];
+  for (int d = threadIdx.x; d < RS_RADIX; d += RS_THREADS) h[d] = 0;
+  __syncthreads();
+  const int base = blockIdx.x * RS_TILE;
+  for (int r = 0; r < RS_ROUNDS; ++r) {
+    const int i = base + r * RS_THREADS + threadIdx.x;
+    if (i < n) atomicAdd(&h[((uint32_t)keys[i] >> shift) & (RS_RADIX - 1)], 1);  // integer counts
+  }
+  __syncthreads();
+  for (int d = threadIdx.x; d < RS_RADIX; d += RS_THREADS) {
+    hist[(size_t)blockIdx.x * RS_RADIX + d] = h[d];  // tile-major, coalesced
+    if (h[d]) atomicAdd(tot + d, h[d]);             // digit totals (integer: order-free)
+  }
+}
+
+// Scatter offsets offs[tile][d] = (items of digits < d) + (items of digit d in earlier
+// tiles): workgroup w owns digits [64 w, 64 w + 64), its 16 waves a slice of the tiles
+// each (loads in flight together); slices and digits are combined in fixed order.
+#define RS_OFFS_SL 16
+__global__ __launch_bounds__(1024) void k_rs_offs(const int32_t* __restrict__ hist, int32_t* __restrict__ tot,
+                                                 int32_t* __restrict__ offs, int ntile) {
+  __shared__ int s_sl[RS_OFFS_SL][64];
+  __shared__ int s_tot[RS_RADIX];
+  __shared__ int s_base;
+  const int tid = threadIdx.x, dl = tid & 63, sl = tid >> 6;
+  const int d = blockIdx.x * 64 + dl;
+  s_tot[tid] = tot[tid];  // 1024 threads == RS_RADIX digits
+  __syncthreads();
+  if (tid == 0) {
+    int b = 0;
+    for (int q = 0; q < blockIdx.x * 64; ++q) b += s_tot[q];
+    s_base = b;
+  }
+  const int per = (ntile + RS_OFFS_SL - 1) / RS_OFFS_SL;
+  const int b0 = min(ntile, sl * per), b1 = min(ntile, b0 + per);
+  int sum = 0;
+  for (int c = b0; c < b1; c += 16) {
+    int v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = c + q < b1 ? hist[(size_t)(c + q) * RS_RADIX + d] : 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) sum += v[q];
+  }
+  s_sl[sl][dl] = sum;
+  __syncthreads();
+  int run = s_base;
+  for (int q = 0; q < dl; ++q) run += s_tot[blockIdx.x * 64 + q];
+  for (int q = 0; q < sl; ++q) run += s_sl[q][dl];
+  for (int c = b0; c < b1; c += 16) {
+    int v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) v[q] = c + q < b1 ? hist[(size_t)(c + q) * RS_RADIX + d] : 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      if (c + q < b1) offs[(size_t)(c + q) * RS_RADIX + d] = run;
+      run += v[q];
+    }
+  }
+}
+
+// tot: the pass's digit totals, read by k_rs_offs; zeroed here for the next call's same
+// pass (the workspace starts zeroed), so no memset node sits in the captured step.
+__global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const int32_t* kin, const int32_t* vin, int32_t* kout,
+                                                          int32_t* vout, int n, int shift, const int32_t* offs,
+                                                          int ntile, int32_t* tot) {
+  __shared__ int run[RS_RADIX];
+  __shared__ int wcnt[RS_THREADS / 64][RS_RADIX];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (blockIdx.x == 0)
+    for (int d = tid; d < RS_RADIX; d += RS_THREADS) tot[d] = 0;
+  for (int d = tid; d < RS_RADIX; d += RS_THREADS) {
+    run[d] = offs[(size_t)blockIdx.x * RS_RADIX + d];
+#pragma unroll
+    for (int w = 0; w < RS_THREADS / 64; ++w) wcnt[w][d] = 0;
+  }
+  __syncthreads();
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  const int base = blockIdx.x * RS_TILE;
+  for (int r = 0; r < RS_ROUNDS; ++r) {
+    const int i = base + r * RS_THREADS + tid;
+    const bool live = i < n;
+    const int key = live ? kin[i] : 0;
+    const int val = live ? vin[i] : 0;
+    const int d = ((uint32_t)key >> shift) & (RS_RADIX - 1);
+    unsigned long long match = __ballot(live);
+#pragma unroll
+    for (int b = 0; b < RS_BITS; ++b) {
+      const unsigned long long bb = __ballot((d >> b) & 1);
+      match &= ((d >> b) & 1) ? bb : ~bb;
+    }
+    const int before = __popcll(match & lt);
+    if (live && before == 0) wcnt[wave][d] = __popcll(match);  // the digit's first lane in the wave
+    __syncthreads();
+    if (live) {
+      int pos = run[d] + before;
+      for (int w = 0; w < wave; ++w) pos += wcnt[w][d];
+      kout[pos] = key;
+      vout[pos] = val;
+    }
+    __syncthreads();
+    for (int q = tid; q < RS_RADIX; q += RS_THREADS) {
+      int t = 0;
+#pragma unroll
+      for (int w = 0; w < RS_THREADS / 64; ++w) { t += wcnt[w][q]; wcnt[w][q] = 0; }
+      run[q] += t;
+    }
+    __syncthreads();
+  }
+}
+
+int sort_mode() {  // 0: own radix (default), 1: hipCUB, 2: rocPRIM Onesweep
+  const char* e = getenv("GTR_SORT");
+  if (e && (e[0] == 'm' || e[0] == 'M' || e[0] == 'h' || e[0] == 'H')) return 1;
+  if (e && (e[0] == 'o' || e[0] == 'O')) return 2;
+  return 0;
+}
+
+size_t rs_bytes(int n) {
+  const size_t ntile = (size_t)(n + RS_TILE - 1) / RS_TILE;
+  return 4 * (size_t)n * sizeof(int32_t) + 2 * (size_t)RS_RADIX * ntile * sizeof(int32_t) +
+         4 * RS_RADIX * sizeof(int32_t) + 256;
+}
+
+hipError_t rs_sort(void* tmp, const int32_t* keys, int32_t* skeys, const int32_t* vals, int32_t* svals, int n,
+                   int bits, hipStream_t s) {
+  const int ntile = (n + RS_TILE - 1) / RS_TILE;
+  int32_t* k1 = static_cast<int32_t*>(tmp);
+  int32_t* v1 = k1 + n;
+  int32_t* k2 = v1 + n;
+  int32_t* v2 = k2 + n;
+  int32_t* hist = v2 + n;
+  int32_t* offs = hist + (size_t)RS_RADIX * ntile;
+  int32_t* tot = offs + (size_t)RS_RADIX * ntile;  // [passes][RS_RADIX] digit totals (kept zero between calls)
+  const int passes = (bits + RS_BITS - 1) / RS_BITS;  // <= 3 for int32 keys below 2^30
+  if (passes > 4) return hipErrorInvalidValue;
+  const int32_t* ki = keys;
+  const int32_t* vi = vals;
+  for (int p = 0; p < passes; ++p) {
+    const bool last = p == passes - 1;
+    int32_t* ko = last ? skeys : (p % 2 == 0 ? k1 : k2);
+    int32_t* vo = last ? svals : (p % 2 == 0 ? v1 : v2);
+    int32_t* tp = tot + p * RS_RADIX;
+    hipLaunchKernelGGL(k_rs_hist, dim3(ntile), dim3(RS_THREADS), 0, s, ki, n, p * RS_BITS, hist, tp);
+    hipLaunchKernelGGL(k_rs_offs, dim3(RS_RADIX / 64), dim3(1024), 0, s, hist, tp, offs, ntile);
+    hipLaunchKernelGGL(k_rs_scatter, dim3(ntile), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, n, p * RS_BITS, offs,
+                       ntile, tp);
+    ki = ko;
+    vi = vo;
+  }
+  return hipGetLastError();
+}
+
+// Stable (key, slot) sort of the contribution list, GTR_SORT selecting the algorithm:
+//   default  the own radix above (6 launches for keys < 2^20);
+//   merge    hipCUB / rocPRIM's default config: block sort + merge passes below 1M items
+//            (~20 launches at m_cap ~ 855k);
+//   onesweep rocPRIM Onesweep (merge-sort limit 0): one histogram launch + one per digit.
+//            Correct standalone and in a captured graph (scripts/dbg/onesweep.hip), but it
+//            faulted (illegal address in radix_sort_onesweep_iteration) inside the C3
+//            B = 8192 fused step with a workspace sized by this same config; not used.
+// All three are stable, so they sort identically.  The workspace query and the sort MUST
+// use the same algorithm (gtr_contrib_sort checks the size).
 using OnesweepConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                                   rocprim::default_config, 0>;
-bool sort_onesweep() {
-  const char* e = getenv("GTR_SORT");
-  return e && (e[0] == 'o' || e[0] == 'O');
-}
 hipError_t sort_pairs(void* tmp, size_t& bytes, const int32_t* keys, int32_t* skeys, const int32_t* vals,
                       int32_t* svals, int n, int bits, hipStream_t s) {
-  if (sort_onesweep())
+  if (sort_mode() == 0) {
+    if (!tmp) {
+      bytes = rs_bytes(n);
+      return hipSuccess;
+    }
+    return rs_sort(tmp, keys, skeys, vals, svals, n, bits, s);
+  }
+  if (sort_mode() == 2)
     return rocprim::radix_sort_pairs<OnesweepConfig>(tmp, bytes, keys, skeys, vals, svals, (size_t)n, 0, bits, s);
   return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, keys, skeys, vals, svals, n, 0, bits, s);
 }

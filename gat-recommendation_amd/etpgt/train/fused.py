@@ -229,10 +229,11 @@ class FusedTrainStep:
                 if i < slots:
                     acc += wts[i]
             sw.dim = eng.D
-            # 128 extra workgroups per launch: with streaming sweep accesses and split-bf16
-            # GEMMs the slices, not the row groups, bounded each launch at 64 (C2 285k ->
-            # 323k, C3 174k -> 214k sessions/s; 96-160 within 1 %)
-            sw.blocks = int(os.environ.get("GTR_SWEEP_BLOCKS", 128))
+            # extra workgroups per launch: 0 = fill the CUs the launch's row groups leave
+            # (C2: 224-232 per launch, 352k sessions/s against 342k at a fixed 128; every
+            # workgroup on a CU of its own, the row groups packable onto one XCD); at D = 128
+            # a fixed 128 measured 2 % faster (C3 193k against 189k)
+            sw.blocks = int(os.environ.get("GTR_SWEEP_BLOCKS", 0 if eng.D <= 64 else 128))
             sw.lag = 1 if self.lagged else 0
             sw.consts = self.lazy_consts.data_ptr() if self.lagged else None
             self.sweep = sw

@@ -269,7 +269,7 @@ typedef struct gtr_sweep {
   gtr_adam opt;       /* by value: the kernels copy it (opt.step_dev is a device pointer) */
   int64_t bounds[GTR_SWEEP_SLOTS + 1];
   int32_t dim;
-  int32_t blocks;
+  int32_t blocks;     /* workgroups per launch; <= 0: the CUs the launch's own workgroups leave */
   /* lag = 1 (lazy-table stamps, "current through step s"): the launches of step t bring
    * every row with stamp < t-1 forward to t-1 (the previous step's zero-gradient update,
    * older steps from consts as gtr_lazy) and stamp it; the rows the step reads were
@@ -292,6 +292,8 @@ int gtr_adamw_small(float* param, float* m, float* v, float* grad_out, int64_t t
  * stamp[row] = step+1.  m_cap = n_cap + b_cap*(1+n).                          */
 int gtr_contrib_prep(const gtr_batch* bt, int num_items, int32_t* keys, int32_t* vals,
                      int32_t* stamp, const int64_t* step_dev, gtr_stream_t stream);
+/* tmp (gtr_contrib_sort_bytes) must be zero-initialised once and otherwise left to the
+ * sort: the default radix keeps per-pass digit totals there, zero between calls.       */
 int gtr_contrib_sort_bytes(int m_cap, int num_items, size_t* bytes);
 int gtr_contrib_sort(const int32_t* keys, const int32_t* vals, int32_t* skeys, int32_t* svals,
                      int m_cap, int num_items, void* tmp, size_t tmp_bytes, gtr_stream_t stream);
