@@ -27,6 +27,8 @@ if [ "${PMC:-1}" = "1" ]; then
   rm -rf gpurun_out/pmc_${TAG}_FETCH_SIZE gpurun_out/pmc_${TAG}_WRITE_SIZE
   python3 -c "import json;d=json.load(open('gpurun_out/${TAG}_pmc.json'));print('pmc per step', d.get('_per_step'))"
 fi
+# the bench line reads its PMC traffic from profiles/rNN/<name>_pmc.json of these sources
+[ -f gpurun_out/${TAG}_pmc.json ] && mkdir -p profiles/${ROUND:-r02} && cp gpurun_out/${TAG}_pmc.json profiles/${ROUND:-r02}/${TAG}_pmc.json
 timeout -k 10 600 python3 bench.py ${BENCH_ARGS_FULL:-$LEAN} > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err \
   || { tail -30 gpurun_out/${TAG}_bench.err; exit 1; }
 cat gpurun_out/${TAG}_bench.json

@@ -46,8 +46,12 @@ def main():
             "hbm_bytes_per_launch": (2 * fa * 1024 if fa is not None else 0) + (wa * 1024 if wa is not None else 0),
         }
     # per training step: every kernel's bytes x its launches, over the step count (one
-    # k_step_begin per step; copies included)
-    steps = out.get("k_step_begin", out.get("k_counters", {})).get("dispatches", 0)
+    # tail per step -- the bench's tail probe must be off; copies included)
+    steps = 0
+    for k in ("k_step_tail", "k_dp_tail", "k_shard_update", "k_step_begin", "k_counters"):
+        if k in out:
+            steps = out[k]["dispatches"]
+            break
     if steps:
         # HIP kernels of the library (k_*, incl. the rocprim sort's) + the blob copy;
         # torch fill kernels belong to setup, not to the step
