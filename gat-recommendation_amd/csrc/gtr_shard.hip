@@ -81,6 +81,7 @@ __global__ __launch_bounds__(RB_THREADS) void k_route_count(RouteK a) {
 __global__ __launch_bounds__(RB_THREADS) void k_route_scan(RouteK a) {
   __shared__ int s_part[RB_THREADS][SH_MAXP];
   const int tid = threadIdx.x;
+  if (tid == 0) a.status[0] = 0;  // this step's flag (a kernel write: no memset node in the captured step)
   const int per = (a.nblk + RB_THREADS - 1) / RB_THREADS;
   const int b0 = min(a.nblk, tid * per), b1 = min(a.nblk, b0 + per);
   for (int q = 0; q < a.P; ++q) {
@@ -422,7 +423,6 @@ int gtr_shard_route(const gtr_batch* bt, const int32_t* skeys, const int32_t* sv
   }
   k.bcnt = static_cast<int32_t*>(scratch);
   hipStream_t s = (hipStream_t)stream;
-  (void)hipMemsetAsync(sh->status, 0, sizeof(int32_t), s);
   hipLaunchKernelGGL(k_route_count, dim3(k.nblk), dim3(RB_THREADS), 0, s, k);
   GTR_HIP_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(RB_THREADS), 0, s, k);
