@@ -9,6 +9,8 @@
 // k_wgrad: lin_{query,key,value,skip} weight/bias, lin_beta and LapPE projection
 //   gradients as deterministic per-chunk partial slabs (summed by the optimizer).
 
+#include <string.h>
+
 #include "gtr_layer.cuh"
 #include "gtr_wgrad.cuh"
 
@@ -619,6 +621,10 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
 // weight gradients
 // ------------------------------------------------------------------------------------
 
+#ifndef GTR_WGRAD_MFMA_ROWS
+#define GTR_WGRAD_MFMA_ROWS 128  // rows per split-K chunk from which the QKVS job runs on MFMA
+#endif
+
 __global__ __launch_bounds__(GTR_BLOCK) void k_wgrad(WgradK a) {
   const int blk = blockIdx.x;
   int jid = 0;
@@ -631,10 +637,14 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_wgrad(WgradK a) {
   const int t0 = p * per;
   const int t1 = min(N, t0 + per);
   const int64_t so = (int64_t)p * a.stride;
-  wgrad_tile(J, tile, t0, t1, a.D, [&](int which, int64_t idx, float v) {
+  auto emit = [&](int which, int64_t idx, float v) {
     if (which == 0) J.outW[so + idx] = v;
     else J.outB[so + idx] = v;
-  });
+  };
+  auto emit4 = [&](int64_t idx, float4 v) { *reinterpret_cast<float4*>(J.outW + so + idx) = v; };
+  if (J.mfma == 1) wgrad_tile_mfma<false>(J, tile, t0, t1, emit, emit4);
+  else if (J.mfma == 2) wgrad_tile_mfma<true>(J, tile, t0, t1, emit, emit4);
+  else wgrad_tile(J, tile, t0, t1, a.D, emit);
 }
 
 }  // namespace
@@ -739,9 +749,34 @@ extern "C" int gtr_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_l
   k.stride = slab_stride;
   if (l_begin < 0 || l_end > Lc || l_begin > l_end) { set_error("gtr_wgrad: bad layer range"); return GTR_E_ARG; }
   int nj = 0, blocks = 0;
+  // MFMA tiles for the QKVS weight once a chunk holds enough rows to amortize them
+  // (GTR_WGRAD=mfma|valu overrides; the float4 slab stores need 16 B aligned slabs)
+  const char* wm = getenv("GTR_WGRAD");
+  const int rows_per_chunk = (bt->n_cap + n_chunks - 1) / n_chunks;
+  bool mfma = rows_per_chunk >= GTR_WGRAD_MFMA_ROWS;
+  if (wm && !strcmp(wm, "mfma")) mfma = true;
+  if (wm && !strcmp(wm, "valu")) mfma = false;
+  if (slab_stride % 4) mfma = false;
+  for (int l = l_begin; l < l_end; ++l)
+    if (reinterpret_cast<uintptr_t>(layer_slab[l]) % 16) mfma = false;
   const int rc = build_wjobs(cfg, bt, layers, dx0, pe_tab, layer_slab, pe_slab, nullptr, nullptr, n_chunks, l_begin,
-                             l_end, k.jobs, nj, blocks);
+                             l_end, k.jobs, nj, blocks, mfma);
   if (rc) return rc;
+  if (const char* jm = getenv("GTR_WGRAD_JOBS")) {  // diagnostics (timing only): keep job types in the mask
+    const int mask = atoi(jm);
+    int kept = 0;
+    blocks = 0;
+    for (int i = 0; i < nj; ++i) {
+      const bool pe = k.jobs[i].type == WJ_MM && k.jobs[i].M1 == D;
+      const int bit = pe ? 8 : 1 << k.jobs[i].type;
+      if (!(mask & bit)) continue;
+      WJob j = k.jobs[i];
+      j.blk0 = blocks;
+      blocks += j.nt * n_chunks;
+      k.jobs[kept++] = j;
+    }
+    nj = kept;
+  }
   k.njobs = nj;
   if (nj == 0 || blocks == 0) return GTR_OK;
   hipStream_t s = (hipStream_t)stream;

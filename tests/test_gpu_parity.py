@@ -174,11 +174,35 @@ def test_fused_steps_large_batch():
     _fused_vs_reference(64, 2, 0, "bpr", "adamw", True, B=1400, steps=2)
 
 
-def test_fused_steps_large_batch_c3_shape():
+@pytest.mark.parametrize("wgrad", ["default", "valu"])
+def test_fused_steps_large_batch_c3_shape(wgrad, monkeypatch):
     """The C3 / C5 layer shape (D = 128, 4 heads, LapPE k = 16, listwise) at a batch whose
     node capacity passes 8192 rows: row groups of R = 16 rows (hundreds of groups), the
-    bucketed last-arriver merges of the forward (count, mean, M2) and backward sums."""
+    bucketed last-arriver merges of the forward (count, mean, M2) and backward sums.  The
+    weight gradients run on MFMA tiles there by default (>= 128 rows per split-K chunk:
+    QKVS weight with the bias column sums folded in, narrow LapPE projection tiles);
+    GTR_WGRAD=valu forces the register-tile path."""
+    if wgrad != "default":
+        monkeypatch.setenv("GTR_WGRAD", wgrad)
     _fused_vs_reference(128, 4, 16, "listwise", "adamw", True, B=2400, steps=2, expect_ncap=8192)
+
+
+@pytest.mark.parametrize("D,H,K,loss", [(64, 1, 0, "bpr"), (128, 4, 16, "listwise")])
+def test_fused_steps_tail_wgrad(D, H, K, loss, monkeypatch):
+    """GTR_TAILW=1: the weight gradients of a small batch computed inside the step tail
+    (k_step_tail_wgrad, one chunk over all rows, AdamW applied in place) -- the same
+    trajectory as the oracle."""
+    monkeypatch.setenv("GTR_TAILW", "1")
+    fused = _fused_vs_reference(D, H, K, loss, "adamw", True, B=32, steps=3)
+    assert fused.tail_wgrad
+
+
+@pytest.mark.parametrize("mode", ["mfma", "valu"])
+def test_fused_steps_wgrad_tiles_forced(mode, monkeypatch):
+    """Both weight-gradient tile forms at a small batch (B = 32: VALU by default) and the
+    C3 layer shape: GTR_WGRAD=mfma forces the MFMA tiles onto 32-row chunks."""
+    monkeypatch.setenv("GTR_WGRAD", mode)
+    _fused_vs_reference(128, 4, 16, "listwise", "adamw", True, B=32, steps=3)
 
 
 def _fused_vs_reference(D, H, K, loss, opt, use_graph, B, steps, expect_ncap=0):
@@ -215,6 +239,7 @@ def _fused_vs_reference(D, H, K, loss, opt, use_graph, B, steps, expect_ncap=0):
         if "running" in name:
             assert_close_norm(dict(m.named_buffers())[name], b, rtol=1e-3, name=name)
     assert int(dict(m.named_buffers())["batch_norms.0.num_batches_tracked"]) == len(bl)
+    return fused
 
 
 def test_fused_dropout_deterministic_and_finite():
