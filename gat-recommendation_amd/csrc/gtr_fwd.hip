@@ -219,7 +219,7 @@ __device__ __forceinline__ int wfrag_off(int kb, int lg, int split) {
 }
 
 template <int D, bool SPLIT>
-__global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
+__device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
   using G = LayerGeom<D>;
   static_assert(G::F_WORDS >= GTR_BEGIN_MCAP + CONV_WAVES * 64, "LDS carve too small for the fused begin");
   constexpr int VPL = G::VPL, RMAX = G::RMAX, XS = G::XS, KPE = G::KPE, TPR = G::TPR, CH = G::CH;
@@ -238,15 +238,6 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
   __bf16* XH = reinterpret_cast<__bf16*>(sm + G::F_XH);
   __bf16* XL = reinterpret_cast<__bf16*>(sm + G::F_XL);
 
-  const int rb = role_block(a.main_grid, a.xpack);
-  if (rb >= a.main_grid + a.nbeg) {  // extra workgroups: untouched-row AdamW slice
-    sweep_slice(a.sw, a.sw_slot, rb - a.main_grid - a.nbeg, gridDim.x - a.main_grid - a.nbeg);
-    return;
-  }
-  if (rb >= a.main_grid) {  // fused step begin (layer 0)
-    begin_slice(a.bt, a.beg, rb - a.main_grid, reinterpret_cast<uint32_t*>(sm));
-    return;
-  }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   GTR_PH(a.layer, 0);
   GTR_PH_CLK(a.layer, 6);
@@ -674,6 +665,23 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
   }
 }
 
+template <int D, bool SPLIT>
+__global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
+  using G = LayerGeom<D>;
+  static_assert(G::F_WORDS >= GTR_BEGIN_MCAP + CONV_WAVES * 64, "LDS carve too small for the fused begin");
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const int rb = role_block(a.main_grid, a.xpack);
+  if (rb >= a.main_grid + a.nbeg) {  // extra workgroups: untouched-row AdamW slice
+    sweep_slice(a.sw, a.sw_slot, rb - a.main_grid - a.nbeg, gridDim.x - a.main_grid - a.nbeg);
+    return;
+  }
+  if (rb >= a.main_grid) {  // fused step begin (layer 0)
+    begin_slice(a.bt, a.beg, rb - a.main_grid, reinterpret_cast<uint32_t*>(sm));
+    return;
+  }
+  conv_fwd_body<D, SPLIT>(a, rb);
+}
+
 struct ReadoutK {
   gtr_batch bt;
   int L1, train, flags, loss_kind, cred, fin, pad0, pad1;
@@ -718,7 +726,7 @@ struct ReadoutK {
 #define RO_WAVES (RO_BLOCK / 64)
 
 template <int D>
-__global__ __launch_bounds__(RO_BLOCK) void k_readout(ReadoutK a) {
+__device__ __forceinline__ void readout_body(const ReadoutK& a, int rb) {
   constexpr int VPL = D >= 64 ? D / 64 : 1;
   constexpr int KR = 32 / VPL;       // scoring rows per wave held in registers
   constexpr int CHN = RO_WAVES * KR; // negatives per chunk
@@ -729,11 +737,6 @@ __global__ __launch_bounds__(RO_BLOCK) void k_readout(ReadoutK a) {
   __shared__ float s_red[RO_WAVES][2 * D];
   __shared__ float s_loss[RO_WAVES][2];
   __shared__ int s_flag;
-  const int rb = role_block(a.main_grid, a.xpack);
-  if (rb >= a.main_grid) {  // extra workgroups: untouched-row AdamW slice
-    sweep_slice(a.sw, a.sw_slot, rb - a.main_grid, gridDim.x - a.main_grid);
-    return;
-  }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   GTR_PH(16, 0);
   const int B = a.bt.hdr[1];
@@ -1023,6 +1026,16 @@ __global__ __launch_bounds__(RO_BLOCK) void k_readout(ReadoutK a) {
   }
   if (do_bwd) block_sum_rows<RO_BLOCK>(a.gpart, a.main_grid, 2 * D, (size_t)2 * D, a.gsum, &s_red[0][0]);
   if (tid == 0) reset_counter(a.cnt);
+}
+
+template <int D>
+__global__ __launch_bounds__(RO_BLOCK) void k_readout(ReadoutK a) {
+  const int rb = role_block(a.main_grid, a.xpack);
+  if (rb >= a.main_grid) {  // extra workgroups: untouched-row AdamW slice
+    sweep_slice(a.sw, a.sw_slot, rb - a.main_grid, gridDim.x - a.main_grid);
+    return;
+  }
+  readout_body<D>(a, rb);
 }
 
 // Large-batch readout (b_cap >= ro_wave_min_b(), D <= 128): wave per session, grid-strided;
@@ -1352,6 +1365,87 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
   if (tid == 0) reset_counter(a.cnt);
 }
 
+
+// ------------------------------------------------------------------------------------
+// k_chain_mid: conv_fwd(1..L-1) -> readout (+ loss fwd/bwd) -> conv_bwd(L-1..0) in ONE
+// launch for small single-GPU batches (consumer-side BatchNorm reductions, <= 32 row
+// groups).  The chain workgroups (XCD-packed: one XCD's CUs) run each layer body of the
+// per-launch kernels unchanged, over the same row groups / sessions, and meet at an
+// in-launch barrier where a kernel boundary used to be: every reduction is consumer-side,
+// so a phase only needs the previous phase's stores, which the barrier publishes
+// (agent-scope release -> arrival counter -> agent-scope acquire).  The other workgroups
+// run the untouched-row AdamW slices of slots 1..2L (stamps complete: the step begin ran
+// in conv_fwd(0)) and never wait on anything, so they cannot hold a chain workgroup off
+// the chip.  Every spin is bounded: a barrier that has not filled after ~0.2 s records
+// status 1 in bar[2] and lets the workgroup through (results void, no hang).
+// ------------------------------------------------------------------------------------
+#include "gtr_bwd_body.cuh"
+
+#define GTR_CHAIN_MAXL 2
+#define GTR_CHAIN_MAXG 32
+#define GTR_CHAIN_SPIN 200000
+
+struct ChainMidK {
+  ConvFwdK fwd[GTR_CHAIN_MAXL - 1];  // layers 1..L-1
+  ReadoutK ro;
+  ConvBwdK bwd[GTR_CHAIN_MAXL];      // by layer
+  gtr_sweep sw;                      // slots 1..2L merged into bounds[0..1]
+  uint32_t* bar;                     // [0] arrivals, [1] exits, [2] status
+  int L, nchain, fwd_grid, ro_grid, xpack, pad;
+};
+
+__device__ __forceinline__ void chain_barrier(uint32_t* bar, uint32_t target) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int spins = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > GTR_CHAIN_SPIN) {
+        __hip_atomic_store(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+template <int D, bool SPLIT>
+__global__ __launch_bounds__(CONV_BLOCK) void k_chain_mid(ChainMidK m) {
+  const int rb = role_block(m.nchain, m.xpack);
+  if (rb >= m.nchain) {  // untouched-row AdamW: slots 1..2L of the chain sweep
+    sweep_slice(m.sw, 0, rb - m.nchain, gridDim.x - m.nchain);
+    return;
+  }
+  const uint32_t nch = (uint32_t)m.nchain;
+  uint32_t target = 0;
+  for (int l = 1; l < m.L; ++l) {
+    if (rb < m.fwd_grid) conv_fwd_body<D, SPLIT>(m.fwd[l - 1], rb);
+    target += nch;
+    chain_barrier(m.bar, target);
+  }
+  if (rb < m.ro_grid) readout_body<D>(m.ro, rb);
+  for (int l = m.L - 1; l >= 0; --l) {
+    target += nch;
+    chain_barrier(m.bar, target);
+    if (rb < m.fwd_grid) conv_bwd_body<D, SPLIT>(m.bwd[l], rb);
+  }
+  // every chain workgroup is past its last barrier: the last one out re-arms the counters
+  // for the next launch (stream order makes them visible to it)
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(m.bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == nch - 1) {
+      __hip_atomic_store(m.bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(m.bar + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // Sessions per batch from which the wave-per-session readout runs (env GTR_RO_WAVE_MIN_B
 // overrides, for tests); below it the block-per-session kernel has the lower latency.
 int ro_wave_min_b() {
@@ -1381,16 +1475,9 @@ void drop_params(const gtr_config* c, uint32_t& thresh, float& scale, int& on) {
   scale = on ? (float)(1.0 / (1.0 - p)) : 1.0f;
 }
 
-}  // namespace
-
-GTR_PH_READER(gtr_dbg_fwd_phases)
-
-extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_embed* emb,
-                            const gtr_layer* layers, int l, gtr_stream_t stream) {
-  if (!cfg || !bt || !layers || l < 0 || l >= cfg->num_layers) {
-    set_error("gtr_conv_fwd: bad arguments");
-    return GTR_E_ARG;
-  }
+// Arguments of conv_fwd_body for layer l (launch geometry left to the caller).
+int make_fwd_args(const gtr_config* cfg, const gtr_batch* bt, const gtr_embed* emb, const gtr_layer* layers,
+                  int l, ConvFwdK& k) {
   if (!check_dims(cfg, "gtr_conv_fwd")) return GTR_E_ARG;
   if (!bt->grp_row || !bt->grp_edge) { set_error("gtr_conv_fwd: batch lacks row-group ranges"); return GTR_E_ARG; }
   if (l == 0 && (!emb || !emb->table)) { set_error("gtr_conv_fwd: layer 0 needs the table"); return GTR_E_ARG; }
@@ -1399,7 +1486,7 @@ extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     return GTR_E_ARG;
   }
   const gtr_layer& L = layers[l];
-  ConvFwdK k{};
+  k = ConvFwdK{};
   k.bt = *bt;
   k.H = cfg->heads;
   k.C = cfg->dim / cfg->heads;
@@ -1435,6 +1522,70 @@ extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   k.xin = L.xin; k.qkvs = L.qkvs; k.alpha = L.alpha; k.agg = L.agg; k.gate = L.gate; k.out = L.out;
   k.bn_part = L.bn_part; k.cnt = L.cnt; k.bn_stats = L.bn_stats; k.bn_rmean = L.bn_rmean;
   k.bn_rvar = L.bn_rvar; k.bn_nbt = L.bn_nbt;
+  return GTR_OK;
+}
+
+// Arguments of readout_body (launch geometry left to the caller).
+int make_readout_args(const gtr_config* cfg, const gtr_batch* bt, const float* table, const gtr_layer* layers,
+                      const gtr_head* head, ReadoutK& k) {
+  if (!check_dims(cfg, "gtr_readout_loss")) return GTR_E_ARG;
+  if ((head->flags & GTR_RO_LOSS) && (head->loss_kind < GTR_LOSS_BPR || head->loss_kind > GTR_LOSS_DUAL || bt->n_neg <= 0 || !table)) {
+    set_error("gtr_readout_loss: bad loss configuration");
+    return GTR_E_ARG;
+  }
+  if ((head->flags & GTR_RO_BWD) && !cfg->training) {
+    set_error("gtr_readout_loss: backward requires training mode (batch statistics)");
+    return GTR_E_ARG;
+  }
+  const int L1 = cfg->num_layers - 1;
+  const gtr_layer& L = layers[L1];
+  k = ReadoutK{};
+  k.bt = *bt;
+  k.L1 = L1;
+  k.train = cfg->training;
+  k.flags = head->flags;
+  k.loss_kind = head->loss_kind;
+  k.cred = cfg->consumer_reduce;
+  // finalise in-kernel unless a consumer takes over: the BN sums go to conv_bwd and the
+  // loss to gtr_step_end in the fused step; a loss-only call always finalises itself.
+  k.fin = (!cfg->consumer_reduce || !(head->flags & GTR_RO_BWD)) ? 1 : 0;
+  k.temperature = head->temperature;
+  k.dual_alpha = head->dual_alpha;
+  k.bn_eps = cfg->bn_eps;
+  k.bn_mom = cfg->bn_momentum;
+  drop_params(cfg, k.thresh, k.scale, k.drop_on);
+  k.seed = cfg->seed;
+  k.rng_ctr = cfg->rng_ctr;
+  k.ctr_add = (uint32_t)cfg->ctr_add;
+  k.table = table;
+  k.out = L.out; k.xin = L.xin; k.stats = L.bn_stats; k.part = L.bn_part; k.gamma = L.bn_gamma; k.beta = L.bn_beta;
+  k.rmean = L.bn_rmean; k.rvar = L.bn_rvar; k.nbt = L.bn_nbt;
+  k.se = head->se; k.dse_in = head->dse_in; k.dse_out = head->dse_out; k.coef_tgt = head->coef_tgt;
+  k.coef_neg = head->coef_neg;
+  k.loss_part = head->loss_part; k.loss_out = head->loss_out; k.cnt = head->cnt;
+  k.dy = L.dy; k.gpart = L.bn_gpart; k.gsum = L.bn_gsum;
+  k.sync = cfg->sync_bn;
+  k.part_all = L.bn_part_all;
+  k.nparts = L.nparts_fwd;
+  if (cfg->sync_bn && ((head->flags & GTR_RO_FWD) && cfg->training) && (!L.bn_part_all || L.nparts_fwd <= 0 || !cfg->consumer_reduce)) {
+    set_error("gtr_readout_loss: sync_bn needs consumer_reduce and the gathered partials of the last layer");
+    return GTR_E_ARG;
+  }
+  return GTR_OK;
+}
+
+}  // namespace
+
+GTR_PH_READER(gtr_dbg_fwd_phases)
+
+extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_embed* emb,
+                            const gtr_layer* layers, int l, gtr_stream_t stream) {
+  if (!cfg || !bt || !layers || l < 0 || l >= cfg->num_layers) {
+    set_error("gtr_conv_fwd: bad arguments");
+    return GTR_E_ARG;
+  }
+  ConvFwdK k;
+  if (const int rc = make_fwd_args(cfg, bt, emb, layers, l, k)) return rc;
   int grid = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;
   if (grid <= 0) return GTR_OK;
   k.main_grid = grid;
@@ -1480,49 +1631,8 @@ extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
 extern "C" int gtr_readout_loss(const gtr_config* cfg, const gtr_batch* bt, const float* table,
                                 const gtr_layer* layers, const gtr_head* head, gtr_stream_t stream) {
   if (!cfg || !bt || !layers || !head) { set_error("gtr_readout_loss: bad arguments"); return GTR_E_ARG; }
-  if (!check_dims(cfg, "gtr_readout_loss")) return GTR_E_ARG;
-  if ((head->flags & GTR_RO_LOSS) && (head->loss_kind < GTR_LOSS_BPR || head->loss_kind > GTR_LOSS_DUAL || bt->n_neg <= 0 || !table)) {
-    set_error("gtr_readout_loss: bad loss configuration");
-    return GTR_E_ARG;
-  }
-  if ((head->flags & GTR_RO_BWD) && !cfg->training) {
-    set_error("gtr_readout_loss: backward requires training mode (batch statistics)");
-    return GTR_E_ARG;
-  }
-  const int L1 = cfg->num_layers - 1;
-  const gtr_layer& L = layers[L1];
-  ReadoutK k{};
-  k.bt = *bt;
-  k.L1 = L1;
-  k.train = cfg->training;
-  k.flags = head->flags;
-  k.loss_kind = head->loss_kind;
-  k.cred = cfg->consumer_reduce;
-  // finalise in-kernel unless a consumer takes over: the BN sums go to conv_bwd and the
-  // loss to gtr_step_end in the fused step; a loss-only call always finalises itself.
-  k.fin = (!cfg->consumer_reduce || !(head->flags & GTR_RO_BWD)) ? 1 : 0;
-  k.temperature = head->temperature;
-  k.dual_alpha = head->dual_alpha;
-  k.bn_eps = cfg->bn_eps;
-  k.bn_mom = cfg->bn_momentum;
-  drop_params(cfg, k.thresh, k.scale, k.drop_on);
-  k.seed = cfg->seed;
-  k.rng_ctr = cfg->rng_ctr;
-  k.ctr_add = (uint32_t)cfg->ctr_add;
-  k.table = table;
-  k.out = L.out; k.xin = L.xin; k.stats = L.bn_stats; k.part = L.bn_part; k.gamma = L.bn_gamma; k.beta = L.bn_beta;
-  k.rmean = L.bn_rmean; k.rvar = L.bn_rvar; k.nbt = L.bn_nbt;
-  k.se = head->se; k.dse_in = head->dse_in; k.dse_out = head->dse_out; k.coef_tgt = head->coef_tgt;
-  k.coef_neg = head->coef_neg;
-  k.loss_part = head->loss_part; k.loss_out = head->loss_out; k.cnt = head->cnt;
-  k.dy = L.dy; k.gpart = L.bn_gpart; k.gsum = L.bn_gsum;
-  k.sync = cfg->sync_bn;
-  k.part_all = L.bn_part_all;
-  k.nparts = L.nparts_fwd;
-  if (cfg->sync_bn && ((head->flags & GTR_RO_FWD) && cfg->training) && (!L.bn_part_all || L.nparts_fwd <= 0 || !cfg->consumer_reduce)) {
-    set_error("gtr_readout_loss: sync_bn needs consumer_reduce and the gathered partials of the last layer");
-    return GTR_E_ARG;
-  }
+  ReadoutK k;
+  if (const int rc = make_readout_args(cfg, bt, table, layers, head, k)) return rc;
   int grid = gtr_readout_grid(bt->b_cap);
   k.main_grid = grid;
   if (cfg->sweep && cfg->num_layers < GTR_SWEEP_SLOTS &&
@@ -1548,6 +1658,71 @@ extern "C" int gtr_readout_loss(const gtr_config* cfg, const gtr_batch* bt, cons
     case 128: hipLaunchKernelGGL(k_readout<128>, dim3(grid), dim3(RO_BLOCK), 0, s, k); break;
     default: hipLaunchKernelGGL(k_readout<256>, dim3(grid), dim3(RO_BLOCK), 0, s, k); break;
   }
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+extern "C" int gtr_chain_mid_ok(const gtr_config* cfg, const gtr_batch* bt) {
+  if (!cfg || !bt) return 0;
+  const int fg = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;
+  const int rg = gtr_readout_grid(bt->b_cap);
+  return cfg->training && !cfg->sync_bn && cfg->consumer_reduce && cfg->num_layers >= 2 &&
+         cfg->num_layers <= GTR_CHAIN_MAXL && fg > 0 && fg <= GTR_CHAIN_MAXG && rg <= GTR_CHAIN_MAXG &&
+         bt->b_cap < ro_wave_min_b() && cfg->dim <= 128;
+}
+
+extern "C" int gtr_chain_mid(const gtr_config* cfg, const gtr_batch* bt, const float* table, const gtr_layer* layers,
+                             const gtr_head* head, float* dx0, uint32_t* bar, gtr_stream_t stream) {
+  if (!cfg || !bt || !layers || !head || !dx0 || !bar) { set_error("gtr_chain_mid: bad arguments"); return GTR_E_ARG; }
+  if (!gtr_chain_mid_ok(cfg, bt)) {
+    set_error("gtr_chain_mid: needs training, no sync_bn, consumer_reduce, 2 <= L <= %d, <= %d row groups and "
+              "sessions, the block-per-session readout and d <= 128", GTR_CHAIN_MAXL, GTR_CHAIN_MAXG);
+    return GTR_E_ARG;
+  }
+  if (head->flags != (GTR_RO_FWD | GTR_RO_LOSS | GTR_RO_BWD)) {
+    set_error("gtr_chain_mid: the readout must run forward, loss and backward");
+    return GTR_E_ARG;
+  }
+  const int Lc = cfg->num_layers;
+  static_assert(sizeof(ChainMidK) <= 4096, "kernel argument block too large");
+  ChainMidK m{};
+  for (int l = 1; l < Lc; ++l)
+    if (const int rc = make_fwd_args(cfg, bt, nullptr, layers, l, m.fwd[l - 1])) return rc;
+  if (const int rc = make_readout_args(cfg, bt, table, layers, head, m.ro)) return rc;
+  for (int l = 0; l < Lc; ++l)
+    if (const int rc = make_bwd_args(cfg, bt, layers, l, dx0, m.bwd[l])) return rc;
+  m.L = Lc;
+  m.fwd_grid = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;
+  m.ro_grid = gtr_readout_grid(bt->b_cap);
+  m.nchain = m.fwd_grid > m.ro_grid ? m.fwd_grid : m.ro_grid;
+  for (int l = 1; l < Lc; ++l) m.fwd[l - 1].main_grid = m.fwd_grid;
+  for (int l = 0; l < Lc; ++l) m.bwd[l].main_grid = m.fwd_grid;
+  m.ro.main_grid = m.ro_grid;
+  m.bar = bar;
+  int grid = m.nchain;
+  const int s0 = 1, s1 = 2 * Lc + 1;  // slots conv_fwd(1) .. conv_bwd(0)
+  if (cfg->sweep && s1 <= GTR_SWEEP_SLOTS && cfg->sweep->bounds[s1] > cfg->sweep->bounds[s0]) {
+    m.sw = *cfg->sweep;
+    m.sw.bounds[0] = cfg->sweep->bounds[s0];
+    m.sw.bounds[1] = cfg->sweep->bounds[s1];
+    grid += sweep_blocks(cfg->sweep, grid);
+  }
+  m.xpack = xcd_pack(m.nchain, grid);
+  hipStream_t s = (hipStream_t)stream;
+#define GTR_CHAIN(DD, SP)                                                                                 \
+  {                                                                                                       \
+    constexpr size_t lds = (size_t)(LayerGeom<DD>::F_WORDS > LayerGeom<DD>::B_WORDS ? LayerGeom<DD>::F_WORDS \
+                                                                                    : LayerGeom<DD>::B_WORDS) * 4; \
+    set_lds_limit<DD>(k_chain_mid<DD, SP>, lds);                                                          \
+    hipLaunchKernelGGL((k_chain_mid<DD, SP>), dim3(grid), dim3(CONV_BLOCK), lds, s, m);                   \
+  }
+  const bool sp = gemm_split(cfg->dim) != 0;
+  switch (cfg->dim) {
+    case 32: if (sp) GTR_CHAIN(32, true) else GTR_CHAIN(32, false) break;
+    case 64: if (sp) GTR_CHAIN(64, true) else GTR_CHAIN(64, false) break;
+    default: if (sp) GTR_CHAIN(128, true) else GTR_CHAIN(128, false) break;
+  }
+#undef GTR_CHAIN
   GTR_HIP_CHECK_LAUNCH();
   return GTR_OK;
 }

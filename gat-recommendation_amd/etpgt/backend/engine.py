@@ -322,6 +322,12 @@ class Engine:
         self.run_head(ws, cfg, bs, flags, loss_kind, temperature, alpha)
 
     def run_head(self, ws, cfg, bs, flags, loss_kind=0, temperature=1.0, alpha=0.7, dse_out=False, table=None):
+        h, tab = self.fill_head(ws, flags, loss_kind, temperature, alpha, dse_out, table)
+        L.check(L.lib().gtr_readout_loss(C.byref(cfg), C.byref(bs), tab, ws.structs, C.byref(h), self.stream()),
+                "readout_loss")
+
+    def fill_head(self, ws, flags, loss_kind=0, temperature=1.0, alpha=0.7, dse_out=False, table=None):
+        """The readout's gtr_head (workspace pointers + loss settings) and table pointer."""
         h = ws.head
         h.flags = flags
         h.loss_kind = loss_kind
@@ -336,8 +342,7 @@ class Engine:
         h.loss_out = ws.loss_out.data_ptr()
         h.cnt = ws.head_cnt.data_ptr()
         tab = self.model.item_embedding.weight.data_ptr() if table is None else table
-        L.check(L.lib().gtr_readout_loss(C.byref(cfg), C.byref(bs), tab, ws.structs, C.byref(h), self.stream()),
-                "readout_loss")
+        return h, tab
 
     def _wgrad(self, ws, cfg, bs, l0, l1, st):
         pe_tab = None

@@ -90,7 +90,8 @@ def _train_and_compare(m, ref, fused, batches, kind, lr, dropout=0.0, also=()):
     is itself not that accurate (Adam turns a gradient that nearly cancels -- a sum whose
     rounding differs between any two summation orders -- into an update that differs by
     a fraction of lr): there the HIP value may deviate from fp32 by at most 8 times the
-    fp32 oracle's own distance to fp64.  Elements whose first gradient is at the fp32
+    fp32 oracle's own distance to fp64, or at most the fp32 oracle's worst distance to fp64
+    anywhere in the same tensor from fp64 itself.  Elements whose first gradient is at the fp32
     noise floor are bounded by 2 lr per step (see the module docstring)."""
     import copy
 
@@ -168,14 +169,22 @@ def _close_trained(a, b, c, allow, bound, name):
     scale = float(b.abs().max()) if b.numel() else 0.0
     tol = 1e-3 * (b.abs() + 1e-2 * scale) + 8 * (b - c).abs() + 1e-12
     err = (a - b).abs()
-    bad = err > tol
+    # fp32 noise level of the tensor: the worst distance of the fp32 oracle itself from the
+    # fp64 oracle anywhere in it.  An element that misses the elementwise bar above is still
+    # accepted when the HIP value is no further from the fp64 result than that (a gradient
+    # that nearly cancels is rounded differently by any two fp32 summation orders, and the
+    # fp32 oracle can land close to fp64 on that element by chance).
+    floor = float((b - c).abs().max()) if b.numel() else 0.0
+    near = err > tol
+    bad = near & ((a - c).abs() > floor)
     if bool(bad.any()):
-        i = int(torch.argmax(err - tol))
+        i = int(torch.argmax((err - tol) * bad))
         raise AssertionError(f"{name}: {int(bad.sum())}/{b.numel()} mismatches; worst: hip {a[i].item():.7g} "
-                             f"oracle fp32 {b[i].item():.7g} fp64 {c[i].item():.7g}")
+                             f"oracle fp32 {b[i].item():.7g} fp64 {c[i].item():.7g} (fp32 noise level {floor:.3g})")
     ill = int(((b - c).abs() > 1e-3 * (b.abs() + 1e-2 * scale)).sum())
     print(f"{name}: {b.numel()} elements within 1e-3 of the fp32 oracle or of its own fp64 distance "
-          f"({ill} where fp32 itself is off by more than 1e-3)")
+          f"({ill} where fp32 itself is off by more than 1e-3; {int(near.sum())} within the tensor's fp32 "
+          f"noise level {floor:.3g} of fp64 only)")
 
 
 def test_c2_full_table_matches_oracle():
