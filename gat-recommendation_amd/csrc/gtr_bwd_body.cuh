@@ -1,7 +1,8 @@
-// gtr_bwd_body.cuh — the TransformerConv layer backward (k_conv_bwd) as a device body
-// over one row group, shared by the per-layer launch (gtr_bwd.hip) and the fused chain
-// launch (k_chain_mid in gtr_fwd.hip).  Included inside an anonymous namespace after
-// GTR_PH_DECL; see gtr_bwd.hip for the algorithm.
+// gtr_bwd_body.cuh — the TransformerConv layer backward (k_conv_bwd) as a device body over
+// one row group plus its argument builder, so that other translation units can compose it
+// with the forward bodies (a single-launch step middle was built on these and measured
+// slower than the launches).  Included inside an anonymous namespace
+// after GTR_PH_DECL; see gtr_bwd.hip for the algorithm.
 #pragma once
 
 struct ConvBwdK {

@@ -1366,85 +1366,6 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
 }
 
 
-// ------------------------------------------------------------------------------------
-// k_chain_mid: conv_fwd(1..L-1) -> readout (+ loss fwd/bwd) -> conv_bwd(L-1..0) in ONE
-// launch for small single-GPU batches (consumer-side BatchNorm reductions, <= 32 row
-// groups).  The chain workgroups (XCD-packed: one XCD's CUs) run each layer body of the
-// per-launch kernels unchanged, over the same row groups / sessions, and meet at an
-// in-launch barrier where a kernel boundary used to be: every reduction is consumer-side,
-// so a phase only needs the previous phase's stores, which the barrier publishes
-// (agent-scope release -> arrival counter -> agent-scope acquire).  The other workgroups
-// run the untouched-row AdamW slices of slots 1..2L (stamps complete: the step begin ran
-// in conv_fwd(0)) and never wait on anything, so they cannot hold a chain workgroup off
-// the chip.  Every spin is bounded: a barrier that has not filled after ~0.2 s records
-// status 1 in bar[2] and lets the workgroup through (results void, no hang).
-// ------------------------------------------------------------------------------------
-#include "gtr_bwd_body.cuh"
-
-#define GTR_CHAIN_MAXL 2
-#define GTR_CHAIN_MAXG 32
-#define GTR_CHAIN_SPIN 200000
-
-struct ChainMidK {
-  ConvFwdK fwd[GTR_CHAIN_MAXL - 1];  // layers 1..L-1
-  ReadoutK ro;
-  ConvBwdK bwd[GTR_CHAIN_MAXL];      // by layer
-  gtr_sweep sw;                      // slots 1..2L merged into bounds[0..1]
-  uint32_t* bar;                     // [0] arrivals, [1] exits, [2] status
-  int L, nchain, fwd_grid, ro_grid, xpack, pad;
-};
-
-__device__ __forceinline__ void chain_barrier(uint32_t* bar, uint32_t target) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int spins = 0;
-    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins > GTR_CHAIN_SPIN) {
-        __hip_atomic_store(bar + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-}
-
-template <int D, bool SPLIT>
-__global__ __launch_bounds__(CONV_BLOCK) void k_chain_mid(ChainMidK m) {
-  const int rb = role_block(m.nchain, m.xpack);
-  if (rb >= m.nchain) {  // untouched-row AdamW: slots 1..2L of the chain sweep
-    sweep_slice(m.sw, 0, rb - m.nchain, gridDim.x - m.nchain);
-    return;
-  }
-  const uint32_t nch = (uint32_t)m.nchain;
-  uint32_t target = 0;
-  for (int l = 1; l < m.L; ++l) {
-    if (rb < m.fwd_grid) conv_fwd_body<D, SPLIT>(m.fwd[l - 1], rb);
-    target += nch;
-    chain_barrier(m.bar, target);
-  }
-  if (rb < m.ro_grid) readout_body<D>(m.ro, rb);
-  for (int l = m.L - 1; l >= 0; --l) {
-    target += nch;
-    chain_barrier(m.bar, target);
-    if (rb < m.fwd_grid) conv_bwd_body<D, SPLIT>(m.bwd[l], rb);
-  }
-  // every chain workgroup is past its last barrier: the last one out re-arms the counters
-  // for the next launch (stream order makes them visible to it)
-  if (threadIdx.x == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(m.bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == nch - 1) {
-      __hip_atomic_store(m.bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(m.bar + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
 
 // Sessions per batch from which the wave-per-session readout runs (env GTR_RO_WAVE_MIN_B
 // overrides, for tests); below it the block-per-session kernel has the lower latency.
@@ -1662,67 +1583,3 @@ extern "C" int gtr_readout_loss(const gtr_config* cfg, const gtr_batch* bt, cons
   return GTR_OK;
 }
 
-extern "C" int gtr_chain_mid_ok(const gtr_config* cfg, const gtr_batch* bt) {
-  if (!cfg || !bt) return 0;
-  const int fg = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;
-  const int rg = gtr_readout_grid(bt->b_cap);
-  return cfg->training && !cfg->sync_bn && cfg->consumer_reduce && cfg->num_layers >= 2 &&
-         cfg->num_layers <= GTR_CHAIN_MAXL && fg > 0 && fg <= GTR_CHAIN_MAXG && rg <= GTR_CHAIN_MAXG &&
-         bt->b_cap < ro_wave_min_b() && cfg->dim <= 128;
-}
-
-extern "C" int gtr_chain_mid(const gtr_config* cfg, const gtr_batch* bt, const float* table, const gtr_layer* layers,
-                             const gtr_head* head, float* dx0, uint32_t* bar, gtr_stream_t stream) {
-  if (!cfg || !bt || !layers || !head || !dx0 || !bar) { set_error("gtr_chain_mid: bad arguments"); return GTR_E_ARG; }
-  if (!gtr_chain_mid_ok(cfg, bt)) {
-    set_error("gtr_chain_mid: needs training, no sync_bn, consumer_reduce, 2 <= L <= %d, <= %d row groups and "
-              "sessions, the block-per-session readout and d <= 128", GTR_CHAIN_MAXL, GTR_CHAIN_MAXG);
-    return GTR_E_ARG;
-  }
-  if (head->flags != (GTR_RO_FWD | GTR_RO_LOSS | GTR_RO_BWD)) {
-    set_error("gtr_chain_mid: the readout must run forward, loss and backward");
-    return GTR_E_ARG;
-  }
-  const int Lc = cfg->num_layers;
-  static_assert(sizeof(ChainMidK) <= 4096, "kernel argument block too large");
-  ChainMidK m{};
-  for (int l = 1; l < Lc; ++l)
-    if (const int rc = make_fwd_args(cfg, bt, nullptr, layers, l, m.fwd[l - 1])) return rc;
-  if (const int rc = make_readout_args(cfg, bt, table, layers, head, m.ro)) return rc;
-  for (int l = 0; l < Lc; ++l)
-    if (const int rc = make_bwd_args(cfg, bt, layers, l, dx0, m.bwd[l])) return rc;
-  m.L = Lc;
-  m.fwd_grid = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;
-  m.ro_grid = gtr_readout_grid(bt->b_cap);
-  m.nchain = m.fwd_grid > m.ro_grid ? m.fwd_grid : m.ro_grid;
-  for (int l = 1; l < Lc; ++l) m.fwd[l - 1].main_grid = m.fwd_grid;
-  for (int l = 0; l < Lc; ++l) m.bwd[l].main_grid = m.fwd_grid;
-  m.ro.main_grid = m.ro_grid;
-  m.bar = bar;
-  int grid = m.nchain;
-  const int s0 = 1, s1 = 2 * Lc + 1;  // slots conv_fwd(1) .. conv_bwd(0)
-  if (cfg->sweep && s1 <= GTR_SWEEP_SLOTS && cfg->sweep->bounds[s1] > cfg->sweep->bounds[s0]) {
-    m.sw = *cfg->sweep;
-    m.sw.bounds[0] = cfg->sweep->bounds[s0];
-    m.sw.bounds[1] = cfg->sweep->bounds[s1];
-    grid += sweep_blocks(cfg->sweep, grid);
-  }
-  m.xpack = xcd_pack(m.nchain, grid);
-  hipStream_t s = (hipStream_t)stream;
-#define GTR_CHAIN(DD, SP)                                                                                 \
-  {                                                                                                       \
-    constexpr size_t lds = (size_t)(LayerGeom<DD>::F_WORDS > LayerGeom<DD>::B_WORDS ? LayerGeom<DD>::F_WORDS \
-                                                                                    : LayerGeom<DD>::B_WORDS) * 4; \
-    set_lds_limit<DD>(k_chain_mid<DD, SP>, lds);                                                          \
-    hipLaunchKernelGGL((k_chain_mid<DD, SP>), dim3(grid), dim3(CONV_BLOCK), lds, s, m);                   \
-  }
-  const bool sp = gemm_split(cfg->dim) != 0;
-  switch (cfg->dim) {
-    case 32: if (sp) GTR_CHAIN(32, true) else GTR_CHAIN(32, false) break;
-    case 64: if (sp) GTR_CHAIN(64, true) else GTR_CHAIN(64, false) break;
-    default: if (sp) GTR_CHAIN(128, true) else GTR_CHAIN(128, false) break;
-  }
-#undef GTR_CHAIN
-  GTR_HIP_CHECK_LAUNCH();
-  return GTR_OK;
-}

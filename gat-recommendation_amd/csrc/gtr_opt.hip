@@ -467,9 +467,11 @@ __device__ __forceinline__ void window_rows(int w, const gtr_batch& bt, int T, c
     if (key <= 0 || key >= T) continue;
     const int e = q + 1 < nb ? s_bnd[q + 1] : w1;
     const size_t base = (size_t)key * C4 + gl;
-    float4 pv = reinterpret_cast<const float4*>(tl.table)[base];
-    float4 mv = reinterpret_cast<const float4*>(tl.table_m)[base];
-    float4 vv = reinterpret_cast<const float4*>(tl.table_v)[base];
+    // p / m / v streamed (non-temporal): every row is touched once, so keeping them out of
+    // L2 leaves it to the session rows se[b] that every target / negative contribution reads
+    float4 pv = sw_ld(reinterpret_cast<const float4*>(tl.table) + base);
+    float4 mv = sw_ld(reinterpret_cast<const float4*>(tl.table_m) + base);
+    float4 vv = sw_ld(reinterpret_cast<const float4*>(tl.table_v) + base);
     float4 g = piece_sum<D>(bt, tl.svals, s0, e, tl.dx0, tl.se, tl.coef_tgt, tl.coef_neg, gl, gb);
     if (e == w1) {  // the segment may continue: add the carries in window order
       for (int w2 = w + 1; w2 * TW < m_cap && tl.skeys[w2 * TW] == key; ++w2) {
@@ -482,9 +484,9 @@ __device__ __forceinline__ void window_rows(int w, const gtr_batch& bt, int T, c
     st.apply(pv.y, mv.y, vv.y, g.y);
     st.apply(pv.z, mv.z, vv.z, g.z);
     st.apply(pv.w, mv.w, vv.w, g.w);
-    reinterpret_cast<float4*>(tl.table)[base] = pv;
-    reinterpret_cast<float4*>(tl.table_m)[base] = mv;
-    reinterpret_cast<float4*>(tl.table_v)[base] = vv;
+    sw_st(reinterpret_cast<float4*>(tl.table) + base, pv);
+    sw_st(reinterpret_cast<float4*>(tl.table_m) + base, mv);
+    sw_st(reinterpret_cast<float4*>(tl.table_v) + base, vv);
     if (lazy_stamp && gl == 0) lazy_stamp[key] = lazy_t;
   }
 }

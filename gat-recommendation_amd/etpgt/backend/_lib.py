@@ -92,7 +92,7 @@ class GtrTail(C.Structure):
 
 
 SWEEP_SLOTS = 8
-ABI_VERSION = 4  # GTR_ABI_VERSION of include/gtr.h
+ABI_VERSION = 3  # GTR_ABI_VERSION of include/gtr.h
 
 
 class GtrLazy(C.Structure):
@@ -143,8 +143,6 @@ _SIGS = {
     "gtr_conv_fwd": (C.c_int, [P, P, P, P, C.c_int, P]),
     "gtr_readout_loss": (C.c_int, [P, P, P, P, P, P]),
     "gtr_conv_bwd": (C.c_int, [P, P, P, C.c_int, P, P]),
-    "gtr_chain_mid_ok": (C.c_int, [P, P]),
-    "gtr_chain_mid": (C.c_int, [P, P, P, P, P, P, P, P]),
     "gtr_wgrad": (C.c_int, [P, P, P, P, P, P, P, C.c_int, i64, C.c_int, C.c_int, P]),
     "gtr_adamw_small": (C.c_int, [P, P, P, P, i64, P, C.c_int, P, P]),
     "gtr_contrib_prep": (C.c_int, [P, C.c_int, P, P, P, P, P]),

@@ -278,12 +278,6 @@ class FusedTrainStep:
             self.layer_flat = (C.c_int64 * (3 * eng.L))(*[lay.seg(f"{l}.{n}").begin for l in range(eng.L)
                                                           for n in ("w_all", "b_all", "w_beta")])
             self.pe_flat = (C.c_int64 * 2)(lay.seg("pe.w").begin, lay.seg("pe.b").begin) if eng.K > 0 else None
-        # small single-GPU batches: conv_fwd(1..L-1), the readout and conv_bwd(L-1..0) as one
-        # launch with in-launch barriers (gtr_chain_mid), bitwise the separate launches
-        self.chain_mid = (self.dp is None and self.shard is None and not self.sync_bn
-                          and os.environ.get("GTR_CHAIN_MID", "0") != "0"
-                          and bool(L.lib().gtr_chain_mid_ok(C.byref(self.cfg), C.byref(self.bs))))
-        self.chain_bar = torch.zeros(4, dtype=torch.int32, device=self.dev) if self.chain_mid else None
         self.graph = None
         self.graph_pe = None
         self.graph_b = None
@@ -401,19 +395,8 @@ class FusedTrainStep:
         bs = self.bs_pe if with_pe else self.bs
         st = torch.cuda.current_stream(self.dev).cuda_stream
         self._begin(bs, st)
-        flags = L.RO_FWD | L.RO_LOSS | L.RO_BWD
-        if self.chain_mid:
-            lib = L.lib()
-            L.check(lib.gtr_conv_fwd(C.byref(cfg), C.byref(bs), C.byref(eng.fill_embed()), ws.structs, 0, st),
-                    "conv_fwd")
-            h, tab = eng.fill_head(ws, flags, self.loss_kind, self.temperature, self.alpha)
-            L.check(lib.gtr_chain_mid(C.byref(cfg), C.byref(bs), tab, ws.structs, C.byref(h), ws.dx0.data_ptr(),
-                                      self.chain_bar.data_ptr(), st), "chain_mid")
-            if not self.tail_wgrad:
-                eng._wgrad(ws, cfg, bs, 0, eng.L, st)
-        else:
-            eng.run_forward(ws, cfg, bs, flags, self.loss_kind, self.temperature, self.alpha)
-            eng.run_backward(ws, cfg, bs, wgrad=not self.tail_wgrad)
+        eng.run_forward(ws, cfg, bs, L.RO_FWD | L.RO_LOSS | L.RO_BWD, self.loss_kind, self.temperature, self.alpha)
+        eng.run_backward(ws, cfg, bs, wgrad=not self.tail_wgrad)
         if self.dp is not None:
             self.dp.launch_pack(bs, st)
 

@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GTR_ABI_VERSION 4 /* 4: gtr_chain_mid; 3: gtr_config.begin / ctr_add, gtr_tail.rng_inc */
+#define GTR_ABI_VERSION 3 /* 3: gtr_config.begin / ctr_add, gtr_tail.rng_inc (begin fused into conv_fwd(0)) */
 
 #define GTR_OK 0
 #define GTR_E_ARG 1001      /* bad argument / unsupported shape */
@@ -225,19 +225,6 @@ int gtr_readout_loss(const gtr_config* cfg, const gtr_batch* bt, const float* ta
  * layers[l].dqkvs/du and either layers[l-1].dy (+ its BN sums) or dx0.        */
 int gtr_conv_bwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l,
                  float* dx0, gtr_stream_t stream);
-
-/* conv_fwd(1..L-1) -> readout (forward, loss, backward) -> conv_bwd(L-1..0) as ONE launch
- * (same arithmetic as those calls, bitwise): the chain workgroups meet at in-launch
- * barriers where the launch boundaries were, the other workgroups run the chain sweep's
- * slots 1..2L.  For small single-GPU training batches: gtr_chain_mid_ok(cfg, bt) != 0
- * (consumer_reduce, no sync_bn, L == 2, <= 32 row groups and sessions, the
- * block-per-session readout, d <= 128).  bar: 4 device words, zero before the first
- * launch; each launch leaves [0], [1] zero and sets [2] = 1 if a barrier timed out.
- * Replaces graph_transformer.py:171-180 + base.py:80-155 (forward after layer 0 and the
- * loss) and their autograd (trainer.py:80-133, loss.backward()).                     */
-int gtr_chain_mid_ok(const gtr_config* cfg, const gtr_batch* bt);
-int gtr_chain_mid(const gtr_config* cfg, const gtr_batch* bt, const float* table, const gtr_layer* layers,
-                  const gtr_head* head, float* dx0, uint32_t* bar, gtr_stream_t stream);
 
 /* Weight-gradient partial slabs for layers [l_begin, l_end) (+ LapPE projection
  * when l_begin == 0).
