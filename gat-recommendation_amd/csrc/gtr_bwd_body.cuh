@@ -167,8 +167,10 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
   constexpr int CPW = NCT > CONV_WAVES ? NCT / CONV_WAVES : 1;  // column tiles per wave
   constexpr int WPC = NCT >= CONV_WAVES ? 1 : CONV_WAVES / NCT; // waves sharing a column tile
   constexpr int ASB = 4 * D + 8;                                // LDS split dQKVS row stride (bf16)
+  constexpr int AS32 = 4 * D + 4;                               // LDS fp32 dQKVS row stride
   constexpr int RTW = (RMAX / 16 + WPC - 1) / WPC;              // row tiles per wave
   static_assert(!G::KV || RMAX * ASB <= G::B_RN, "split dQKVS rows must fit the K|V|Q|dA region");
+  static_assert(!G::KV || RMAX * AS32 <= G::B_RN, "fp32 dQKVS rows must fit the K|V|Q|dA region");
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* Ks = sm + G::B_R;
   float* Vs = Ks + RMAX * XS;
@@ -215,6 +217,20 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
   const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
   const float invN = 1.0f / (float)N;
   const int prow = tid / TPR, pchunk = tid - prow * TPR, f0 = pchunk * CH;
+  // W_all fragments of this wave's dX column tile, requested now so the L2 / MALL round trips
+  // overlap the staging and the attention phases instead of sitting inside the dX MFMA chain
+  // (f32 GEMM, one column tile per wave)
+  constexpr bool PREB = !SPLIT && CPW == 1 && D <= 128;
+  float4 wb[PREB ? D / 4 : 1];
+  if constexpr (PREB) {
+    const int ct0 = WPC > 1 ? wave % NCT : wave;
+    const float* bcol = a.w_all + (size_t)((lane >> 4) * 4) * D + ct0 * 16 + (lane & 15);
+#pragma unroll
+    for (int kb = 0; kb < D / 4; ++kb) {
+      const float* bp = bcol + (size_t)(kb * 16) * D;
+      wb[kb] = make_float4(bp[0], bp[D], bp[2 * D], bp[3 * D]);
+    }
+  }
 
   // ---- this layer's BatchNorm backward sums: reduce the producer's partials (cred)
   if (a.cred) {
@@ -406,6 +422,22 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
         *reinterpret_cast<float4*>(drow + 2 * D + c) = make_float4(dv[c], dv[c + 1], dv[c + 2], dv[c + 3]);
       }
     }
+    if constexpr (!SPLIT) {
+      // the group's dQKVS rows (fp32, row stride AS32) over the K | V | Q | dA rows (dead from
+      // here on): the A operand of phase X from LDS instead of L2
+      __syncthreads();
+      if (live) {
+        float* ar = sm + G::B_R + prow * AS32 + f0;
+        const float* parts[4] = {dq, dk, dv, dsv};
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+#pragma unroll
+          for (int c = 0; c < CH; c += 4)
+            *reinterpret_cast<float4*>(ar + p * D + c) =
+                make_float4(parts[p][c], parts[p][c + 1], parts[p][c + 2], parts[p][c + 3]);
+        }
+      }
+    }
     if constexpr (SPLIT) {
       // the group's dQKVS rows, split into bf16 hi | lo, over the K | V | Q | dA rows (dead
       // from here on): the A operand of phase X, read from LDS by every wave
@@ -522,7 +554,67 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
       }
     }
   }
-  for (int rt = r0 + rs * 16; !(SPLIT && fast) && rt < r1; rt += 16 * WPC) {
+  if constexpr (!SPLIT && G::KV) {
+    if (fast) {
+      // f32 MFMA, A rows from LDS, B from the prefetched fragments; the wave's live row
+      // tiles advance together (every output element still sums its k terms in the order
+      // of the one-tile-at-a-time loop below, so the results are bitwise those of it)
+      const float* A = sm + G::B_R;
+      auto tiles = [&](auto nr_c) {
+        constexpr int NR = decltype(nr_c)::value;
+#pragma unroll
+        for (int c = 0; c < CPW; ++c) {
+          const int ct = (WPC > 1 ? wave % NCT : wave) + c * CONV_WAVES;
+          const float* bcol = a.w_all + (size_t)(lg * 4) * D + ct * 16 + lr;
+          f32x4 acc[NR];
+#pragma unroll
+          for (int r = 0; r < NR; ++r) acc[r] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll  // whole: wb[] stays in registers only with constant indices
+          for (int kb = 0; kb < D / 4; ++kb) {
+            float4 bv;
+            if constexpr (PREB) {
+              bv = wb[kb];
+            } else {
+              const float* bp = bcol + (size_t)(kb * 16) * D;
+              bv = make_float4(bp[0], bp[D], bp[2 * D], bp[3 * D]);
+            }
+#pragma unroll
+            for (int r = 0; r < NR; ++r)
+              acc[r] = mfma4(*reinterpret_cast<const float4*>(A + ((rs + r * WPC) * 16 + lr) * AS32 + kb * 16 + lg * 4),
+                             bv, acc[r]);
+          }
+          const int col = ct * 16 + lr;
+#pragma unroll
+          for (int r = 0; r < NR; ++r) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int row = r0 + (rs + r * WPC) * 16 + lg * 4 + i;
+              if (row < r1) {
+                const size_t o = (size_t)row * D + col;
+                const float dx = a.dy[o] + acc[r][i];
+                if (a.has_prev) {
+                  const float d = dx * dr.mul(st_prev, (uint32_t)o);
+                  a.p_dy[o] = d;
+                  s1[c] += d;
+                  s2[c] += d * ((a.p_out[o] - pm[c]) * pr[c]);
+                } else {
+                  a.dx0[o] = dx;
+                }
+              }
+            }
+          }
+        }
+      };
+      // live row tiles of this wave: rs, rs + WPC, ... below the group's row count
+      const int nlive = rs * 16 < nrow ? min(RTW, ((nrow + 15) / 16 - rs + WPC - 1) / WPC) : 0;
+      if (nlive == 1) tiles(std::integral_constant<int, 1>{});
+      if constexpr (RTW >= 2) if (nlive == 2) tiles(std::integral_constant<int, 2>{});
+      if constexpr (RTW >= 3) if (nlive == 3) tiles(std::integral_constant<int, 3>{});
+      if constexpr (RTW >= 4) if (nlive == 4) tiles(std::integral_constant<int, 4>{});
+      static_assert(RTW <= 4, "row tiles per wave");
+    }
+  }
+  for (int rt = r0 + rs * 16; !fast && rt < r1; rt += 16 * WPC) {
     const int ar = min(rt + lr, r1 - 1);  // clamp: rows past the group are computed, never stored
     const float* arow = a.dqkvs + (size_t)ar * (4 * D) + lg * 4;
 #pragma unroll

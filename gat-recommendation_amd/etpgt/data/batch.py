@@ -16,6 +16,8 @@ captured hipGraph can be replayed over batches of any shape within capacity.
 
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 
 import numpy as np
@@ -44,6 +46,15 @@ class Caps:
         # a group's rows are R plus the tail of its last session, and the LDS fast path of
         # the layer kernels takes <= 32 rows at D = 128 (RMAX): R = 32 sent nearly every
         # group of a large batch down the global-memory path
+        # small batches (<= 32 groups of 8): a group of ~8 rows fills ONE 16-row MFMA tile in
+        # the QKVS projection and dX instead of two, and its attention phases are half as
+        # long; the groups are still few enough to share one XCD (measured C2 0.0903 ->
+        # 0.0866 ms, C3 0.150 -> 0.142 ms per step; R = 8 at B = 8192 took 1.25 -> 1.70 ms)
+        r = os.environ.get("GTR_ROW_GROUP")  # experiments: a fixed width
+        if r:
+            return int(r)
+        if self.n_cap <= 256:
+            return 8
         return 16 if self.n_cap <= 65536 else 32
 
     @property

@@ -412,3 +412,12 @@ def test_train_grads_gemm_modes(gemm, D, H, K, loss, monkeypatch):
     single-step gradients against the oracle at 2e-3."""
     monkeypatch.setenv("GTR_GEMM", gemm)
     test_train_grads(D, H, K, loss)
+
+
+@pytest.mark.parametrize("rg", ["8", "16"])
+def test_row_group_widths_match_oracle(rg, monkeypatch):
+    """Both row-group widths the step picks (8 rows for <= 32 groups, 16 above) on the same
+    C2- and C3-shaped batches: per-step losses and trained parameters against the oracle."""
+    monkeypatch.setenv("GTR_ROW_GROUP", rg)
+    _fused_vs_reference(64, 1, 0, "bpr", "adamw", True, B=32, steps=3)
+    _fused_vs_reference(128, 4, 16, "listwise", "adamw", True, B=32, steps=3)
