@@ -217,33 +217,46 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
   const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
   const float invN = 1.0f / (float)N;
   const int prow = tid / TPR, pchunk = tid - prow * TPR, f0 = pchunk * CH;
-  // W_all fragments of this wave's dX column tile, requested now so the L2 / MALL round trips
-  // overlap the staging and the attention phases instead of sitting inside the dX MFMA chain
-  // (f32 GEMM, one column tile per wave)
   constexpr bool PREB = !SPLIT && CPW == 1 && D <= 128;
   float4 wb[PREB ? D / 4 : 1];
-  if constexpr (PREB) {
-    const int ct0 = WPC > 1 ? wave % NCT : wave;
-    const float* bcol = a.w_all + (size_t)((lane >> 4) * 4) * D + ct0 * 16 + (lane & 15);
-#pragma unroll
-    for (int kb = 0; kb < D / 4; ++kb) {
-      const float* bp = bcol + (size_t)(kb * 16) * D;
-      wb[kb] = make_float4(bp[0], bp[D], bp[2 * D], bp[3 * D]);
-    }
-  }
 
-  // ---- this layer's BatchNorm backward sums: reduce the producer's partials (cred)
-  if (a.cred) {
-    const int np = a.sync ? a.nparts_bwd : (a.gpart_n >= 0 ? a.gpart_n : Gn);
-    const float* gp = a.sync ? a.gpart_all : a.gpart;
-    for (int j = tid; j < 2 * D; j += CONV_BLOCK) {
-      float acc = 0.0f;
-#pragma unroll 8
-      for (int q = 0; q < np; ++q) acc += gp[(size_t)q * 2 * D + j];
-      s_gs[j] = acc;
-      if (g == 0) a.gsum[j] = acc;
+  // ---- this layer's BatchNorm backward sums: reduce the producer's partials (cred).
+  //      D <= 64: the first GPR partial rows are requested into registers here and summed
+  //      after the staging loads below have been issued, so the two round trips overlap
+  //      (same order of the sum: rows ascending)
+  constexpr int GPR = (D <= 64 && 2 * D <= CONV_BLOCK) ? 32 : 0;
+  const int np = a.sync ? a.nparts_bwd : (a.gpart_n >= 0 ? a.gpart_n : Gn);
+  const float* gp = a.sync ? a.gpart_all : a.gpart;
+  float gpr[GPR > 0 ? GPR : 1];
+  if constexpr (GPR > 0) {
+    if (a.cred && tid < 2 * D) {
+#pragma unroll
+      for (int q = 0; q < GPR; ++q) gpr[q] = q < np ? gp[(size_t)q * 2 * D + tid] : 0.0f;
     }
   }
+  auto reduce_gsum = [&]() {
+    if (!a.cred) return;
+    if constexpr (GPR > 0) {
+      if (tid < 2 * D) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int q = 0; q < GPR; ++q)
+          if (q < np) acc += gpr[q];
+        for (int q = GPR; q < np; ++q) acc += gp[(size_t)q * 2 * D + tid];
+        s_gs[tid] = acc;
+        if (g == 0) a.gsum[tid] = acc;
+      }
+    } else {
+      for (int j = tid; j < 2 * D; j += CONV_BLOCK) {
+        float acc = 0.0f;
+#pragma unroll 8
+        for (int q = 0; q < np; ++q) acc += gp[(size_t)q * 2 * D + j];
+        s_gs[j] = acc;
+        if (g == 0) a.gsum[j] = acc;
+      }
+    }
+  };
+  if (!fast) reduce_gsum();
 
   if (fast) {
     // ---- stage: CSR slices (by destination and by source), alpha, K | V | Q rows
@@ -268,6 +281,19 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
       *reinterpret_cast<float4*>(Vs + i * XS + c) = *reinterpret_cast<const float4*>(src + 2 * D + c);
       *reinterpret_cast<float4*>(Qs + i * XS + c) = *reinterpret_cast<const float4*>(src + c);
     }
+  // W_all fragments of this wave's dX column tile, requested once the staging loads are
+  // out (vector loads retire in order: issued first they would hold up the staging) so
+  // they arrive during the attention phases instead of inside the dX MFMA chain
+  if constexpr (PREB) {
+    const int ct0 = WPC > 1 ? wave % NCT : wave;
+    const float* bcol = a.w_all + (size_t)((lane >> 4) * 4) * D + ct0 * 16 + (lane & 15);
+#pragma unroll
+    for (int kb = 0; kb < D / 4; ++kb) {
+      const float* bp = bcol + (size_t)(kb * 16) * D;
+      wb[kb] = make_float4(bp[0], bp[D], bp[2 * D], bp[3 * D]);
+    }
+  }
+    reduce_gsum();
     __syncthreads();
     GTR_PH(a.layer, 1);
 
@@ -459,6 +485,18 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
       }
     }
   } else {
+  // W_all fragments of this wave's dX column tile, requested once the staging loads are
+  // out (vector loads retire in order: issued first they would hold up the staging) so
+  // they arrive during the attention phases instead of inside the dX MFMA chain
+  if constexpr (PREB) {
+    const int ct0 = WPC > 1 ? wave % NCT : wave;
+    const float* bcol = a.w_all + (size_t)((lane >> 4) * 4) * D + ct0 * 16 + (lane & 15);
+#pragma unroll
+    for (int kb = 0; kb < D / 4; ++kb) {
+      const float* bp = bcol + (size_t)(kb * 16) * D;
+      wb[kb] = make_float4(bp[0], bp[D], bp[2 * D], bp[3 * D]);
+    }
+  }
     __syncthreads();
     GTR_PH(a.layer, 1);
     // ---- general path: wave per row against global memory (any group size / dim)

@@ -264,8 +264,22 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
   const int d0 = lane * VPL;
   const bool act = d0 < D;
 
+  // ---- the CSR slice and the node items, requested before the weights: vector loads
+  //      retire in order, so the LDS stores of these values below wait only for them and
+  //      not for the 16-64 KB weight fetch issued after them (nrow <= RMAX <= 64 and
+  //      ne <= EMAX = 2 * CONV_BLOCK on the fast path: at most one / two per thread)
+  static_assert(G::EMAX <= 2 * CONV_BLOCK && RMAX < CONV_BLOCK, "one CSR pass per thread");
+  int c_ip0 = 0, c_ip1 = 0, c_src0 = 0, c_src1 = 0, c_item = 0;
+  if (fast) {
+    if (tid <= nrow) c_ip0 = a.bt.in_ptr[r0 + tid];
+    if (tid < nrow) c_ip1 = a.bt.in_ptr[r0 + tid + 1];
+    if (tid < ne) c_src0 = a.bt.in_src[e_lo + tid];
+    if (tid + CONV_BLOCK < ne) c_src1 = a.bt.in_src[e_lo + tid + CONV_BLOCK];
+  }
+  if (a.first && tid < min(RMAX, nrow)) c_item = a.bt.node_item[r0 + tid];
+
   // ---- W fragments of this wave's first column tiles and the gate weights, issued
-  //      before anything else so the weight fetch overlaps the staging round trip
+  //      early so the weight fetch overlaps the staging round trip
   constexpr int PRE = D <= 64 ? (NCT / CONV_WAVES) : 1;
   float4 wpre[PRE][D / 16];
 #pragma unroll
@@ -296,6 +310,28 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
     load_vec<VPL>(w3, a.w_beta + 2 * D + d0, act);
   }
 
+  // ---- layers >= 1: the first chunk's previous-layer rows (out, xin) requested now, so they
+  //      arrive while the BatchNorm partials are reduced and the CSR slice is staged
+  constexpr int C4 = D / 4;
+  constexpr int PRL = (RMAX * C4 + CONV_BLOCK - 1) / CONV_BLOCK;  // float4 per thread and chunk
+  constexpr bool PREROWS = D <= 64;  // D = 128 has no registers to spare (spills)
+  float4 ppo[PREROWS ? PRL : 1], ppx[PREROWS ? PRL : 1];
+  if (PREROWS && !a.first) {
+    const int m0 = min(RMAX, nrow);
+#pragma unroll
+    for (int u = 0; u < PRL; ++u) {
+      const int idx = tid + u * CONV_BLOCK;
+      if (idx < m0 * C4) {
+        const int i = idx / C4, j = (idx - i * C4) * 4;
+        const size_t o = (size_t)(r0 + i) * D + j;
+        if constexpr (PREROWS) {
+          ppo[u] = *reinterpret_cast<const float4*>(a.p_out + o);
+          ppx[u] = *reinterpret_cast<const float4*>(a.p_xin + o);
+        }
+      }
+    }
+  }
+
   // ---- stage: previous BN stats, CSR slice, node items, LapPE projection weight
   if (!a.first) {
     prev_bn_stats<D, CONV_BLOCK>(a.train, a.cred, a.sync ? a.p_nparts : Gn, a.sync ? a.p_part_all : a.p_part,
@@ -303,12 +339,11 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
                                  a.bn_mom, s_bn, s_bn + D, XO, LOG, g == 0);
   }
   if (fast) {
-    for (int i = tid; i <= nrow; i += CONV_BLOCK) iptr[i] = a.bt.in_ptr[r0 + i] - e_lo;
-    for (int k = tid; k < ne; k += CONV_BLOCK) isrc[k] = a.bt.in_src[e_lo + k] - r0;
-    for (int i = tid; i < nrow; i += CONV_BLOCK) {
-      const int k1 = a.bt.in_ptr[r0 + i + 1] - e_lo;
-      for (int k = a.bt.in_ptr[r0 + i] - e_lo; k < k1; ++k) edst[k] = i;
-    }
+    if (tid <= nrow) iptr[tid] = c_ip0 - e_lo;
+    if (tid < ne) isrc[tid] = c_src0 - r0;
+    if (tid + CONV_BLOCK < ne) isrc[tid + CONV_BLOCK] = c_src1 - r0;
+    if (tid < nrow)
+      for (int k = c_ip0 - e_lo; k < c_ip1 - e_lo; ++k) edst[k] = tid;
   }
   if (pe_lds) {  // LapPE projection weight [D][KPE], zero-padded past pe_k
     for (int idx = tid; idx < D * KPE; idx += CONV_BLOCK) {
@@ -316,9 +351,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
       PEs[idx] = k < a.pe_k ? a.wpe[j * a.pe_k + k] : 0.0f;
     }
   }
-  if (a.first) {
-    for (int i = tid; i < min(RMAX, nrow); i += CONV_BLOCK) items[i] = a.bt.node_item[r0 + i];
-  }
+  if (a.first && tid < min(RMAX, nrow)) items[tid] = c_item;
   __syncthreads();
   GTR_PH(a.layer, 1);
 
@@ -332,8 +365,10 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
     }
     // layer input rows, float4 per thread: item row + LapPE projection (layer 0) or
     // drop(bn(prev out) + prev in) (layers >= 1); both global gathers of a row in flight together
-    constexpr int C4 = D / 4;
-    for (int idx = tid; idx < m * C4; idx += CONV_BLOCK) {
+#pragma unroll(PREROWS ? PRL : 1)
+    for (int u = 0; u < PRL; ++u) {  // m <= RMAX: at most PRL float4 per thread
+      const int idx = tid + u * CONV_BLOCK;
+      if (idx >= m * C4) break;
       const int i = idx / C4, j = (idx - i * C4) * 4;
       const int r = rc + i;
       const size_t o = (size_t)r * D + j;
@@ -368,8 +403,15 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
           val.w = val.w + (acc[3] + a.bpe[j + 3]);
         }
       } else {
-        const float4 po = *reinterpret_cast<const float4*>(a.p_out + o);
-        const float4 px = *reinterpret_cast<const float4*>(a.p_xin + o);
+        float4 po, px;
+        if constexpr (PREROWS) {
+          const bool pre = rc == r0;
+          po = pre ? ppo[u] : *reinterpret_cast<const float4*>(a.p_out + o);
+          px = pre ? ppx[u] : *reinterpret_cast<const float4*>(a.p_xin + o);
+        } else {
+          po = *reinterpret_cast<const float4*>(a.p_out + o);
+          px = *reinterpret_cast<const float4*>(a.p_xin + o);
+        }
         const float4 pg = *reinterpret_cast<const float4*>(a.p_gamma + j);
         const float4 pb = *reinterpret_cast<const float4*>(a.p_beta + j);
         const float4 mu = *reinterpret_cast<const float4*>(s_bn + j);
@@ -756,6 +798,23 @@ __device__ __forceinline__ void readout_body(const ReadoutK& a, int rb) {
   const float inv_t = 1.0f / a.temperature;
   const int nchunk = do_loss ? (n + CHN - 1) / CHN : 0;
 
+  // scoring rows of the block's next session (chunk 0: target + first CHN negatives),
+  // requested before anything that waits: they depend only on the batch, so the first
+  // session's gathers overlap the prologue's BatchNorm reduction
+  float tv[VPL], rv[KR][VPL], sk[KR];
+  auto issue = [&](int b) {
+    if (!do_loss || b >= B) return;
+    const int* ng = a.bt.negatives + (size_t)b * n;
+    load_vec<VPL>(tv, a.table + (size_t)a.bt.target[b] * D + d0, act);
+    const int kq = wave + lane * RO_WAVES;
+    const int nid = (lane < KR && kq < n) ? ng[kq] : 0;
+#pragma unroll
+    for (int q = 0; q < KR; ++q) {
+      const int id = __shfl(nid, q);
+      if (wave + q * RO_WAVES < n) load_vec<VPL>(rv[q], a.table + (size_t)id * D + d0, act);
+    }
+  };
+  issue(rb);
   if (do_fwd) {
     prev_bn_stats<D, RO_BLOCK>(a.train, a.cred, a.sync ? a.nparts : a.bt.hdr[4], a.sync ? a.part_all : a.part,
                                a.stats, a.rmean, a.rvar, a.nbt, a.bn_eps,
@@ -783,18 +842,7 @@ __device__ __forceinline__ void readout_body(const ReadoutK& a, int rb) {
     const int n0 = a.bt.node_ptr[b], n1 = a.bt.node_ptr[b + 1];
     const float cnt = (float)(n1 - n0);
     const int* negs = a.bt.negatives + (size_t)b * n;
-    // ---- (1) scoring rows of chunk 0 requested first (independent of the embedding)
-    float tv[VPL], rv[KR][VPL], sk[KR];
-    if (do_loss) {
-      load_vec<VPL>(tv, a.table + (size_t)a.bt.target[b] * D + d0, act);
-      const int kq = wave + lane * RO_WAVES;
-      const int nid = (lane < KR && kq < n) ? negs[kq] : 0;
-#pragma unroll
-      for (int q = 0; q < KR; ++q) {
-        const int id = __shfl(nid, q);
-        if (wave + q * RO_WAVES < n) load_vec<VPL>(rv[q], a.table + (size_t)id * D + d0, act);
-      }
-    }
+    // ---- (1) scoring rows of chunk 0: requested by issue() before this iteration
     // ---- (2) session embedding: mean over node rows of drop(bn(out) + xin)
     float se[VPL];
     constexpr int NBR = 2;  // node rows per wave whose conv output stays in registers for (5)
@@ -993,6 +1041,7 @@ __device__ __forceinline__ void readout_body(const ReadoutK& a, int rb) {
         store_vec<VPL>(a.dy + (size_t)i * D + d0, dyv, act);
       }
     }
+    issue(b + a.main_grid);  // the next session's rows (rv / tv are free from here)
   }
 
   GTR_PH(16, 2);

@@ -142,10 +142,30 @@ __device__ __forceinline__ void bn_fold_parts_(const float* part, int G, float e
   float* s_sum = scr;              // [NSL][D]
   float* s_n = scr + NSL * D;      // [NSL][D] (the count repeated per feature)
   float* s_mu = scr + 2 * NSL * D; // [D]
+  // the slice's first QR rows are loaded whole (count, mean, M2) in one round trip and
+  // kept in registers for the M2 pass (same summation order as re-reading them)
+  constexpr int QR = (32 + NSL - 1) / NSL < 8 ? (32 + NSL - 1) / NSL : 8;
+  float rc[QR], rmu[QR], rm2[QR];
   if (sl < NSL) {
+#pragma unroll
+    for (int u = 0; u < QR; ++u) {
+      const int q = sl + u * NSL;
+      if (q < G) {
+        const float* pp = part + (size_t)q * rstride;
+        rc[u] = pp[0];
+        rmu[u] = pp[1 + j];
+        rm2[u] = pp[1 + D + j];
+      }
+    }
     float n = 0.0f, sum = 0.0f;
+#pragma unroll
+    for (int u = 0; u < QR; ++u)
+      if (sl + u * NSL < G) {
+        n += rc[u];
+        sum += rc[u] * rmu[u];
+      }
 #pragma unroll 8
-    for (int q = sl; q < G; q += NSL) {
+    for (int q = sl + QR * NSL; q < G; q += NSL) {
       const float* pp = part + (size_t)q * rstride;
       const float c = pp[0];
       n += c;
@@ -164,8 +184,14 @@ __device__ __forceinline__ void bn_fold_parts_(const float* part, int G, float e
   if (sl < NSL) {
     const float mean = s_mu[j];
     float m2 = 0.0f;
+#pragma unroll
+    for (int u = 0; u < QR; ++u)
+      if (sl + u * NSL < G) {
+        const float d = rmu[u] - mean;
+        m2 += rm2[u] + rc[u] * d * d;
+      }
 #pragma unroll 8
-    for (int q = sl; q < G; q += NSL) {
+    for (int q = sl + QR * NSL; q < G; q += NSL) {
       const float* pp = part + (size_t)q * rstride;
       const float d = pp[1 + j] - mean;
       m2 += pp[1 + D + j] + pp[0] * d * d;

@@ -34,7 +34,10 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--config", default="c2")
     ap.add_argument("--batch-size", type=int, default=32)
+    ap.add_argument("--out", default=None, help="also save the raw stamps (npz)")
     args = ap.parse_args()
+    # stamps are indexed by hardware block: keep row group g on block g (no XCD packing)
+    os.environ.setdefault("GTR_XCD_PACK", "0")
     dev = torch.device("cuda", 0)
     sys.path.insert(0, ROOT)
     import bench
@@ -54,6 +57,7 @@ def main():
         step.run()
     torch.cuda.synchronize()
     rows = {}
+    detail = {}
     for i in range(args.steps):
         b = staged[i % len(staged)]
         step.load_blob(b)
@@ -63,7 +67,7 @@ def main():
         assert h.gtr_dbg_fwd_phases(fwd.ctypes.data, fwd.nbytes) == 0
         assert h.gtr_dbg_bwd_phases(bwd.ctypes.data, bwd.nbytes) == 0
         t_ref = int(fwd[0, :Gn, 0].min())
-        ro_grid = max(1, min((caps.b_cap + 3) // 4, 256))
+        ro_grid = max(1, min(caps.b_cap, 256))  # gtr_readout_grid
         for arr, names, nph, kind in ((fwd, FWD_NAMES, 5, "f"), (bwd, BWD_NAMES, 5, "b")):
             for kid, name in names.items():
                 ng = ro_grid if kid == 16 else Gn
@@ -79,6 +83,16 @@ def main():
                 rec["span"].append((end.max() - start.min()) * 10e-3)
                 rec["skew"].append((start.max() - start.min()) * 10e-3)
                 rec["ph"].append(np.diff(st, axis=1).mean(0) * 10e-3)
+                if kind == "f" and kid != 16:
+                    cols = [0, 10, 1, 11, 2, 5, 8, 3, 4]
+                    sub = arr[kid, :ng][:, cols].astype(np.int64)
+                    detail.setdefault(name, []).append(np.diff(sub, axis=1).mean(0) * 10e-3)
+    if detail:  # forward sub-phases from the fast path's extra stamps
+        seq = [(0, "ranges"), (10, "csr+bn"), (1, "rows"), (11, "mfma"), (2, "logits"), (5, "softmax"), (8, "agg+gate"),
+               (3, "bnpart"), (4, None)]
+        for name, d in detail.items():
+            m = np.median(np.stack(d), axis=0)
+            print(f"{name:14s} detail: " + " ".join(f"{seq[i][1]}={m[i]:.2f}" for i in range(len(seq) - 1)))
     print(f"{'kernel':14s} {'begin_us':>9s} {'span_us':>8s} {'skew_us':>8s}  phases (mean us per workgroup)")
     order = sorted(rows, key=lambda n: np.median(rows[n]["begin"]))
     for name in order:
