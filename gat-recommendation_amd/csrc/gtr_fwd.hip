@@ -19,6 +19,10 @@
 #include "gtr_layer.cuh"
 #include "gtr_rows.cuh"
 
+#ifndef GTR_WPRE_MAXD
+#define GTR_WPRE_MAXD 64  // widths whose projection weights are prefetched whole (per wave); 128 measured slower
+#endif
+
 namespace {
 
 using namespace gtr;
@@ -277,10 +281,13 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
     if (tid + CONV_BLOCK < ne) c_src1 = a.bt.in_src[e_lo + tid + CONV_BLOCK];
   }
   if (a.first && tid < min(RMAX, nrow)) c_item = a.bt.node_item[r0 + tid];
+  GTR_PH(a.layer, 12);
 
   // ---- W fragments of this wave's first column tiles and the gate weights, issued
   //      early so the weight fetch overlaps the staging round trip
-  constexpr int PRE = D <= 64 ? (NCT / CONV_WAVES) : 1;
+  // every column tile of the wave prefetched up to D = GTR_WPRE_MAXD; beyond, one tile ahead
+  // (D = 128 with all 4 tiles held, 128 VGPRs: C3 0.1398 -> 0.1436 ms per step)
+  constexpr int PRE = D <= GTR_WPRE_MAXD ? (NCT / CONV_WAVES) : 1;
   float4 wpre[PRE][D / 16];
 #pragma unroll
   for (int pi = 0; pi < PRE; ++pi) {
@@ -310,6 +317,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
     load_vec<VPL>(w3, a.w_beta + 2 * D + d0, act);
   }
 
+  GTR_PH(a.layer, 13);
   // ---- layers >= 1: the first chunk's previous-layer rows (out, xin) requested now, so they
   //      arrive while the BatchNorm partials are reduced and the CSR slice is staged
   constexpr int C4 = D / 4;
@@ -338,6 +346,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
                                  a.p_stats, a.p_rmean, a.p_rvar, a.p_nbt, a.bn_eps,
                                  a.bn_mom, s_bn, s_bn + D, XO, LOG, g == 0);
   }
+  GTR_PH(a.layer, 14);
   if (fast) {
     if (tid <= nrow) iptr[tid] = c_ip0 - e_lo;
     if (tid < ne) isrc[tid] = c_src0 - r0;
@@ -352,6 +361,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
     }
   }
   if (a.first && tid < min(RMAX, nrow)) items[tid] = c_item;
+  GTR_PH(a.layer, 15);
   __syncthreads();
   GTR_PH(a.layer, 1);
 

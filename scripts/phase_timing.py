@@ -84,11 +84,11 @@ def main():
                 rec["skew"].append((start.max() - start.min()) * 10e-3)
                 rec["ph"].append(np.diff(st, axis=1).mean(0) * 10e-3)
                 if kind == "f" and kid != 16:
-                    cols = [0, 10, 1, 11, 2, 5, 8, 3, 4]
+                    cols = [0, 10, 12, 13, 14, 15, 1, 11, 2, 5, 8, 3, 4]
                     sub = arr[kid, :ng][:, cols].astype(np.int64)
                     detail.setdefault(name, []).append(np.diff(sub, axis=1).mean(0) * 10e-3)
     if detail:  # forward sub-phases from the fast path's extra stamps
-        seq = [(0, "ranges"), (10, "csr+bn"), (1, "rows"), (11, "mfma"), (2, "logits"), (5, "softmax"), (8, "agg+gate"),
+        seq = [(0, "ranges"), (10, "csr_ld"), (12, "w_ld"), (13, "rows_ld"), (14, "bn+csr_st"), (15, "sync"), (1, "rows"), (11, "mfma"), (2, "logits"), (5, "softmax"), (8, "agg+gate"),
                (3, "bnpart"), (4, None)]
         for name, d in detail.items():
             m = np.median(np.stack(d), axis=0)

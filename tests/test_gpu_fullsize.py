@@ -91,15 +91,21 @@ def _train_and_compare(m, ref, fused, batches, kind, lr, dropout=0.0, also=()):
     rounding differs between any two summation orders -- into an update that differs by
     a fraction of lr): there the HIP value may deviate from fp32 by at most 8 times the
     fp32 oracle's own distance to fp64, or at most the fp32 oracle's worst distance to fp64
-    anywhere in the same tensor from fp64 itself.  Elements whose first gradient is at the fp32
-    noise floor are bounded by 2 lr per step (see the module docstring)."""
+    anywhere in the same tensor from fp64 itself.  The fp32 oracle runs in two summation
+    orders (the box's CPU threads, and one thread) and the larger of its two distances to
+    fp64 is the element's fp32 noise: one order can land on fp64 by chance where a nearly
+    cancelling gradient makes the element sensitive (C3: one table element of 1.9M moved
+    1.3e-6 between the fp32 oracle on 16 and 8 threads).  Elements whose first gradient is
+    at the fp32 noise floor are bounded by 2 lr per step (see the module docstring)."""
     import copy
 
+    ref1 = copy.deepcopy(ref)  # fp32, one CPU thread: a second summation order
     ref64 = copy.deepcopy(ref).double()
     if getattr(ref64, "laplacian_pe", None) is not None and ref64.laplacian_pe._cached_pe is not None:
         ref64.laplacian_pe._cached_pe = ref64.laplacian_pe._cached_pe.double()
     ropt = torch.optim.AdamW(ref.parameters(), lr=lr, weight_decay=1e-5)
     ropt64 = torch.optim.AdamW(ref64.parameters(), lr=lr, weight_decay=1e-5)
+    ropt1 = torch.optim.AdamW(ref1.parameters(), lr=lr, weight_decay=1e-5)
     seen = {n: torch.zeros_like(p, dtype=torch.bool) for n, p in ref.named_parameters()}
     noise = {n: torch.zeros_like(p, dtype=torch.bool) for n, p in ref.named_parameters()}
     steps = 0
@@ -114,6 +120,12 @@ def _train_and_compare(m, ref, fused, batches, kind, lr, dropout=0.0, also=()):
         rb = R.ref_batch_from(sb)
         rloss, rse = _ref_step(ref, rb, ropt, kind, masks)
         _, rse64 = _ref_step(ref64, rb, ropt64, kind, masks)
+        nthr = torch.get_num_threads()
+        torch.set_num_threads(1)
+        try:
+            _, rse1 = _ref_step(ref1, rb, ropt1, kind, masks)
+        finally:
+            torch.set_num_threads(nthr)
         steps += 1
         assert abs(loss - rloss) <= 1e-3 * abs(rloss), (steps, loss, rloss)
         for o in other:
@@ -130,12 +142,13 @@ def _train_and_compare(m, ref, fused, batches, kind, lr, dropout=0.0, also=()):
     # the last step's forward runs on parameters that noise-driven first updates moved
     # (see above): held to the same fp32-or-own-fp64-distance bar as the parameters
     _close_trained(fused.ws.se[:B].detach().cpu(), rse, rse64, torch.zeros_like(rse, dtype=torch.bool), 0.0,
-                   "session embeddings (last step)")
+                   "session embeddings (last step)", rse1)
     touched = torch.zeros(ref.item_embedding.weight.shape[0], dtype=torch.bool)
     for sb in batches:
         for t in (sb.x, sb.target_item, sb.negative_items):
             touched[t.reshape(-1)] = True
     p64 = dict(ref64.named_parameters())
+    p1 = dict(ref1.named_parameters())
     for model, _ in [(m, fused)] + list(also):
         hp = dict(model.named_parameters())
         model.state_dict()  # state access flushes a lazy table first
@@ -143,38 +156,45 @@ def _train_and_compare(m, ref, fused, batches, kind, lr, dropout=0.0, also=()):
             a = hp[n].detach().cpu()
             b = p.detach()
             c = p64[n].detach()
+            b1 = p1[n].detach()
             allow = noise[n]
             if n == "item_embedding.weight":
                 _close_trained(a[touched], b[touched], c[touched], allow[touched], 2 * lr * steps,
-                               f"{n} touched rows ({int(touched.sum())})")
+                               f"{n} touched rows ({int(touched.sum())})", b1[touched])
                 assert_close(a[~touched], b[~touched], name=f"{n} untouched rows ({int((~touched).sum())})")
             else:
-                _close_trained(a, b, c, allow, 2 * lr * steps, n)
+                _close_trained(a, b, c, allow, 2 * lr * steps, n, b1)
         bufs = dict(model.named_buffers())
         b64 = dict(ref64.named_buffers())
+        bb1 = dict(ref1.named_buffers())
         for n, b in ref.named_buffers():
             if "running" in n:  # batch statistics of forwards on the trained parameters
-                _close_trained(bufs[n].detach().cpu(), b, b64[n], torch.zeros_like(b, dtype=torch.bool), 0.0, n)
+                _close_trained(bufs[n].detach().cpu(), b, b64[n], torch.zeros_like(b, dtype=torch.bool), 0.0, n,
+                               bb1[n])
             if n.endswith("num_batches_tracked"):
                 assert int(bufs[n]) == steps
     return steps
 
 
-def _close_trained(a, b, c, allow, bound, name):
-    """a: HIP, b: fp32 oracle, c: fp64 oracle (see _train_and_compare)."""
+def _close_trained(a, b, c, allow, bound, name, b1=None):
+    """a: HIP, b: fp32 oracle, c: fp64 oracle, b1: fp32 oracle in a second summation order
+    (see _train_and_compare)."""
     if bool(allow.any()):
         assert float((a[allow] - b[allow]).abs().max()) <= bound + 1e-7, name
     keep = ~allow
     a, b, c = a[keep], b[keep], c[keep].float()
+    dev = (b - c).abs()
+    if b1 is not None:
+        dev = torch.maximum(dev, (b1.detach()[keep] - c).abs())
     scale = float(b.abs().max()) if b.numel() else 0.0
-    tol = 1e-3 * (b.abs() + 1e-2 * scale) + 8 * (b - c).abs() + 1e-12
+    tol = 1e-3 * (b.abs() + 1e-2 * scale) + 8 * dev + 1e-12
     err = (a - b).abs()
     # fp32 noise level of the tensor: the worst distance of the fp32 oracle itself from the
     # fp64 oracle anywhere in it.  An element that misses the elementwise bar above is still
     # accepted when the HIP value is no further from the fp64 result than that (a gradient
     # that nearly cancels is rounded differently by any two fp32 summation orders, and the
     # fp32 oracle can land close to fp64 on that element by chance).
-    floor = float((b - c).abs().max()) if b.numel() else 0.0
+    floor = float(dev.max()) if b.numel() else 0.0
     near = err > tol
     bad = near & ((a - c).abs() > floor)
     if bool(bad.any()):
