@@ -212,7 +212,7 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
   const int H = a.H, C = a.C;
   const int ne = e_hi - e_lo;
   const bool fast = G::KV && nrow <= RMAX && ne <= G::EMAX && ne * H <= G::EH && H <= 8 && C >= CH;
-  const uint32_t ctr = a.rng_ctr ? *a.rng_ctr + a.ctr_add : 0u;
+  const uint32_t ctr = a.rng_ctr ? load_step_ctr(a.rng_ctr) + a.ctr_add : 0u;
   const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
   const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
   const float invN = 1.0f / (float)N;
@@ -259,23 +259,58 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
   if (!fast) reduce_gsum();
 
   if (fast) {
-    // ---- stage: CSR slices (by destination and by source), alpha, K | V | Q rows
-    for (int i = tid; i <= nrow; i += CONV_BLOCK) {
-      iptr[i] = a.bt.in_ptr[r0 + i] - e_lo;
-      optr[i] = a.bt.out_ptr[r0 + i] - o_lo;
+    // ---- stage: CSR slices (by destination and by source), alpha, K | V | Q rows.  Each
+    //      thread's first element of every array is loaded into registers before any LDS
+    //      store (a store waits for its load and vector loads retire in order: one round
+    //      trip for the stage instead of one per array); elements past CONV_BLOCK (groups
+    //      with > 512 edges, (edge, head) pairs or row float4s) follow in plain loops.
+    int s_ip = 0, s_ip1 = 0, s_op = 0, s_is = 0, s_oe = 0, s_od = 0;
+    float s_al = 0.0f;
+    float4 s_k = make_float4(0.f, 0.f, 0.f, 0.f), s_v = s_k, s_q = s_k;
+    constexpr int C4 = D / 4;
+    const int i0 = tid / C4, c0 = (tid - i0 * C4) * 4;
+    if (tid <= nrow) {
+      s_ip = a.bt.in_ptr[r0 + tid];
+      s_op = a.bt.out_ptr[r0 + tid];
     }
-    for (int i = tid; i < nrow; i += CONV_BLOCK) {
-      const int k1 = a.bt.in_ptr[r0 + i + 1] - e_lo;
-      for (int k = a.bt.in_ptr[r0 + i] - e_lo; k < k1; ++k) edst[k] = i;
+    if (tid < nrow) s_ip1 = a.bt.in_ptr[r0 + tid + 1];
+    if (tid < ne) {
+      s_is = a.bt.in_src[e_lo + tid];
+      s_oe = a.bt.out_edge[o_lo + tid];
+      s_od = a.bt.out_dst[o_lo + tid];
     }
-    for (int k = tid; k < ne; k += CONV_BLOCK) {
+    if (tid < ne * H) s_al = a.alpha[(size_t)e_lo * H + tid];
+    if (tid < nrow * C4) {
+      const float* src = a.qkvs + (size_t)(r0 + i0) * (4 * D);
+      s_k = *reinterpret_cast<const float4*>(src + D + c0);
+      s_v = *reinterpret_cast<const float4*>(src + 2 * D + c0);
+      s_q = *reinterpret_cast<const float4*>(src + c0);
+    }
+    if (tid <= nrow) {
+      iptr[tid] = s_ip - e_lo;
+      optr[tid] = s_op - o_lo;
+    }
+    if (tid < nrow)
+      for (int k = s_ip - e_lo; k < s_ip1 - e_lo; ++k) edst[k] = tid;
+    if (tid < ne) {
+      isrc[tid] = s_is - r0;
+      oedge[tid] = s_oe - e_lo;
+      odst[tid] = s_od - r0;
+    }
+    if (tid < ne * H) AL[tid] = s_al;
+    if (tid < nrow * C4) {
+      *reinterpret_cast<float4*>(Ks + i0 * XS + c0) = s_k;
+      *reinterpret_cast<float4*>(Vs + i0 * XS + c0) = s_v;
+      *reinterpret_cast<float4*>(Qs + i0 * XS + c0) = s_q;
+    }
+    for (int k = tid + CONV_BLOCK; k < ne; k += CONV_BLOCK) {
       isrc[k] = a.bt.in_src[e_lo + k] - r0;
       oedge[k] = a.bt.out_edge[o_lo + k] - e_lo;
       odst[k] = a.bt.out_dst[o_lo + k] - r0;
     }
-    for (int k = tid; k < ne * H; k += CONV_BLOCK) AL[k] = a.alpha[(size_t)e_lo * H + k];
-    for (int idx = tid; idx < nrow * (D / 4); idx += CONV_BLOCK) {
-      const int i = idx / (D / 4), c = (idx - i * (D / 4)) * 4;
+    for (int k = tid + CONV_BLOCK; k < ne * H; k += CONV_BLOCK) AL[k] = a.alpha[(size_t)e_lo * H + k];
+    for (int idx = tid + CONV_BLOCK; idx < nrow * C4; idx += CONV_BLOCK) {
+      const int i = idx / C4, c = (idx - i * C4) * 4;
       const float* src = a.qkvs + (size_t)(r0 + i) * (4 * D);
       *reinterpret_cast<float4*>(Ks + i * XS + c) = *reinterpret_cast<const float4*>(src + D + c);
       *reinterpret_cast<float4*>(Vs + i * XS + c) = *reinterpret_cast<const float4*>(src + 2 * D + c);

@@ -68,6 +68,14 @@ __device__ __forceinline__ uint32_t drop_stream(uint32_t kind, uint32_t layer, u
   return (kind << 28) ^ (layer << 20) ^ (ctr * 0x632BE5ABu);
 }
 
+// The step's dropout counter, read through the scalar (constant) path: it is written only
+// by the step tail / counter kernels, never during the kernels that read it, and a scalar
+// load waits on its own counter (lgkmcnt) instead of joining the in-order vector-load queue
+// ahead of the staging loads.
+__device__ __forceinline__ uint32_t load_step_ctr(const uint32_t* p) {
+  return *(const __attribute__((address_space(4))) uint32_t*)p;
+}
+
 struct Drop {
   uint32_t seed, thresh;
   float scale;

@@ -82,14 +82,16 @@ struct ConvFwdK {
 template <int D, int BLK>
 __device__ __forceinline__ void prev_bn_stats(int train, int cred, int G, const float* part, float* stats,
                                               float* rmean, float* rvar, int64_t* nbt, float eps, float mom,
-                                              float* s_mean, float* s_rstd, float* s_uvar, float* scr, bool lead) {
+                                              float* s_mean, float* s_rstd, float* s_uvar, float* scr, bool lead,
+                                              bool have_pre, const BnParts<D, BLK>& pre) {
   if (!train) {
     for (int j = threadIdx.x; j < D; j += BLK) {
       s_mean[j] = rmean[j];
       s_rstd[j] = 1.0f / sqrtf(rvar[j] + eps);
     }
   } else if (cred) {
-    bn_stats_from_parts<D, BLK>(part, G, eps, s_mean, s_rstd, s_uvar, scr);
+    if (have_pre) bn_stats_from_loaded<D, BLK>(part, G, eps, s_mean, s_rstd, s_uvar, scr, pre);
+    else bn_stats_from_parts<D, BLK>(part, G, eps, s_mean, s_rstd, s_uvar, scr);
     if (lead) {
       for (int j = threadIdx.x; j < D; j += BLK) {
         stats[j] = s_mean[j];
@@ -241,6 +243,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
   int* s_flag = reinterpret_cast<int*>(sm + G::F_FLAG);
   __bf16* XH = reinterpret_cast<__bf16*>(sm + G::F_XH);
   __bf16* XL = reinterpret_cast<__bf16*>(sm + G::F_XL);
+  float* WB = sm + G::F_WB;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   GTR_PH(a.layer, 0);
@@ -260,7 +263,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
   // every thread's CH-feature chunk lies inside one head
   const bool fast = G::KV && nrow <= RMAX && ne <= G::EMAX && ne * a.H <= G::EH && a.H <= 8 && a.C >= CH;
   if (fast) GTR_PH(a.layer, 10);
-  const uint32_t ctr = a.rng_ctr ? *a.rng_ctr + a.ctr_add : 0u;
+  const uint32_t ctr = a.rng_ctr ? load_step_ctr(a.rng_ctr) + a.ctr_add : 0u;
   const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
   const bool pe_lds = a.first && a.pe_k > 0 && a.pe_k <= KPE;
   const int lr = lane & 15, lg = lane >> 4;
@@ -281,6 +284,21 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
     if (tid + CONV_BLOCK < ne) c_src1 = a.bt.in_src[e_lo + tid + CONV_BLOCK];
   }
   if (a.first && tid < min(RMAX, nrow)) c_item = a.bt.node_item[r0 + tid];
+  float4 c_wb = make_float4(0.f, 0.f, 0.f, 0.f);  // gate weights [w1 | w2 | w3] -> LDS (fast path)
+  if (fast && tid < (3 * D) / 4) c_wb = *reinterpret_cast<const float4*>(a.w_beta + 4 * tid);
+  // layers >= 1, consumer-side BatchNorm: the previous layer's partial rows, also before the
+  // weights (the reduction consumes them first)
+  const bool pre_bn = !a.first && a.train && a.cred;
+  const int bn_G = a.sync ? a.p_nparts : Gn;
+  const float* bn_part = a.sync ? a.p_part_all : a.p_part;
+  BnParts<D, CONV_BLOCK> bnr;
+  if (pre_bn) bn_parts_load<D, CONV_BLOCK>(bn_part, bn_G, 1 + 2 * D, bnr);
+  if (pe_lds) {  // LapPE projection weight [D][KPE], zero-padded past pe_k (stored right away)
+    for (int idx = tid; idx < D * KPE; idx += CONV_BLOCK) {
+      const int j = idx / KPE, k = idx - j * KPE;
+      PEs[idx] = k < a.pe_k ? a.wpe[j * a.pe_k + k] : 0.0f;
+    }
+  }
   GTR_PH(a.layer, 12);
 
   // ---- W fragments of this wave's first column tiles and the gate weights, issued
@@ -296,26 +314,10 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
     for (int kb = 0; kb < D / 16; ++kb)
       wpre[pi][kb] = *reinterpret_cast<const float4*>(wrow + wfrag_off(kb, lg, SPLIT));
   }
-  // gate weights: the row-parallel fast path holds this thread's CH-feature chunk,
-  // the wave-per-row general path VPL features per lane
+  // gate weights: the row-parallel fast path reads its thread's CH-feature chunk from the
+  // LDS copy (one 3D-float load per workgroup instead of one per thread); the wave-per-row
+  // general path loads VPL features per lane right before its attention loop
   const int prow = tid / TPR, pchunk = tid - prow * TPR, f0 = pchunk * CH;
-  float w1c[CH], w2c[CH], w3c[CH];
-  float w1[VPL], w2[VPL], w3[VPL];
-  if (fast) {
-#pragma unroll
-    for (int c = 0; c < CH; c += 4) {
-      const float4 x1 = *reinterpret_cast<const float4*>(a.w_beta + f0 + c);
-      const float4 x2 = *reinterpret_cast<const float4*>(a.w_beta + D + f0 + c);
-      const float4 x3 = *reinterpret_cast<const float4*>(a.w_beta + 2 * D + f0 + c);
-      w1c[c] = x1.x; w1c[c + 1] = x1.y; w1c[c + 2] = x1.z; w1c[c + 3] = x1.w;
-      w2c[c] = x2.x; w2c[c + 1] = x2.y; w2c[c + 2] = x2.z; w2c[c + 3] = x2.w;
-      w3c[c] = x3.x; w3c[c + 1] = x3.y; w3c[c + 2] = x3.z; w3c[c + 3] = x3.w;
-    }
-  } else {
-    load_vec<VPL>(w1, a.w_beta + d0, act);
-    load_vec<VPL>(w2, a.w_beta + D + d0, act);
-    load_vec<VPL>(w3, a.w_beta + 2 * D + d0, act);
-  }
 
   GTR_PH(a.layer, 13);
   // ---- layers >= 1: the first chunk's previous-layer rows (out, xin) requested now, so they
@@ -342,9 +344,8 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
 
   // ---- stage: previous BN stats, CSR slice, node items, LapPE projection weight
   if (!a.first) {
-    prev_bn_stats<D, CONV_BLOCK>(a.train, a.cred, a.sync ? a.p_nparts : Gn, a.sync ? a.p_part_all : a.p_part,
-                                 a.p_stats, a.p_rmean, a.p_rvar, a.p_nbt, a.bn_eps,
-                                 a.bn_mom, s_bn, s_bn + D, XO, LOG, g == 0);
+    prev_bn_stats<D, CONV_BLOCK>(a.train, a.cred, bn_G, bn_part, a.p_stats, a.p_rmean, a.p_rvar, a.p_nbt,
+                                 a.bn_eps, a.bn_mom, s_bn, s_bn + D, XO, LOG, g == 0, pre_bn, bnr);
   }
   GTR_PH(a.layer, 14);
   if (fast) {
@@ -354,13 +355,8 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
     if (tid < nrow)
       for (int k = c_ip0 - e_lo; k < c_ip1 - e_lo; ++k) edst[k] = tid;
   }
-  if (pe_lds) {  // LapPE projection weight [D][KPE], zero-padded past pe_k
-    for (int idx = tid; idx < D * KPE; idx += CONV_BLOCK) {
-      const int j = idx / KPE, k = idx - j * KPE;
-      PEs[idx] = k < a.pe_k ? a.wpe[j * a.pe_k + k] : 0.0f;
-    }
-  }
   if (a.first && tid < min(RMAX, nrow)) items[tid] = c_item;
+  if (fast && tid < (3 * D) / 4) *reinterpret_cast<float4*>(WB + 4 * tid) = c_wb;
   GTR_PH(a.layer, 15);
   __syncthreads();
   GTR_PH(a.layer, 1);
@@ -375,7 +371,8 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
     }
     // layer input rows, float4 per thread: item row + LapPE projection (layer 0) or
     // drop(bn(prev out) + prev in) (layers >= 1); both global gathers of a row in flight together
-#pragma unroll(PREROWS ? PRL : 1)
+    constexpr int PRU = PREROWS ? PRL : 1;
+#pragma unroll PRU
     for (int u = 0; u < PRL; ++u) {  // m <= RMAX: at most PRL float4 per thread
       const int idx = tid + u * CONV_BLOCK;
       if (idx >= m * C4) break;
@@ -620,7 +617,8 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
         sv[c] = v.x; sv[c + 1] = v.y; sv[c + 2] = v.z; sv[c + 3] = v.w;
       }
 #pragma unroll
-      for (int c = 0; c < CH; ++c) u += w1c[c] * ag[c] + w2c[c] * sv[c] + w3c[c] * (ag[c] - sv[c]);
+      for (int c = 0; c < CH; ++c)
+        u += WB[f0 + c] * ag[c] + WB[D + f0 + c] * sv[c] + WB[2 * D + f0 + c] * (ag[c] - sv[c]);
     }
 #pragma unroll
     for (int o = 1; o < TPR; o <<= 1) u += __shfl_xor(u, o);
@@ -641,6 +639,10 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
       if (pchunk == 0) a.gate[r0 + grow] = beta;
     }
   } else {
+    float w1[VPL], w2[VPL], w3[VPL];
+    load_vec<VPL>(w1, a.w_beta + d0, act);
+    load_vec<VPL>(w2, a.w_beta + D + d0, act);
+    load_vec<VPL>(w3, a.w_beta + 2 * D + d0, act);
     for (int t = r0 + wave; t < r1; t += CONV_WAVES)
       attn_row<D>(a, t, t, a.qkvs, a.qkvs + 3 * D, a.qkvs + D, a.qkvs + 2 * D, 4 * D, a.bt.in_ptr, a.bt.in_src, 0,
                   lane, dr, st_attn, w1, w2, w3, nullptr);
@@ -795,7 +797,7 @@ __device__ __forceinline__ void readout_body(const ReadoutK& a, int rb) {
   const int n = a.bt.n_neg;
   const int d0 = lane * VPL;
   const bool act = d0 < D;
-  const uint32_t ctr = a.rng_ctr ? *a.rng_ctr + a.ctr_add : 0u;
+  const uint32_t ctr = a.rng_ctr ? load_step_ctr(a.rng_ctr) + a.ctr_add : 0u;
   const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
   const uint32_t st = drop_stream(1, (uint32_t)a.L1, ctr);
   const bool do_fwd = a.flags & GTR_RO_FWD, do_loss = a.flags & GTR_RO_LOSS, do_bwd = a.flags & GTR_RO_BWD;
@@ -824,11 +826,17 @@ __device__ __forceinline__ void readout_body(const ReadoutK& a, int rb) {
       if (wave + q * RO_WAVES < n) load_vec<VPL>(rv[q], a.table + (size_t)id * D + d0, act);
     }
   };
+  // consumer-side BatchNorm partials first (consumed first: vector loads retire in order)
+  const bool pre_bn = do_fwd && a.train && a.cred;
+  const int bn_G = a.sync ? a.nparts : a.bt.hdr[4];
+  const float* bn_part = a.sync ? a.part_all : a.part;
+  BnParts<D, RO_BLOCK> bnr;
+  if (pre_bn) bn_parts_load<D, RO_BLOCK>(bn_part, bn_G, 1 + 2 * D, bnr);
   issue(rb);
   if (do_fwd) {
-    prev_bn_stats<D, RO_BLOCK>(a.train, a.cred, a.sync ? a.nparts : a.bt.hdr[4], a.sync ? a.part_all : a.part,
+    prev_bn_stats<D, RO_BLOCK>(a.train, a.cred, bn_G, bn_part,
                                a.stats, a.rmean, a.rvar, a.nbt, a.bn_eps,
-                               a.bn_mom, s_bn, s_bn + D, s_bn + 2 * D, s_scr, rb == 0);
+                               a.bn_mom, s_bn, s_bn + D, s_bn + 2 * D, s_scr, rb == 0, pre_bn, bnr);
   } else if (do_bwd) {
     for (int j = tid; j < D; j += RO_BLOCK) { s_bn[j] = a.stats[j]; s_bn[D + j] = a.stats[D + j]; }
   }
@@ -1224,7 +1232,7 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
   const bool lead = (lane & 15) == 0;
   const int B = a.bt.hdr[1];
   const int n = a.bt.n_neg;
-  const uint32_t ctr = a.rng_ctr ? *a.rng_ctr + a.ctr_add : 0u;
+  const uint32_t ctr = a.rng_ctr ? load_step_ctr(a.rng_ctr) + a.ctr_add : 0u;
   const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
   const uint32_t st = drop_stream(1, (uint32_t)a.L1, ctr);
   const bool do_fwd = a.flags & GTR_RO_FWD, do_loss = a.flags & GTR_RO_LOSS, do_bwd = a.flags & GTR_RO_BWD;
@@ -1239,7 +1247,7 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
   if (do_fwd) {
     prev_bn_stats<D, RW_BLOCK>(a.train, a.cred, a.sync ? a.nparts : a.bt.hdr[4], a.sync ? a.part_all : a.part,
                                a.stats, a.rmean, a.rvar, a.nbt, a.bn_eps,
-                               a.bn_mom, s_bn, s_bn + D, s_bn + 2 * D, s_scr, rb == 0);
+                               a.bn_mom, s_bn, s_bn + D, s_bn + 2 * D, s_scr, rb == 0, false, BnParts<D, RW_BLOCK>{});
   } else if (do_bwd) {
     for (int j = tid; j < D; j += RW_BLOCK) { s_bn[j] = a.stats[j]; s_bn[D + j] = a.stats[D + j]; }
   }

@@ -40,7 +40,8 @@ struct LayerGeom {
   static constexpr int XSB = D + 8;                           // padded bf16 row (16B aligned)
   static constexpr int F_XH = F_FLAG + 4;                     // [RMAX][XSB] bf16 hi part of X rows
   static constexpr int F_XL = F_XH + RMAX * XSB / 2;          // [RMAX][XSB] bf16 lo part (split GEMM)
-  static constexpr int F_WORDS = F_XL + RMAX * XSB / 2;
+  static constexpr int F_WB = F_XL + RMAX * XSB / 2;          // [3D] gate weights w_beta (fast path)
+  static constexpr int F_WORDS = F_WB + 3 * D;
   // ---- backward LDS carve (4-byte words)
   static constexpr int B_RN = KV ? 4 * RMAX * XS : 0;
   static constexpr int B_R = 0;                               // [4][RMAX][XS] K | V | Q | dA rows
@@ -131,38 +132,54 @@ __device__ __forceinline__ void store_vec(float* p, const float (&x)[VPL], bool 
 // consumer_reduce = 0), gtr_layer.bn_part row b*GTR_PART_BUCKET therefore holds bucket
 // b's MERGED row, not group b*GTR_PART_BUCKET's partial: nothing may re-read bn_part
 // as per-group partials after such a forward.
-// scr: >= 2*BLK + D floats of LDS.  Call with the whole block.
+// The first QR partial rows of each slice, loaded whole (count, mean, M2) into registers
+// by bn_parts_load -- which a caller may issue early, before loads whose wait it must not
+// join (vector loads retire in order) -- and kept for both passes of bn_fold_parts_ (same
+// summation order as re-reading them).
 template <int D, int BLK>
-__device__ __forceinline__ void bn_fold_parts_(const float* part, int G, float eps, float* s_mean,
-                                               float* s_rstd, float* s_uvar, float* scr, size_t rstride,
-                                               float* merged) {
-  constexpr int NSL = BLK / D >= 1 ? BLK / D : 1;
+struct BnParts {
+  static constexpr int NSL = BLK / D >= 1 ? BLK / D : 1;
+  static constexpr int QR = (32 + NSL - 1) / NSL < 8 ? (32 + NSL - 1) / NSL : 8;
+  float rc[QR], rmu[QR], rm2[QR];
+};
+
+template <int D, int BLK>
+__device__ __forceinline__ void bn_parts_load(const float* part, int G, size_t rstride, BnParts<D, BLK>& r) {
+  constexpr int NSL = BnParts<D, BLK>::NSL, QR = BnParts<D, BLK>::QR;
   const int tid = threadIdx.x;
   const int j = tid % D, sl = tid / D;
-  float* s_sum = scr;              // [NSL][D]
-  float* s_n = scr + NSL * D;      // [NSL][D] (the count repeated per feature)
-  float* s_mu = scr + 2 * NSL * D; // [D]
-  // the slice's first QR rows are loaded whole (count, mean, M2) in one round trip and
-  // kept in registers for the M2 pass (same summation order as re-reading them)
-  constexpr int QR = (32 + NSL - 1) / NSL < 8 ? (32 + NSL - 1) / NSL : 8;
-  float rc[QR], rmu[QR], rm2[QR];
   if (sl < NSL) {
 #pragma unroll
     for (int u = 0; u < QR; ++u) {
       const int q = sl + u * NSL;
       if (q < G) {
         const float* pp = part + (size_t)q * rstride;
-        rc[u] = pp[0];
-        rmu[u] = pp[1 + j];
-        rm2[u] = pp[1 + D + j];
+        r.rc[u] = pp[0];
+        r.rmu[u] = pp[1 + j];
+        r.rm2[u] = pp[1 + D + j];
       }
     }
+  }
+}
+
+// scr: >= 2*BLK + D floats of LDS.  Call with the whole block, after bn_parts_load.
+template <int D, int BLK>
+__device__ __forceinline__ void bn_fold_parts_(const float* part, int G, float eps, float* s_mean,
+                                               float* s_rstd, float* s_uvar, float* scr, size_t rstride,
+                                               float* merged, const BnParts<D, BLK>& r) {
+  constexpr int NSL = BnParts<D, BLK>::NSL, QR = BnParts<D, BLK>::QR;
+  const int tid = threadIdx.x;
+  const int j = tid % D, sl = tid / D;
+  float* s_sum = scr;              // [NSL][D]
+  float* s_n = scr + NSL * D;      // [NSL][D] (the count repeated per feature)
+  float* s_mu = scr + 2 * NSL * D; // [D]
+  if (sl < NSL) {
     float n = 0.0f, sum = 0.0f;
 #pragma unroll
     for (int u = 0; u < QR; ++u)
       if (sl + u * NSL < G) {
-        n += rc[u];
-        sum += rc[u] * rmu[u];
+        n += r.rc[u];
+        sum += r.rc[u] * r.rmu[u];
       }
 #pragma unroll 8
     for (int q = sl + QR * NSL; q < G; q += NSL) {
@@ -187,8 +204,8 @@ __device__ __forceinline__ void bn_fold_parts_(const float* part, int G, float e
 #pragma unroll
     for (int u = 0; u < QR; ++u)
       if (sl + u * NSL < G) {
-        const float d = rmu[u] - mean;
-        m2 += rm2[u] + rc[u] * d * d;
+        const float d = r.rmu[u] - mean;
+        m2 += r.rm2[u] + r.rc[u] * d * d;
       }
 #pragma unroll 8
     for (int q = sl + QR * NSL; q < G; q += NSL) {
@@ -220,13 +237,25 @@ template <int D, int BLK>
 __device__ __forceinline__ void bn_stats_from_parts(const float* part, int G, float eps, float* s_mean,
                                                     float* s_rstd, float* s_uvar, float* scr,
                                                     size_t rstride = 1 + 2 * D) {
-  bn_fold_parts_<D, BLK>(part, G, eps, s_mean, s_rstd, s_uvar, scr, rstride, nullptr);
+  BnParts<D, BLK> r;
+  bn_parts_load<D, BLK>(part, G, rstride, r);
+  bn_fold_parts_<D, BLK>(part, G, eps, s_mean, s_rstd, s_uvar, scr, rstride, nullptr, r);
+}
+
+// The same with the partial rows already requested by bn_parts_load.
+template <int D, int BLK>
+__device__ __forceinline__ void bn_stats_from_loaded(const float* part, int G, float eps, float* s_mean,
+                                                     float* s_rstd, float* s_uvar, float* scr,
+                                                     const BnParts<D, BLK>& r, size_t rstride = 1 + 2 * D) {
+  bn_fold_parts_<D, BLK>(part, G, eps, s_mean, s_rstd, s_uvar, scr, rstride, nullptr, r);
 }
 
 template <int D, int BLK>
 __device__ __forceinline__ void bn_merge_parts(const float* part, int G, float* scr, size_t rstride,
                                                float* merged) {
-  bn_fold_parts_<D, BLK>(part, G, 0.0f, nullptr, nullptr, nullptr, scr, rstride, merged);
+  BnParts<D, BLK> r;
+  bn_parts_load<D, BLK>(part, G, rstride, r);
+  bn_fold_parts_<D, BLK>(part, G, 0.0f, nullptr, nullptr, nullptr, scr, rstride, merged, r);
 }
 
 // Row groups whose partials one last-arriving workgroup combines; past that the groups
