@@ -814,8 +814,17 @@ __device__ __forceinline__ void readout_body(const ReadoutK& a, int rb) {
   // requested before anything that waits: they depend only on the batch, so the first
   // session's gathers overlap the prologue's BatchNorm reduction
   float tv[VPL], rv[KR][VPL], sk[KR];
+  float pov[VPL], pxv[VPL];  // the wave's first node row of the session (out, xin), consumed first
   auto issue = [&](int b) {
-    if (!do_loss || b >= B) return;
+    if (b >= B) return;
+    if (do_fwd) {
+      const int i = a.bt.node_ptr[b] + wave;
+      if (i < a.bt.node_ptr[b + 1]) {
+        load_vec<VPL>(pov, a.out + (size_t)i * D + d0, act);
+        load_vec<VPL>(pxv, a.xin + (size_t)i * D + d0, act);
+      }
+    }
+    if (!do_loss) return;
     const int* ng = a.bt.negatives + (size_t)b * n;
     load_vec<VPL>(tv, a.table + (size_t)a.bt.target[b] * D + d0, act);
     const int kq = wave + lane * RO_WAVES;
@@ -871,8 +880,13 @@ __device__ __forceinline__ void readout_body(const ReadoutK& a, int rb) {
       for (int v = 0; v < VPL; ++v) acc[v] = 0.0f;
       for (int i = n0 + wave, q = 0; i < n1; i += RO_WAVES, ++q) {
         float ov[VPL], xv[VPL];
-        load_vec<VPL>(ov, a.out + (size_t)i * D + d0, act);
-        load_vec<VPL>(xv, a.xin + (size_t)i * D + d0, act);
+        if (q == 0) {  // requested by issue()
+#pragma unroll
+          for (int v = 0; v < VPL; ++v) { ov[v] = pov[v]; xv[v] = pxv[v]; }
+        } else {
+          load_vec<VPL>(ov, a.out + (size_t)i * D + d0, act);
+          load_vec<VPL>(xv, a.xin + (size_t)i * D + d0, act);
+        }
 #pragma unroll
         for (int c = 0; c < NBR; ++c)
           if (q == c) {
