@@ -36,9 +36,6 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
 // weight gradients
 // ------------------------------------------------------------------------------------
 
-#ifndef GTR_WGRAD_MFMA_ROWS
-#define GTR_WGRAD_MFMA_ROWS 128  // rows per split-K chunk from which the QKVS job runs on MFMA
-#endif
 
 __global__ __launch_bounds__(GTR_BLOCK) void k_wgrad(WgradK a) {
   const int blk = blockIdx.x;

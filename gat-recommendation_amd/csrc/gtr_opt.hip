@@ -18,6 +18,8 @@
 #include <cstdio>
 
 #include "gtr_rows.cuh"
+#include <string.h>
+
 #include "gtr_wgrad.cuh"
 
 namespace gtr {
@@ -225,7 +227,6 @@ __device__ __forceinline__ void lazy_claim_row(int key, int T, int D, int32_t t,
 // ---- fused step: begin (counters, stamps, sorted contribution list) -------------------
 #define GTR_BEGIN_BLOCK 1024
 #define GTR_BEGIN_WAVES (GTR_BEGIN_BLOCK / 64)
-#define GTR_TAILW_NCAP 512  // node-row capacity up to which the tail computes the weight gradients
 
 // Rank sort: composite keys (row << 13 | slot) are unique, so the stable order by row
 // is the plain order of the composites and slot j goes to rank #{composites < c_j}.
@@ -538,20 +539,25 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_step_tail(TailK a) {
              reinterpret_cast<float4*>(a.tl.table_v), st, a.vbegin);
 }
 
-// ---- small batches: the weight gradients inside the tail ------------------------------
-// Workgroups: [touched rows | weight-gradient tiles (gtr_wgrad.cuh jobs, one chunk over
-// all node rows) + their AdamW | BatchNorm gamma / beta segments (bn_gsum) + the loss |
-// untouched rows].  Replaces k_wgrad + the tail's slab sums for batches whose whole
-// weight-gradient reduction is a few row rounds (n_cap <= GTR_TAILW_NCAP): one launch less
-// on the step's dependency chain, bitwise the result of k_wgrad with one chunk.
+// ---- small batches: the weight gradients and the optimizer tail in ONE launch ----------
+// Workgroups: [weight-gradient tile chunks | touched rows | BatchNorm gamma / beta + loss].
+// Each (tile, row chunk) workgroup computes its split-K partial slab exactly as k_wgrad
+// does and records the slab indices it wrote in LDS; the tile's P-th arriving chunk
+// (agent-scope last-arriver election) then sums the P partials of each of those indices in
+// chunk order -- the sum the tail's small-parameter part takes -- and applies AdamW to the
+// flat parameter.  Touched rows and the bn_gsum segments depend only on the backward, so
+// they run beside the tiles.  One launch less on the step's chain, bitwise equal to
+// gtr_wgrad + gtr_step_tail (trainer.py:123-127: backward + optimizer.step()).
 #define GTR_TAILW_SEGS 16
+#define GTR_WT_LIST 4352  // slab indices one tile writes: <= 64 x 64 W + 64 bias, or 64 x (K + 1)
 struct TailWK {
   gtr_batch bt;
   gtr_tail tl;
   gtr_adam opt;
-  int T, nb_rows, nb_wg, nb_small, nb_sweep, njobs, D, nseg;
-  int64_t vbegin, nvec;
-  int vpr_log2, small_total;
+  int T, nb_rows, nb_wg, nb_small, njobs, D, nseg, P;
+  int64_t stride;
+  int small_total, pad0;
+  uint32_t* cnt;  // one arrival counter per tile (zero between launches)
   gtr_segment segs[GTR_TAILW_SEGS];
   WJob jobs[GTR_MAX_WJOBS];
 };
@@ -561,16 +567,71 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_step_tail_wgrad(TailWK a) {
   __shared__ AdamStep s_st;
   __shared__ int32_t s_t;
   __shared__ float s_acc[GTR_BLOCK];
+  __shared__ uint32_t s_list[GTR_WT_LIST];
+  __shared__ int s_n;
+  __shared__ int s_flag;
   const int tid = threadIdx.x;
   if (tid == 0) {
     const int64_t t = *a.opt.step_dev + a.opt.step_offset;
     s_st.init(a.opt, t);
     s_t = (int32_t)t;
+    s_n = 0;
   }
   __syncthreads();
   const AdamStep st = s_st;
   int blk = blockIdx.x;
   if (blk == 0 && tid == 0 && a.tl.rng_inc) *a.tl.rng_inc += 1;  // fused begin: the step's dropout counter
+  if (blk < a.nb_wg) {
+    int jid = 0;
+    while (jid + 1 < a.njobs && blk >= a.jobs[jid + 1].blk0) ++jid;
+    const WJob& J = a.jobs[jid];
+    const int local = blk - J.blk0;
+    const int tile = local / a.P, p = local - tile * a.P;
+    const int N = a.bt.hdr[0];
+    const int per = (N + a.P - 1) / a.P;
+    const int t0 = p * per, t1 = min(N, t0 + per);
+    const int64_t so = (int64_t)p * a.stride;
+    // slab index codes: bits 31..30 = 0 W element, 1 bias element, 2 four W elements
+    auto rec = [&](uint32_t code) { s_list[atomicAdd(&s_n, 1)] = code; };
+    auto emit = [&](int which, int64_t idx, float v) {
+      if (which == 0) J.outW[so + idx] = v;
+      else J.outB[so + idx] = v;
+      rec(((uint32_t)which << 30) | (uint32_t)idx);
+    };
+    auto emit4 = [&](int64_t idx, float4 v) {
+      *reinterpret_cast<float4*>(J.outW + so + idx) = v;
+      rec((2u << 30) | (uint32_t)idx);
+    };
+    if (J.mfma == 1) wgrad_tile_mfma<false>(J, tile, t0, t1, emit, emit4);
+    else if (J.mfma == 2) wgrad_tile_mfma<true>(J, tile, t0, t1, emit, emit4);
+    else wgrad_tile(J, tile, t0, t1, a.D, emit);
+    if (!arrive_last(a.cnt + J.tile0 + tile, (uint32_t)a.P, &s_flag)) return;
+    const int n = s_n;
+    float* P = a.tl.flat;
+    float* M = a.tl.flat_m;
+    float* V = a.tl.flat_v;
+    for (int k = tid; k < n; k += GTR_BLOCK) {
+      const uint32_t code = s_list[k];
+      const uint32_t kind = code >> 30;
+      const int64_t idx = code & 0x3FFFFFFFu;
+      const float* src = kind == 1 ? J.outB : J.outW;
+      const int64_t f0 = kind == 1 ? J.fB : J.fW;
+      const int cnt = kind == 2 ? 4 : 1;
+      for (int c = 0; c < cnt; ++c) {
+        float g = 0.0f;
+        for (int q = 0; q < a.P; ++q) g += src[(int64_t)q * a.stride + idx + c];
+        const int64_t e = f0 + idx + c;
+        float pv = P[e], mv = M[e], vv = V[e];
+        st.apply(pv, mv, vv, g);
+        P[e] = pv;
+        M[e] = mv;
+        V[e] = vv;
+      }
+    }
+    if (tid == 0) reset_counter(a.cnt + J.tile0 + tile);
+    return;
+  }
+  blk -= a.nb_wg;
   if (blk < a.nb_rows) {
     rows_body<D>(blk * GTR_BLOCK + tid, a.bt, a.T, a.tl.skeys, a.tl.svals, a.tl.dx0, a.tl.se, a.tl.coef_tgt,
                  a.tl.coef_neg, a.tl.table, a.tl.table_m, a.tl.table_v, nullptr, st,
@@ -578,24 +639,6 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_step_tail_wgrad(TailWK a) {
     return;
   }
   blk -= a.nb_rows;
-  if (blk < a.nb_wg) {
-    int jid = 0;
-    while (jid + 1 < a.njobs && blk >= a.jobs[jid + 1].blk0) ++jid;
-    const WJob& J = a.jobs[jid];
-    float* P = a.tl.flat;
-    float* M = a.tl.flat_m;
-    float* V = a.tl.flat_v;
-    wgrad_tile(J, blk - J.blk0, 0, a.bt.hdr[0], a.D, [&](int which, int64_t idx, float g) {
-      const int64_t e = (which == 0 ? J.fW : J.fB) + idx;
-      float pv = P[e], mv = M[e], vv = V[e];
-      st.apply(pv, mv, vv, g);
-      P[e] = pv;
-      M[e] = mv;
-      V[e] = vv;
-    });
-    return;
-  }
-  blk -= a.nb_wg;
   if (blk < a.nb_small) {
     int64_t i = (int64_t)blk * GTR_BLOCK + tid;  // index into the concatenated segments
     if (i < a.small_total) {
@@ -603,7 +646,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_step_tail_wgrad(TailWK a) {
       while (i >= a.segs[sg].len) { i -= a.segs[sg].len; ++sg; }
       const gtr_segment& S = a.segs[sg];
       float g = 0.0f;
-      for (int p = 0; p < S.nparts; ++p) g += S.src[(int64_t)p * S.pstride + i];
+      for (int q = 0; q < S.nparts; ++q) g += S.src[(int64_t)q * S.pstride + i];
       const int64_t e = S.begin + i;
       float pv = a.tl.flat[e], mv = a.tl.flat_m[e], vv = a.tl.flat_v[e];
       st.apply(pv, mv, vv, g);
@@ -623,11 +666,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_step_tail_wgrad(TailWK a) {
         a.tl.loss_out[0] = t;
       }
     }
-    return;
   }
-  blk -= a.nb_small;
-  sweep_body(blk, a.nb_sweep, a.nvec, a.vpr_log2, a.tl.stamp, s_t, reinterpret_cast<float4*>(a.tl.table),
-             reinterpret_cast<float4*>(a.tl.table_m), reinterpret_cast<float4*>(a.tl.table_v), st, a.vbegin);
 }
 
 template <int D>
@@ -1411,19 +1450,26 @@ int gtr_step_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* t
 }
 
 int gtr_step_tail_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, const float* pe_tab,
+                        float* const* layer_slab, float* pe_slab, int n_chunks, int64_t slab_stride,
                         const int64_t* layer_flat, const int64_t* pe_flat, int num_items, const gtr_tail* tail,
-                        const gtr_segment* segs, int nseg, const gtr_adam* opt, gtr_stream_t stream) {
-  if (!cfg || !bt || !layers || !layer_flat || !tail || !opt || !opt->step_dev || num_items <= 0 || nseg < 0 ||
-      nseg > GTR_TAILW_SEGS || (nseg > 0 && !segs) || !dim_ok(cfg->dim) || 3 * cfg->num_layers + 1 > GTR_MAX_WJOBS) {
+                        const gtr_segment* segs, int nseg, const gtr_adam* opt, uint32_t* tile_cnt, int tile_cnt_len,
+                        gtr_stream_t stream) {
+  if (!cfg || !bt || !layers || !layer_slab || !layer_flat || !tail || !opt || !opt->step_dev || num_items <= 0 ||
+      nseg < 0 || nseg > GTR_TAILW_SEGS || (nseg > 0 && !segs) || !dim_ok(cfg->dim) || n_chunks <= 0 ||
+      !tile_cnt || 3 * cfg->num_layers + 1 > GTR_MAX_WJOBS) {
     set_error("gtr_step_tail_wgrad: bad arguments");
     return GTR_E_ARG;
   }
   const gtr_tail& t = *tail;
   const int D = cfg->dim;
   const int m_cap = bt->n_cap + bt->b_cap * (1 + bt->n_neg);
-  if (m_cap > GTR_BEGIN_MCAP || bt->n_cap > GTR_TAILW_NCAP) {
-    set_error("gtr_step_tail_wgrad: batch too large (m_cap %d > %d or n_cap %d > %d): use gtr_wgrad + gtr_step_tail",
-              m_cap, GTR_BEGIN_MCAP, bt->n_cap, GTR_TAILW_NCAP);
+  if (m_cap > GTR_BEGIN_MCAP) {
+    set_error("gtr_step_tail_wgrad: batch too large (m_cap %d > %d): use gtr_wgrad + gtr_step_tail", m_cap,
+              GTR_BEGIN_MCAP);
+    return GTR_E_ARG;
+  }
+  if (!t.lazy_consts && t.sweep_from < num_items) {
+    set_error("gtr_step_tail_wgrad: the untouched-row sweep must run in the chain (sweep_from == num_items)");
     return GTR_E_ARG;
   }
   if (!t.skeys || !t.svals || !t.dx0 || !t.se || !t.coef_tgt || !t.coef_neg || !t.table || !t.table_m ||
@@ -1437,10 +1483,31 @@ int gtr_step_tail_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_la
   k.opt = *opt;
   k.T = num_items;
   k.D = D;
+  k.P = n_chunks;
+  k.stride = slab_stride;
+  k.cnt = tile_cnt;
+  // the same tile form k_wgrad would pick for these chunks (GTR_WGRAD=mfma|valu overrides)
+  const char* wm = getenv("GTR_WGRAD");
+  bool mfma = (bt->n_cap + n_chunks - 1) / n_chunks >= GTR_WGRAD_MFMA_ROWS;
+  if (wm && !strcmp(wm, "mfma")) mfma = true;
+  if (wm && !strcmp(wm, "valu")) mfma = false;
+  if (slab_stride % 4) mfma = false;
+  for (int l = 0; l < cfg->num_layers; ++l)
+    if (reinterpret_cast<uintptr_t>(layer_slab[l]) % 16) mfma = false;
   int nj = 0, wblocks = 0;
-  const int rc = build_wjobs(cfg, bt, layers, t.dx0, pe_tab, nullptr, nullptr, layer_flat, pe_flat, 1, 0,
-                             cfg->num_layers, k.jobs, nj, wblocks);
+  const int rc = build_wjobs(cfg, bt, layers, t.dx0, pe_tab, layer_slab, pe_slab, layer_flat, pe_flat, n_chunks, 0,
+                             cfg->num_layers, k.jobs, nj, wblocks, mfma);
   if (rc) return rc;
+  int tiles = 0;
+  for (int i = 0; i < nj; ++i) {
+    k.jobs[i].tile0 = tiles;
+    tiles += k.jobs[i].nt;
+    if (k.jobs[i].fW < 0 && k.jobs[i].fB < 0) { set_error("gtr_step_tail_wgrad: a job without flat offsets"); return GTR_E_ARG; }
+  }
+  if (tiles > tile_cnt_len) {
+    set_error("gtr_step_tail_wgrad: %d tile counters needed, %d given", tiles, tile_cnt_len);
+    return GTR_E_ARG;
+  }
   k.njobs = nj;
   k.nb_wg = wblocks;
   k.nb_rows = (int)(((int64_t)m_cap * (D / 4) + GTR_BLOCK - 1) / GTR_BLOCK);
@@ -1450,15 +1517,7 @@ int gtr_step_tail_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_la
   k.small_total = (int)tot;
   k.nb_small = (int)((tot + GTR_BLOCK - 1) / GTR_BLOCK);
   if (k.nb_small == 0 && t.loss_part) k.nb_small = 1;
-  k.nvec = (int64_t)num_items * D / 4;
-  k.vpr_log2 = 0;
-  while ((1 << k.vpr_log2) < D / 4) ++k.vpr_log2;
-  const int64_t from = t.lazy_consts ? num_items
-                                      : (t.sweep_from < 0 ? 0 : (t.sweep_from > num_items ? num_items : t.sweep_from));
-  k.vbegin = from * (D / 4);
-  const int64_t sw = (k.nvec - k.vbegin + GTR_BLOCK - 1) / GTR_BLOCK;
-  k.nb_sweep = (int)(sw > 2048 ? 2048 : sw);
-  const int grid = k.nb_rows + k.nb_wg + k.nb_small + k.nb_sweep;
+  const int grid = k.nb_wg + k.nb_rows + k.nb_small;
   hipStream_t s = (hipStream_t)stream;
   switch (D) {
     case 32: hipLaunchKernelGGL(k_step_tail_wgrad<32>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;

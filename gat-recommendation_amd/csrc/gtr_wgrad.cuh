@@ -26,9 +26,14 @@ struct WJob {
   float* outW;      // slab destinations (k_wgrad)
   float* outB;
   int64_t fW, fB;   // flat-buffer offsets of the same outputs (fused tail), -1: none
+  int tile0, pad_t; // first arrival counter of the job's tiles (fused tail)
 };
 
 #define GTR_MAX_WJOBS 16
+
+#ifndef GTR_WGRAD_MFMA_ROWS
+#define GTR_WGRAD_MFMA_ROWS 128  // rows per split-K chunk from which the QKVS job runs on MFMA
+#endif
 
 struct WgradK {
   const int32_t* hdr;

@@ -92,7 +92,7 @@ class GtrTail(C.Structure):
 
 
 SWEEP_SLOTS = 8
-ABI_VERSION = 3  # GTR_ABI_VERSION of include/gtr.h
+ABI_VERSION = 4  # GTR_ABI_VERSION of include/gtr.h
 
 
 class GtrLazy(C.Structure):
@@ -158,7 +158,8 @@ _SIGS = {
     "gtr_dp_union_stamp": (C.c_int, [P, i64, C.c_int, P, P, P]),
     "gtr_step_begin": (C.c_int, [P, C.c_int, P, P, P, P, P, P, P, P, C.c_size_t, P]),
     "gtr_step_tail": (C.c_int, [P, C.c_int, C.c_int, P, P, C.c_int, P, P]),
-    "gtr_step_tail_wgrad": (C.c_int, [P, P, P, P, P, P, C.c_int, P, P, C.c_int, P, P]),
+    "gtr_step_tail_wgrad": (C.c_int, [P, P, P, P, P, P, C.c_int, C.c_int64, P, P, C.c_int, P, P, C.c_int, P, P,
+                                      C.c_int, P]),
     "gtr_step_begin_lazy": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P, P, P, P, C.c_size_t, P, P]),
     "gtr_lazy_flush": (C.c_int, [C.c_int, C.c_int, P, P, P, P]),
     "gtr_tail_carry_floats": (C.c_int, [C.c_int, C.c_int]),

@@ -241,8 +241,6 @@ class Engine:
     def choose_R(self, caps: Caps) -> int:
         return caps.R
 
-    TAILW_NCAP = 512  # GTR_TAILW_NCAP (csrc/gtr_opt.hip)
-
     def choose_P(self, caps: Caps) -> int:
         # split-K of the weight gradients: <= 32 node rows per workgroup, <= 64 slabs (one
         # chunk over ~110 rows made k_wgrad 2x slower at C2: measured 0.105 -> 0.119 ms/step)

@@ -264,10 +264,14 @@ class FusedTrainStep:
             self.dp = DpExchange(self, self.group)
         if self.sync_bn:
             self._sync_alloc()
-        # small batches: the weight gradients ride in the tail launch (gtr_step_tail_wgrad)
+        # opt-in (GTR_TAILW=1): weight gradients and optimizer tail in one launch
+        # (gtr_step_tail_wgrad: split-K tiles, each tile's last arriving chunk applies AdamW);
+        # bitwise the two launches but slower (C2 0.083 -> 0.102 ms: one workgroup per tile
+        # walks its 4k elements' partials serially); needs the sweep in the chain or a lazy table
         self.tail_wgrad = (self.dp is None and self.shard is None and m_cap <= 8192
-                           and caps.n_cap <= eng.TAILW_NCAP and os.environ.get("GTR_TAILW", "0") == "1")
+                           and (self.lazy or t.sweep_from >= eng.T) and os.environ.get("GTR_TAILW", "0") == "1")
         if self.tail_wgrad:
+            self.tile_cnt = torch.zeros(4096, dtype=torch.int32, device=self.dev)
             lay = eng.flat.layout
             gb = [i for i in range(self.nseg)
                   if any(self.segs[i].begin == lay.seg(f"{l}.{n}").begin for l in range(eng.L) for n in ("gamma", "beta"))]
@@ -409,10 +413,14 @@ class FusedTrainStep:
             self.dp.launch_tail(bs, st)
         elif self.tail_wgrad:
             pe = self.model.laplacian_pe._cached_pe if eng.K > 0 else None
-            L.check(L.lib().gtr_step_tail_wgrad(C.byref(self.cfg), C.byref(bs), self.ws.structs,
-                                                None if pe is None else pe.data_ptr(), self.layer_flat,
-                                                self.pe_flat, eng.T, C.byref(self.tail), self.segs_gb,
-                                                self.nseg_gb, C.byref(self.adam), st), "step_tail_wgrad")
+            ws = self.ws
+            L.check(L.lib().gtr_step_tail_wgrad(C.byref(self.cfg), C.byref(bs), ws.structs,
+                                                None if pe is None else pe.data_ptr(), ws.slab_ptrs,
+                                                None if ws.pe_slab is None else ws.pe_slab.data_ptr(), ws.P,
+                                                eng.flat.layout.slab_stride, self.layer_flat, self.pe_flat, eng.T,
+                                                C.byref(self.tail), self.segs_gb, self.nseg_gb, C.byref(self.adam),
+                                                self.tile_cnt.data_ptr(), self.tile_cnt.numel(), st),
+                    "step_tail_wgrad")
         else:
             L.check(L.lib().gtr_step_tail(C.byref(bs), eng.T, eng.D, C.byref(self.tail), self.segs, self.nseg,
                                           C.byref(self.adam), st), "step_tail")

@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GTR_ABI_VERSION 3 /* 3: gtr_config.begin / ctr_add, gtr_tail.rng_inc (begin fused into conv_fwd(0)) */
+#define GTR_ABI_VERSION 4 /* 4: gtr_step_tail_wgrad on split-K slabs; 3: gtr_config.begin / ctr_add, gtr_tail.rng_inc */
 
 #define GTR_OK 0
 #define GTR_E_ARG 1001      /* bad argument / unsupported shape */
@@ -394,16 +394,22 @@ int gtr_tail_carry_floats(int m_cap, int dim);
 int gtr_step_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tail,
                   const gtr_segment* segs, int nseg, const gtr_adam* opt, gtr_stream_t stream);
 
-/* Small batches (n_cap <= 512, m_cap <= 8192): gtr_step_tail with the weight gradients of
- * gtr_wgrad (one row chunk) computed inside the same launch and applied by AdamW directly,
- * one launch less on the step's chain (trainer.py:123-127: backward + optimizer.step()).
- * layer_flat [L][3] = element offsets into tail->flat of each layer's w_all / b_all /
- * w_beta; pe_flat [2] = offsets of the LapPE projection weight / bias (NULL without
- * LapPE); segs = the remaining dense segments (BatchNorm gamma / beta from bn_gsum,
- * <= 16).  Bitwise equal to gtr_wgrad(n_chunks = 1) + gtr_step_tail.                    */
+/* Small batches (m_cap <= 8192, untouched-row sweep in the chain or a lazy table):
+ * gtr_wgrad + gtr_step_tail as ONE launch (trainer.py:123-127: backward +
+ * optimizer.step()).  The weight-gradient tiles write their split-K partial slabs
+ * (layer_slab / pe_slab, n_chunks, slab_stride as gtr_wgrad); each tile's last arriving
+ * chunk sums the n_chunks partials of its outputs in chunk order and applies AdamW;
+ * touched rows and the bn_gsum segments run beside the tiles.  layer_flat [L][3] =
+ * element offsets into tail->flat of each layer's w_all / b_all / w_beta; pe_flat [2] =
+ * offsets of the LapPE projection weight / bias (NULL without LapPE); segs = the other
+ * dense segments (BatchNorm gamma / beta from bn_gsum, <= 16); tile_cnt = tile_cnt_len
+ * zeroed counters (one per tile; each launch leaves them zero).  Bitwise equal to
+ * gtr_wgrad + gtr_step_tail.                                                          */
 int gtr_step_tail_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, const float* pe_tab,
+                        float* const* layer_slab, float* pe_slab, int n_chunks, int64_t slab_stride,
                         const int64_t* layer_flat, const int64_t* pe_flat, int num_items, const gtr_tail* tail,
-                        const gtr_segment* segs, int nseg, const gtr_adam* opt, gtr_stream_t stream);
+                        const gtr_segment* segs, int nseg, const gtr_adam* opt, uint32_t* tile_cnt, int tile_cnt_len,
+                        gtr_stream_t stream);
 
 /* ---- data-parallel step (one process per GPU; etpgt.train.distributed) --------
  * Each rank packs its gradients into `pack` (words per rank = layout.words):

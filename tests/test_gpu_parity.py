@@ -187,14 +187,39 @@ def test_fused_steps_large_batch_c3_shape(wgrad, monkeypatch):
     _fused_vs_reference(128, 4, 16, "listwise", "adamw", True, B=2400, steps=2, expect_ncap=8192)
 
 
-@pytest.mark.parametrize("D,H,K,loss", [(64, 1, 0, "bpr"), (128, 4, 16, "listwise")])
-def test_fused_steps_tail_wgrad(D, H, K, loss, monkeypatch):
-    """GTR_TAILW=1: the weight gradients of a small batch computed inside the step tail
-    (k_step_tail_wgrad, one chunk over all rows, AdamW applied in place) -- the same
-    trajectory as the oracle."""
+@pytest.mark.parametrize("D,H,K,loss,wgrad", [(64, 1, 0, "bpr", "default"), (128, 4, 16, "listwise", "default"),
+                                               (128, 4, 16, "listwise", "mfma"), (32, 2, 8, "dual", "default")])
+def test_tail_wgrad_bitwise_equals_separate_launches(D, H, K, loss, wgrad, monkeypatch):
+    """gtr_step_tail_wgrad (opt-in GTR_TAILW=1: weight-gradient tiles and the
+    optimizer tail in one launch, each tile's last arriving chunk summing the split-K
+    partials in chunk order and applying AdamW) against gtr_wgrad + gtr_step_tail
+    (GTR_TAILW=0): losses, parameters, buffers and moments bit for bit, dropout on."""
+    if wgrad != "default":
+        monkeypatch.setenv("GTR_WGRAD", wgrad)
+    T = data().table_rows
+    n = 100 if loss == "listwise" else 5
+    m1, _ = make_pair(T, D, H, K=K, dropout=0.1, seed=9)
+    m2 = copy.deepcopy(m1)
+    m1.train(); m2.train()
+    bl = batches(data(), 32, n, 4, seed=17)
+    monkeypatch.setenv("GTR_TAILW", "0")
+    f1 = FusedTrainStep(m1, loss=loss)
+    first = float(f1(bl[0].to("cuda")))
     monkeypatch.setenv("GTR_TAILW", "1")
-    fused = _fused_vs_reference(D, H, K, loss, "adamw", True, B=32, steps=3)
-    assert fused.tail_wgrad
+    f2 = FusedTrainStep(m2, loss=loss)
+    assert first == float(f2(bl[0].to("cuda")))
+    assert not f1.tail_wgrad and f2.tail_wgrad
+    for sb in bl[1:]:
+        dsb = sb.to("cuda")
+        assert float(f1(dsb)) == float(f2(dsb))
+    for (name, a), (_, b) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert torch.equal(a, b), name
+    for (name, a), (_, b) in zip(m1.named_buffers(), m2.named_buffers()):
+        if a is not None:
+            assert torch.equal(a, b), name
+    for name in ("m_tab", "v_tab", "m_flat", "v_flat"):
+        assert torch.equal(getattr(f1, name), getattr(f2, name)), name
+    assert int(f2.tile_cnt.abs().sum()) == 0  # every tile's counter re-armed
 
 
 @pytest.mark.parametrize("mode", ["mfma", "valu"])
