@@ -286,6 +286,34 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
       s_v = *reinterpret_cast<const float4*>(src + 2 * D + c0);
       s_q = *reinterpret_cast<const float4*>(src + c0);
     }
+    // (D1)'s own inputs of this thread's row (dy, out, agg, S, gate, BatchNorm mean / rstd,
+    // gamma) requested with the staging loads instead of after its barrier (D <= 64: the
+    // registers are free here)
+    constexpr bool PRED1 = D <= 64;
+    float4 d1_dy[PRED1 ? CH / 4 : 1], d1_o[PRED1 ? CH / 4 : 1], d1_ag[PRED1 ? CH / 4 : 1], d1_s[PRED1 ? CH / 4 : 1];
+    float d1_mean[PRED1 ? CH : 1], d1_rstd[PRED1 ? CH : 1], d1_gam[PRED1 ? CH : 1], d1_beta = 0.0f;
+    if (PRED1 && prow < nrow) {
+      const int t1 = r0 + prow;
+      const size_t ro1 = (size_t)t1 * D + f0;
+      d1_beta = a.gate[t1];
+#pragma unroll
+      for (int c = 0; c < CH; c += 4) {
+        if constexpr (PRED1) {
+          d1_dy[c / 4] = *reinterpret_cast<const float4*>(a.dy + ro1 + c);
+          d1_o[c / 4] = *reinterpret_cast<const float4*>(a.out + ro1 + c);
+          d1_ag[c / 4] = *reinterpret_cast<const float4*>(a.agg + ro1 + c);
+          d1_s[c / 4] = *reinterpret_cast<const float4*>(a.qkvs + (size_t)t1 * (4 * D) + 3 * D + f0 + c);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < CH; ++c) {
+        if constexpr (PRED1) {
+          d1_mean[c] = a.stats[f0 + c];
+          d1_rstd[c] = a.stats[D + f0 + c];
+          d1_gam[c] = a.gamma[f0 + c];
+        }
+      }
+    }
     if (tid <= nrow) {
       iptr[tid] = s_ip - e_lo;
       optr[tid] = s_op - o_lo;
@@ -340,22 +368,29 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
     if (live) {
       const size_t ro = (size_t)t * D + f0;
       const float* gs = a.cred ? s_gs : a.gsum;
-      beta = a.gate[t];
+      beta = PRED1 ? d1_beta : a.gate[t];
 #pragma unroll
       for (int c = 0; c < CH; c += 4) {
-        const float4 dy4 = *reinterpret_cast<const float4*>(a.dy + ro + c);
-        const float4 o4 = *reinterpret_cast<const float4*>(a.out + ro + c);
-        const float4 ag4 = *reinterpret_cast<const float4*>(a.agg + ro + c);
-        const float4 s4 = *reinterpret_cast<const float4*>(a.qkvs + (size_t)t * (4 * D) + 3 * D + f0 + c);
+        float4 dy4, o4, ag4, s4;
+        if constexpr (PRED1) {
+          dy4 = d1_dy[c / 4]; o4 = d1_o[c / 4]; ag4 = d1_ag[c / 4]; s4 = d1_s[c / 4];
+        } else {
+          dy4 = *reinterpret_cast<const float4*>(a.dy + ro + c);
+          o4 = *reinterpret_cast<const float4*>(a.out + ro + c);
+          ag4 = *reinterpret_cast<const float4*>(a.agg + ro + c);
+          s4 = *reinterpret_cast<const float4*>(a.qkvs + (size_t)t * (4 * D) + 3 * D + f0 + c);
+        }
         const float dyv[4] = {dy4.x, dy4.y, dy4.z, dy4.w}, ov[4] = {o4.x, o4.y, o4.z, o4.w};
         const float agl[4] = {ag4.x, ag4.y, ag4.z, ag4.w}, svl[4] = {s4.x, s4.y, s4.z, s4.w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int j = f0 + c + q;
-          const float mean = a.stats[j], rstd = a.stats[D + j];
+          const float mean = PRED1 ? d1_mean[(c + q) % CH] : a.stats[j];
+          const float rstd = PRED1 ? d1_rstd[(c + q) % CH] : a.stats[D + j];
+          const float gam = PRED1 ? d1_gam[(c + q) % CH] : a.gamma[j];
           const float xh = (ov[q] - mean) * rstd;
           const float s1 = gs[j] * invN, s2 = gs[D + j] * invN;
-          gv[c + q] = (dyv[q] - s1 - xh * s2) * rstd * a.gamma[j];
+          gv[c + q] = (dyv[q] - s1 - xh * s2) * rstd * gam;
           sv[c + q] = svl[q];
           agv[c + q] = agl[q];
           dbeta += gv[c + q] * (svl[q] - agl[q]);
