@@ -454,7 +454,7 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
     //      GL lanes per (row, head), edges strided over the lanes, sum by shuffles
     {
       const int pairs = nrow * H;
-      const int GL = pair_lanes(pairs, CONV_BLOCK);
+      const int GL = pair_lanes_deg(pairs, CONV_BLOCK, ne, nrow);
       for (int base = 0; base < pairs; base += CONV_BLOCK / GL) {
         const int pidx = base + tid / GL, gl = tid & (GL - 1);
         int h = 0, e0 = 0, e1 = 0;

@@ -49,6 +49,17 @@ __device__ __forceinline__ int pair_lanes(int pairs, int blk) {
   return gl;
 }
 
+// The same, but no wider than the group's mean in-degree rounded up to a power of two:
+// every lane beyond a pair's edge count only adds shuffle rounds (each a cross-lane LDS
+// permute) to the max / sum, while a hub row's few lanes loop over its edges.
+__device__ __forceinline__ int pair_lanes_deg(int pairs, int blk, int edges, int rows) {
+  const int deg = rows > 0 ? (edges + rows - 1) / rows : 1;
+  int gl = 1;
+  while (gl < deg && gl < 64) gl <<= 1;
+  const int cap = pair_lanes(pairs, blk);
+  return gl < cap ? gl : cap;
+}
+
 // Counter-based dropout stream: one 32-bit hash per (seed, stream, element).
 __device__ __forceinline__ uint32_t mix3(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t h = a * 0x9E3779B1u;
