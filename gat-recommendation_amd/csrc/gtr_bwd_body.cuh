@@ -397,8 +397,7 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
         }
       }
     }
-#pragma unroll
-    for (int o = 1; o < TPR; o <<= 1) dbeta += __shfl_xor(dbeta, o);
+    dbeta = group_sum_c<TPR>(dbeta);
     if (live) {
       const float du = dbeta * beta * (1.0f - beta);
       if (pchunk == 0) a.du[t] = du;
@@ -442,8 +441,8 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
           }
         }
         if (SPL == 4) {
-          dot += __shfl_xor(dot, 1);
-          dot += __shfl_xor(dot, 2);
+          dot = bfly_add<1>(dot);
+          dot = bfly_add<2>(dot);
         }
         if (idx < nit && idx == it * SPL) DL[it] = dot * dr.mul(st_attn, (uint32_t)(e_lo * H + it));
       }
@@ -764,8 +763,8 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
   for (int c = 0; c < CPW; ++c) {
     const int ct = (WPC > 1 ? wave % NCT : wave) + c * CONV_WAVES;
     float x1 = s1[c], x2 = s2[c];
-    x1 += __shfl_xor(x1, 16); x1 += __shfl_xor(x1, 32);
-    x2 += __shfl_xor(x2, 16); x2 += __shfl_xor(x2, 32);
+    x1 = bfly_add<32>(bfly_add<16>(x1));
+    x2 = bfly_add<32>(bfly_add<16>(x2));
     if (lg == 0) {
       s_bnp[rs * 2 * D + ct * 16 + lr] = x1;
       s_bnp[rs * 2 * D + D + ct * 16 + lr] = x2;

@@ -16,27 +16,80 @@ namespace gtr {
 
 void set_error(const char* fmt, ...);
 
-__device__ __forceinline__ float wave_sum(float x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+// Cross-lane butterflies, offsets 1..8 without the LDS crossbar.  Step O of an ASCENDING butterfly
+// (offsets 1, 2, 4, ...) combines each lane with its xor-O partner:
+//  - O = 1, 2: DPP quad_perm, an exact xor permutation inside a quad;
+//  - O = 4, 8: every lane of an aligned O-group already holds the same value, so the
+//    mirrors inside 8 / 16 lanes (DPP row_half_mirror / row_mirror) deliver the xor
+//    partner's value;
+// These are VALU operand modifiers; a __shfl_xor is a ds_bpermute round trip through LDS.
+// O = 16, 32 stay __shfl_xor: the v_permlane16/32_swap route (both swap outputs into
+// one commutative op) miscompiles here -- with both operands the same value the
+// compiler folds the two outputs into one (measured: v_add_f32 vN, vN, vN).
+template <int O>
+__device__ __forceinline__ float dpp_partner(float x) {
+  static_assert(O == 1 || O == 2 || O == 4 || O == 8, "DPP butterfly offset");
+  constexpr int CTRL = O == 1 ? 0xB1 : O == 2 ? 0x4E : O == 4 ? 0x141 : 0x140;
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+
+template <int O>
+__device__ __forceinline__ float bfly_add(float x) {
+  if constexpr (O <= 8) return x + dpp_partner<O>(x);
+  else return x + __shfl_xor(x, O);
+}
+
+template <int O>
+__device__ __forceinline__ float bfly_max(float x) {
+  if constexpr (O <= 8) return fmaxf(x, dpp_partner<O>(x));
+  else return fmaxf(x, __shfl_xor(x, O));
+}
+
+// Ascending butterfly sum over aligned groups of G lanes (G a compile-time power of two).
+template <int G>
+__device__ __forceinline__ float group_sum_c(float x) {
+  if constexpr (G > 1) x = bfly_add<1>(x);
+  if constexpr (G > 2) x = bfly_add<2>(x);
+  if constexpr (G > 4) x = bfly_add<4>(x);
+  if constexpr (G > 8) x = bfly_add<8>(x);
+  if constexpr (G > 16) x = bfly_add<16>(x);
+  if constexpr (G > 32) x = bfly_add<32>(x);
   return x;
 }
 
-__device__ __forceinline__ float wave_max(float x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
+template <int G>
+__device__ __forceinline__ float group_max_c(float x) {
+  if constexpr (G > 1) x = bfly_max<1>(x);
+  if constexpr (G > 2) x = bfly_max<2>(x);
+  if constexpr (G > 4) x = bfly_max<4>(x);
+  if constexpr (G > 8) x = bfly_max<8>(x);
+  if constexpr (G > 16) x = bfly_max<16>(x);
+  if constexpr (G > 32) x = bfly_max<32>(x);
   return x;
 }
 
-// Sum inside aligned groups of `gl` lanes (gl a power of two <= 64).
+__device__ __forceinline__ float wave_sum(float x) { return group_sum_c<64>(x); }
+__device__ __forceinline__ float wave_max(float x) { return group_max_c<64>(x); }
+
+// Sum inside aligned groups of `gl` lanes (gl a power of two <= 64; wave-uniform).
 __device__ __forceinline__ float group_sum(float x, int gl) {
-  for (int o = 1; o < gl; o <<= 1) x += __shfl_xor(x, o);
+  if (gl > 1) x = bfly_add<1>(x);
+  if (gl > 2) x = bfly_add<2>(x);
+  if (gl > 4) x = bfly_add<4>(x);
+  if (gl > 8) x = bfly_add<8>(x);
+  if (gl > 16) x = bfly_add<16>(x);
+  if (gl > 32) x = bfly_add<32>(x);
   return x;
 }
 
-// Max inside aligned groups of `gl` lanes (gl a power of two <= 64).
+// Max inside aligned groups of `gl` lanes (gl a power of two <= 64; wave-uniform).
 __device__ __forceinline__ float group_max(float x, int gl) {
-  for (int o = 1; o < gl; o <<= 1) x = fmaxf(x, __shfl_xor(x, o));
+  if (gl > 1) x = bfly_max<1>(x);
+  if (gl > 2) x = bfly_max<2>(x);
+  if (gl > 4) x = bfly_max<4>(x);
+  if (gl > 8) x = bfly_max<8>(x);
+  if (gl > 16) x = bfly_max<16>(x);
+  if (gl > 32) x = bfly_max<32>(x);
   return x;
 }
 

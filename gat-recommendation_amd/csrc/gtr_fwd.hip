@@ -544,8 +544,8 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
         }
       }
       if (SPL == 4) {
-        dot += __shfl_xor(dot, 1);
-        dot += __shfl_xor(dot, 2);
+        dot = bfly_add<1>(dot);
+        dot = bfly_add<2>(dot);
       }
       if (idx < nit && idx == it * SPL) LOG[it] = dot / a.sqrt_c;
     }
@@ -620,8 +620,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
       for (int c = 0; c < CH; ++c)
         u += WB[f0 + c] * ag[c] + WB[D + f0 + c] * sv[c] + WB[2 * D + f0 + c] * (ag[c] - sv[c]);
     }
-#pragma unroll
-    for (int o = 1; o < TPR; o <<= 1) u += __shfl_xor(u, o);
+    u = group_sum_c<TPR>(u);
     if (live && es == 0) {
       const float beta = 1.0f / (1.0f + expf(-u));
       const size_t ro = (size_t)(r0 + grow) * D + f0;
@@ -1155,8 +1154,8 @@ __device__ __forceinline__ void st_row(float* p, const float (&x)[EPL]) {
 
 // sum over the 4 row groups (lanes l, l^16, l^32, l^48)
 __device__ __forceinline__ float sum_groups(float x) {
-  x += __shfl_xor(x, 16);
-  x += __shfl_xor(x, 32);
+  x = bfly_add<16>(x);
+  x = bfly_add<32>(x);
   return x;
 }
 
@@ -1342,8 +1341,7 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
 #pragma unroll
       for (int e = 0; e < EPL; ++e) dse[e] = sum_groups(A.dse[e]);
       if (use_lw) {
-        float M = fmaxf(A.mg, __shfl_xor(A.mg, 16));
-        M = fmaxf(M, __shfl_xor(M, 32));
+        const float M = bfly_max<32>(bfly_max<16>(A.mg));
         const float f = A.zg > 0.0f ? expf(A.mg - M) : 0.0f;
         const float Z = sum_groups(A.zg * f);
         const float lse = M + logf(Z);

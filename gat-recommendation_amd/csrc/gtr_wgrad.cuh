@@ -247,11 +247,8 @@ __device__ __forceinline__ void wgrad_tile_mfma(const WJob& J, int tile, int t0,
     a0 = a2; b0 = b2; a1 = a3; b1 = b3;
   }
   if (colsum) {  // the four row lanes of a column, then the row splits in order
-#pragma unroll
-    for (int o = 16; o < 64; o <<= 1) {
-      cs.x += __shfl_xor(cs.x, o); cs.y += __shfl_xor(cs.y, o);
-      cs.z += __shfl_xor(cs.z, o); cs.w += __shfl_xor(cs.w, o);
-    }
+    cs.x = bfly_add<32>(bfly_add<16>(cs.x)); cs.y = bfly_add<32>(bfly_add<16>(cs.y));
+    cs.z = bfly_add<32>(bfly_add<16>(cs.z)); cs.w = bfly_add<32>(bfly_add<16>(cs.w));
   }
   for (int s = 1; s < kw; ++s) {
     if (colsum && ks == s) red[wt][0][lane] = f32x4{cs.x, cs.y, cs.z, cs.w};
