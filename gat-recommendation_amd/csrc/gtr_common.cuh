@@ -16,16 +16,19 @@ namespace gtr {
 
 void set_error(const char* fmt, ...);
 
-// Cross-lane butterflies, offsets 1..8 without the LDS crossbar.  Step O of an ASCENDING butterfly
+// Cross-lane butterflies without the LDS crossbar.  Step O of an ASCENDING butterfly
 // (offsets 1, 2, 4, ...) combines each lane with its xor-O partner:
 //  - O = 1, 2: DPP quad_perm, an exact xor permutation inside a quad;
 //  - O = 4, 8: every lane of an aligned O-group already holds the same value, so the
 //    mirrors inside 8 / 16 lanes (DPP row_half_mirror / row_mirror) deliver the xor
 //    partner's value;
-// These are VALU operand modifiers; a __shfl_xor is a ds_bpermute round trip through LDS.
-// O = 16, 32 stay __shfl_xor: the v_permlane16/32_swap route (both swap outputs into
-// one commutative op) miscompiles here -- with both operands the same value the
-// compiler folds the two outputs into one (measured: v_add_f32 vN, vN, vN).
+//  - O = 16, 32: gfx950's v_permlane16_swap / v_permlane32_swap exchange the odd rows
+//    (upper half) of one copy with the even rows (lower half) of another, so a
+//    commutative op over the two swapped copies gives every lane op(x[l], x[l^O]).
+// All VALU work, bitwise what the __shfl_xor (ds_bpermute through LDS) butterfly gives.
+// The swaps are inline asm: the builtin folds its two outputs into one when both
+// operands carry the same value (measured: v_add_f32 vN, vN, vN).  The s_nop pairs
+// cover the VALU-write -> permlane-read hazards the compiler cannot see inside asm.
 template <int O>
 __device__ __forceinline__ float dpp_partner(float x) {
   static_assert(O == 1 || O == 2 || O == 4 || O == 8, "DPP butterfly offset");
@@ -34,15 +37,34 @@ __device__ __forceinline__ float dpp_partner(float x) {
 }
 
 template <int O>
+__device__ __forceinline__ void swap_halves(float& a, float& b) {
+  static_assert(O == 16 || O == 32, "permlane swap offset");
+  if constexpr (O == 16)
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+  else
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1\n\ts_nop 1" : "+v"(a), "+v"(b));
+}
+
+template <int O>
 __device__ __forceinline__ float bfly_add(float x) {
-  if constexpr (O <= 8) return x + dpp_partner<O>(x);
-  else return x + __shfl_xor(x, O);
+  if constexpr (O <= 8) {
+    return x + dpp_partner<O>(x);
+  } else {
+    float a = x, b = x;
+    swap_halves<O>(a, b);
+    return a + b;
+  }
 }
 
 template <int O>
 __device__ __forceinline__ float bfly_max(float x) {
-  if constexpr (O <= 8) return fmaxf(x, dpp_partner<O>(x));
-  else return fmaxf(x, __shfl_xor(x, O));
+  if constexpr (O <= 8) {
+    return fmaxf(x, dpp_partner<O>(x));
+  } else {
+    float a = x, b = x;
+    swap_halves<O>(a, b);
+    return fmaxf(a, b);
+  }
 }
 
 // Ascending butterfly sum over aligned groups of G lanes (G a compile-time power of two).
