@@ -294,8 +294,13 @@ struct AdamStep {
   __device__ __forceinline__ void init(const gtr_adam& o, int64_t t) {
     lr = o.lr; b1 = o.beta1; b2 = o.beta2; eps = o.eps; wd = o.weight_decay;
     decoupled = o.decoupled;
+#ifdef GTR_PROBE_NOPOW  // timing probe only: what the step-scalar computation costs
+    double bc1 = 1.0 - (double)o.beta1 * (double)t * 1e-3;
+    double bc2 = 1.0 - (double)o.beta2 * (double)t * 1e-3;
+#else
     double bc1 = 1.0 - pow((double)o.beta1, (double)t);
     double bc2 = 1.0 - pow((double)o.beta2, (double)t);
+#endif
     step_size = (float)((double)o.lr / bc1);
     bc2_sqrt = (float)sqrt(bc2);
     decay_mul = (float)(1.0 - (double)o.lr * (double)o.weight_decay);

@@ -73,12 +73,14 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_contrib_prep(gtr_batch bt, int T,
 // Touched rows: one thread per (segment start, float4 column).  p/m/v of the row are
 // fetched up front (they depend only on the key), the segment's contributions are
 // summed in sorted (stable) order, then AdamW — or the dense gradient is written.
-template <int D>
+// wait(): called after every load is issued, before `st` / `lazy_t` are first read.
+template <int D, class Wait = NoWait>
 __device__ __forceinline__ void rows_body(int gid, const gtr_batch& bt, int T, const int32_t* skeys,
                                           const int32_t* svals, const float* dx0, const float* se,
                                           const float* coef_tgt, const float* coef_neg, float* table, float* m,
                                           float* v, float* grad_dense, const AdamStep& st,
-                                          int32_t* lazy_stamp = nullptr, int32_t lazy_t = 0) {
+                                          int32_t* lazy_stamp = nullptr, const int32_t& lazy_t = 0,
+                                          Wait wait = Wait{}) {
   constexpr int C4 = D / 4;
   const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
   const int i = gid / C4, c = gid - (gid / C4) * C4;
@@ -119,6 +121,7 @@ __device__ __forceinline__ void rows_body(int gid, const gtr_batch& bt, int T, c
     reinterpret_cast<float4*>(grad_dense)[base] = g;
     return;
   }
+  wait();
   st.apply(pv.x, mv.x, vv.x, g.x);
   st.apply(pv.y, mv.y, vv.y, g.y);
   st.apply(pv.z, mv.z, vv.z, g.z);
@@ -492,34 +495,51 @@ __device__ __forceinline__ void window_rows(int w, const gtr_batch& bt, int T, c
   }
 }
 
+// One wave more than the body waves: it loads the step counter and computes the step's
+// AdamW scalars (two f64 pow, ~1.7 us at C2 when every wave waited for them) while the
+// body waves issue their loads; they wait on s_ready only right before AdamW.
+#define GTR_TAIL_BLOCK (GTR_BLOCK + 64)
+
 template <int D>
-__global__ __launch_bounds__(GTR_BLOCK) void k_step_tail(TailK a) {
+__global__ __launch_bounds__(GTR_TAIL_BLOCK) void k_step_tail(TailK a) {
   __shared__ AdamStep s_st;
   __shared__ int32_t s_t;
+  __shared__ int s_ready;
   __shared__ float s_acc[GTR_BLOCK];
   const int tid = threadIdx.x;
-  if (tid == 0) {
-    const int64_t t = *a.opt.step_dev + a.opt.step_offset;
-    s_st.init(a.opt, t);
-    s_t = (int32_t)t;
-  }
+  if (tid == 0) s_ready = 0;
   __syncthreads();
-  const AdamStep st = s_st;
+  if (tid >= GTR_BLOCK) {  // the step-scalar wave
+    if (tid == GTR_BLOCK) {
+      const int64_t t = *a.opt.step_dev + a.opt.step_offset;
+      s_st.init(a.opt, t);
+      s_t = (int32_t)t;
+      __hip_atomic_store(&s_ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    return;
+  }
+  auto wait = [&]() {
+    while (__hip_atomic_load(&s_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+      __builtin_amdgcn_s_sleep(1);
+  };
   const int blk = blockIdx.x;
   if (blk == 0 && tid == 0 && a.tl.rng_inc) *a.tl.rng_inc += 1;  // fused begin: the step's dropout counter
   if (blk < a.nb_rows && a.windowed) {
+    wait();
+    const AdamStep st = s_st;
     window_rows<D>(blk, a.bt, a.T, a.tl, st, a.tl.lazy_consts ? a.tl.stamp : nullptr, s_t);
     return;
   }
   if (blk < a.nb_rows) {
     rows_body<D>(blk * GTR_BLOCK + tid, a.bt, a.T, a.tl.skeys, a.tl.svals, a.tl.dx0, a.tl.se, a.tl.coef_tgt,
-                 a.tl.coef_neg, a.tl.table, a.tl.table_m, a.tl.table_v, nullptr, st,
-                 a.tl.lazy_consts ? a.tl.stamp : nullptr, s_t);
+                 a.tl.coef_neg, a.tl.table, a.tl.table_m, a.tl.table_v, nullptr, s_st,
+                 a.tl.lazy_consts ? a.tl.stamp : nullptr, s_t, wait);
     return;
   }
   if (blk < a.nb_rows + a.nb_small) {
     const int sb = blk - a.nb_rows;
-    small_body((int64_t)sb * GTR_BLOCK + tid, a.segs, a.nseg, a.tl.flat, a.tl.flat_m, a.tl.flat_v, nullptr, st);
+    small_body((int64_t)sb * GTR_BLOCK + tid, a.segs, a.nseg, a.tl.flat, a.tl.flat_m, a.tl.flat_v, nullptr, s_st,
+               wait);
     if (sb == 0 && a.tl.loss_part) {  // loss of the step: the readout's partials, fixed order
       float acc = 0.0f;
       for (int q = tid; q < a.tl.loss_nparts; q += GTR_BLOCK)
@@ -534,6 +554,8 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_step_tail(TailK a) {
     }
     return;
   }
+  wait();
+  const AdamStep st = s_st;
   sweep_body(blk - a.nb_rows - a.nb_small, a.nb_sweep, a.nvec, a.vpr_log2, a.tl.stamp, s_t,
              reinterpret_cast<float4*>(a.tl.table), reinterpret_cast<float4*>(a.tl.table_m),
              reinterpret_cast<float4*>(a.tl.table_v), st, a.vbegin);
@@ -1440,10 +1462,10 @@ int gtr_step_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* t
   for (int i = 0; i < nseg; ++i) k.segs[i] = segs[i];
   const int grid = k.nb_rows + k.nb_small + k.nb_sweep;
   switch (dim) {
-    case 32: hipLaunchKernelGGL(k_step_tail<32>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
-    case 64: hipLaunchKernelGGL(k_step_tail<64>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
-    case 128: hipLaunchKernelGGL(k_step_tail<128>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
-    default: hipLaunchKernelGGL(k_step_tail<256>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
+    case 32: hipLaunchKernelGGL(k_step_tail<32>, dim3(grid), dim3(GTR_TAIL_BLOCK), 0, s, k); break;
+    case 64: hipLaunchKernelGGL(k_step_tail<64>, dim3(grid), dim3(GTR_TAIL_BLOCK), 0, s, k); break;
+    case 128: hipLaunchKernelGGL(k_step_tail<128>, dim3(grid), dim3(GTR_TAIL_BLOCK), 0, s, k); break;
+    default: hipLaunchKernelGGL(k_step_tail<256>, dim3(grid), dim3(GTR_TAIL_BLOCK), 0, s, k); break;
   }
   GTR_HIP_CHECK_LAUNCH();
   return GTR_OK;

@@ -27,9 +27,16 @@ __device__ __forceinline__ int contrib_key(const gtr_batch& bt, int T, int j, in
   return key;
 }
 
+// No-op stand-in for the step-scalar wait of k_step_tail (bodies called with ready scalars).
+struct NoWait {
+  __device__ __forceinline__ void operator()() const {}
+};
+
 // Small parameters: element e of the flat buffer; its segment's gradient partials summed.
+// wait(): called after every load is issued, before `st` is first read.
+template <class Wait = NoWait>
 __device__ __forceinline__ void small_body(int64_t e, const gtr_segment* segs, int nseg, float* param, float* m,
-                                           float* v, float* grad_out, const AdamStep& st) {
+                                           float* v, float* grad_out, const AdamStep& st, Wait wait = Wait{}) {
   int s = -1;
   for (int i = 0; i < nseg; ++i)
     if (e >= segs[i].begin && e < segs[i].begin + segs[i].len) s = i;
@@ -43,6 +50,7 @@ __device__ __forceinline__ void small_body(int64_t e, const gtr_segment* segs, i
     return;
   }
   float pv = param[e], mv = m[e], vv = v[e];
+  wait();
   st.apply(pv, mv, vv, g);
   param[e] = pv;
   m[e] = mv;

@@ -244,7 +244,8 @@ class Engine:
     def choose_P(self, caps: Caps) -> int:
         # split-K of the weight gradients: <= 32 node rows per workgroup, <= 64 slabs (one
         # chunk over ~110 rows made k_wgrad 2x slower at C2: measured 0.105 -> 0.119 ms/step)
-        return max(1, min(64, (caps.n_cap + 31) // 32))
+        rows = max(1, int(os.environ.get("GTR_WGRAD_ROWS", "32")))  # diagnostics / tuning
+        return max(1, min(64, (caps.n_cap + rows - 1) // rows))
 
     def workspace(self, caps: Caps, fresh: bool = False) -> Workspace:
         if fresh:
