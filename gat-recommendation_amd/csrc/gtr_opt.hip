@@ -495,28 +495,40 @@ __device__ __forceinline__ void window_rows(int w, const gtr_batch& bt, int T, c
   }
 }
 
-// One wave more than the body waves: it loads the step counter and computes the step's
-// AdamW scalars (two f64 pow, ~1.7 us at C2 when every wave waited for them) while the
-// body waves issue their loads; they wait on s_ready only right before AdamW.
+// DEFER (small batches): one wave more than the body waves loads the step counter and
+// computes the step's AdamW scalars (two f64 pow, ~1.7 us at C2 when every wave waited
+// for them) while the body waves issue their loads; they wait on s_ready only right
+// before AdamW.  Large batches (windowed rows, HBM-bound) keep four-wave blocks: a fifth
+// wave costs them a resident block per CU (C3 B = 8192: 1.195 -> 1.232 ms).
 #define GTR_TAIL_BLOCK (GTR_BLOCK + 64)
 
-template <int D>
-__global__ __launch_bounds__(GTR_TAIL_BLOCK) void k_step_tail(TailK a) {
+template <int D, bool DEFER>
+__global__ __launch_bounds__(DEFER ? GTR_TAIL_BLOCK : GTR_BLOCK) void k_step_tail(TailK a) {
   __shared__ AdamStep s_st;
   __shared__ int32_t s_t;
   __shared__ int s_ready;
   __shared__ float s_acc[GTR_BLOCK];
   const int tid = threadIdx.x;
-  if (tid == 0) s_ready = 0;
-  __syncthreads();
-  if (tid >= GTR_BLOCK) {  // the step-scalar wave
-    if (tid == GTR_BLOCK) {
+  if constexpr (DEFER) {
+    if (tid == 0) s_ready = 0;
+    __syncthreads();
+    if (tid >= GTR_BLOCK) {  // the step-scalar wave
+      if (tid == GTR_BLOCK) {
+        const int64_t t = *a.opt.step_dev + a.opt.step_offset;
+        s_st.init(a.opt, t);
+        s_t = (int32_t)t;
+        __hip_atomic_store(&s_ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      return;
+    }
+  } else {
+    if (tid == 0) {
       const int64_t t = *a.opt.step_dev + a.opt.step_offset;
       s_st.init(a.opt, t);
       s_t = (int32_t)t;
-      __hip_atomic_store(&s_ready, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      s_ready = 1;
     }
-    return;
+    __syncthreads();
   }
   auto wait = [&]() {
     while (__hip_atomic_load(&s_ready, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
@@ -1462,10 +1474,13 @@ int gtr_step_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* t
   for (int i = 0; i < nseg; ++i) k.segs[i] = segs[i];
   const int grid = k.nb_rows + k.nb_small + k.nb_sweep;
   switch (dim) {
-    case 32: hipLaunchKernelGGL(k_step_tail<32>, dim3(grid), dim3(GTR_TAIL_BLOCK), 0, s, k); break;
-    case 64: hipLaunchKernelGGL(k_step_tail<64>, dim3(grid), dim3(GTR_TAIL_BLOCK), 0, s, k); break;
-    case 128: hipLaunchKernelGGL(k_step_tail<128>, dim3(grid), dim3(GTR_TAIL_BLOCK), 0, s, k); break;
-    default: hipLaunchKernelGGL(k_step_tail<256>, dim3(grid), dim3(GTR_TAIL_BLOCK), 0, s, k); break;
+#define GTR_TAIL(DD) if (k.windowed) hipLaunchKernelGGL((k_step_tail<DD, false>), dim3(grid), dim3(GTR_BLOCK), 0, s, k); \
+  else hipLaunchKernelGGL((k_step_tail<DD, true>), dim3(grid), dim3(GTR_TAIL_BLOCK), 0, s, k)
+    case 32: GTR_TAIL(32); break;
+    case 64: GTR_TAIL(64); break;
+    case 128: GTR_TAIL(128); break;
+    default: GTR_TAIL(256); break;
+#undef GTR_TAIL
   }
   GTR_HIP_CHECK_LAUNCH();
   return GTR_OK;
