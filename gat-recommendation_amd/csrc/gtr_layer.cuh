@@ -163,6 +163,9 @@ __device__ __forceinline__ void bn_parts_load(const float* part, int G, size_t r
 }
 
 // scr: >= 2*BLK + D floats of LDS.  Call with the whole block, after bn_parts_load.
+// Three barriers: each slice thread forms the slice totals itself (same order as one
+// thread per feature would), so the mean needs no LDS round of its own; the count of a
+// slice is the same for every feature and is kept once per slice.
 template <int D, int BLK>
 __device__ __forceinline__ void bn_fold_parts_(const float* part, int G, float eps, float* s_mean,
                                                float* s_rstd, float* s_uvar, float* scr, size_t rstride,
@@ -171,8 +174,8 @@ __device__ __forceinline__ void bn_fold_parts_(const float* part, int G, float e
   const int tid = threadIdx.x;
   const int j = tid % D, sl = tid / D;
   float* s_sum = scr;              // [NSL][D]
-  float* s_n = scr + NSL * D;      // [NSL][D] (the count repeated per feature)
-  float* s_mu = scr + 2 * NSL * D; // [D]
+  float* s_m2 = scr + NSL * D;     // [NSL][D]
+  float* s_n = scr + 2 * NSL * D;  // [NSL] (a slice's count)
   if (sl < NSL) {
     float n = 0.0f, sum = 0.0f;
 #pragma unroll
@@ -189,17 +192,14 @@ __device__ __forceinline__ void bn_fold_parts_(const float* part, int G, float e
       sum += c * pp[1 + j];
     }
     s_sum[sl * D + j] = sum;
-    s_n[sl * D + j] = n;
+    if (j == 0) s_n[sl] = n;
   }
   __syncthreads();
-  if (tid < D) {
-    float n = 0.0f, sum = 0.0f;
-    for (int q = 0; q < NSL; ++q) { n += s_n[q * D + tid]; sum += s_sum[q * D + tid]; }
-    s_mu[tid] = n > 0.0f ? sum / n : 0.0f;  // a bucket of empty groups merges to (0, 0, 0)
-  }
-  __syncthreads();
+  float n_tot = 0.0f, mean = 0.0f;
   if (sl < NSL) {
-    const float mean = s_mu[j];
+    float sum = 0.0f;
+    for (int q = 0; q < NSL; ++q) { n_tot += s_n[q]; sum += s_sum[q * D + j]; }
+    mean = n_tot > 0.0f ? sum / n_tot : 0.0f;  // a bucket of empty groups merges to (0, 0, 0)
     float m2 = 0.0f;
 #pragma unroll
     for (int u = 0; u < QR; ++u)
@@ -213,21 +213,21 @@ __device__ __forceinline__ void bn_fold_parts_(const float* part, int G, float e
       const float d = pp[1 + j] - mean;
       m2 += pp[1 + D + j] + pp[0] * d * d;
     }
-    s_sum[sl * D + j] = m2;
+    s_m2[sl * D + j] = m2;
   }
   __syncthreads();
-  if (tid < D) {
-    float n = 0.0f, m2 = 0.0f;
-    for (int q = 0; q < NSL; ++q) { n += s_n[q * D + tid]; m2 += s_sum[q * D + tid]; }
+  if (tid < D) {  // slice 0's threads: tid == j, n_tot and mean already formed
+    float m2 = 0.0f;
+    for (int q = 0; q < NSL; ++q) m2 += s_m2[q * D + tid];
     if (merged) {  // the G partials combined into one (count, mean, M2) row (may alias row 0)
-      merged[1 + tid] = s_mu[tid];
+      merged[1 + tid] = mean;
       merged[1 + D + tid] = m2;
-      if (tid == 0) merged[0] = n;
+      if (tid == 0) merged[0] = n_tot;
     } else {
-      const float var = m2 / n;
-      s_mean[tid] = s_mu[tid];
+      const float var = m2 / n_tot;
+      s_mean[tid] = mean;
       s_rstd[tid] = 1.0f / sqrtf(var + eps);
-      s_uvar[tid] = n > 1.0f ? m2 / (n - 1.0f) : var;
+      s_uvar[tid] = n_tot > 1.0f ? m2 / (n_tot - 1.0f) : var;
     }
   }
   __syncthreads();
