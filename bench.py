@@ -77,9 +77,10 @@ def main():
     ap.add_argument("--num-batches", type=int, default=64, help="distinct pre-staged batches per GPU")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--resident", action="store_true",
-                    help="launch on the pre-staged batch images (one graph per image) instead of copying each "
-                         "into the step's blob")
+    ap.add_argument("--resident", type=int, default=None,
+                    help="1: launch on the pre-staged batch images (one graph per image); 0: copy each image "
+                         "into the step's blob per step (default: 1 on one GPU without the sharded table, "
+                         "else 0)")
     ap.add_argument("--dp", action="store_true", help="force the data-parallel step (exchange) even at N=1")
     ap.add_argument("--global-batch", type=int, default=None,
                     help="strong scaling: fixed global batch split over the ranks, SyncBN (1 GPU semantics)")
@@ -153,10 +154,13 @@ def main():
                                                                    "touched", "stats"))
     log(f"data: T={T} sessions={data.num_sessions} edges={data.edge_keys.size} setup {time.time()-t0:.1f}s {st}")
 
-    # default: each step copies its pre-staged batch image into the step's blob (one D2D
-    # copy, inside the timed step); --resident launches straight on the images instead
-    # (FusedTrainStep.bind_resident: one captured graph per image) -- measured equal
-    resident = args.resident
+    # one GPU: each step launches straight on its pre-staged batch image, already in HBM
+    # (FusedTrainStep.bind_resident: one captured graph per image; C2 0.0808 -> 0.0796 ms).
+    # --resident 0, and N > 1 (data-parallel exchange, not exercised on resident images) or
+    # the sharded table: each step copies its image into the step's blob (one D2D copy,
+    # inside the timed step).
+    resident = bool(args.resident) if args.resident is not None else (world == 1 and not shard and not args.dp
+                                                                          and not args.sync_bn and not args.no_graph)
     if resident:
         step.bind_resident(staged)
 
@@ -262,7 +266,7 @@ def main():
                 "dp_exchange": ("row-sharded table: all-to-all of row ids, rows and row gradients "
                                 f"({step.shard.volume()})") if shard else step.dp is not None,
                 "hip_graph": not args.no_graph,
-                "batch_images": "resident, one graph per image" if args.resident else "copied per step (D2D)",
+                "batch_images": "resident, one graph per image" if resident else "copied per step (D2D)",
                 "lazy_table": lazy,
                 "lagged_sweep": lagged,
                 "gemm": gemm_mode(D),

@@ -405,9 +405,11 @@ def test_lazy_table_flushes_before_eval_forward():
     assert not f2._dirty
 
 
-def test_resident_images_equal_copied_blob():
+@pytest.mark.parametrize("lazy", [False, True])
+def test_resident_images_equal_copied_blob(lazy):
     """bind_resident / run_resident (one captured graph per resident batch image, no copy
-    into the step's blob) trains bit for bit like load + run, images reused included."""
+    into the step's blob; bench.py's one-GPU default) trains bit for bit like load + run,
+    images reused included, with the eager sweep and with the lazy table."""
     from etpgt.data.batch import Caps
 
     T = data().table_rows
@@ -416,8 +418,8 @@ def test_resident_images_equal_copied_blob():
     m1.train(); m2.train()
     bl = batches(data(), 32, 5, 3, seed=14)
     caps = Caps(max(b.num_nodes for b in bl), 32, max(b.num_edges for b in bl), 5)
-    f1 = FusedTrainStep(m1, loss="bpr", caps=caps)
-    f2 = FusedTrainStep(m2, loss="bpr", caps=caps)
+    f1 = FusedTrainStep(m1, loss="bpr", caps=caps, lazy=lazy)
+    f2 = FusedTrainStep(m2, loss="bpr", caps=caps, lazy=lazy)
     staged = [torch.from_numpy(b.packed(f2.caps)[1]).cuda() for b in bl]
     f2.bind_resident(staged)
     order = [0, 1, 2, 1, 0, 2]
@@ -426,6 +428,9 @@ def test_resident_images_equal_copied_blob():
     f2.prepare_resident()
     for i in order[2:]:
         assert float(f1(bl[i].to("cuda"))) == float(f2.run_resident(i))
+    if lazy:
+        f1.flush()
+        f2.flush()
     for a, b in zip(m1.parameters(), m2.parameters()):
         assert torch.equal(a, b)
 
