@@ -173,6 +173,8 @@ def main():
     for i in range(args.warmup):
         one(i)
     if resident and not args.no_graph:
+        if args.warmup == 0:
+            one(0)  # the images' graphs are captured after one eager step (FusedTrainStep)
         step.prepare_resident()  # no capture inside the timed region
     torch.cuda.synchronize(dev)
     if world > 1:
