@@ -79,6 +79,7 @@ struct BBK {
   int32_t* scratch;             // [2 * b_cap]: edge offset, node offset per session
   int32_t* status;              // [2]: this batch's code (1 over capacity, 2 negatives unsatisfiable), sticky OR
   int32_t B, T, max_len, R, S, seed;
+  int64_t stride;               // cursor advance per batch (B; the global batch across ranks)
 };
 
 // The session's last max_len clicks (one per lane, lanes >= len hold INT_MAX), its
@@ -218,7 +219,7 @@ __global__ __launch_bounds__(BB_SCAN_BLOCK) void k_bb_scan(BBK a) {
     a.status[0] = over ? 1 : 0;
     if (over) a.status[1] |= 1;  // sticky over the batches built since the host cleared it
     *a.start = cur;
-    *a.cursor = cur + B;
+    *a.cursor = cur + a.stride;
   }
   if (over) return;
   int32_t* node_ptr = const_cast<int32_t*>(bt.node_ptr);
@@ -382,15 +383,16 @@ extern "C" int gtr_session_counts(const gtr_sessions* ss, const uint64_t* slots,
   return GTR_OK;
 }
 
-extern "C" int gtr_build_batch(const gtr_sessions* ss, const uint64_t* slots, int64_t num_slots, int max_len,
-                               const int32_t* order, int64_t* cursor, int B, int row_group, uint32_t seed,
-                               const gtr_batch* out, int32_t* scratch, int64_t* start, int32_t* status,
-                               gtr_stream_t stream) {
+extern "C" int gtr_build_batch_strided(const gtr_sessions* ss, const uint64_t* slots, int64_t num_slots,
+                                       int max_len, const int32_t* order, int64_t* cursor, int B, int64_t stride,
+                                       int row_group, uint32_t seed, const gtr_batch* out, int32_t* scratch,
+                                       int64_t* start, int32_t* status, gtr_stream_t stream) {
   if (!ss || !ss->sess_ptr || !ss->sess_items || !ss->sess_nodes || !ss->sess_edges || !slots || !order ||
       !cursor || !out || !scratch || !start || !status || B <= 0 || B > BB_BMAX || B > out->b_cap ||
       max_len < 2 || max_len > 64 || row_group <= 0 || ss->num_items < 2 || ss->num_sessions <= 0 ||
-      out->n_neg <= 0) {
-    set_error("gtr_build_batch: bad arguments (1 <= B <= min(b_cap, %d), 2 <= max_len <= 64)", BB_BMAX);
+      out->n_neg <= 0 || stride < B) {
+    set_error("gtr_build_batch: bad arguments (1 <= B <= min(b_cap, %d), 2 <= max_len <= 64, stride >= B)",
+              BB_BMAX);
     return GTR_E_ARG;
   }
   BBK k{};
@@ -402,10 +404,19 @@ extern "C" int gtr_build_batch(const gtr_sessions* ss, const uint64_t* slots, in
   k.scratch = scratch; k.status = status;
   k.B = B; k.T = ss->num_items; k.max_len = max_len; k.R = row_group; k.S = ss->num_sessions;
   k.seed = (int32_t)seed;
+  k.stride = stride;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_bb_scan, dim3(1), dim3(BB_SCAN_BLOCK), 0, s, k);
   GTR_HIP_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_bb_write, dim3((B + BB_WAVES - 1) / BB_WAVES), dim3(BB_BLOCK), 0, s, k);
   GTR_HIP_CHECK_LAUNCH();
   return GTR_OK;
+}
+
+extern "C" int gtr_build_batch(const gtr_sessions* ss, const uint64_t* slots, int64_t num_slots, int max_len,
+                               const int32_t* order, int64_t* cursor, int B, int row_group, uint32_t seed,
+                               const gtr_batch* out, int32_t* scratch, int64_t* start, int32_t* status,
+                               gtr_stream_t stream) {
+  return gtr_build_batch_strided(ss, slots, num_slots, max_len, order, cursor, B, (int64_t)B, row_group, seed, out,
+                                 scratch, start, status, stream);
 }

@@ -1114,10 +1114,9 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const int32_t* kin, c
   }
 }
 
-int sort_mode() {  // 0: own radix (default), 1: hipCUB, 2: rocPRIM Onesweep
+int sort_mode() {  // 0: own radix (default), 1: hipCUB
   const char* e = getenv("GTR_SORT");
   if (e && (e[0] == 'm' || e[0] == 'M' || e[0] == 'h' || e[0] == 'H')) return 1;
-  if (e && (e[0] == 'o' || e[0] == 'O')) return 2;
   return 0;
 }
 
@@ -1159,15 +1158,10 @@ hipError_t rs_sort(void* tmp, const int32_t* keys, int32_t* skeys, const int32_t
 // Stable (key, slot) sort of the contribution list, GTR_SORT selecting the algorithm:
 //   default  the own radix above (6 launches for keys < 2^20);
 //   merge    hipCUB / rocPRIM's default config: block sort + merge passes below 1M items
-//            (~20 launches at m_cap ~ 855k);
-//   onesweep rocPRIM Onesweep (merge-sort limit 0): one histogram launch + one per digit.
-//            Correct standalone and in a captured graph (scripts/dbg/onesweep.hip), but it
-//            faulted (illegal address in radix_sort_onesweep_iteration) inside the C3
-//            B = 8192 fused step with a workspace sized by this same config; not used.
-// All three are stable, so they sort identically.  The workspace query and the sort MUST
-// use the same algorithm (gtr_contrib_sort checks the size).
-using OnesweepConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                                  rocprim::default_config, 0>;
+//            (~20 launches at m_cap ~ 855k).
+// Both are stable, so they sort identically.  The workspace query and the sort MUST use
+// the same algorithm (gtr_contrib_sort checks the size).  (A rocPRIM Onesweep option was
+// removed in round 3: it faulted inside the C3 B = 8192 step without a found cause.)
 hipError_t sort_pairs(void* tmp, size_t& bytes, const int32_t* keys, int32_t* skeys, const int32_t* vals,
                       int32_t* svals, int n, int bits, hipStream_t s) {
   if (sort_mode() == 0) {
@@ -1177,8 +1171,6 @@ hipError_t sort_pairs(void* tmp, size_t& bytes, const int32_t* keys, int32_t* sk
     }
     return rs_sort(tmp, keys, skeys, vals, svals, n, bits, s);
   }
-  if (sort_mode() == 2)
-    return rocprim::radix_sort_pairs<OnesweepConfig>(tmp, bytes, keys, skeys, vals, svals, (size_t)n, 0, bits, s);
   return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, keys, skeys, vals, svals, n, 0, bits, s);
 }
 
@@ -1256,8 +1248,7 @@ int gtr_contrib_sort_bytes(int m_cap, int num_items, size_t* bytes) {
 int gtr_contrib_sort(const int32_t* keys, const int32_t* vals, int32_t* skeys, int32_t* svals, int m_cap,
                      int num_items, void* tmp, size_t tmp_bytes, gtr_stream_t stream) {
   // The temporary storage must be sized by the SAME algorithm and key width as this call
-  // (gtr_contrib_sort_bytes): round 1's rocPRIM Onesweep trial faulted (illegal address)
-  // because its workspace was still sized for hipCUB's merge-sort path, which needs less.
+  // (gtr_contrib_sort_bytes): a workspace sized for another algorithm is refused.
   size_t need = 0;
   if (gtr_contrib_sort_bytes(m_cap, num_items, &need) != GTR_OK) return GTR_E_ARG;
   if (!keys || !vals || !skeys || !svals || !tmp || tmp_bytes < need) {

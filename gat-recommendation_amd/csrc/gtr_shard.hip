@@ -23,7 +23,8 @@
 //
 // Slot 0 of every peer block carries the block's count; capacities are fixed so that the
 // collectives and kernels replay from one captured hipGraph.  A block that would overflow
-// its capacity sets status[0] (sticky in status[1]); the host checks it.
+// its capacity sets status[0] (sticky in status[1]); the flag travels in the small pack, so
+// every owner applies such a step as a zero-gradient step and every rank's host raises.
 
 #include "gtr_rows.cuh"
 
@@ -226,6 +227,7 @@ struct PackK {
   const int32_t* ckeys;
   float* send_grads;
   float* small_pack;
+  const int32_t* status;  // this rank's overflow flag of the step (status[0]) -> small_pack[F + 1]
   int T, nb_rows, nseg, m_cap;
   gtr_segment segs[GTR_SMALL_MAX_SEG];
 };
@@ -285,6 +287,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_shard_pack(PackK a) {
         t = a.tl.loss_out[0];
       }
       a.small_pack[a.tl.flat_total] = t;
+      a.small_pack[a.tl.flat_total + 1] = a.status[0] != 0 ? 1.0f : 0.0f;
     }
   }
 }
@@ -329,7 +332,15 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_shard_update(UpdateK a) {
   const int32_t t = s_t;
   const int W = sh.world;
   const float inv_w = 1.0f / (float)W;
+  // a step on which ANY rank overflowed an exchange block carries incomplete gradients: it
+  // is applied as a zero-gradient step (touched rows stay at t - 1 and are caught up with
+  // g = 0 when next read; the small parameters take g = 0), and every rank's sticky status
+  // records it, so the host raises on every rank and no partial update is ever applied
+  bool bad = false;
+  for (int q = 0; q < W; ++q) bad = bad || a.small_all[(size_t)q * a.small_words + a.tl.flat_total + 1] != 0.0f;
+  if (bad && blockIdx.x == 0 && tid == 0) atomicOr(sh.status + 1, 2);
   if ((int)blockIdx.x < a.nb_rows) {
+    if (bad) return;
     const int64_t gid = (int64_t)blockIdx.x * GTR_BLOCK + tid;
     const int64_t e = gid / C4;
     const int c = (int)(gid - e * C4);
@@ -366,7 +377,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_shard_update(UpdateK a) {
   if (e < F) {
     float g = 0.0f;
     for (int q = 0; q < W; ++q) g += a.small_all[(size_t)q * a.small_words + e];
-    g *= inv_w;
+    g = bad ? 0.0f : g * inv_w;
     float pv = a.tl.flat[e], mv = a.tl.flat_m[e], vv = a.tl.flat_v[e];
     st.apply(pv, mv, vv, g);
     a.tl.flat[e] = pv;
@@ -468,6 +479,7 @@ int gtr_shard_pack(const gtr_batch* bt, const gtr_shard* sh, const gtr_tail* tai
   k.ckeys = ckeys;
   k.send_grads = send_grads;
   k.small_pack = small_pack;
+  k.status = sh->status;
   k.T = sh->num_items;
   k.m_cap = bt->n_cap + bt->b_cap * (1 + bt->n_neg);
   const int NG = GTR_BLOCK / (sh->dim / 4);
@@ -490,7 +502,7 @@ int gtr_shard_pack(const gtr_batch* bt, const gtr_shard* sh, const gtr_tail* tai
 
 int gtr_shard_update(const gtr_shard* sh, const gtr_tail* tail, const int32_t* recv_ids, const float* recv_grads,
                      const float* small_all, int64_t small_words, gtr_stream_t stream) {
-  if (!shard_ok(sh) || !tail || !recv_ids || !recv_grads || !small_all || small_words < tail->flat_total + 1 ||
+  if (!shard_ok(sh) || !tail || !recv_ids || !recv_grads || !small_all || small_words < tail->flat_total + 2 ||
       (tail->flat_total > 0 && (!tail->flat || !tail->flat_m || !tail->flat_v))) {
     set_error("gtr_shard_update: bad arguments");
     return GTR_E_ARG;

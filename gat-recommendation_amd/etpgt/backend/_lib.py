@@ -167,6 +167,7 @@ _SIGS = {
     "gtr_edge_hash_build": (C.c_int, [P, i64, P, i64, P]),
     "gtr_session_counts": (C.c_int, [P, P, i64, C.c_int, P, P, P]),
     "gtr_build_batch": (C.c_int, [P, P, i64, C.c_int, P, P, C.c_int, C.c_int, u32, P, P, P, P, P]),
+    "gtr_build_batch_strided": (C.c_int, [P, P, i64, C.c_int, P, P, C.c_int, i64, C.c_int, u32, P, P, P, P, P]),
     "gtr_lap_build": (C.c_int, [P, P, C.c_int, P, P, P]),
     "gtr_lap_plan": (C.c_int, [P, C.c_int, C.c_int, P, P, P, P, P]),
     "gtr_lap_spmm": (C.c_int, [P, P, C.c_int, C.c_int, P, i64, P, i64, P, P, P, f32, f32, P]),

@@ -86,13 +86,21 @@ class GpuSessionStore:
 class GpuBatchBuilder:
     """Batches of ``batch_size`` sessions in epoch order, built on the device."""
 
-    def __init__(self, store: GpuSessionStore, batch_size: int, num_negatives: int, seed: int = 0):
+    def __init__(self, store: GpuSessionStore, batch_size: int, num_negatives: int, seed: int = 0,
+                 stride: int | None = None):
+        """``stride``: positions the cursor advances per batch (default ``batch_size``); a
+        data-parallel rank r of P builds its share of each global batch with
+        ``stride = P * batch_size`` from a cursor started at ``r * batch_size``
+        (gtr_build_batch_strided)."""
         if batch_size <= 0 or batch_size > 16384:
             raise ValueError("batch_size must be in [1, 16384] on the GPU batch constructor")
         if num_negatives <= 0:
             raise ValueError("num_negatives must be positive")
+        if stride is not None and stride < batch_size:
+            raise ValueError("stride must be >= batch_size")
         self.store = store
         self.B = int(batch_size)
+        self.stride = int(batch_size if stride is None else stride)
         self.n_neg = int(num_negatives)
         self.seed = int(seed) & 0x7FFFFFFF
         dev = store.device
@@ -112,19 +120,24 @@ class GpuBatchBuilder:
             raise ValueError("order must list session ids in [0, S)")
         self.order_h = o
         self.order_d = torch.from_numpy(o.astype(np.int32)).to(self.store.device)
+        self.seek(position)
+
+    def seek(self, position: int) -> None:
+        """Put the cursor at ``position`` (the next batch's first session)."""
         self.cursor.fill_(int(position))
         self.pos = int(position)
 
     def batch_sizes(self, num_batches: int, position: int = 0) -> tuple[np.ndarray, np.ndarray]:
         """(N, E) of the next ``num_batches`` batches from ``position`` (host, from the counts)."""
-        idx = (position + np.arange(num_batches * self.B)) % self.order_h.size
-        sess = self.order_h[idx].reshape(num_batches, self.B)
+        idx = (position + self.stride * np.arange(num_batches)[:, None] + np.arange(self.B)[None, :]) \
+            % self.order_h.size
+        sess = self.order_h[idx]
         return self.store.nodes[sess].sum(1), self.store.edges[sess].sum(1)
 
     def plan_caps(self, num_batches: int | None = None, position: int = 0) -> Caps:
         """Capacities covering the next ``num_batches`` batches (default: one epoch)."""
         if num_batches is None:
-            num_batches = max(1, -(-self.order_h.size // self.B))
+            num_batches = max(1, -(-self.order_h.size // self.stride))
         N, E = self.batch_sizes(num_batches, position)
         return Caps.bucket(int(N.max()), self.B, max(int(E.max()), 1), self.n_neg)
 
@@ -137,11 +150,13 @@ class GpuBatchBuilder:
         if self.scratch is None or self.scratch.numel() < 2 * caps.b_cap:
             self.scratch = torch.zeros(2 * caps.b_cap, dtype=torch.int32, device=self.store.device)
         st = self.store
-        L.check(L.lib().gtr_build_batch(C.byref(st.ss), st.slots.data_ptr(), st.num_slots, st.max_len,
-                                        self.order_d.data_ptr(), self.cursor.data_ptr(), B, caps.R,
-                                        self.seed, C.byref(bs), self.scratch.data_ptr(), self.start.data_ptr(),
-                                        self.status.data_ptr(), stream), "build_batch")
-        self.pos += B
+        stride = max(self.stride, B)
+        L.check(L.lib().gtr_build_batch_strided(C.byref(st.ss), st.slots.data_ptr(), st.num_slots, st.max_len,
+                                                self.order_d.data_ptr(), self.cursor.data_ptr(), B, stride, caps.R,
+                                                self.seed, C.byref(bs), self.scratch.data_ptr(),
+                                                self.start.data_ptr(), self.status.data_ptr(), stream),
+                "build_batch")
+        self.pos += stride
 
     def check_status(self) -> None:
         """Raise if any batch built since the last check failed (host sync)."""

@@ -120,17 +120,14 @@ def session_example(data: SyntheticData, s: int, num_neg: int, rng: np.random.Ge
     pos = np.minimum(pos, data.edge_keys.shape[0] - 1)
     hit = data.edge_keys[pos] == k
     ei = np.stack([ia[hit], ib[hit]]).astype(np.int64)
-    seen = set(int(v) for v in seq)
+    seen = np.unique(seq)
     negs = np.empty(num_neg, np.int64)
     filled = 0
-    while filled < num_neg:
+    while filled < num_neg:  # the first candidates outside the session, in draw order
         cand = rng.integers(1, T, size=num_neg * 2)
-        for c in cand:
-            if int(c) not in seen:
-                negs[filled] = c
-                filled += 1
-                if filled == num_neg:
-                    break
+        ok = cand[~np.isin(cand, seen)][: num_neg - filled]
+        negs[filled: filled + ok.size] = ok
+        filled += ok.size
     return {"x": uniq.astype(np.int64), "edge_index": ei, "target_item": int(seq[-1]), "negative_items": negs}
 
 

@@ -118,14 +118,18 @@ def collate_fn(batch: list[dict]) -> SessionBatch:
 def create_dataloader(sessions_path: Path | str, graph_edges_path: Path | str, batch_size: int = 32,
                       num_negatives: int = 5, max_session_length: int = 50, shuffle: bool = True,
                       num_workers: int = 0, device_builder: bool = False, device: str = "cuda",
-                      seed: int = 0):
+                      seed: int = 0, rank: int = 0, world: int = 1):
     """dataloader.py:205-241.  ``device_builder=True`` returns a ``DeviceSessionLoader``:
     the same epochs (order, batch sizes, last partial batch) built on the GPU
     (etpgt.data.gpu_batch) instead of host workers; ``Trainer`` then captures the build
-    inside the fused step."""
+    inside the fused step.  ``rank`` / ``world`` (device builder only): this rank's share
+    of each global batch of ``world * batch_size`` sessions (data parallel)."""
     ds = SessionDataset(sessions_path, graph_edges_path, num_negatives, max_session_length)
     if device_builder:
-        return DeviceSessionLoader(ds, batch_size, num_negatives, shuffle=shuffle, device=device, seed=seed)
+        return DeviceSessionLoader(ds, batch_size, num_negatives, shuffle=shuffle, device=device, seed=seed,
+                                   rank=rank, world=world)
+    if world > 1:
+        raise NotImplementedError("data-parallel training builds its batches on the GPU (device_builder=True)")
     return torch.utils.data.DataLoader(ds, batch_size=batch_size, shuffle=shuffle, num_workers=num_workers,
                                        collate_fn=collate_fn)
 
@@ -134,10 +138,17 @@ class DeviceSessionLoader:
     """The epochs of ``DataLoader(SessionDataset, batch_size, shuffle, collate_fn)`` with
     every batch built on the GPU.
 
-    * Order: ``shuffle=True`` draws each epoch's permutation exactly as the DataLoader's
-      ``RandomSampler`` does (a generator seeded from the global torch RNG, then
-      ``torch.randperm``), so a run seeded like the reference visits sessions in the
-      reference's order; ``shuffle=False`` walks session-id order.
+    * Order: every epoch consumes the global torch RNG exactly as iterating a
+      ``DataLoader(shuffle=...)`` does: one int64 draw for the iterator's ``_base_seed``
+      (``_BaseDataLoaderIter.__init__``), then -- ``shuffle=True`` -- the
+      ``RandomSampler``'s seed draw and ``torch.randperm`` under it; ``shuffle=False``
+      walks session-id order.  A run seeded like the reference therefore visits its first
+      epoch in the reference's order (pinned against a real DataLoader in
+      tests/test_host.py), and every later epoch too when nothing else draws from the
+      global CPU generator between epochs -- true for the reference's CUDA runs with
+      ``num_workers > 0`` (its default 4: the per-sample ``torch.randint`` negatives of
+      dataloader.py:107-124 draw inside the workers).  With ``num_workers=0`` those draws
+      consume the main process's generator, so later epochs' orders differ.
     * Batches: ``len(loader)`` = ceil(S / batch_size), the last one partial
       (``drop_last=False``).
     * Per session: the reference's example (last ``max_session_length`` clicks, target,
@@ -147,29 +158,52 @@ class DeviceSessionLoader:
       fresh every epoch).
     Iterating yields ``DeviceBatch`` objects (PyG-Batch-like views of HBM images) for any
     consumer; ``Trainer``'s fused step instead attaches ``builder`` and builds inside its
-    captured graph."""
+    captured graph.
+
+    Data parallel (``world`` > 1, one process per GPU): every rank draws the same epoch
+    order (same seed, same global-RNG draws) and rank r builds sessions
+    [i*P*B + r*B, +B) of it for global batch i -- with the position-keyed negatives a
+    single GPU draws for that global batch of P*B sessions (gtr_build_batch_strided).  The
+    epoch is the full global batches, then -- when the remaining R sessions give every rank
+    at least one -- a last global batch of P*floor(R/P) sessions split evenly; the
+    R mod P sessions left over are dropped (DistributedSampler's drop_last rule, so that
+    every rank's loss mean weighs equally)."""
 
     def __init__(self, dataset: SessionDataset, batch_size: int, num_negatives: int, shuffle: bool = True,
-                 device: str = "cuda", seed: int = 0):
+                 device: str = "cuda", seed: int = 0, rank: int = 0, world: int = 1):
         from etpgt.data.gpu_batch import GpuBatchBuilder, GpuSessionStore
 
+        if not 0 <= rank < world:
+            raise ValueError("rank must lie in [0, world)")
         self.dataset = dataset
         self.batch_size = int(batch_size)
         self.shuffle = bool(shuffle)
+        self.rank, self.world = int(rank), int(world)
         self.store = GpuSessionStore.from_dataset(dataset, device)
-        self.builder = GpuBatchBuilder(self.store, self.batch_size, num_negatives, seed=seed)
+        self.builder = GpuBatchBuilder(self.store, self.batch_size, num_negatives, seed=seed,
+                                       stride=self.batch_size * self.world)
         self.epoch = -1
         self.order = None
 
     def __len__(self) -> int:
-        return -(-len(self.dataset) // self.batch_size)
+        return len(self.batch_sizes())
 
     def batch_sizes(self) -> list[int]:
-        S, B = len(self.dataset), self.batch_size
-        return [min(B, S - i * B) for i in range(len(self))]
+        """Sessions of this rank's batches in an epoch."""
+        S, B, P = len(self.dataset), self.batch_size, self.world
+        full, rem = divmod(S, B * P)
+        last = rem // P
+        return [B] * full + ([last] if last > 0 else [])
+
+    def batch_start(self, i: int) -> int:
+        """Cursor position (epoch order, plus epoch * S) of this rank's batch i."""
+        S, B, P = len(self.dataset), self.batch_size, self.world
+        b = self.batch_sizes()[i]
+        return self.epoch * S + i * B * P + self.rank * b
 
     def _epoch_order(self) -> np.ndarray:
         n = len(self.dataset)
+        torch.empty((), dtype=torch.int64).random_()  # _BaseDataLoaderIter.__init__: _base_seed
         if not self.shuffle:
             return np.arange(n, dtype=np.int64)
         seed = int(torch.empty((), dtype=torch.int64).random_().item())  # RandomSampler.__iter__
@@ -181,9 +215,10 @@ class DeviceSessionLoader:
         """Draw the next epoch's order and put the builder at its start."""
         self.epoch += 1
         self.order = self._epoch_order()
-        self.builder.set_epoch_order(self.order, position=self.epoch * len(self.dataset))
+        self.builder.set_epoch_order(self.order, position=self.epoch * len(self.dataset) + self.rank * self.batch_size)
 
     def __iter__(self):
         self.start_epoch()
-        for b in self.batch_sizes():
+        for i, b in enumerate(self.batch_sizes()):
+            self.builder.seek(self.batch_start(i))
             yield self.builder.build_device_batch(b)

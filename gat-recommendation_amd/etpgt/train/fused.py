@@ -210,13 +210,15 @@ class FusedTrainStep:
         # data parallel: the union of the ranks' touched rows is known once the sorted keys
         # are all-gathered (early, overlapped with the forward), so only the launches after
         # the union stamp (readout, conv_bwd) can sweep
+        # (never with the row-sharded table: its moments / stamps live in the shards, and the
+        # model's table copy is stale -- no chain sweep may touch them)
         self.early_union = (self.data_parallel and chain and not self.sync_bn and not self.lagged
-                            and os.environ.get("GTR_DP_EARLY", "0") == "1")
+                            and not self.shard_table and os.environ.get("GTR_DP_EARLY", "0") == "1")
         if self.early_union:
             wts = [0.0] * eng.L + wts[eng.L:]
         slots = len(wts)
-        if chain and (not self.data_parallel or self.early_union or self.lagged) and self.ws.g_cap <= 128 \
-                and slots <= L.SWEEP_SLOTS:
+        if chain and not self.shard_table and (not self.data_parallel or self.early_union or self.lagged) \
+                and self.ws.g_cap <= 128 and slots <= L.SWEEP_SLOTS:
             sw = L.GtrSweep()
             sw.table = eng.model.item_embedding.weight.data_ptr()
             sw.m, sw.v, sw.stamp = self.m_tab.data_ptr(), self.v_tab.data_ptr(), self.stamp.data_ptr()

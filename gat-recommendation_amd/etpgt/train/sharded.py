@@ -105,9 +105,18 @@ class ShardState:
         return True
 
     def check_status(self, block: bool = False):
-        """Raise if any step since the last check overflowed an exchange block (the
-        status word is copied asynchronously after each step and read one step later)."""
-        if self._status_event is not None and (block or self._status_event.query()):
+        """Raise if any step since the last check overflowed an exchange block.  The
+        per-step check copies the status word asynchronously and reads it one step later;
+        ``block=True`` (sync_table / export) waits for every queued step and reads the
+        word as it stands after the LAST one."""
+        if block:
+            torch.cuda.current_stream(self.step.dev).synchronize()
+            self._status_event = None
+            if int(self.status[1].item()) != 0:
+                raise RuntimeError("row-sharded table: a batch requested more rows from one owner than the "
+                                   "exchange capacity holds (raise GTR_SHARD_SLACK)")
+            return
+        if self._status_event is not None and self._status_event.query():
             self._status_event.synchronize()
             if int(self.status_host[1]) != 0:
                 raise RuntimeError("row-sharded table: a batch requested more rows from one owner than the "
@@ -177,7 +186,7 @@ class ShardExchange:
         L.check(L.lib().gtr_shard_route_scratch(self.m_cap, P, C.byref(nb)), "shard_route_scratch")
         self.scratch = torch.zeros(max(int(nb.value), 16), dtype=torch.uint8, device=dev)
         F = eng.flat.layout.total
-        self.small_words = (F + 1 + 3) & ~3
+        self.small_words = (F + 2 + 3) & ~3  # flat gradient | loss | overflow flag
         self.small_pack = torch.zeros(self.small_words, **f32)
         self.small_all = torch.zeros(P, self.small_words, **f32)
         self.bs_c = self._compact(step.bs)

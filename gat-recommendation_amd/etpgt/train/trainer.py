@@ -42,7 +42,16 @@ class Trainer:
     def __init__(self, model: nn.Module, train_loader, val_loader, optimizer: torch.optim.Optimizer,
                  device: str = "cuda", output_dir: Path | str = "outputs", max_epochs: int = 100,
                  patience: int = 10, eval_every: int = 1, k_values: list[int] | None = None,
-                 loss_fn: nn.Module | None = None, fused: bool | None = None):
+                 loss_fn: nn.Module | None = None, fused: bool | None = None, sync_bn: bool | None = None):
+        """Reference signature (trainer.py:23-67) plus two optional keywords: ``fused``
+        (force / forbid the fused HIP step) and ``sync_bn`` (data parallel: BatchNorm
+        statistics over every rank's batch; default on when the default process group spans
+        more than one rank, so P ranks train exactly like one GPU on the global batch).
+        Under a process group only rank 0 writes checkpoints and history.json."""
+        from etpgt.train.distributed import world_info
+
+        self.rank, self.world = world_info()
+        self.sync_bn = (self.world > 1) if sync_bn is None else bool(sync_bn)
         self.model = model.to(device)
         self.train_loader = train_loader
         self.val_loader = val_loader
@@ -89,7 +98,8 @@ class Trainer:
         g = opt.param_groups[0]
         self._fused = FusedTrainStep(self.model, lr=g["lr"], betas=g["betas"], eps=g["eps"],
                                      weight_decay=g["weight_decay"], decoupled=type(opt) is torch.optim.AdamW,
-                                     loss=spec[0], temperature=spec[1], alpha=spec[2])
+                                     loss=spec[0], temperature=spec[1], alpha=spec[2],
+                                     sync_bn=self.sync_bn and self.world > 1)
         return self._fused
 
     def _sync_optimizer_state(self):
@@ -112,8 +122,12 @@ class Trainer:
             if not fused.caps.fits(caps.n_cap, caps.b_cap, caps.e_cap, caps.n_neg):
                 fused.attach_builder(bld, num_batches=len(sizes))
         total = torch.zeros((), dtype=torch.float64, device=self.device)
-        for b in sizes:
-            loss = fused.run() if b == loader.batch_size else fused.run_partial(b)
+        for i, b in enumerate(sizes):
+            if b == loader.batch_size:
+                loss = fused.run()  # the captured build advances the cursor by the global batch
+            else:
+                bld.seek(loader.batch_start(i))  # last, partial batch: this rank's even share
+                loss = fused.run_partial(b)
             total += loss
         bld.check_status()
         return float(total.item()) / max(len(sizes), 1)
@@ -169,6 +183,8 @@ class Trainer:
 
     def save_checkpoint(self, is_best: bool = False) -> None:
         self._sync_optimizer_state()
+        if self.rank != 0:  # replicas are identical: one writer
+            return
         ckpt = {
             "epoch": self.current_epoch,
             "model_state_dict": self.model.state_dict(),
@@ -201,6 +217,7 @@ class Trainer:
                     logger.info(f"Early stopping at epoch {epoch}")
                     break
         self._sync_optimizer_state()
-        with open(self.output_dir / "history.json", "w") as f:
-            json.dump(self.history, f, indent=2)
+        if self.rank == 0:
+            with open(self.output_dir / "history.json", "w") as f:
+                json.dump(self.history, f, indent=2)
         return self.history

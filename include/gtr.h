@@ -465,7 +465,8 @@ typedef struct gtr_shard {
   float* consts;       /* [consts_cap][2] per-step AdamW scalars (gtr_lazy)     */
   int32_t consts_cap;
   int32_t pad;
-  int32_t* status;     /* [2]: [0] this step overflowed a block, [1] sticky     */
+  int32_t* status;     /* [2]: [0] this step overflowed a block, [1] sticky:
+                        * bit 0 this rank overflowed, bit 1 some rank did      */
   gtr_adam opt;        /* by value; step_offset 0 (runs after gtr_step_begin)   */
 } gtr_shard;
 
@@ -484,13 +485,15 @@ int gtr_shard_route(const gtr_batch* bt, const int32_t* skeys, const int32_t* sv
  * to step t-1, into send_rows [P][cap][D] (row j of block r = recv_ids[r][j]).       */
 int gtr_shard_serve(const gtr_shard* sh, const int32_t* recv_ids, float* send_rows, gtr_stream_t stream);
 /* Requester: summed table-gradient row of every requested row -> send_grads [P][cap][D]
- * at its compact slot; summed small-parameter gradient [flat_total] + local loss ->
- * small_pack [flat_total + 1].                                                        */
+ * at its compact slot; summed small-parameter gradient [flat_total] + local loss +
+ * this step's overflow flag -> small_pack [flat_total + 2].                           */
 int gtr_shard_pack(const gtr_batch* bt, const gtr_shard* sh, const gtr_tail* tail, const int32_t* ckeys,
                    const gtr_segment* segs, int nseg, float* send_grads, float* small_pack, gtr_stream_t stream);
 /* Owner: AdamW at step t of every requested row with the rank-averaged gradient (peers
  * summed in rank order), stamps t, consts[t]; small parameters from small_all
- * [P][small_words] (rank-averaged) and the rank-averaged loss -> tail->loss_out.      */
+ * [P][small_words >= flat_total + 2] (rank-averaged) and the rank-averaged loss ->
+ * tail->loss_out.  If any rank's pack carries the overflow flag, the step is applied
+ * with zero gradients (rows unstamped, caught up later) and status[1] |= 2.          */
 int gtr_shard_update(const gtr_shard* sh, const gtr_tail* tail, const int32_t* recv_ids, const float* recv_grads,
                      const float* small_all, int64_t small_words, gtr_stream_t stream);
 
@@ -547,6 +550,14 @@ int gtr_build_batch(const gtr_sessions* ss, const uint64_t* slots, int64_t num_s
                     const int32_t* order, int64_t* cursor, int B, int row_group, uint32_t seed,
                     const gtr_batch* out, int32_t* scratch, int64_t* start, int32_t* status,
                     gtr_stream_t stream);
+/* The same with the cursor advancing by ``stride`` >= B per batch instead of B: rank r of
+ * P data-parallel ranks, its cursor started at r*B, builds sessions [i*P*B + r*B, +B) of
+ * the epoch order -- its share of global batch i, with the same position-keyed negatives
+ * a single GPU draws for that global batch (stride = P*B).                            */
+int gtr_build_batch_strided(const gtr_sessions* ss, const uint64_t* slots, int64_t num_slots, int max_len,
+                            const int32_t* order, int64_t* cursor, int B, int64_t stride, int row_group,
+                            uint32_t seed, const gtr_batch* out, int32_t* scratch, int64_t* start, int32_t* status,
+                            gtr_stream_t stream);
 
 /* ---- Laplacian positional-encoding precompute (etpgt.encodings.laplacian_gpu) ------
  * Replaces the host eigsh of compute_laplacian_pe (etpgt/encodings/laplacian_pe.py:19-66:

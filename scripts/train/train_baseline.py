@@ -17,6 +17,14 @@ Differences, each deliberate:
   step (``create_dataloader(device_builder=True)``), default on for CUDA runs of the
   graph-transformer models; ``off`` keeps the host DataLoader + collate_fn.
 * GAT / GraphSAGE are outside the hot-path scope: ``--model gat|graphsage`` raises.
+* Data parallel (added; the reference trains on one GPU): under ``torchrun`` /
+  ``torch.distributed.run`` (WORLD_SIZE > 1) every process joins the default process
+  group (RCCL; gloo with every rank on cuda:0 when GTR_SHARE_DEVICE=1), binds
+  cuda:LOCAL_RANK, and trains on its share of each global batch of
+  ``world * --batch-size`` sessions (``DeviceSessionLoader(rank, world)``) with gradients
+  averaged and BatchNorm statistics synchronised across the ranks (SyncBN), i.e. like one
+  GPU on the global batch.  Every rank evaluates the full validation set (the replicas
+  are identical); rank 0 writes the outputs.
 """
 
 from __future__ import annotations
@@ -82,10 +90,32 @@ def parse_args(argv=None):
     return p.parse_args(argv)
 
 
+def init_distributed(args) -> tuple[int, int]:
+    """Join the launcher's process group (one process per GPU); returns (rank, world)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return 0, 1
+    import torch.distributed as dist
+
+    if torch.device(args.device).type != "cuda":
+        raise NotImplementedError("data-parallel training runs on the GPUs (one process per GPU)")
+    share = os.environ.get("GTR_SHARE_DEVICE") == "1"  # rehearsal: every rank on cuda:0, gloo
+    dev_index = 0 if share else int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(dev_index)
+    args.device = f"cuda:{dev_index}"
+    if not dist.is_initialized():
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+    return dist.get_rank(), dist.get_world_size()
+
+
 def main(argv=None):
     args = parse_args(argv)
     if args.gcs_bucket:
         raise NotImplementedError("GCS I/O (--gcs-bucket) is outside the MI355X hot-path scope; stage files locally")
+    rank, world = init_distributed(args)
     set_seed(args.seed)
     logger.info("Training arguments:")
     logger.info(json.dumps(vars(args), indent=2))
@@ -102,10 +132,14 @@ def main(argv=None):
     logger.info("Creating data loaders%s...", " (batches built on the GPU)" if dev_batches else "")
     kw = dict(graph_edges_path=args.graph_edges, batch_size=args.batch_size, num_negatives=args.num_negatives,
               max_session_length=args.max_session_length, num_workers=args.num_workers)
+    if world > 1 and not dev_batches:
+        raise NotImplementedError("data-parallel training builds its batches on the GPU (--device-batches on)")
     if dev_batches:
         kw.update(device_builder=True, device=args.device, seed=args.seed)
-    train_loader = create_dataloader(sessions_path=args.train_sessions, shuffle=True, **kw)
-    val_loader = create_dataloader(sessions_path=args.val_sessions, shuffle=False, **kw)
+    train_loader = create_dataloader(sessions_path=args.train_sessions, shuffle=True, rank=rank, world=world, **kw)
+    val_loader = create_dataloader(sessions_path=args.val_sessions, shuffle=False, **kw)  # full set on every rank
+    if world > 1:
+        logger.info(f"Data parallel: rank {rank} of {world}, global batch {world * args.batch_size} sessions")
     data_items = max(train_loader.dataset.num_items, val_loader.dataset.num_items)
     num_items = int(split_info.get("num_items", data_items))
     if num_items < data_items:

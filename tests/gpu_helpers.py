@@ -122,3 +122,94 @@ def assert_close_norm(a, b, rtol=1e-3, name=""):
     den = float(b.norm())
     err = float((a - b).norm()) / den if den > 0 else float((a - b).norm())
     assert err <= rtol, f"{name}: relative error {err:.3g} > {rtol}"
+
+
+def close_trained(a, b, c, allow, bound, name, b1=None):
+    """Elementwise bar for TRAINED parameters.  a: HIP, b: fp32 oracle, c: fp64 oracle, b1:
+    the fp32 oracle in a second summation order (one CPU thread); allow: elements whose
+    first gradient was at the fp32 noise floor (bounded by ``bound`` = 2 lr per step).
+
+    An element matches when |a - b| <= 1e-3 (|b| + 1e-2 max|b|) + 8 * (its fp32 oracle's
+    distance to fp64, the larger of the two orders); one that misses is still accepted
+    when the HIP value is no further from fp64 than the fp32 oracle's worst distance to
+    fp64 anywhere in the tensor (Adam turns a gradient that nearly cancels -- rounded
+    differently by any two fp32 summation orders -- into an update that differs by a
+    fraction of lr)."""
+    a = a.detach().float().cpu()
+    b = b.detach().float().cpu()
+    c = c.detach().cpu()
+    allow = allow.cpu()
+    if bool(allow.any()):
+        assert float((a[allow] - b[allow]).abs().max()) <= bound + 1e-7, name
+    keep = ~allow
+    a, b, c = a[keep], b[keep], c[keep].float()
+    dev = (b - c).abs()
+    if b1 is not None:
+        dev = torch.maximum(dev, (b1.detach().float().cpu()[keep] - c).abs())
+    scale = float(b.abs().max()) if b.numel() else 0.0
+    tol = 1e-3 * (b.abs() + 1e-2 * scale) + 8 * dev + 1e-12
+    err = (a - b).abs()
+    floor = float(dev.max()) if b.numel() else 0.0
+    near = err > tol
+    bad = near & ((a - c).abs() > floor)
+    if bool(bad.any()):
+        i = int(torch.argmax((err - tol) * bad))
+        raise AssertionError(f"{name}: {int(bad.sum())}/{b.numel()} mismatches; worst: hip {a[i].item():.7g} "
+                             f"oracle fp32 {b[i].item():.7g} fp64 {c[i].item():.7g} (fp32 noise level {floor:.3g})")
+    ill = int(((b - c).abs() > 1e-3 * (b.abs() + 1e-2 * scale)).sum())
+    print(f"{name}: {b.numel()} elements within 1e-3 of the fp32 oracle or of its own fp64 distance "
+          f"({ill} where fp32 itself is off by more than 1e-3; {int(near.sum())} within the tensor's fp32 "
+          f"noise level {floor:.3g} of fp64 only)")
+
+
+class OracleTrio:
+    """One oracle training run replayed three ways -- fp32 (the reference's precision),
+    fp32 on one CPU thread (a second summation order) and fp64 -- so that trained HIP
+    parameters can be held to ``close_trained`` ELEMENTWISE.  ``make_opt(params)`` builds
+    the run's optimizer; ``step(fn)`` runs ``fn(model, opt) -> loss`` on all three and
+    records which elements' first gradient was at the fp32 noise floor."""
+
+    def __init__(self, ref, make_opt):
+        import copy
+
+        self.ref = ref
+        self.ref1 = copy.deepcopy(ref)
+        self.ref64 = copy.deepcopy(ref).double()
+        lp = getattr(self.ref64, "laplacian_pe", None)
+        if lp is not None and lp._cached_pe is not None:
+            lp._cached_pe = lp._cached_pe.double()
+        self.opt = make_opt(self.ref.parameters())
+        self.opt1 = make_opt(self.ref1.parameters())
+        self.opt64 = make_opt(self.ref64.parameters())
+        self.seen = {n: torch.zeros_like(p, dtype=torch.bool) for n, p in ref.named_parameters()}
+        self.noise = {n: torch.zeros_like(p, dtype=torch.bool) for n, p in ref.named_parameters()}
+        self.steps = 0
+
+    def step(self, fn):
+        loss = fn(self.ref, self.opt)
+        fn(self.ref64, self.opt64)
+        nthr = torch.get_num_threads()
+        torch.set_num_threads(1)
+        try:
+            fn(self.ref1, self.opt1)
+        finally:
+            torch.set_num_threads(nthr)
+        self.steps += 1
+        for n, p in self.ref.named_parameters():
+            g = p.grad
+            if g is None:
+                continue
+            if n.endswith("lin_key.bias"):  # d loss / d key bias == 0 exactly: all noise
+                self.noise[n][:] = True
+                continue
+            fresh = (g != 0) & ~self.seen[n]
+            self.noise[n] |= fresh & (g.abs() <= 1e-5 * float(g.abs().max()))
+            self.seen[n] |= g != 0
+        return loss
+
+    def compare(self, hip_params: dict, lr: float, prefix=""):
+        """Every trained parameter (name -> HIP tensor) against the trio."""
+        p1 = dict(self.ref1.named_parameters())
+        p64 = dict(self.ref64.named_parameters())
+        for n, p in self.ref.named_parameters():
+            close_trained(hip_params[n], p, p64[n], self.noise[n], 2 * lr * self.steps, prefix + n, p1[n])

@@ -32,7 +32,7 @@ if not torch.cuda.is_available():  # pragma: no cover - collected only on the GP
     pytest.skip("no GPU", allow_module_level=True)
 
 import etpgt_ref as R  # noqa: E402
-from gpu_helpers import assert_close  # noqa: E402
+from gpu_helpers import assert_close, close_trained  # noqa: E402
 
 from etpgt.data.synthetic import YOOCHOOSE_SCALE, make_batches, make_sessions_and_graph, random_pe_table  # noqa: E402
 from etpgt.model import create_graph_transformer_optimized  # noqa: E402
@@ -176,35 +176,7 @@ def _train_and_compare(m, ref, fused, batches, kind, lr, dropout=0.0, also=()):
     return steps
 
 
-def _close_trained(a, b, c, allow, bound, name, b1=None):
-    """a: HIP, b: fp32 oracle, c: fp64 oracle, b1: fp32 oracle in a second summation order
-    (see _train_and_compare)."""
-    if bool(allow.any()):
-        assert float((a[allow] - b[allow]).abs().max()) <= bound + 1e-7, name
-    keep = ~allow
-    a, b, c = a[keep], b[keep], c[keep].float()
-    dev = (b - c).abs()
-    if b1 is not None:
-        dev = torch.maximum(dev, (b1.detach()[keep] - c).abs())
-    scale = float(b.abs().max()) if b.numel() else 0.0
-    tol = 1e-3 * (b.abs() + 1e-2 * scale) + 8 * dev + 1e-12
-    err = (a - b).abs()
-    # fp32 noise level of the tensor: the worst distance of the fp32 oracle itself from the
-    # fp64 oracle anywhere in it.  An element that misses the elementwise bar above is still
-    # accepted when the HIP value is no further from the fp64 result than that (a gradient
-    # that nearly cancels is rounded differently by any two fp32 summation orders, and the
-    # fp32 oracle can land close to fp64 on that element by chance).
-    floor = float(dev.max()) if b.numel() else 0.0
-    near = err > tol
-    bad = near & ((a - c).abs() > floor)
-    if bool(bad.any()):
-        i = int(torch.argmax((err - tol) * bad))
-        raise AssertionError(f"{name}: {int(bad.sum())}/{b.numel()} mismatches; worst: hip {a[i].item():.7g} "
-                             f"oracle fp32 {b[i].item():.7g} fp64 {c[i].item():.7g} (fp32 noise level {floor:.3g})")
-    ill = int(((b - c).abs() > 1e-3 * (b.abs() + 1e-2 * scale)).sum())
-    print(f"{name}: {b.numel()} elements within 1e-3 of the fp32 oracle or of its own fp64 distance "
-          f"({ill} where fp32 itself is off by more than 1e-3; {int(near.sum())} within the tensor's fp32 "
-          f"noise level {floor:.3g} of fp64 only)")
+_close_trained = close_trained  # shared with the drop-in / C1 tests (gpu_helpers)
 
 
 def test_c2_full_table_matches_oracle():

@@ -1,0 +1,156 @@
+"""GPU: the multi-GPU entry points as the driver and a user reach them.
+
+* ``bench.py --gpus N`` without a launcher starts N ranks itself (torch.distributed.run
+  as a child process) and prints ONE line with ``n_gpus == N``; on the one-GPU box the
+  ranks share cuda:0 over gloo (GTR_SHARE_DEVICE=1), on an 8-GPU node they are RCCL
+  ranks.  The default C2 (replicated data parallel) and the C4 mode (row-sharded table,
+  SyncBN, fixed global batch) both report identical replicas.
+* ``scripts/train/train_baseline.py`` under a 2-rank process group trains like ONE GPU on
+  the global batch (device-built batches sharded per rank, SyncBN, averaged gradients).
+"""
+
+from __future__ import annotations
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+if not torch.cuda.is_available():  # pragma: no cover - collected only on the GPU box
+    pytest.skip("no GPU", allow_module_level=True)
+
+from gpu_helpers import assert_close_norm  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LEAN = ["--cpu-seconds", "0", "--gather-batch", "0", "--recall-steps", "0", "--e2e-steps", "0", "--c1-reps", "0",
+        "--tail-probe", "0"]
+
+
+def _bench(args, timeout=420):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["GTR_SHARE_DEVICE"] = "1"
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), *args, *LEAN], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]  # the bench line is the only stdout line
+    return json.loads(lines[0])
+
+
+def test_bench_gpus2_launches_two_ranks():
+    out = _bench(["--gpus", "2", "--steps", "4", "--warmup", "2", "--num-batches", "4"])
+    assert out["n_gpus"] == 2
+    cfg = out["config"]
+    assert cfg["process_group_world"] == 2 and cfg["launcher"].startswith("bench.py --gpus")
+    assert cfg["replicas_identical"] is True
+    assert cfg["parallelism"] == "dp2" and cfg["global_batch"] == 64 and out["scaling"] == "weak"
+    assert out["value"] > 0
+
+
+def test_bench_c4_gpus2_sharded_strong():
+    out = _bench(["--config", "c4", "--gpus", "2", "--global-batch", "512", "--steps", "3", "--warmup", "1",
+                  "--num-batches", "2"])
+    assert out["n_gpus"] == 2 and out["scaling"] == "strong"
+    cfg = out["config"]
+    assert cfg["global_batch"] == 512 and cfg["per_gpu_batch"] == 256
+    assert cfg["parallelism"] == "dp2+rowshard" and cfg["sync_bn"] is True
+    assert cfg["replicas_identical"] is True
+
+
+def test_bench_c4_one_gpu_line():
+    """N = 1 of the C4 mode: the same sharded step at world 1 (the curve's first point)."""
+    out = _bench(["--config", "c4", "--global-batch", "256", "--steps", "3", "--warmup", "1", "--num-batches", "2"])
+    assert out["n_gpus"] == 1 and out["config"]["parallelism"] == "dp1+rowshard"
+    assert out["config"]["process_group_world"] is None
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _script():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("train_baseline_cp",
+                                                  os.path.join(ROOT, "scripts", "train", "train_baseline.py"))
+    tb = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(tb)
+    return tb
+
+
+def _args(d, out, B):
+    return ["--model", "graph_transformer_optimized", "--train-sessions", str(d / "train.csv"),
+            "--val-sessions", str(d / "val.csv"), "--graph-edges", str(d / "graph_edges.csv"),
+            "--embedding-dim", "32", "--hidden-dim", "32", "--num-layers", "2", "--num-heads", "2",
+            "--dropout", "0", "--batch-size", str(B), "--num-negatives", "5", "--max-epochs", "2",
+            "--num-workers", "0", "--output-dir", str(out)]
+
+
+def _rank_main(rank, world, port, d, out, B, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank), GTR_SHARE_DEVICE="1")
+    try:
+        tr = _script().main(_args(d, out, B))
+        sd = {k: v.detach().cpu().numpy() for k, v in tr.model.state_dict().items()}
+        q.put((rank, tr.history, sd))
+    finally:
+        import torch.distributed as dist
+
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_train_baseline_two_ranks_equal_one_gpu_global_batch(tmp_path):
+    from dropin_helpers import write_csvs
+
+    d = write_csvs(tmp_path, num_train=150)  # 150 sessions: 9 global batches of 16 + a last one of 6
+    world, B = 2, 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, d, tmp_path / "dp", B, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            rank, hist, sd = q.get(timeout=500)
+            res[rank] = (hist, sd)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    for k, v in res[0][1].items():
+        assert np.array_equal(v, res[1][1][k]), f"replicas diverged: {k}"
+    assert os.path.exists(tmp_path / "dp" / "graph_transformer_optimized" / "history.json")
+    # one GPU on the global batch (2 x 8 sessions), same seed / order / negatives
+    tr = _script().main(_args(d, tmp_path / "one", world * B))
+    hist = tr.history
+    np.testing.assert_allclose(res[0][0]["train_loss"], hist["train_loss"], rtol=1e-4)
+    sd1 = tr.model.state_dict()
+    for k, v in sd1.items():
+        if k.endswith("lin_key.bias"):  # exactly-zero gradient: noise-driven on both sides
+            continue
+        a = torch.from_numpy(res[0][1][k])
+        if "num_batches_tracked" in k:
+            assert int(a) == int(v), k
+            continue
+        assert_close_norm(a, v, rtol=1e-4, name=k)
+        # elementwise: all but a sliver of Adam-flipped noise elements within 1e-3 relative
+        b = v.detach().float().cpu()
+        ok = (a - b).abs() <= 1e-3 * (b.abs() + 1e-2 * float(b.abs().max()))
+        assert float(ok.float().mean()) >= 0.999, (k, float(ok.float().mean()))
+    for r0, r1 in zip(res[0][0]["val_metrics"], hist["val_metrics"]):
+        assert abs(r0["recall@10"] - r1["recall@10"]) <= 2.0 / 40 + 1e-9

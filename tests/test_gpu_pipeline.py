@@ -17,6 +17,7 @@ if not torch.cuda.is_available():  # pragma: no cover - collected only on the GP
     pytest.skip("no GPU", allow_module_level=True)
 
 import etpgt_ref as R  # noqa: E402
+from gpu_helpers import OracleTrio  # noqa: E402
 
 from etpgt.model import create_graph_transformer_optimized  # noqa: E402
 from etpgt import pipeline as P  # noqa: E402
@@ -47,20 +48,22 @@ def test_c1_pipeline_matches_oracle():
     ref.load_state_dict(init.state_dict())
     assert sum(p.numel() for p in ref.parameters()) == res["param_count"]
     rb = R.ref_batch_from(batch)
-    opt = torch.optim.Adam(ref.parameters(), lr=0.001)
-    rl = []
-    for _ in range(3):
-        ref.train()
+    trio = OracleTrio(ref, lambda ps: torch.optim.Adam(ps, lr=0.001))
+
+    def epoch(mod, opt):
+        mod.train()
         opt.zero_grad()
-        se = ref(rb)
-        loss = R.ref_loss("listwise", se, rb.target_item, rb.negative_items.view(se.shape[0], -1), ref.item_embedding)
+        se = mod(rb)
+        loss = R.ref_loss("listwise", se, rb.target_item, rb.negative_items.view(se.shape[0], -1), mod.item_embedding)
         loss.backward()
         opt.step()
-        rl.append(float(loss))
+        return float(loss)
+
+    rl = [trio.step(epoch) for _ in range(3)]
     np.testing.assert_allclose(res["losses"], rl, rtol=1e-3)
+    # every trained parameter ELEMENTWISE (gpu_helpers.close_trained)
     m = res["model_obj"]
-    w, rw = m.item_embedding.weight.detach().cpu(), ref.item_embedding.weight.detach()
-    assert float((w - rw).norm() / rw.norm()) <= 1e-3
+    trio.compare({n: p.detach().cpu() for n, p in m.named_parameters()}, lr=1e-3)
 
 
 def test_c1_pipeline_reference_config_runs():

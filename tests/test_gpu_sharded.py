@@ -82,6 +82,49 @@ def test_shard_overflow_is_reported(monkeypatch):
         f.sync_table()
 
 
+def test_shard_overflow_on_the_last_step_is_reported(monkeypatch):
+    """an overflow on the FINAL step (no later step to carry the asynchronous
+    status read) is still raised by sync_table(), and the flagged step is applied as a
+    zero-gradient step (no partial update)."""
+    monkeypatch.setenv("GTR_SHARD_SLACK", "0.0001")  # blocks of 64 rows
+    data = small_data()
+    T = data.table_rows
+    m, _ = make_pair(T, 64, 2, seed=47)
+    m.train()
+    f = FusedTrainStep(m, lr=1e-2, weight_decay=1e-2, loss="bpr", shard_table=True)
+    for sb in batches(data, 4, 5, 2, seed=48):  # B = 4: well under 64 distinct rows
+        f(sb.to("cuda"))
+    f.shard_state.check_status(block=True)  # nothing overflowed so far
+    small_before = f.eng.flat.flat.clone()
+    big = batches(data, 16, 5, 1, seed=49)[0]  # > 64 distinct rows from the one owner
+    f(big.to("cuda"))
+    with pytest.raises(RuntimeError, match="exchange capacity"):
+        f.sync_table()
+    assert int(f.shard_state.status[1].item()) & 2  # the owner saw the flag in the pack
+    # the flagged step moved the small parameters by a zero-gradient AdamW update only
+    assert torch.isfinite(f.eng.flat.flat).all()
+    assert float((f.eng.flat.flat - small_before).abs().max()) < 0.05
+
+
+def test_shard_table_never_takes_the_early_union_or_chain_sweep(monkeypatch):
+    """GTR_DP_EARLY=1 must not install the chain sweep (whose table / moment
+    pointers are the model's stale copy and 1-row placeholders) on a sharded step."""
+    monkeypatch.setenv("GTR_DP_EARLY", "1")
+    data = small_data()
+    T = data.table_rows
+    m1, _ = make_pair(T, 64, 2, seed=50)
+    m2 = copy.deepcopy(m1)
+    m1.train(); m2.train()
+    f1 = FusedTrainStep(m1, lr=1e-2, weight_decay=1e-2, loss="bpr", lazy=True)
+    f2 = FusedTrainStep(m2, lr=1e-2, weight_decay=1e-2, loss="bpr", shard_table=True)
+    for sb in batches(data, 16, 5, 3, seed=51):
+        assert float(f1(sb.to("cuda"))) == float(f2(sb.to("cuda")))
+    assert not f2.early_union and f2.sweep is None
+    f1.flush()
+    f2.sync_table()
+    assert torch.equal(m1.item_embedding.weight, m2.item_embedding.weight)
+
+
 def _free_port() -> int:
     s = socket.socket()
     s.bind(("127.0.0.1", 0))

@@ -394,3 +394,36 @@ def test_reference_directed_lappe_input_has_no_eigen_answer():
     res = np.linalg.norm(L @ v - v * w, axis=0)
     assert np.abs(w - 1.0).max() > 0.1  # the "eigenvalues" are not the spectrum {1}
     assert res.min() > 0.05             # and the vectors are not eigenvectors
+
+
+def test_device_loader_epoch_order_matches_torch_dataloader():
+    """DeviceSessionLoader visits each epoch's sessions in the order a
+    ``DataLoader(shuffle=True)`` over the same dataset does under the same global seed --
+    the iterator's ``_base_seed`` draw precedes the RandomSampler's seed draw -- including
+    a non-shuffled validation loader iterated between training epochs (its iterator draws
+    a ``_base_seed`` too)."""
+    from torch.utils.data import DataLoader
+
+    from etpgt.train.dataloader import DeviceSessionLoader
+
+    ds = list(range(37))
+
+    def dev_loader(shuffle):
+        dl = DeviceSessionLoader.__new__(DeviceSessionLoader)  # order logic only (no GPU store)
+        dl.dataset, dl.shuffle = ds, shuffle
+        return dl
+
+    torch.manual_seed(42)
+    ref = []
+    for _ in range(3):
+        for shuffle in (True, False):
+            loader = DataLoader(ds, batch_size=5, shuffle=shuffle, collate_fn=lambda b: b)
+            ref.append([int(v) for b in loader for v in b])
+    torch.manual_seed(42)
+    tr, va = dev_loader(True), dev_loader(False)
+    got = []
+    for _ in range(3):
+        got.append(tr._epoch_order().tolist())
+        got.append(va._epoch_order().tolist())
+    assert got == ref
+    assert got[0] != got[2]  # fresh permutation per epoch
