@@ -32,6 +32,13 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_bwd(ConvBwdK a) {
   conv_bwd_body<D, SPLIT>(a, rb);
 }
 
+// Split path (large batches): the attention backward of one row group per workgroup
+// (gtr_attn_bwd); dX runs in k_dx (gtr_qkvs_bwd).
+template <int D>
+__global__ __launch_bounds__(CONV_BLOCK) void k_attn_bwd(ConvBwdK a) {
+  conv_bwd_body<D, false, false>(a, blockIdx.x);
+}
+
 // ------------------------------------------------------------------------------------
 // weight gradients
 // ------------------------------------------------------------------------------------
@@ -96,6 +103,37 @@ extern "C" int gtr_conv_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     default: GTR_BWD(256, false); break;  // no LDS-staged rows at D = 256: f32 MFMA from L2
   }
 #undef GTR_BWD
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+extern "C" int gtr_attn_bwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l,
+                            gtr_stream_t stream) {
+  if (!cfg || !bt || !layers || l < 0 || l >= cfg->num_layers) {
+    set_error("gtr_attn_bwd: bad arguments");
+    return GTR_E_ARG;
+  }
+  if (cfg->consumer_reduce || cfg->sync_bn) {
+    set_error("gtr_attn_bwd: the split path reads producer-finalized BatchNorm sums (consumer_reduce 0)");
+    return GTR_E_ARG;
+  }
+  ConvBwdK k;
+  float dummy = 0.0f;  // dx0 is written by gtr_qkvs_bwd, not here
+  if (const int rc = make_bwd_args(cfg, bt, layers, l, &dummy, k)) return rc;
+  k.dx0 = nullptr;
+  const int grid = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;
+  if (grid <= 0) return GTR_OK;
+  k.main_grid = grid;
+  hipStream_t s = (hipStream_t)stream;
+#define GTR_ABW(DD) set_lds_limit<DD>(k_attn_bwd<DD>, (size_t)LayerGeom<DD>::B_WORDS * 4); \
+  hipLaunchKernelGGL((k_attn_bwd<DD>), dim3(grid), dim3(CONV_BLOCK), (size_t)LayerGeom<DD>::B_WORDS * 4, s, k)
+  switch (cfg->dim) {
+    case 32: GTR_ABW(32); break;
+    case 64: GTR_ABW(64); break;
+    case 128: GTR_ABW(128); break;
+    default: GTR_ABW(256); break;
+  }
+#undef GTR_ABW
   GTR_HIP_CHECK_LAUNCH();
   return GTR_OK;
 }

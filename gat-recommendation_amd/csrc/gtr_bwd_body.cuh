@@ -159,7 +159,9 @@ __device__ __forceinline__ void bwd_src_row(const ConvBwdK& a, int s, int sl, co
   store_vec<VPL>(a.dqkvs + (size_t)s * (4 * D) + D + d0, dk, act);
   store_vec<VPL>(a.dqkvs + (size_t)s * (4 * D) + 2 * D + d0, dv, act);
 }
-template <int D, bool SPLIT>
+// DX = false: the split path's attention backward (gtr_attn_bwd): stops once dqkvs, du and
+// dlogit are written; dX and the previous layer's BatchNorm sums run in k_dx (gtr_gemm.hip).
+template <int D, bool SPLIT, bool DX = true>
 __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
   using G = LayerGeom<D>;
   constexpr int VPL = G::VPL, RMAX = G::RMAX, XS = G::XS, TPR = G::TPR, CH = G::CH;
@@ -217,7 +219,7 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
   const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
   const float invN = 1.0f / (float)N;
   const int prow = tid / TPR, pchunk = tid - prow * TPR, f0 = pchunk * CH;
-  constexpr bool PREB = !SPLIT && CPW == 1 && D <= 128;
+  constexpr bool PREB = DX && !SPLIT && CPW == 1 && D <= 128;
   float4 wb[PREB ? D / 4 : 1];
 
   // ---- this layer's BatchNorm backward sums: reduce the producer's partials (cred).
@@ -517,6 +519,7 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
         *reinterpret_cast<float4*>(drow + 2 * D + c) = make_float4(dv[c], dv[c + 1], dv[c + 2], dv[c + 3]);
       }
     }
+    if constexpr (!DX) return;
     if constexpr (!SPLIT) {
       // the group's dQKVS rows (fp32, row stride AS32) over the K | V | Q | dA rows (dead from
       // here on): the A operand of phase X from LDS instead of L2
@@ -591,6 +594,7 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
     for (int s = r0 + wave; s < r1; s += CONV_WAVES)
       bwd_src_row<D>(a, s, s, a.qkvs, 4 * D, a.dagg, D, a.bt.out_ptr, a.bt.out_edge, a.bt.out_dst, a.alpha,
                      a.dlogit, 0, lane, dr, st_attn);
+    if constexpr (!DX) return;
   }
   __syncthreads();
   GTR_PH(a.layer, 3);

@@ -224,7 +224,10 @@ __device__ __forceinline__ int wfrag_off(int kb, int lg, int split) {
   return split ? ((kb >> 1) * 32 + lg * 8 + (kb & 1) * 4) : (kb * 16 + lg * 4);
 }
 
-template <int D, bool SPLIT>
+// PROJ = false: the split path's attention kernel (gtr_attn_fwd): xin / qkvs were written
+// by gtr_qkvs_fwd (k_proj), so the input build and the projection are left out and the
+// group's Q | K | V | S rows are staged from qkvs instead.
+template <int D, bool SPLIT, bool PROJ = true>
 __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
   using G = LayerGeom<D>;
   static_assert(G::F_WORDS >= GTR_BEGIN_MCAP + CONV_WAVES * 64, "LDS carve too small for the fused begin");
@@ -283,17 +286,17 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
     if (tid < ne) c_src0 = a.bt.in_src[e_lo + tid];
     if (tid + CONV_BLOCK < ne) c_src1 = a.bt.in_src[e_lo + tid + CONV_BLOCK];
   }
-  if (a.first && tid < min(RMAX, nrow)) c_item = a.bt.node_item[r0 + tid];
+  if (PROJ && a.first && tid < min(RMAX, nrow)) c_item = a.bt.node_item[r0 + tid];
   float4 c_wb = make_float4(0.f, 0.f, 0.f, 0.f);  // gate weights [w1 | w2 | w3] -> LDS (fast path)
   if (fast && tid < (3 * D) / 4) c_wb = *reinterpret_cast<const float4*>(a.w_beta + 4 * tid);
   // layers >= 1, consumer-side BatchNorm: the previous layer's partial rows, also before the
   // weights (the reduction consumes them first)
-  const bool pre_bn = !a.first && a.train && a.cred;
+  const bool pre_bn = PROJ && !a.first && a.train && a.cred;
   const int bn_G = a.sync ? a.p_nparts : Gn;
   const float* bn_part = a.sync ? a.p_part_all : a.p_part;
   BnParts<D, CONV_BLOCK> bnr;
   if (pre_bn) bn_parts_load<D, CONV_BLOCK>(bn_part, bn_G, 1 + 2 * D, bnr);
-  if (pe_lds) {  // LapPE projection weight [D][KPE], zero-padded past pe_k (stored right away)
+  if (PROJ && pe_lds) {  // LapPE projection weight [D][KPE], zero-padded past pe_k (stored right away)
     for (int idx = tid; idx < D * KPE; idx += CONV_BLOCK) {
       const int j = idx / KPE, k = idx - j * KPE;
       PEs[idx] = k < a.pe_k ? a.wpe[j * a.pe_k + k] : 0.0f;
@@ -305,10 +308,10 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
   //      early so the weight fetch overlaps the staging round trip
   // every column tile of the wave prefetched up to D = GTR_WPRE_MAXD; beyond, one tile ahead
   // (D = 128 with all 4 tiles held, 128 VGPRs: C3 0.1398 -> 0.1436 ms per step)
-  constexpr int PRE = D <= GTR_WPRE_MAXD ? (NCT / CONV_WAVES) : 1;
+  constexpr int PRE = !PROJ ? 1 : D <= GTR_WPRE_MAXD ? (NCT / CONV_WAVES) : 1;
   float4 wpre[PRE][D / 16];
 #pragma unroll
-  for (int pi = 0; pi < PRE; ++pi) {
+  for (int pi = 0; pi < (PROJ ? PRE : 0); ++pi) {
     const float* wrow = a.w_all + (size_t)((wave + pi * CONV_WAVES) * 16 + lr) * D;
 #pragma unroll
     for (int kb = 0; kb < D / 16; ++kb)
@@ -326,7 +329,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
   constexpr int PRL = (RMAX * C4 + CONV_BLOCK - 1) / CONV_BLOCK;  // float4 per thread and chunk
   constexpr bool PREROWS = D <= 64;  // D = 128 has no registers to spare (spills)
   float4 ppo[PREROWS ? PRL : 1], ppx[PREROWS ? PRL : 1];
-  if (PREROWS && !a.first) {
+  if (PROJ && PREROWS && !a.first) {
     const int m0 = min(RMAX, nrow);
 #pragma unroll
     for (int u = 0; u < PRL; ++u) {
@@ -343,7 +346,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
   }
 
   // ---- stage: previous BN stats, CSR slice, node items, LapPE projection weight
-  if (!a.first) {
+  if (PROJ && !a.first) {
     prev_bn_stats<D, CONV_BLOCK>(a.train, a.cred, bn_G, bn_part, a.p_stats, a.p_rmean, a.p_rvar, a.p_nbt,
                                  a.bn_eps, a.bn_mom, s_bn, s_bn + D, XO, LOG, g == 0, pre_bn, bnr);
   }
@@ -355,15 +358,28 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
     if (tid < nrow)
       for (int k = c_ip0 - e_lo; k < c_ip1 - e_lo; ++k) edst[k] = tid;
   }
-  if (a.first && tid < min(RMAX, nrow)) items[tid] = c_item;
+  if (PROJ && a.first && tid < min(RMAX, nrow)) items[tid] = c_item;
   if (fast && tid < (3 * D) / 4) *reinterpret_cast<float4*>(WB + 4 * tid) = c_wb;
   GTR_PH(a.layer, 15);
   __syncthreads();
   GTR_PH(a.layer, 1);
 
   // ---- phase P+M: layer input rows -> LDS -> QKVS projection (MFMA f32), chunks of RMAX rows
+  //      (split path: the group's Q | K | V | S rows of qkvs -> LDS instead)
   const uint32_t st_prev = drop_stream(1, (uint32_t)(a.layer - 1), ctr);
-  for (int rc = r0; rc < r1; rc += RMAX) {
+  if constexpr (!PROJ) {
+    if (fast) {
+      for (int idx = tid; idx < nrow * D; idx += CONV_BLOCK) {  // D float4 per row: Q | K | V | S
+        const int i = idx / D, c4 = idx - i * D;
+        const int part = c4 / (D / 4), c = (c4 - part * (D / 4)) * 4;
+        const float4 v = *reinterpret_cast<const float4*>(a.qkvs + (size_t)(r0 + i) * (4 * D) + part * D + c);
+        float* dst = part == 0 ? QSs : part == 1 ? KVs : part == 2 ? KVs + RMAX * XS : QSs + RMAX * XS;
+        *reinterpret_cast<float4*>(dst + i * XS + c) = v;
+      }
+      __syncthreads();
+    }
+  }
+  for (int rc = r0; PROJ && rc < r1; rc += RMAX) {
     const int m = min(RMAX, r1 - rc);
     if (a.first && rc != r0) {
       for (int i = tid; i < m; i += CONV_BLOCK) items[i] = a.bt.node_item[rc + i];
@@ -733,6 +749,13 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
     return;
   }
   conv_fwd_body<D, SPLIT>(a, rb);
+}
+
+// Split path (large batches): the attention + gate + BatchNorm partial of one row group
+// per workgroup, reading the qkvs rows k_proj wrote (gtr_attn_fwd).
+template <int D>
+__global__ __launch_bounds__(CONV_BLOCK) void k_attn_fwd(ConvFwdK a) {
+  conv_fwd_body<D, false, false>(a, blockIdx.x);
 }
 
 struct ReadoutK {
@@ -1477,11 +1500,11 @@ void drop_params(const gtr_config* c, uint32_t& thresh, float& scale, int& on) {
 
 // Arguments of conv_fwd_body for layer l (launch geometry left to the caller).
 int make_fwd_args(const gtr_config* cfg, const gtr_batch* bt, const gtr_embed* emb, const gtr_layer* layers,
-                  int l, ConvFwdK& k) {
+                  int l, ConvFwdK& k, bool attn_only = false) {
   if (!check_dims(cfg, "gtr_conv_fwd")) return GTR_E_ARG;
   if (!bt->grp_row || !bt->grp_edge) { set_error("gtr_conv_fwd: batch lacks row-group ranges"); return GTR_E_ARG; }
-  if (l == 0 && (!emb || !emb->table)) { set_error("gtr_conv_fwd: layer 0 needs the table"); return GTR_E_ARG; }
-  if (l == 0 && cfg->pe_k > 0 && (!emb->wpe || !emb->bpe || (!emb->pe_tab && !bt->node_pe))) {
+  if (!attn_only && l == 0 && (!emb || !emb->table)) { set_error("gtr_conv_fwd: layer 0 needs the table"); return GTR_E_ARG; }
+  if (!attn_only && l == 0 && cfg->pe_k > 0 && (!emb->wpe || !emb->bpe || (!emb->pe_tab && !bt->node_pe))) {
     set_error("gtr_conv_fwd: Laplacian PE not precomputed");
     return GTR_E_ARG;
   }
@@ -1506,7 +1529,7 @@ int make_fwd_args(const gtr_config* cfg, const gtr_batch* bt, const gtr_embed* e
   k.sync = cfg->sync_bn;
   if (cfg->sync_bn && !cfg->consumer_reduce) { set_error("gtr_conv_fwd: sync_bn needs consumer_reduce"); return GTR_E_ARG; }
   if (l == 0) {
-    k.table = emb->table; k.pe_tab = emb->pe_tab; k.wpe = emb->wpe; k.bpe = emb->bpe;
+    if (emb) { k.table = emb->table; k.pe_tab = emb->pe_tab; k.wpe = emb->wpe; k.bpe = emb->bpe; }
   } else {
     const gtr_layer& P = layers[l - 1];
     k.p_part_all = P.bn_part_all;
@@ -1624,6 +1647,35 @@ extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     default: GTR_FWD(256, false); break;  // D = 256: f32 MFMA (no registers for the split fragments)
   }
 #undef GTR_FWD
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+extern "C" int gtr_attn_fwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l,
+                            gtr_stream_t stream) {
+  if (!cfg || !bt || !layers || l < 0 || l >= cfg->num_layers) {
+    set_error("gtr_attn_fwd: bad arguments");
+    return GTR_E_ARG;
+  }
+  if (cfg->training && (cfg->consumer_reduce || cfg->sync_bn)) {
+    set_error("gtr_attn_fwd: the split path finalizes its BatchNorm statistics in the producer (consumer_reduce 0)");
+    return GTR_E_ARG;
+  }
+  ConvFwdK k;
+  if (const int rc = make_fwd_args(cfg, bt, nullptr, layers, l, k, true)) return rc;
+  const int grid = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;
+  if (grid <= 0) return GTR_OK;
+  k.main_grid = grid;
+  hipStream_t s = (hipStream_t)stream;
+#define GTR_ATT(DD) set_lds_limit<DD>(k_attn_fwd<DD>, (size_t)LayerGeom<DD>::F_WORDS * 4); \
+  hipLaunchKernelGGL((k_attn_fwd<DD>), dim3(grid), dim3(CONV_BLOCK), (size_t)LayerGeom<DD>::F_WORDS * 4, s, k)
+  switch (cfg->dim) {
+    case 32: GTR_ATT(32); break;
+    case 64: GTR_ATT(64); break;
+    case 128: GTR_ATT(128); break;
+    default: GTR_ATT(256); break;
+  }
+#undef GTR_ATT
   GTR_HIP_CHECK_LAUNCH();
   return GTR_OK;
 }

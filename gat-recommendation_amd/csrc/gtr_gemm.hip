@@ -1,0 +1,508 @@
+// gtr_gemm.hip — the dense GEMMs of the TransformerConv layer as persistent f32-MFMA
+// kernels, for the large-batch ("split") layer path (gtr_qkvs_fwd / gtr_qkvs_bwd).
+//
+// At large batches the fused layer kernels (k_conv_fwd / k_conv_bwd) spend most of their
+// time in the per-row-group projection: every 16-row group re-fetches the layer's whole
+// W_all (256 KB at D = 128) for 16 rows of reuse and pads its 16-20 rows to two 16-row
+// MFMA tiles.  Here the GEMMs run over ALL node rows instead:
+//
+//   k_proj<D>  X = [layer 0: item row + LapPE projection | layer >= 1: dropout(BN(prev out)
+//              + prev in)] (graph_transformer.py:140-152,175-177) -> xin, and
+//              qkvs = X . W_all^T + b_all (the four PyG TransformerConv Linears,
+//              SURVEY.md Appendix A);
+//   k_dx<D>    dX = dQKVS . W_all + dy (the residual), the previous layer's dropout mask,
+//              -> that layer's dy (or dx0 at layer 0), and its BatchNorm backward sums.
+//
+// One workgroup per CU, 8 waves, persistent over 16- (D = 128) or 32-row (D = 64) tiles.
+// Each wave keeps ITS column tiles of W_all in registers for the whole launch (128 VGPRs
+// at D = 128: loaded once per CU instead of once per row group), the row tile is staged
+// in LDS (double-buffered; the next tile's rows are fetched while the MFMAs run), and the
+// MFMAs run exactly the k order of the fused kernels' mfma4 chains (k = kb*16 + lg*4 + j),
+// so qkvs / dX are BITWISE those of k_conv_fwd / k_conv_bwd (tests/test_gpu_split.py).
+// The attention phases then run in gtr_attn_fwd / gtr_attn_bwd (the fused kernels' row
+// group bodies with the projection / dX phase left out).
+
+#include "gtr_layer.cuh"
+
+namespace {
+
+using namespace gtr;
+
+#define GM_BLOCK 512
+#define GM_WAVES (GM_BLOCK / 64)
+
+template <int D>
+struct ProjGeom {
+  static constexpr int NCT = 4 * D / 16;          // output column tiles of qkvs
+  static constexpr int CT = NCT / GM_WAVES;       // per wave (D = 64: 2, D = 128: 4)
+  static constexpr int RT = D <= 64 ? 2 : 1;      // 16-row MFMA tiles per block tile
+  static constexpr int BM = 16 * RT;
+  static constexpr int XS = D + 4;                // padded LDS row
+  static constexpr int C4 = D / 4;
+  static constexpr int KPE = 16;                  // LapPE width staged in LDS
+  static_assert(BM * C4 == GM_BLOCK, "one float4 of X per thread and tile");
+};
+
+struct ProjK {
+  gtr_batch bt;
+  int first, train, pe_k, layer;
+  float bn_eps, scale;
+  uint32_t seed, thresh;
+  int drop_on;
+  uint32_t ctr_add;
+  const uint32_t* rng_ctr;
+  const float* table;
+  const float* pe_tab;
+  const float* wpe;
+  const float* bpe;
+  const float* p_out;
+  const float* p_xin;
+  const float* p_stats;
+  const float* p_rmean;
+  const float* p_rvar;
+  const float* p_gamma;
+  const float* p_beta;
+  const float* w_all;
+  const float* b_all;
+  float* xin;
+  float* qkvs;
+};
+
+// Inputs of one thread's float4 of X for one tile: layer 0 the item row (+ its LapPE row),
+// layers >= 1 the previous layer's out and in rows.
+struct ProjIn {
+  float4 u, v;
+  float4 pe[4];
+};
+
+template <int D>
+__global__ __launch_bounds__(GM_BLOCK) void k_proj(ProjK a) {
+  using G = ProjGeom<D>;
+  constexpr int CT = G::CT, RT = G::RT, BM = G::BM, XS = G::XS, C4 = G::C4, KPE = G::KPE;
+  __shared__ __attribute__((aligned(16))) float Xs[2][BM * XS];
+  __shared__ __attribute__((aligned(16))) float s_pw[D * KPE];  // W_pe [D][KPE] (layer 0)
+  __shared__ __attribute__((aligned(16))) float s_c[4 * D];     // bpe | mean | rstd | gamma | beta
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
+  const int N = a.bt.hdr[0];
+  const int ntile = (N + BM - 1) / BM;
+  if ((int)blockIdx.x >= ntile) return;  // block-uniform
+  // ---- W fragments of this wave's column tiles (ct = wave + c * GM_WAVES, the fused
+  //      kernel's assignment) and biases, held in registers for every tile of the block
+  float4 wf[CT][D / 16];
+  float bias[CT];
+#pragma unroll
+  for (int c = 0; c < CT; ++c) {
+    const int ct = wave + c * GM_WAVES;
+    const float* wrow = a.w_all + (size_t)(ct * 16 + lr) * D;
+#pragma unroll
+    for (int kb = 0; kb < D / 16; ++kb) wf[c][kb] = *reinterpret_cast<const float4*>(wrow + kb * 16 + lg * 4);
+    bias[c] = a.b_all[ct * 16 + lr];
+  }
+  const bool pe_lds = a.first && a.pe_k > 0 && a.pe_k <= KPE;
+  if (a.first) {
+    if (pe_lds)
+      for (int idx = tid; idx < D * KPE; idx += GM_BLOCK) {
+        const int j = idx / KPE, k = idx - j * KPE;
+        s_pw[idx] = k < a.pe_k ? a.wpe[j * a.pe_k + k] : 0.0f;
+      }
+    if (a.pe_k > 0)
+      for (int j = tid; j < D; j += GM_BLOCK) s_c[j] = a.bpe[j];
+  } else {
+    for (int j = tid; j < D; j += GM_BLOCK) {
+      // the previous layer's BatchNorm: batch statistics (finalized by its producer) or,
+      // in eval mode, the running statistics -- as prev_bn_stats of k_conv_fwd
+      s_c[D + j] = a.train ? a.p_stats[j] : a.p_rmean[j];
+      s_c[2 * D + j] = a.train ? a.p_stats[D + j] : 1.0f / sqrtf(a.p_rvar[j] + a.bn_eps);
+      s_c[3 * D + j] = a.p_gamma[j];
+    }
+  }
+  __syncthreads();
+  const uint32_t ctr = a.rng_ctr ? load_step_ctr(a.rng_ctr) + a.ctr_add : 0u;
+  const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
+  const uint32_t st_prev = drop_stream(1, (uint32_t)(a.layer - 1), ctr);
+  const int xi = tid / C4, xj = (tid - (tid / C4) * C4) * 4;  // this thread's row / column of X
+  float4 pg = make_float4(0.f, 0.f, 0.f, 0.f), pb = pg, mu = pg, rs = pg;
+  if (!a.first) {
+    mu = *reinterpret_cast<const float4*>(s_c + D + xj);
+    rs = *reinterpret_cast<const float4*>(s_c + 2 * D + xj);
+    pg = *reinterpret_cast<const float4*>(s_c + 3 * D + xj);
+    pb = *reinterpret_cast<const float4*>(a.p_beta + xj);
+  }
+
+  auto item_of = [&](int t) -> int {
+    const int r = t * BM + xi;
+    return (a.first && t < ntile && r < N) ? a.bt.node_item[r] : 0;
+  };
+  auto fetch = [&](int t, int item, ProjIn& in) {
+    const int r = t * BM + xi;
+    const bool live = r < N;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    in.u = z;
+    in.v = z;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) in.pe[q] = z;
+    if (!live) return;
+    if (a.first) {
+      in.u = *reinterpret_cast<const float4*>(a.table + (size_t)item * D + xj);
+      if (pe_lds && (a.pe_k & 3) == 0) {
+        const float* pr = a.bt.node_pe ? a.bt.node_pe + (size_t)r * a.pe_k : a.pe_tab + (size_t)item * a.pe_k;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (4 * q < a.pe_k) in.pe[q] = *reinterpret_cast<const float4*>(pr + 4 * q);
+      }
+    } else {
+      const size_t o = (size_t)r * D + xj;
+      in.u = *reinterpret_cast<const float4*>(a.p_out + o);
+      in.v = *reinterpret_cast<const float4*>(a.p_xin + o);
+    }
+  };
+  // X of one tile -> LDS (rows past N: zero) and xin; the arithmetic of k_conv_fwd's
+  // input build, expression for expression (bitwise the same rows)
+  auto produce = [&](int t, int item, const ProjIn& in, float* X) {
+    const int r = t * BM + xi;
+    float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (r < N) {
+      const size_t o = (size_t)r * D + xj;
+      if (a.first) {
+        val = in.u;
+        if (a.pe_k > 0) {
+          float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+          if (pe_lds && (a.pe_k & 3) == 0) {
+#pragma unroll
+            for (int kq = 0; kq < 4; ++kq) {  // k = 0, 4, .. < pe_k: the fused loop's order
+              if (4 * kq >= a.pe_k) break;
+              const int k = 4 * kq;
+              const float4 p4 = in.pe[kq];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                const float4 w4 = *reinterpret_cast<const float4*>(s_pw + (xj + q) * KPE + k);
+                acc[q] += p4.x * w4.x;
+                acc[q] += p4.y * w4.y;
+                acc[q] += p4.z * w4.z;
+                acc[q] += p4.w * w4.w;
+              }
+            }
+          } else {
+            const float* pr = a.bt.node_pe ? a.bt.node_pe + (size_t)r * a.pe_k : a.pe_tab + (size_t)item * a.pe_k;
+            for (int k = 0; k < a.pe_k; ++k) {
+              const float pk = pr[k];
+#pragma unroll
+              for (int q = 0; q < 4; ++q) acc[q] += pk * a.wpe[(size_t)(xj + q) * a.pe_k + k];
+            }
+          }
+          val.x = val.x + (acc[0] + s_c[xj]);
+          val.y = val.y + (acc[1] + s_c[xj + 1]);
+          val.z = val.z + (acc[2] + s_c[xj + 2]);
+          val.w = val.w + (acc[3] + s_c[xj + 3]);
+        }
+      } else {
+        const float4 po = in.u, px = in.v;
+        val.x = (((po.x - mu.x) * rs.x * pg.x + pb.x) + px.x) * dr.mul(st_prev, (uint32_t)o);
+        val.y = (((po.y - mu.y) * rs.y * pg.y + pb.y) + px.y) * dr.mul(st_prev, (uint32_t)(o + 1));
+        val.z = (((po.z - mu.z) * rs.z * pg.z + pb.z) + px.z) * dr.mul(st_prev, (uint32_t)(o + 2));
+        val.w = (((po.w - mu.w) * rs.w * pg.w + pb.w) + px.w) * dr.mul(st_prev, (uint32_t)(o + 3));
+      }
+      *reinterpret_cast<float4*>(a.xin + o) = val;
+    }
+    *reinterpret_cast<float4*>(X + xi * XS + xj) = val;
+  };
+
+  int t = blockIdx.x;
+  int it = item_of(t);
+  ProjIn cur;
+  fetch(t, it, cur);
+  int it_next = item_of(t + gridDim.x);
+  int buf = 0;
+  for (; t < ntile; t += gridDim.x) {
+    float* X = Xs[buf];
+    produce(t, it, cur, X);
+    __syncthreads();
+    // the next tile's rows (its ids were requested one tile earlier) and the ids after it
+    const int t2 = t + gridDim.x;
+    ProjIn nxt;
+    fetch(t2, it_next, nxt);  // past the last tile: zeros, nothing loaded
+    const int it2 = item_of(t2 + gridDim.x);
+    // ---- QKVS = X . W_all^T (f32 MFMA, k order of the fused kernel)
+    f32x4 acc[RT][CT];
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int c = 0; c < CT; ++c) acc[r][c] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int kb = 0; kb < D / 16; ++kb) {
+      float4 av[RT];
+#pragma unroll
+      for (int r = 0; r < RT; ++r) av[r] = *reinterpret_cast<const float4*>(X + (r * 16 + lr) * XS + kb * 16 + lg * 4);
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+#pragma unroll
+        for (int c = 0; c < CT; ++c) acc[r][c] = mfma4(av[r], wf[c][kb], acc[r][c]);
+    }
+#pragma unroll
+    for (int r = 0; r < RT; ++r)
+#pragma unroll
+      for (int c = 0; c < CT; ++c) {
+        const int col = (wave + c * GM_WAVES) * 16 + lr;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = t * BM + r * 16 + lg * 4 + i;
+          if (row < N) a.qkvs[(size_t)row * (4 * D) + col] = acc[r][c][i] + bias[c];
+        }
+      }
+    cur = nxt;
+    it = it_next;
+    it_next = it2;
+    buf ^= 1;
+  }
+}
+
+template <int D>
+struct DxGeom {
+  static constexpr int NCT = D / 16;                 // output column tiles of dX
+  static constexpr int WPC = GM_WAVES / NCT;         // waves per column tile (D = 64: 2, D = 128: 1)
+  static constexpr int BM = 16 * WPC;                // rows per block tile: one 16-row tile per wave
+  static constexpr int K = 4 * D;
+  static constexpr int AS = K + 4;                   // padded LDS row
+  static constexpr int PER = BM * K / 4 / GM_BLOCK;  // float4 of dQKVS per thread and tile
+  static_assert(NCT * WPC == GM_WAVES, "waves cover the column tiles");
+  static_assert(PER * 4 * GM_BLOCK == BM * K, "whole float4 per thread");
+};
+
+struct DxK {
+  gtr_batch bt;
+  int has_prev, layer;
+  float scale;
+  uint32_t seed, thresh;
+  int drop_on;
+  uint32_t ctr_add;
+  const uint32_t* rng_ctr;
+  const float* dqkvs;
+  const float* w_all;
+  const float* dy;
+  const float* p_out;
+  const float* p_stats;
+  float* p_dy;
+  float* p_gpart;
+  float* p_gsum;
+  uint32_t* p_cnt;
+  float* dx0;
+};
+
+template <int D>
+__global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
+  using G = DxGeom<D>;
+  constexpr int NCT = G::NCT, BM = G::BM, K = G::K, AS = G::AS, PER = G::PER;
+  __shared__ __attribute__((aligned(16))) float As[2][BM * AS];
+  __shared__ float s_bnp[GM_WAVES / NCT][2 * D];
+  __shared__ int s_flag;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
+  const int N = a.bt.hdr[0];
+  const int ntile = (N + BM - 1) / BM;
+  const int ct = wave % NCT, rs = wave / NCT;  // this wave's column tile and 16-row slice
+  const int col = ct * 16 + lr;
+  // ---- W_all column fragments (B[k][col] = W_all[k][col], k = kb*16 + lg*4 + j): the
+  //      fused kernel's bv, held in registers for every tile
+  float4 wb[K / 16];
+  {
+    const float* bcol = a.w_all + (size_t)(lg * 4) * D + col;
+#pragma unroll
+    for (int kb = 0; kb < K / 16; ++kb) {
+      const float* bp = bcol + (size_t)(kb * 16) * D;
+      wb[kb] = make_float4(bp[0], bp[D], bp[2 * D], bp[3 * D]);
+    }
+  }
+  const uint32_t ctr = a.rng_ctr ? load_step_ctr(a.rng_ctr) + a.ctr_add : 0u;
+  const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
+  const uint32_t st_prev = drop_stream(1, (uint32_t)(a.layer - 1), ctr);
+  float pm = 0.0f, pr = 0.0f;
+  if (a.has_prev) { pm = a.p_stats[col]; pr = a.p_stats[D + col]; }
+  float s1 = 0.0f, s2 = 0.0f;
+  // this thread's float4s of a tile's dQKVS rows: row i = idx / (K/4), column (idx % (K/4))*4
+  auto fetch = [&](int t, float4 (&v)[PER]) {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int idx = tid + u * GM_BLOCK;
+      const int i = idx / (K / 4), c = (idx - i * (K / 4)) * 4;
+      const int r = t * BM + i;
+      v[u] = (t < ntile && r < N) ? *reinterpret_cast<const float4*>(a.dqkvs + (size_t)r * K + c)
+                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  int t = blockIdx.x;
+  float4 cur[PER];
+  fetch(t, cur);
+  int buf = 0;
+  for (; t < ntile; t += gridDim.x) {
+    float* A = As[buf];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int idx = tid + u * GM_BLOCK;
+      const int i = idx / (K / 4), c = (idx - i * (K / 4)) * 4;
+      *reinterpret_cast<float4*>(A + i * AS + c) = cur[u];
+    }
+    __syncthreads();
+    fetch(t + gridDim.x, cur);  // the next tile's rows, in flight during the MFMAs
+    f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
+    const float* arow = A + (rs * 16 + lr) * AS + lg * 4;
+#pragma unroll
+    for (int kb = 0; kb < K / 16; ++kb) acc = mfma4(*reinterpret_cast<const float4*>(arow + kb * 16), wb[kb], acc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = t * BM + rs * 16 + lg * 4 + i;
+      if (row < N) {
+        const size_t o = (size_t)row * D + col;
+        const float dx = a.dy[o] + acc[i];
+        if (a.has_prev) {
+          const float d = dx * dr.mul(st_prev, (uint32_t)o);
+          a.p_dy[o] = d;
+          s1 += d;
+          s2 += d * ((a.p_out[o] - pm) * pr);
+        } else {
+          a.dx0[o] = dx;
+        }
+      }
+    }
+    buf ^= 1;
+  }
+  if (!a.has_prev) return;
+  // ---- the previous layer's BatchNorm backward sums: one partial row per workgroup (its
+  //      tiles in order), reduced by the bucketed last arrivers (fixed order: deterministic)
+  s1 = bfly_add<32>(bfly_add<16>(s1));
+  s2 = bfly_add<32>(bfly_add<16>(s2));
+  if (lg == 0) {
+    s_bnp[rs][col] = s1;
+    s_bnp[rs][D + col] = s2;
+  }
+  __syncthreads();
+  float* part = a.p_gpart + (size_t)blockIdx.x * 2 * D;
+  for (int j = tid; j < 2 * D; j += GM_BLOCK) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int q = 0; q < GM_WAVES / NCT; ++q) acc += s_bnp[q][j];
+    part[j] = acc;
+  }
+  const int Gn = gridDim.x;
+  const int nbk = (Gn + GTR_PART_BUCKET - 1) / GTR_PART_BUCKET;
+  float* scr = As[0];
+  if (nbk > 1) {
+    const int bk = blockIdx.x / GTR_PART_BUCKET, b0 = bk * GTR_PART_BUCKET;
+    if (!arrive_last(a.p_cnt + 4 + 2 * bk, (uint32_t)min(GTR_PART_BUCKET, Gn - b0), &s_flag)) return;
+    float* row0 = a.p_gpart + (size_t)b0 * 2 * D;
+    block_sum_rows<GM_BLOCK>(row0, min(GTR_PART_BUCKET, Gn - b0), 2 * D, (size_t)2 * D, row0, scr);
+    if (tid == 0) reset_counter(a.p_cnt + 4 + 2 * bk);
+    if (!arrive_last(a.p_cnt, (uint32_t)nbk, &s_flag)) return;
+    block_sum_rows<GM_BLOCK>(a.p_gpart, nbk, 2 * D, (size_t)GTR_PART_BUCKET * 2 * D, a.p_gsum, scr);
+  } else {
+    if (!arrive_last(a.p_cnt, (uint32_t)Gn, &s_flag)) return;
+    block_sum_rows<GM_BLOCK>(a.p_gpart, Gn, 2 * D, (size_t)2 * D, a.p_gsum, scr);
+  }
+  if (tid == 0) reset_counter(a.p_cnt);
+}
+
+// Persistent grid: `per_cu` workgroups per CU (the register / LDS budget: 2 at D = 64,
+// 1 at D = 128), never more than the tiles.
+int gemm_grid(int tiles, int per_cu) {
+  static int cus = 0;
+  if (cus <= 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  }
+  const char* e = getenv("GTR_GEMM_GRID");  // tuning / tests
+  const int cap = e ? atoi(e) : cus * per_cu;
+  return tiles < cap ? (tiles > 0 ? tiles : 1) : (cap > 0 ? cap : 1);
+}
+
+}  // namespace
+
+extern "C" int gtr_qkvs_fwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_embed* emb,
+                            const gtr_layer* layers, int l, gtr_stream_t stream) {
+  if (!cfg || !bt || !layers || l < 0 || l >= cfg->num_layers) {
+    set_error("gtr_qkvs_fwd: bad arguments");
+    return GTR_E_ARG;
+  }
+  const int D = cfg->dim;
+  if (D != 64 && D != 128) { set_error("gtr_qkvs_fwd: dim %d (the split layer path covers 64 / 128)", D); return GTR_E_ARG; }
+  if (l == 0 && (!emb || !emb->table)) { set_error("gtr_qkvs_fwd: layer 0 needs the table"); return GTR_E_ARG; }
+  if (l == 0 && cfg->pe_k > 0 && (!emb->wpe || !emb->bpe || (!emb->pe_tab && !bt->node_pe))) {
+    set_error("gtr_qkvs_fwd: Laplacian PE not precomputed");
+    return GTR_E_ARG;
+  }
+  if (cfg->pe_k < 0 || cfg->pe_k > 256) { set_error("gtr_qkvs_fwd: pe_k out of range"); return GTR_E_ARG; }
+  if (l > 0 && cfg->training && (cfg->consumer_reduce || cfg->sync_bn)) {
+    set_error("gtr_qkvs_fwd: the split path reads producer-finalized BatchNorm statistics (consumer_reduce 0)");
+    return GTR_E_ARG;
+  }
+  const gtr_layer& L = layers[l];
+  ProjK k{};
+  k.bt = *bt;
+  k.first = l == 0;
+  k.train = cfg->training;
+  k.pe_k = cfg->pe_k;
+  k.layer = l;
+  k.bn_eps = cfg->bn_eps;
+  k.drop_on = (cfg->training && cfg->dropout > 0.0f) ? 1 : 0;
+  {
+    double p = cfg->dropout >= 1.0f ? 0.999999 : cfg->dropout;
+    k.thresh = (uint32_t)(p * 4294967296.0);
+    k.scale = k.drop_on ? (float)(1.0 / (1.0 - p)) : 1.0f;
+  }
+  k.seed = cfg->seed;
+  k.rng_ctr = cfg->rng_ctr;
+  k.ctr_add = (uint32_t)cfg->ctr_add;
+  if (l == 0) {
+    k.table = emb->table; k.pe_tab = emb->pe_tab; k.wpe = emb->wpe; k.bpe = emb->bpe;
+  } else {
+    const gtr_layer& P = layers[l - 1];
+    k.p_out = P.out; k.p_xin = P.xin; k.p_stats = P.bn_stats; k.p_rmean = P.bn_rmean; k.p_rvar = P.bn_rvar;
+    k.p_gamma = P.bn_gamma; k.p_beta = P.bn_beta;
+  }
+  k.w_all = L.w_all; k.b_all = L.b_all; k.xin = L.xin; k.qkvs = L.qkvs;
+  const int bm = D == 64 ? ProjGeom<64>::BM : ProjGeom<128>::BM;
+  const int grid = gemm_grid((bt->n_cap + bm - 1) / bm, D == 64 ? 2 : 1);
+  hipStream_t s = (hipStream_t)stream;
+  if (D == 64) hipLaunchKernelGGL(k_proj<64>, dim3(grid), dim3(GM_BLOCK), 0, s, k);
+  else hipLaunchKernelGGL(k_proj<128>, dim3(grid), dim3(GM_BLOCK), 0, s, k);
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+extern "C" int gtr_qkvs_bwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l, float* dx0,
+                            gtr_stream_t stream) {
+  if (!cfg || !bt || !layers || l < 0 || l >= cfg->num_layers || (l == 0 && !dx0)) {
+    set_error("gtr_qkvs_bwd: bad arguments");
+    return GTR_E_ARG;
+  }
+  const int D = cfg->dim;
+  if (D != 64 && D != 128) { set_error("gtr_qkvs_bwd: dim %d (the split layer path covers 64 / 128)", D); return GTR_E_ARG; }
+  if (!cfg->training) { set_error("gtr_qkvs_bwd: backward requires training mode"); return GTR_E_ARG; }
+  if (cfg->sync_bn) { set_error("gtr_qkvs_bwd: sync_bn runs the fused layer path"); return GTR_E_ARG; }
+  const gtr_layer& L = layers[l];
+  DxK k{};
+  k.bt = *bt;
+  k.has_prev = l > 0;
+  k.layer = l;
+  k.drop_on = (cfg->dropout > 0.0f) ? 1 : 0;
+  {
+    double p = cfg->dropout >= 1.0f ? 0.999999 : cfg->dropout;
+    k.thresh = (uint32_t)(p * 4294967296.0);
+    k.scale = k.drop_on ? (float)(1.0 / (1.0 - p)) : 1.0f;
+  }
+  k.seed = cfg->seed;
+  k.rng_ctr = cfg->rng_ctr;
+  k.ctr_add = (uint32_t)cfg->ctr_add;
+  k.dqkvs = L.dqkvs; k.w_all = L.w_all; k.dy = L.dy; k.dx0 = dx0;
+  if (l > 0) {
+    const gtr_layer& P = layers[l - 1];
+    k.p_out = P.out; k.p_stats = P.bn_stats; k.p_dy = P.dy; k.p_gpart = P.bn_gpart; k.p_gsum = P.bn_gsum;
+    k.p_cnt = P.cnt + 1;
+  }
+  const int bm = D == 64 ? DxGeom<64>::BM : DxGeom<128>::BM;
+  const int grid = gemm_grid((bt->n_cap + bm - 1) / bm, 1);
+  if (grid > 256) { set_error("gtr_qkvs_bwd: more than 256 partial rows"); return GTR_E_ARG; }
+  hipStream_t s = (hipStream_t)stream;
+  if (D == 64) hipLaunchKernelGGL(k_dx<64>, dim3(grid), dim3(GM_BLOCK), 0, s, k);
+  else hipLaunchKernelGGL(k_dx<128>, dim3(grid), dim3(GM_BLOCK), 0, s, k);
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}

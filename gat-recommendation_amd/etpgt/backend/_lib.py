@@ -143,6 +143,10 @@ _SIGS = {
     "gtr_conv_fwd": (C.c_int, [P, P, P, P, C.c_int, P]),
     "gtr_readout_loss": (C.c_int, [P, P, P, P, P, P]),
     "gtr_conv_bwd": (C.c_int, [P, P, P, C.c_int, P, P]),
+    "gtr_qkvs_fwd": (C.c_int, [P, P, P, P, C.c_int, P]),
+    "gtr_attn_fwd": (C.c_int, [P, P, P, C.c_int, P]),
+    "gtr_attn_bwd": (C.c_int, [P, P, P, C.c_int, P]),
+    "gtr_qkvs_bwd": (C.c_int, [P, P, P, C.c_int, P, P]),
     "gtr_wgrad": (C.c_int, [P, P, P, P, P, P, P, C.c_int, i64, C.c_int, C.c_int, P]),
     "gtr_adamw_small": (C.c_int, [P, P, P, P, i64, P, C.c_int, P, P]),
     "gtr_contrib_prep": (C.c_int, [P, C.c_int, P, P, P, P, P]),

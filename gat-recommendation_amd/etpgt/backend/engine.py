@@ -150,6 +150,18 @@ def readout_grid(b_cap: int) -> int:
     return int(L.lib().gtr_readout_grid(int(b_cap)))
 
 
+def split_default(D: int, g_cap: int) -> bool:
+    """The split (GEMM + attention) layer path: GTR_SPLIT=1 / 0 forces it on / off (tests,
+    A/B); by default from 129 row groups on -- where the chain sweep is off too -- at
+    D in {64, 128}."""
+    if D not in (64, 128):
+        return False
+    e = os.environ.get("GTR_SPLIT")
+    if e is not None:
+        return e == "1"
+    return g_cap > 128
+
+
 class Workspace:
     """Capacity-sized activations + gradient buffers for one in-flight batch."""
 
@@ -168,10 +180,17 @@ class Workspace:
                 agg=_f32(n, D, device=dev), gate=_f32(n, device=dev), out=_f32(n, D, device=dev),
                 bn_stats=_f32(2 * D, device=dev), bn_part=_f32(g, 1 + 2 * D, device=dev),
                 bn_gsum=_f32(2 * D, device=dev), bn_gpart=_f32(max(g, 256), 2 * D, device=dev),
-                cnt=_i32(8 + 2 * ((g + 31) // 32), dev), dy=_f32(n, D, device=dev), dqkvs=_f32(n, 4 * D, device=dev),
+                # arrival counters: [0..3] + two per bucket of 32 partial rows -- the row groups
+                # or the <= 256 workgroups of the split path's dX GEMM (gtr_qkvs_bwd)
+                cnt=_i32(8 + 2 * max((g + 31) // 32, 8), dev), dy=_f32(n, D, device=dev),
+                dqkvs=_f32(n, 4 * D, device=dev),
                 du=_f32(n, device=dev), dlogit=_f32(e, H, device=dev), dagg=_f32(n, D, device=dev),
             )
             self.layers.append(t)
+        # large batches: each layer as GEMM + attention launches (gtr_qkvs_* / gtr_attn_*)
+        # instead of one fused launch -- from more row groups than the chip has CUs / 2
+        # (the fused kernels re-fetch W_all per 16-row group), D in {64, 128}
+        self.split = split_default(D, g)
         self.dx0 = _f32(n, D, device=dev)
         self.se = _f32(b, D, device=dev)
         self.dse_in = _f32(b, D, device=dev)
@@ -278,6 +297,8 @@ class Engine:
         # fold every group's partial in its prologue; large grids use the last arriver
         cred = os.environ.get("GTR_CONSUMER_REDUCE")
         cfg.consumer_reduce = int(cred) if cred is not None else (1 if ws.g_cap <= 64 else 0)
+        if ws.split:  # the split path's producers finalize their BatchNorm statistics
+            cfg.consumer_reduce = 0
         return cfg
 
     def fill_embed(self, table: int | None = None):
@@ -311,13 +332,32 @@ class Engine:
         return torch.cuda.current_stream(self.device).cuda_stream
 
     # ------------------------------------------------------------------ launches
-    def run_forward(self, ws: Workspace, cfg: L.GtrConfig, bs: L.GtrBatch, flags: int,
-                    loss_kind: int = 0, temperature: float = 1.0, alpha: float = 0.7):
+    def layer_fwd(self, ws: Workspace, cfg: L.GtrConfig, bs: L.GtrBatch, l: int, emb, st: int,
+                  split: bool | None = None):
+        """Forward of layer l: one fused launch, or (split) the projection GEMM + attention."""
         lib = L.lib()
+        if ws.split if split is None else split:
+            L.check(lib.gtr_qkvs_fwd(C.byref(cfg), C.byref(bs), C.byref(emb), ws.structs, l, st), "qkvs_fwd")
+            L.check(lib.gtr_attn_fwd(C.byref(cfg), C.byref(bs), ws.structs, l, st), "attn_fwd")
+        else:
+            L.check(lib.gtr_conv_fwd(C.byref(cfg), C.byref(bs), C.byref(emb), ws.structs, l, st), "conv_fwd")
+
+    def layer_bwd(self, ws: Workspace, cfg: L.GtrConfig, bs: L.GtrBatch, l: int, st: int,
+                  split: bool | None = None):
+        """Backward of layer l: one fused launch, or (split) the attention backward + dX GEMM."""
+        lib = L.lib()
+        if ws.split if split is None else split:
+            L.check(lib.gtr_attn_bwd(C.byref(cfg), C.byref(bs), ws.structs, l, st), "attn_bwd")
+            L.check(lib.gtr_qkvs_bwd(C.byref(cfg), C.byref(bs), ws.structs, l, ws.dx0.data_ptr(), st), "qkvs_bwd")
+        else:
+            L.check(lib.gtr_conv_bwd(C.byref(cfg), C.byref(bs), ws.structs, l, ws.dx0.data_ptr(), st), "conv_bwd")
+
+    def run_forward(self, ws: Workspace, cfg: L.GtrConfig, bs: L.GtrBatch, flags: int,
+                    loss_kind: int = 0, temperature: float = 1.0, alpha: float = 0.7, split: bool | None = None):
         st = self.stream()
         emb = self.fill_embed()
         for l in range(self.L):
-            L.check(lib.gtr_conv_fwd(C.byref(cfg), C.byref(bs), C.byref(emb), ws.structs, l, st), "conv_fwd")
+            self.layer_fwd(ws, cfg, bs, l, emb, st, split)
         self.run_head(ws, cfg, bs, flags, loss_kind, temperature, alpha)
 
     def run_head(self, ws, cfg, bs, flags, loss_kind=0, temperature=1.0, alpha=0.7, dse_out=False, table=None):
@@ -352,7 +392,7 @@ class Engine:
                                   self.flat.layout.slab_stride, l0, l1, st), "wgrad")
 
     def run_backward(self, ws: Workspace, cfg: L.GtrConfig, bs: L.GtrBatch, side: torch.cuda.Stream | None = None,
-                     wgrad: bool = True):
+                     wgrad: bool = True, split: bool | None = None):
         """conv_bwd(L-1..0) + weight-gradient slabs; expects layers[L-1].dy / bn_gsum.
         With ``side``, layer l >= 1 weight gradients run on that stream concurrently
         with conv_bwd(l-1..0); the caller must join ``side`` before reading slabs.
@@ -361,7 +401,7 @@ class Engine:
         main = torch.cuda.current_stream(self.device)
         st = main.cuda_stream
         for l in range(self.L - 1, -1, -1):
-            L.check(lib.gtr_conv_bwd(C.byref(cfg), C.byref(bs), ws.structs, l, ws.dx0.data_ptr(), st), "conv_bwd")
+            self.layer_bwd(ws, cfg, bs, l, st, split)
             if wgrad and side is not None and l >= 1:
                 side.wait_stream(main)
                 self._wgrad(ws, cfg, bs, l, l + 1, side.cuda_stream)

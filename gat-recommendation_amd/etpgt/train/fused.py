@@ -177,6 +177,9 @@ class FusedTrainStep:
         self.sort_tmp = torch.zeros(max(int(nb.value), 16), dtype=torch.uint8, device=self.dev)
         self.segs, self.nseg = eng.segments(self.ws)
         self.cfg = eng.config(self.ws, True)
+        # large batches: every layer as projection GEMM + attention launches (Engine.layer_fwd /
+        # layer_bwd); SyncBN keeps the fused kernels (their consumer-side partial reduction)
+        self.split = bool(self.ws.split) and not self.sync_bn
         ws = self.ws
         t = L.GtrTail()
         t.skeys, t.svals = self.skeys.data_ptr(), self.svals.data_ptr()
@@ -204,7 +207,7 @@ class FusedTrainStep:
         # conv_fwd(0) (gtr_begin) -- one launch less; that launch stamps the touched rows,
         # so it carries no sweep slice
         self.begin_fused = (not self.data_parallel and not self.lazy and m_cap <= 8192 and eng.T < (1 << 19)
-                            and os.environ.get("GTR_BEGIN_FUSED", "1") != "0")
+                            and not self.split and os.environ.get("GTR_BEGIN_FUSED", "1") != "0")
         if self.begin_fused:
             wts[0] = 0.0
         # data parallel: the union of the ranks' touched rows is known once the sorted keys
@@ -217,7 +220,8 @@ class FusedTrainStep:
         if self.early_union:
             wts = [0.0] * eng.L + wts[eng.L:]
         slots = len(wts)
-        if chain and not self.shard_table and (not self.data_parallel or self.early_union or self.lagged) \
+        if chain and not self.shard_table and not self.split \
+                and (not self.data_parallel or self.early_union or self.lagged) \
                 and self.ws.g_cap <= 128 and slots <= L.SWEEP_SLOTS:
             sw = L.GtrSweep()
             sw.table = eng.model.item_embedding.weight.data_ptr()
@@ -329,14 +333,30 @@ class FusedTrainStep:
         ``run()`` first writes the builder's next batch into the batch image, and the
         build is captured in the step's hipGraph with the rest.  Capacities cover the
         builder's next ``num_batches`` batches (default: one epoch of its order)."""
-        caps = builder.plan_caps(num_batches, int(builder.cursor.item()))
-        if caps.n_neg != (self.caps.n_neg if self.caps is not None else caps.n_neg):
-            raise ValueError("the number of negatives per session must stay fixed")
+        caps = self._planned_caps(builder, num_batches)
         if self.caps is None or not self.caps.fits(caps.n_cap, caps.b_cap, caps.e_cap, caps.n_neg):
             self._bind(caps if self.caps is None else self.caps.grow(caps.n_cap, caps.b_cap, caps.e_cap, caps.n_neg))
         self.builder = builder
         self.graph = self.graph_pe = self.graph_b = None
         self.resident_graphs = None
+
+    def _planned_caps(self, builder, num_batches: int | None) -> Caps:
+        """Capacities of the builder's next batches; data parallel: agreed over the ranks
+        FIRST, so that every rank takes the same rebind decision (a rank-local one would
+        leave the others waiting in _bind's collective)."""
+        caps = builder.plan_caps(num_batches, int(builder.cursor.item()))
+        if caps.n_neg != (self.caps.n_neg if self.caps is not None else caps.n_neg):
+            raise ValueError("the number of negatives per session must stay fixed")
+        return self._agree(caps)
+
+    def refresh_builder_caps(self, num_batches: int | None = None):
+        """Grow the capacities if the attached builder's next ``num_batches`` batches need it
+        (collective in data parallel); the captured graphs survive when nothing grows."""
+        if self.builder is None:
+            raise RuntimeError("no device batch builder attached")
+        caps = self._planned_caps(self.builder, num_batches)
+        if not self.caps.fits(caps.n_cap, caps.b_cap, caps.e_cap, caps.n_neg):
+            self.attach_builder(self.builder, num_batches)
 
     def detach_builder(self):
         self.builder = None
@@ -401,8 +421,9 @@ class FusedTrainStep:
         bs = self.bs_pe if with_pe else self.bs
         st = torch.cuda.current_stream(self.dev).cuda_stream
         self._begin(bs, st)
-        eng.run_forward(ws, cfg, bs, L.RO_FWD | L.RO_LOSS | L.RO_BWD, self.loss_kind, self.temperature, self.alpha)
-        eng.run_backward(ws, cfg, bs, wgrad=not self.tail_wgrad)
+        eng.run_forward(ws, cfg, bs, L.RO_FWD | L.RO_LOSS | L.RO_BWD, self.loss_kind, self.temperature, self.alpha,
+                        split=self.split)
+        eng.run_backward(ws, cfg, bs, wgrad=not self.tail_wgrad, split=self.split)
         if self.dp is not None:
             self.dp.launch_pack(bs, st)
 
@@ -502,15 +523,14 @@ class FusedTrainStep:
             sh.route(bs, st())
 
         def fwd(l):
-            L.check(lib.gtr_conv_fwd(C.byref(cfg), C.byref(bc), C.byref(eng.fill_embed(tab)), ws.structs, l, st()),
-                    "conv_fwd")
+            eng.layer_fwd(ws, cfg, bc, l, eng.fill_embed(tab), st(), self.split)
 
         def head():
             eng.run_head(ws, cfg, bc, L.RO_FWD | L.RO_LOSS | L.RO_BWD, self.loss_kind, self.temperature, self.alpha,
                          table=tab)
 
         def bwd(l):
-            L.check(lib.gtr_conv_bwd(C.byref(cfg), C.byref(bc), ws.structs, l, ws.dx0.data_ptr(), st()), "conv_bwd")
+            eng.layer_bwd(ws, cfg, bc, l, st(), self.split)
             if l == 0:
                 eng._wgrad(ws, cfg, bc, 0, Lc, st())
                 sh.pack(bs, st())
@@ -578,7 +598,7 @@ class FusedTrainStep:
         def fwd():
             emb = eng.fill_embed()
             for l in range(eng.L):
-                L.check(lib.gtr_conv_fwd(C.byref(cfg), C.byref(bs), C.byref(emb), ws.structs, l, st()), "conv_fwd")
+                eng.layer_fwd(ws, cfg, bs, l, emb, st(), self.split)
 
         def keys_wait():
             pending.pop("w").wait()
@@ -587,7 +607,7 @@ class FusedTrainStep:
             L.check(lib.gtr_dp_union_stamp(self.keys_all.data_ptr(), self.keys_all.numel(), eng.T,
                                            self.stamp.data_ptr(), self.step_dev.data_ptr(), st()), "dp_union_stamp")
             eng.run_head(ws, cfg, bs, L.RO_FWD | L.RO_LOSS | L.RO_BWD, self.loss_kind, self.temperature, self.alpha)
-            eng.run_backward(ws, cfg, bs)
+            eng.run_backward(ws, cfg, bs, split=self.split)
             self.dp.launch_pack(bs, st())
 
         return [(begin, keys_start), (fwd, keys_wait), (rest, self.dp.exchange),

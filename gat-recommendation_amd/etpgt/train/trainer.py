@@ -117,10 +117,8 @@ class Trainer:
         bld = loader.builder
         if fused.builder is not bld:
             fused.attach_builder(bld, num_batches=len(sizes))
-        else:  # capacities for this epoch's order (rebinds only if they grew)
-            caps = bld.plan_caps(len(sizes), bld.pos)
-            if not fused.caps.fits(caps.n_cap, caps.b_cap, caps.e_cap, caps.n_neg):
-                fused.attach_builder(bld, num_batches=len(sizes))
+        else:  # capacities for this epoch's order (rebinds only if they grew; agreed over ranks)
+            fused.refresh_builder_caps(len(sizes))
         total = torch.zeros((), dtype=torch.float64, device=self.device)
         for i, b in enumerate(sizes):
             if b == loader.batch_size:

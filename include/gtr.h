@@ -226,6 +226,32 @@ int gtr_readout_loss(const gtr_config* cfg, const gtr_batch* bt, const float* ta
 int gtr_conv_bwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l,
                  float* dx0, gtr_stream_t stream);
 
+/* ---- large-batch ("split") layer path: the same layer as gtr_conv_fwd / gtr_conv_bwd
+ * in two launches each, the dense GEMMs over ALL node rows (persistent f32-MFMA kernels
+ * that keep W_all in registers per CU) and the per-row-group attention apart.  qkvs and
+ * dX are bitwise those of the fused kernels (same k order); the BatchNorm backward sums
+ * are summed in another (fixed) order.  Training needs consumer_reduce = 0 and no
+ * sync_bn; D in {64, 128} for the GEMMs.  Order per layer:
+ *   forward   gtr_qkvs_fwd(l) -> gtr_attn_fwd(l)
+ *   backward  gtr_attn_bwd(l) -> gtr_qkvs_bwd(l)                                     */
+/* X (layer 0: item row + LapPE projection, graph_transformer.py:140-152; l > 0: dropout(
+ * BN(prev out) + prev in), :175-177) -> layers[l].xin; qkvs = X . W_all^T + b_all (PyG
+ * TransformerConv lin_query/key/value/skip) -> layers[l].qkvs.                        */
+int gtr_qkvs_fwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_embed* emb,
+                 const gtr_layer* layers, int l, gtr_stream_t stream);
+/* Attention over in-edges, beta gate and this layer's BatchNorm partials / statistics
+ * from layers[l].qkvs (PyG TransformerConv message/softmax/aggregate). */
+int gtr_attn_fwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l,
+                 gtr_stream_t stream);
+/* BatchNorm backward, gate backward, softmax backward, dQ / dK / dV -> layers[l].dqkvs,
+ * du, dlogit (given layers[l].dy and bn_gsum).                                        */
+int gtr_attn_bwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l,
+                 gtr_stream_t stream);
+/* dX = dQKVS . W_all + dy, the previous layer's dropout mask -> layers[l-1].dy and its
+ * BatchNorm backward sums (bn_gsum), or dx0 at l == 0.                                */
+int gtr_qkvs_bwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l,
+                 float* dx0, gtr_stream_t stream);
+
 /* Weight-gradient partial slabs for layers [l_begin, l_end) (+ LapPE projection
  * when l_begin == 0).
  * Slab layout matches the flat parameter layout of each layer block:

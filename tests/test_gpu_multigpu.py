@@ -154,3 +154,35 @@ def test_train_baseline_two_ranks_equal_one_gpu_global_batch(tmp_path):
         assert float(ok.float().mean()) >= 0.999, (k, float(ok.float().mean()))
     for r0, r1 in zip(res[0][0]["val_metrics"], hist["val_metrics"]):
         assert abs(r0["recall@10"] - r1["recall@10"]) <= 2.0 / 40 + 1e-9
+
+
+def test_rank_sharded_device_loader_equals_the_global_batch(tmp_path):
+    """DeviceSessionLoader(rank, world): rank r's batch i is sessions [i*P*B + r*B, +B) of
+    the epoch order with the negatives a single GPU draws for global batch i (positions),
+    the last global batch split evenly -- in one process, no process group needed."""
+    from dropin_helpers import write_csvs
+
+    from etpgt.train.dataloader import DeviceSessionLoader, SessionDataset
+
+    d = write_csvs(tmp_path, num_train=150)
+    ds = SessionDataset(d / "train.csv", d / "graph_edges.csv", 5, 50)
+
+    def epoch(loader):
+        out = []
+        for b in loader:
+            ptr = b.ptr.cpu()
+            x = b.x.cpu()
+            out.append([(x[ptr[s]:ptr[s + 1]].tolist(), int(b.target_item[s]), b.negative_items.view(-1, 5)[s].tolist())
+                        for s in range(b.num_graphs)])
+        return out
+
+    torch.manual_seed(3)
+    one = epoch(DeviceSessionLoader(ds, 16, 5, shuffle=True, seed=42))
+    ranks = []
+    for r in range(2):
+        torch.manual_seed(3)
+        ranks.append(epoch(DeviceSessionLoader(ds, 8, 5, shuffle=True, seed=42, rank=r, world=2)))
+    assert [len(b) for b in one] == [16] * 9 + [6]
+    assert [len(b) for b in ranks[0]] == [8] * 9 + [3]
+    for i, g in enumerate(one):
+        assert ranks[0][i] + ranks[1][i] == g, i
