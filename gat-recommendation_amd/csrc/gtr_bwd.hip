@@ -113,8 +113,9 @@ extern "C" int gtr_attn_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     set_error("gtr_attn_bwd: bad arguments");
     return GTR_E_ARG;
   }
-  if (cfg->consumer_reduce || cfg->sync_bn) {
-    set_error("gtr_attn_bwd: the split path reads producer-finalized BatchNorm sums (consumer_reduce 0)");
+  if (cfg->sync_bn ? !cfg->split_sync : cfg->consumer_reduce) {
+    set_error("gtr_attn_bwd: the split path reads producer-finalized BatchNorm sums (consumer_reduce 0) or, "
+              "under sync_bn, the gathered per-rank sums (split_sync)");
     return GTR_E_ARG;
   }
   ConvBwdK k;

@@ -71,7 +71,9 @@ struct ConvFwdK {
   uint32_t ctr_add;     // dropout counter read as *rng_ctr + ctr_add (1 with a fused begin)
   int nbeg;             // fused step begin (layer 0): roles [main_grid, main_grid + nbeg)
   gtr_begin beg;
-  int xpack, pad_x;     // XCD-packed roles (role_block)
+  int xpack;            // XCD-packed roles (role_block)
+  int merge_only;       // split path under SyncBN: the last arriver merges the partials into
+                        // bn_part row 0 (count, mean, M2) for the all-gather; no statistics
 };
 
 // Block prologue shared by k_conv_fwd (previous layer) and k_readout (last layer):
@@ -716,10 +718,20 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
     bn_merge_parts<D, CONV_BLOCK>(row0, min(GTR_PART_BUCKET, Gn - b0), red, PW, row0);
     if (tid == 0) reset_counter(a.cnt + 4 + 2 * bk);
     if (!arrive_last(a.cnt, (uint32_t)nbk, s_flag)) return;
+    if (a.merge_only) {  // the buckets' rows -> ONE row (row 0, bucket 0's own row: may alias)
+      bn_merge_parts<D, CONV_BLOCK>(a.bn_part, nbk, red, (size_t)GTR_PART_BUCKET * PW, a.bn_part);
+      if (tid == 0) reset_counter(a.cnt);
+      return;
+    }
     bn_stats_from_parts<D, CONV_BLOCK>(a.bn_part, nbk, a.bn_eps, s_bn, s_bn + D, XO, red,
                                        (size_t)GTR_PART_BUCKET * PW);
   } else {
     if (!arrive_last(a.cnt, (uint32_t)Gn, s_flag)) return;
+    if (a.merge_only) {
+      bn_merge_parts<D, CONV_BLOCK>(a.bn_part, Gn, red, PW, a.bn_part);
+      if (tid == 0) reset_counter(a.cnt);
+      return;
+    }
     bn_stats_from_parts<D, CONV_BLOCK>(a.bn_part, Gn, a.bn_eps, s_bn, s_bn + D, XO, red);
   }
   for (int j = tid; j < D; j += CONV_BLOCK) {
@@ -1571,7 +1583,7 @@ int make_readout_args(const gtr_config* cfg, const gtr_batch* bt, const float* t
   k.cred = cfg->consumer_reduce;
   // finalise in-kernel unless a consumer takes over: the BN sums go to conv_bwd and the
   // loss to gtr_step_end in the fused step; a loss-only call always finalises itself.
-  k.fin = (!cfg->consumer_reduce || !(head->flags & GTR_RO_BWD)) ? 1 : 0;
+  k.fin = (!cfg->consumer_reduce || !(head->flags & GTR_RO_BWD) || cfg->split_sync) ? 1 : 0;
   k.temperature = head->temperature;
   k.dual_alpha = head->dual_alpha;
   k.bn_eps = cfg->bn_eps;
@@ -1657,12 +1669,18 @@ extern "C" int gtr_attn_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     set_error("gtr_attn_fwd: bad arguments");
     return GTR_E_ARG;
   }
-  if (cfg->training && (cfg->consumer_reduce || cfg->sync_bn)) {
-    set_error("gtr_attn_fwd: the split path finalizes its BatchNorm statistics in the producer (consumer_reduce 0)");
+  if (cfg->training && (cfg->sync_bn ? !cfg->split_sync : cfg->consumer_reduce)) {
+    set_error("gtr_attn_fwd: the split path needs producer-finalized BatchNorm statistics (consumer_reduce 0) "
+              "or, under sync_bn, split_sync");
     return GTR_E_ARG;
   }
   ConvFwdK k;
   if (const int rc = make_fwd_args(cfg, bt, nullptr, layers, l, k, true)) return rc;
+  if (cfg->sync_bn && cfg->training) {  // one merged row per rank for the all-gather
+    k.cred = 0;
+    k.merge_only = 1;
+    k.sync = 0;  // no zero rows for empty groups: only live groups arrive
+  }
   const int grid = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;
   if (grid <= 0) return GTR_OK;
   k.main_grid = grid;

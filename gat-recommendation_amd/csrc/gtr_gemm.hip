@@ -57,15 +57,19 @@ struct ProjK {
   const float* bpe;
   const float* p_out;
   const float* p_xin;
-  const float* p_stats;
-  const float* p_rmean;
-  const float* p_rvar;
+  float* p_stats;
+  float* p_rmean;
+  float* p_rvar;
+  int64_t* p_nbt;
   const float* p_gamma;
   const float* p_beta;
   const float* w_all;
   const float* b_all;
   float* xin;
   float* qkvs;
+  int sync, p_nparts;        // split_sync: fold the ranks' merged rows of the previous layer
+  const float* p_part_all;   // [p_nparts][1 + 2D] (count, mean, M2)
+  float bn_mom;
 };
 
 // Inputs of one thread's float4 of X for one tile: layer 0 the item row (+ its LapPE row),
@@ -107,6 +111,22 @@ __global__ __launch_bounds__(GM_BLOCK) void k_proj(ProjK a) {
       }
     if (a.pe_k > 0)
       for (int j = tid; j < D; j += GM_BLOCK) s_c[j] = a.bpe[j];
+  } else if (a.sync && a.train) {
+    // SyncBN (split_sync): every rank's merged (count, mean, M2) row of the previous layer,
+    // folded in rank order; workgroup 0 publishes the statistics (read by the backward) and
+    // updates the running statistics -- prev_bn_stats of k_conv_fwd with P rows
+    float* s_uvar = Xs[1];
+    bn_stats_from_parts<D, GM_BLOCK>(a.p_part_all, a.p_nparts, a.bn_eps, s_c + D, s_c + 2 * D, s_uvar, Xs[0]);
+    for (int j = tid; j < D; j += GM_BLOCK) {
+      s_c[3 * D + j] = a.p_gamma[j];
+      if (blockIdx.x == 0) {
+        a.p_stats[j] = s_c[D + j];
+        a.p_stats[D + j] = s_c[2 * D + j];
+        a.p_rmean[j] = (1.0f - a.bn_mom) * a.p_rmean[j] + a.bn_mom * s_c[D + j];
+        a.p_rvar[j] = (1.0f - a.bn_mom) * a.p_rvar[j] + a.bn_mom * s_uvar[j];
+      }
+    }
+    if (blockIdx.x == 0 && tid == 0 && a.p_nbt) *a.p_nbt += 1;
   } else {
     for (int j = tid; j < D; j += GM_BLOCK) {
       // the previous layer's BatchNorm: batch statistics (finalized by its producer) or,
@@ -429,8 +449,9 @@ extern "C" int gtr_qkvs_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     return GTR_E_ARG;
   }
   if (cfg->pe_k < 0 || cfg->pe_k > 256) { set_error("gtr_qkvs_fwd: pe_k out of range"); return GTR_E_ARG; }
-  if (l > 0 && cfg->training && (cfg->consumer_reduce || cfg->sync_bn)) {
-    set_error("gtr_qkvs_fwd: the split path reads producer-finalized BatchNorm statistics (consumer_reduce 0)");
+  if (l > 0 && cfg->training && (cfg->sync_bn ? !cfg->split_sync : cfg->consumer_reduce)) {
+    set_error("gtr_qkvs_fwd: the split path reads producer-finalized BatchNorm statistics (consumer_reduce 0) "
+              "or, under sync_bn, the ranks' merged rows (split_sync)");
     return GTR_E_ARG;
   }
   const gtr_layer& L = layers[l];
@@ -455,7 +476,17 @@ extern "C" int gtr_qkvs_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   } else {
     const gtr_layer& P = layers[l - 1];
     k.p_out = P.out; k.p_xin = P.xin; k.p_stats = P.bn_stats; k.p_rmean = P.bn_rmean; k.p_rvar = P.bn_rvar;
-    k.p_gamma = P.bn_gamma; k.p_beta = P.bn_beta;
+    k.p_nbt = P.bn_nbt; k.p_gamma = P.bn_gamma; k.p_beta = P.bn_beta;
+    k.bn_mom = cfg->bn_momentum;
+    if (cfg->sync_bn && cfg->training) {
+      if (!P.bn_part_all || P.nparts_fwd <= 0) {
+        set_error("gtr_qkvs_fwd: sync_bn needs the gathered merged rows of layer %d", l - 1);
+        return GTR_E_ARG;
+      }
+      k.sync = 1;
+      k.p_part_all = P.bn_part_all;
+      k.p_nparts = P.nparts_fwd;
+    }
   }
   k.w_all = L.w_all; k.b_all = L.b_all; k.xin = L.xin; k.qkvs = L.qkvs;
   const int bm = D == 64 ? ProjGeom<64>::BM : ProjGeom<128>::BM;
@@ -476,7 +507,7 @@ extern "C" int gtr_qkvs_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   const int D = cfg->dim;
   if (D != 64 && D != 128) { set_error("gtr_qkvs_bwd: dim %d (the split layer path covers 64 / 128)", D); return GTR_E_ARG; }
   if (!cfg->training) { set_error("gtr_qkvs_bwd: backward requires training mode"); return GTR_E_ARG; }
-  if (cfg->sync_bn) { set_error("gtr_qkvs_bwd: sync_bn runs the fused layer path"); return GTR_E_ARG; }
+  if (cfg->sync_bn && !cfg->split_sync) { set_error("gtr_qkvs_bwd: sync_bn needs split_sync"); return GTR_E_ARG; }
   const gtr_layer& L = layers[l];
   DxK k{};
   k.bt = *bt;

@@ -178,8 +178,9 @@ class FusedTrainStep:
         self.segs, self.nseg = eng.segments(self.ws)
         self.cfg = eng.config(self.ws, True)
         # large batches: every layer as projection GEMM + attention launches (Engine.layer_fwd /
-        # layer_bwd); SyncBN keeps the fused kernels (their consumer-side partial reduction)
-        self.split = bool(self.ws.split) and not self.sync_bn
+        # layer_bwd); under SyncBN one merged BatchNorm row per rank and layer is gathered
+        # (gtr_config.split_sync) instead of every row group's partials
+        self.split = bool(self.ws.split)
         ws = self.ws
         t = L.GtrTail()
         t.skeys, t.svals = self.skeys.data_ptr(), self.svals.data_ptr()
@@ -373,15 +374,19 @@ class FusedTrainStep:
         rg = readout_grid(self.caps.b_cap)
         self.sync_bufs = []
         for l in range(Lc):
-            rows_b = rg if l == Lc - 1 else g
-            pa = torch.zeros(W, g * (1 + 2 * D), dtype=torch.float32, device=self.dev)
+            # fused kernels: every row group's partial rows; split path: ONE merged forward row
+            # (count, mean, M2) and the finalized backward sums per rank (gtr_config.split_sync)
+            rows_f = 1 if self.split else g
+            rows_b = 1 if self.split else (rg if l == Lc - 1 else g)
+            pa = torch.zeros(W, rows_f * (1 + 2 * D), dtype=torch.float32, device=self.dev)
             ga = torch.zeros(W, rows_b * 2 * D, dtype=torch.float32, device=self.dev)
             st = ws.structs[l]
             st.bn_part_all, st.bn_gpart_all = pa.data_ptr(), ga.data_ptr()
-            st.nparts_fwd, st.nparts_bwd = W * g, W * rows_b
-            self.sync_bufs.append((pa, ga, g * (1 + 2 * D), rows_b * 2 * D))
+            st.nparts_fwd, st.nparts_bwd = W * rows_f, W * rows_b
+            self.sync_bufs.append((pa, ga, rows_f * (1 + 2 * D), rows_b * 2 * D))
         self.cfg.consumer_reduce = 1
         self.cfg.sync_bn = 1
+        self.cfg.split_sync = 1 if self.split else 0
 
     def _gather_fwd(self, l):
         from etpgt.train.distributed import all_gather_packs
@@ -393,7 +398,8 @@ class FusedTrainStep:
         from etpgt.train.distributed import all_gather_packs
 
         _, ga, _, n = self.sync_bufs[l]
-        all_gather_packs(ga, self.ws.layers[l]["bn_gpart"].view(-1)[:n], self.group)
+        src = self.ws.layers[l]["bn_gsum" if self.split else "bn_gpart"]
+        all_gather_packs(ga, src.view(-1)[:n], self.group)
 
     def _begin(self, bs, st):
         eng = self.eng
@@ -475,8 +481,7 @@ class FusedTrainStep:
             def f():
                 if l == 0:
                     self._begin(bs, st())
-                L.check(lib.gtr_conv_fwd(C.byref(cfg), C.byref(bs), C.byref(eng.fill_embed()), ws.structs, l, st()),
-                        "conv_fwd")
+                eng.layer_fwd(ws, cfg, bs, l, eng.fill_embed(), st(), self.split)
             return f
 
         def head():
@@ -484,8 +489,7 @@ class FusedTrainStep:
 
         def bwd(l):
             def f():
-                L.check(lib.gtr_conv_bwd(C.byref(cfg), C.byref(bs), ws.structs, l, ws.dx0.data_ptr(), st()),
-                        "conv_bwd")
+                eng.layer_bwd(ws, cfg, bs, l, st(), self.split)
                 if l == 0:
                     eng._wgrad(ws, cfg, bs, 0, Lc, st())
                     self.dp.launch_pack(bs, st())

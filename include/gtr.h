@@ -128,7 +128,13 @@ typedef struct gtr_config {
                               slices run by extra workgroups of the layer kernels */
   const gtr_begin* begin;  /* optional: gtr_conv_fwd(layer 0) also runs the step begin */
   int32_t ctr_add;         /* added to *rng_ctr by every kernel (1 with a fused begin)    */
-  int32_t pad_cfg;
+  int32_t split_sync;      /* 1: SyncBN on the split layer path: gtr_attn_fwd merges its
+                              partials into ONE (count, mean, M2) row (bn_part row 0), the
+                              readout and gtr_qkvs_bwd finalize their local backward sums
+                              (bn_gsum); the ranks all-gather those single rows, so
+                              bn_part_all is [P][1 + 2D] and bn_gpart_all [P][2D]
+                              (nparts_fwd = nparts_bwd = P), and the consumers
+                              (gtr_qkvs_fwd, the readout, gtr_attn_bwd) fold P rows     */
 } gtr_config;
 
 

@@ -137,8 +137,8 @@ def _concat(b0, b1):
                         num_graphs=b0.num_graphs + b1.num_graphs)
 
 
-def _sync_worker(rank, world, port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+def _sync_worker(rank, world, port, q, split="0"):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GTR_SPLIT=split)
     import torch.distributed as dist
 
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -148,7 +148,7 @@ def _sync_worker(rank, world, port, q):
         m, _ = make_pair(T, D, H, K=0, seed=25)
         m.train()
         f = FusedTrainStep(m, lr=1e-2, weight_decay=1e-2, loss="listwise", sync_bn=True)
-        assert f.data_parallel and f.world == world and f.sync_bn
+        assert f.data_parallel and f.world == world and f.sync_bn and f.split == (split == "1")
         bl = batches(data, B, NNEG, STEPS * world, seed=26)
         losses = [float(f(bl[s * world + rank].to("cuda"))) for s in range(STEPS)]
         bufs = {n: b.detach().cpu().numpy().copy() for n, b in m.named_buffers() if "running" in n}
@@ -157,16 +157,20 @@ def _sync_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-def test_sync_bn_two_ranks_equal_one_gpu_on_the_global_batch():
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_sync_bn_two_ranks_equal_one_gpu_on_the_global_batch(split, monkeypatch):
     """SyncBN data parallel (2 ranks sharing the GPU, gloo transport for the partials and
     the gradient packs) trains exactly like the single-GPU fused step on the
     concatenated global batch: same losses, parameters and BatchNorm running stats up to
-    reduction order."""
+    reduction order -- on the fused layer kernels (every row group's partials gathered)
+    and on the split path (split = "1": one merged row per rank and BatchNorm,
+    gtr_config.split_sync)."""
+    monkeypatch.setenv("GTR_SPLIT", split)
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_sync_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_sync_worker, args=(r, world, port, q, split)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}

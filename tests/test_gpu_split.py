@@ -67,10 +67,12 @@ def test_split_forward_bitwise_equals_fused(D, H, K, loss, B, monkeypatch):
     assert torch.equal(*top)  # its BatchNorm sums come from the readout in both paths
     assert_close(f2.ws.layers[0]["dqkvs"][:N], f1.ws.layers[0]["dqkvs"][:N], rtol=1e-4, name="dqkvs layer 0")
     assert_close(f2.ws.dx0[:N], f1.ws.dx0[:N], rtol=1e-4, name="dx0")
+    # one AdamW step (lr 1e-2) on gradients that differ by rounding only: Adam moves an
+    # element whose gradient nearly cancels by a visible fraction of lr, so 1e-3 here
     for (n1, p1), (n2, p2) in zip(m1.named_parameters(), m2.named_parameters()):
         if n1.endswith("lin_key.bias"):
             continue
-        assert_close(p2, p1, rtol=1e-4, name=n1)
+        assert_close(p2, p1, rtol=1e-3, name=n1)
 
 
 @pytest.mark.parametrize("D,H,K,loss,B", CASES[:2])
