@@ -213,3 +213,32 @@ class OracleTrio:
         p64 = dict(self.ref64.named_parameters())
         for n, p in self.ref.named_parameters():
             close_trained(hip_params[n], p, p64[n], self.noise[n], 2 * lr * self.steps, prefix + n, p1[n])
+
+
+def collect(q, procs, n, timeout=400.0):
+    """n results from worker processes: polls the queue and fails FAST (instead of blocking
+    for the whole timeout) as soon as a worker has exited with an error -- a dead rank
+    would otherwise leave the test silent until the box's hang watchdog kills it."""
+    import queue
+    import time
+
+    out = []
+    t_end = time.time() + timeout
+    while len(out) < n:
+        try:
+            out.append(q.get(timeout=2.0))
+            continue
+        except queue.Empty:
+            pass
+        bad = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+        if bad:
+            for p in procs:
+                if p.is_alive():
+                    p.terminate()
+            raise AssertionError(f"a worker process failed (exit codes {bad})")
+        if time.time() > t_end:
+            for p in procs:
+                if p.is_alive():
+                    p.terminate()
+            raise AssertionError(f"workers timed out after {timeout:.0f} s")
+    return out

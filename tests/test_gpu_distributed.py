@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 if not torch.cuda.is_available():  # pragma: no cover - collected only on the GPU box
     pytest.skip("no GPU", allow_module_level=True)
 
-from gpu_helpers import assert_close_norm, batches, make_pair, ref_batch, small_data  # noqa: E402
+from gpu_helpers import collect, assert_close_norm, batches, make_pair, ref_batch, small_data  # noqa: E402
 
 from etpgt.train.fused import FusedTrainStep  # noqa: E402
 
@@ -86,8 +86,8 @@ def test_dp_two_ranks_match_oracle_average():
         p.start()
     res = {}
     try:
-        for _ in range(world):
-            rank, losses, params = q.get(timeout=400)
+        for item in collect(q, procs, world):
+            rank, losses, params = item
             res[rank] = (losses, {k: torch.from_numpy(v) for k, v in params.items()})
     finally:
         for p in procs:
@@ -148,9 +148,10 @@ def _sync_worker(rank, world, port, q, split="0"):
         m, _ = make_pair(T, D, H, K=0, seed=25)
         m.train()
         f = FusedTrainStep(m, lr=1e-2, weight_decay=1e-2, loss="listwise", sync_bn=True)
-        assert f.data_parallel and f.world == world and f.sync_bn and f.split == (split == "1")
+        assert f.data_parallel and f.world == world and f.sync_bn
         bl = batches(data, B, NNEG, STEPS * world, seed=26)
         losses = [float(f(bl[s * world + rank].to("cuda"))) for s in range(STEPS)]
+        assert f.split == (split == "1")
         bufs = {n: b.detach().cpu().numpy().copy() for n, b in m.named_buffers() if "running" in n}
         q.put((rank, losses, {n: p.detach().cpu().numpy().copy() for n, p in m.named_parameters()}, bufs))
     finally:
@@ -175,8 +176,8 @@ def test_sync_bn_two_ranks_equal_one_gpu_on_the_global_batch(split, monkeypatch)
         p.start()
     res = {}
     try:
-        for _ in range(world):
-            rank, losses, params, bufs = q.get(timeout=400)
+        for item in collect(q, procs, world):
+            rank, losses, params, bufs = item
             res[rank] = (losses, params, bufs)
     finally:
         for p in procs:
@@ -243,8 +244,8 @@ def test_dp_lagged_sweep_two_ranks_bitwise_equals_eager_dp():
         p.start()
     res = {}
     try:
-        for _ in range(world):
-            rank, same, params = q.get(timeout=400)
+        for item in collect(q, procs, world):
+            rank, same, params = item
             res[rank] = (same, params)
     finally:
         for p in procs:
@@ -289,7 +290,7 @@ def test_dp_rccl_world1_graph_captured_collectives():
     p = ctx.Process(target=_rccl_worker, args=(_free_port(), q))
     p.start()
     try:
-        out, ok_graph, diff = q.get(timeout=300)
+        out, ok_graph, diff = collect(q, [p], 1, 300)[0]
     finally:
         p.join(timeout=60)
     assert p.exitcode == 0
@@ -343,7 +344,7 @@ def test_collective_capture_refusal_falls_back_per_instance():
     p = ctx.Process(target=_refuse_worker, args=(_free_port(), q))
     p.start()
     try:
-        out, same, refused, pieces, other_captures, env = q.get(timeout=300)
+        out, same, refused, pieces, other_captures, env = collect(q, [p], 1, 300)[0]
     finally:
         p.join(timeout=60)
     assert p.exitcode == 0

@@ -27,7 +27,7 @@ pytestmark = pytest.mark.gpu
 if not torch.cuda.is_available():  # pragma: no cover - collected only on the GPU box
     pytest.skip("no GPU", allow_module_level=True)
 
-from gpu_helpers import assert_close_norm  # noqa: E402
+from gpu_helpers import collect, assert_close_norm  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LEAN = ["--cpu-seconds", "0", "--gather-batch", "0", "--recall-steps", "0", "--e2e-steps", "0", "--c1-reps", "0",
@@ -125,8 +125,8 @@ def test_train_baseline_two_ranks_equal_one_gpu_global_batch(tmp_path):
         p.start()
     res = {}
     try:
-        for _ in range(world):
-            rank, hist, sd = q.get(timeout=500)
+        for item in collect(q, procs, world):
+            rank, hist, sd = item
             res[rank] = (hist, sd)
     finally:
         for p in procs:

@@ -25,7 +25,7 @@ pytestmark = pytest.mark.gpu
 if not torch.cuda.is_available():  # pragma: no cover - collected only on the GPU box
     pytest.skip("no GPU", allow_module_level=True)
 
-from gpu_helpers import batches, make_pair, small_data  # noqa: E402
+from gpu_helpers import collect, batches, make_pair, small_data  # noqa: E402
 
 from etpgt.train.fused import FusedTrainStep  # noqa: E402
 
@@ -181,8 +181,8 @@ def test_shard_ranks_bitwise_equal_replicated_dp(world, ncases):
         p.start()
     res = {}
     try:
-        for _ in range(world):
-            rank, out = q.get(timeout=400)
+        for item in collect(q, procs, world):
+            rank, out = item
             res[rank] = out
     finally:
         for p in procs:
