@@ -39,6 +39,221 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_attn_bwd(ConvBwdK a) {
   conv_bwd_body<D, false, false>(a, blockIdx.x);
 }
 
+// Split path, row-parallel attention backward (gtr_attn_bwd at large batches): two
+// launches, one wave per row -- (1) per DESTINATION row: BatchNorm backward from the
+// finalized sums, beta-gate backward, softmax backward -> dS, dQ, dlogit, dagg; (2) per
+// SOURCE row: dK, dV gathered over its out-edges (CSR by source; no atomics) from (1)'s
+// dlogit / dagg.  Small LDS, several workgroups per CU (see k_attn_rows); in-edge /
+// out-edge rows are fetched four at a time.
+#define BR_BLOCK 256
+#define BR_WAVES (BR_BLOCK / 64)
+#define BR_RPW 2
+#define BR_ECH 64
+#define BR_HMAX 8
+
+// This layer's BatchNorm constants per lane: gamma, mean, rstd and the backward sums / N
+// (sync: every rank's gathered sums, N from the gathered counts).
+template <int D>
+__device__ __forceinline__ void bwd_row_consts(const ConvBwdK& a, float* s_gs, int& N, float (&k_g)[LayerGeom<D>::VPL],
+                                               float (&k_mean)[LayerGeom<D>::VPL], float (&k_rstd)[LayerGeom<D>::VPL],
+                                               float (&k_s1)[LayerGeom<D>::VPL], float (&k_s2)[LayerGeom<D>::VPL]) {
+  constexpr int VPL = LayerGeom<D>::VPL;
+  const int tid = threadIdx.x, lane = tid & 63;
+  N = a.bt.hdr[0];
+  const float* gs = a.gsum;
+  if (a.sync) {
+    float n = 0.0f;
+    for (int q = 0; q < a.nparts_fwd; ++q) n += a.part_all[(size_t)q * (1 + 2 * D)];
+    N = (int)(n + 0.5f);
+    for (int j = tid; j < 2 * D; j += blockDim.x) {
+      float acc = 0.0f;
+      for (int q = 0; q < a.nparts_bwd; ++q) acc += a.gpart_all[(size_t)q * 2 * D + j];
+      s_gs[j] = acc;
+    }
+    __syncthreads();
+    gs = s_gs;
+  }
+  const float invN = 1.0f / (float)N;
+  const int d0 = lane * VPL;
+  const int j = d0 < D ? d0 : 0;
+  load_vec<VPL>(k_g, a.gamma + j, true);
+  load_vec<VPL>(k_mean, a.stats + j, true);
+  load_vec<VPL>(k_rstd, a.stats + D + j, true);
+  load_vec<VPL>(k_s1, gs + j, true);
+  load_vec<VPL>(k_s2, gs + D + j, true);
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) { k_s1[v] *= invN; k_s2[v] *= invN; }
+}
+
+template <int D>
+__global__ __launch_bounds__(BR_BLOCK) void k_attn_rows_bwd_dst(ConvBwdK a) {
+  constexpr int VPL = LayerGeom<D>::VPL;
+  __shared__ float s_gs[2 * D];
+  __shared__ float s_da[BR_WAVES][BR_ECH][BR_HMAX];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int N;
+  float k_g[VPL], k_mean[VPL], k_rstd[VPL], k_s1[VPL], k_s2[VPL];
+  bwd_row_consts<D>(a, s_gs, N, k_g, k_mean, k_rstd, k_s1, k_s2);
+  const int Nl = a.bt.hdr[0];
+  const uint32_t ctr = a.rng_ctr ? load_step_ctr(a.rng_ctr) + a.ctr_add : 0u;
+  const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
+  const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
+  const int d0 = lane * VPL;
+  const bool act = d0 < D;
+  const int C = a.C, H = a.H;
+  const int GL = C / VPL;
+  const int head = act ? d0 / C : 0;
+  const bool leader = act && ((lane & (GL - 1)) == 0);
+  float w1[VPL], w2[VPL], w3[VPL];
+  load_vec<VPL>(w1, a.w_beta + d0, act);
+  load_vec<VPL>(w2, a.w_beta + D + d0, act);
+  load_vec<VPL>(w3, a.w_beta + 2 * D + d0, act);
+  const float* K = a.qkvs + D;
+  const float* V = a.qkvs + 2 * D;
+  for (int i = 0; i < BR_RPW; ++i) {
+    const int t = (blockIdx.x * BR_WAVES + wave) * BR_RPW + i;
+    if (t >= Nl) break;  // wave-uniform
+    const int e0 = a.bt.in_ptr[t], e1 = a.bt.in_ptr[t + 1];
+    if (e1 - e0 > BR_ECH || H > BR_HMAX) {  // hub rows: the general wave-per-row body
+      bwd_dst_row<D>(a, t, t, K, V, 4 * D, a.bt.in_ptr, a.bt.in_src, a.alpha, a.dlogit, 0, lane, dr, st_attn, k_g,
+                     k_mean, k_rstd, k_s1, k_s2);
+      continue;
+    }
+    const int ne = e1 - e0;
+    const int my_src = lane < ne ? a.bt.in_src[e0 + lane] : 0;
+    const size_t ro = (size_t)t * D + d0;
+    float dyv[VPL], ov[VPL], agv[VPL], sv[VPL];
+    load_vec<VPL>(dyv, a.dy + ro, act);
+    load_vec<VPL>(ov, a.out + ro, act);
+    load_vec<VPL>(agv, a.agg + ro, act);
+    load_vec<VPL>(sv, a.qkvs + (size_t)t * (4 * D) + 3 * D + d0, act);
+    const float beta = a.gate[t];
+    // BatchNorm backward, then the beta gate (as bwd_dst_row)
+    float gv[VPL];
+    float dbeta = 0.0f;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      const float xh = (ov[v] - k_mean[v]) * k_rstd[v];
+      gv[v] = act ? (dyv[v] - k_s1[v] - xh * k_s2[v]) * k_rstd[v] * k_g[v] : 0.0f;
+      dbeta += gv[v] * (sv[v] - agv[v]);
+    }
+    dbeta = wave_sum(dbeta);
+    const float du = dbeta * beta * (1.0f - beta);
+    if (lane == 0) a.du[t] = du;
+    float dag[VPL], ds[VPL], dq[VPL];
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) {
+      dag[v] = gv[v] * (1.0f - beta) + du * (w1[v] + w3[v]);
+      ds[v] = gv[v] * beta + du * (w2[v] - w3[v]);
+      dq[v] = 0.0f;
+    }
+    store_vec<VPL>(a.dqkvs + (size_t)t * (4 * D) + 3 * D + d0, ds, act);
+    store_vec<VPL>(a.dagg + ro, dag, act);
+    // da = <dA[t], V[src]> * mask per edge (LDS), sdot = sum alpha * da (four V rows in flight)
+    float sdot = 0.0f;
+    for (int j = 0; j < ne; j += 4) {
+      float vv[4][VPL];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int src = __shfl(my_src, (j + u) & 63);
+        load_vec<VPL>(vv[u], V + (size_t)src * (4 * D) + d0, act && j + u < ne);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float d = 0.0f;
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) d += dag[v] * vv[u][v];
+        d = group_sum(d, GL);
+        if (j + u < ne) {
+          const int eg = e0 + j + u;
+          const float da = d * dr.mul(st_attn, (uint32_t)(eg * H + head));
+          sdot += a.alpha[(size_t)eg * H + head] * da;
+          if (leader) s_da[wave][j + u][head] = da;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // dlogit = alpha * (da - sdot); dQ += dlogit / sqrt(C) * K[src] (four K rows in flight)
+    for (int j = 0; j < ne; j += 4) {
+      float kv[4][VPL];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int src = __shfl(my_src, (j + u) & 63);
+        load_vec<VPL>(kv[u], K + (size_t)src * (4 * D) + d0, act && j + u < ne);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (j + u < ne) {
+          const int eg = e0 + j + u;
+          const float al = a.alpha[(size_t)eg * H + head];
+          const float dl = al * (s_da[wave][j + u][head] - sdot);
+          if (leader) a.dlogit[(size_t)eg * H + head] = dl;
+          const float c = dl / a.sqrt_c;
+#pragma unroll
+          for (int v = 0; v < VPL; ++v) dq[v] += c * kv[u][v];
+        }
+      }
+    }
+    store_vec<VPL>(a.dqkvs + (size_t)t * (4 * D) + d0, dq, act);
+    __builtin_amdgcn_wave_barrier();  // s_da is reused by the wave's next row
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(BR_BLOCK) void k_attn_rows_bwd_src(ConvBwdK a) {
+  constexpr int VPL = LayerGeom<D>::VPL;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int Nl = a.bt.hdr[0];
+  const uint32_t ctr = a.rng_ctr ? load_step_ctr(a.rng_ctr) + a.ctr_add : 0u;
+  const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
+  const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
+  const int d0 = lane * VPL;
+  const bool act = d0 < D;
+  const int C = a.C, H = a.H;
+  const int head = act ? d0 / C : 0;
+  const float isc = 1.0f / a.sqrt_c;
+  for (int i = 0; i < BR_RPW; ++i) {
+    const int s = (blockIdx.x * BR_WAVES + wave) * BR_RPW + i;
+    if (s >= Nl) break;
+    const int i0 = a.bt.out_ptr[s], i1 = a.bt.out_ptr[s + 1];
+    float dk[VPL], dv[VPL];
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) { dk[v] = 0.0f; dv[v] = 0.0f; }
+    for (int cb = i0; cb < i1; cb += 64) {
+      const int cnt = min(64, i1 - cb);
+      const int my_p = lane < cnt ? a.bt.out_edge[cb + lane] : 0;
+      const int my_t = lane < cnt ? a.bt.out_dst[cb + lane] : 0;
+      for (int j = 0; j < cnt; j += 4) {
+        float qv[4][VPL], gv[4][VPL];
+        int p[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          p[u] = __shfl(my_p, (j + u) & 63);
+          const int t = __shfl(my_t, (j + u) & 63);
+          load_vec<VPL>(qv[u], a.qkvs + (size_t)t * (4 * D) + d0, act && j + u < cnt);
+          load_vec<VPL>(gv[u], a.dagg + (size_t)t * D + d0, act && j + u < cnt);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (j + u < cnt) {
+            const float dl = a.dlogit[(size_t)p[u] * H + head] * isc;
+            const float ad = a.alpha[(size_t)p[u] * H + head] * dr.mul(st_attn, (uint32_t)(p[u] * H + head));
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) {
+              dk[v] += dl * qv[u][v];
+              dv[v] += ad * gv[u][v];
+            }
+          }
+        }
+      }
+    }
+    store_vec<VPL>(a.dqkvs + (size_t)s * (4 * D) + D + d0, dk, act);
+    store_vec<VPL>(a.dqkvs + (size_t)s * (4 * D) + 2 * D + d0, dv, act);
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // weight gradients
 // ------------------------------------------------------------------------------------
@@ -122,10 +337,30 @@ extern "C" int gtr_attn_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   float dummy = 0.0f;  // dx0 is written by gtr_qkvs_bwd, not here
   if (const int rc = make_bwd_args(cfg, bt, layers, l, &dummy, k)) return rc;
   k.dx0 = nullptr;
+  hipStream_t s = (hipStream_t)stream;
+  const char* am = getenv("GTR_ATTN");  // "group": the fused kernels' row-group body (A/B)
+  if (cfg->dim <= 128 && !(am && am[0] == 'g')) {
+    const int grid = (bt->n_cap + BR_WAVES * BR_RPW - 1) / (BR_WAVES * BR_RPW);
+    switch (cfg->dim) {
+      case 32:
+        hipLaunchKernelGGL(k_attn_rows_bwd_dst<32>, dim3(grid), dim3(BR_BLOCK), 0, s, k);
+        hipLaunchKernelGGL(k_attn_rows_bwd_src<32>, dim3(grid), dim3(BR_BLOCK), 0, s, k);
+        break;
+      case 64:
+        hipLaunchKernelGGL(k_attn_rows_bwd_dst<64>, dim3(grid), dim3(BR_BLOCK), 0, s, k);
+        hipLaunchKernelGGL(k_attn_rows_bwd_src<64>, dim3(grid), dim3(BR_BLOCK), 0, s, k);
+        break;
+      default:
+        hipLaunchKernelGGL(k_attn_rows_bwd_dst<128>, dim3(grid), dim3(BR_BLOCK), 0, s, k);
+        hipLaunchKernelGGL(k_attn_rows_bwd_src<128>, dim3(grid), dim3(BR_BLOCK), 0, s, k);
+        break;
+    }
+    GTR_HIP_CHECK_LAUNCH();
+    return GTR_OK;
+  }
   const int grid = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;
   if (grid <= 0) return GTR_OK;
   k.main_grid = grid;
-  hipStream_t s = (hipStream_t)stream;
 #define GTR_ABW(DD) set_lds_limit<DD>(k_attn_bwd<DD>, (size_t)LayerGeom<DD>::B_WORDS * 4); \
   hipLaunchKernelGGL((k_attn_bwd<DD>), dim3(grid), dim3(CONV_BLOCK), (size_t)LayerGeom<DD>::B_WORDS * 4, s, k)
   switch (cfg->dim) {

@@ -111,6 +111,52 @@ __device__ __forceinline__ void prev_bn_stats(int train, int cred, int G, const 
   }
 }
 
+// This layer's BatchNorm statistics from the Gn per-workgroup (count, mean, M2) partials
+// in bn_part (workgroup g wrote row g): the last arrivers of buckets of GTR_PART_BUCKET
+// merge their rows into the bucket's first row, the last bucket merger derives the
+// statistics (bn_stats) and updates the running statistics -- or, with merge_only (the
+// split path under SyncBN), merges the bucket rows into row 0 for the all-gather.
+// red: >= 2 BLK + D floats of LDS scratch; s_bn: 2 D; s_uvar: D.
+template <int D, int BLK>
+__device__ __forceinline__ void bn_fwd_finalize(const ConvFwdK& a, int g, int Gn, int* s_flag, float* red, float* s_bn,
+                                                float* s_uvar) {
+  const int tid = threadIdx.x;
+  constexpr int PW = 1 + 2 * D;
+  const int nbk = (Gn + GTR_PART_BUCKET - 1) / GTR_PART_BUCKET;
+  if (nbk > 1) {
+    const int bk = g / GTR_PART_BUCKET, b0 = bk * GTR_PART_BUCKET;
+    if (!arrive_last(a.cnt + 4 + 2 * bk, (uint32_t)min(GTR_PART_BUCKET, Gn - b0), s_flag)) return;
+    float* row0 = a.bn_part + (size_t)b0 * PW;
+    bn_merge_parts<D, BLK>(row0, min(GTR_PART_BUCKET, Gn - b0), red, PW, row0);
+    if (tid == 0) reset_counter(a.cnt + 4 + 2 * bk);
+    if (!arrive_last(a.cnt, (uint32_t)nbk, s_flag)) return;
+    if (a.merge_only) {  // the buckets' rows -> ONE row (row 0, bucket 0's own row: may alias)
+      bn_merge_parts<D, BLK>(a.bn_part, nbk, red, (size_t)GTR_PART_BUCKET * PW, a.bn_part);
+      if (tid == 0) reset_counter(a.cnt);
+      return;
+    }
+    bn_stats_from_parts<D, BLK>(a.bn_part, nbk, a.bn_eps, s_bn, s_bn + D, s_uvar, red, (size_t)GTR_PART_BUCKET * PW);
+  } else {
+    if (!arrive_last(a.cnt, (uint32_t)Gn, s_flag)) return;
+    if (a.merge_only) {
+      bn_merge_parts<D, BLK>(a.bn_part, Gn, red, PW, a.bn_part);
+      if (tid == 0) reset_counter(a.cnt);
+      return;
+    }
+    bn_stats_from_parts<D, BLK>(a.bn_part, Gn, a.bn_eps, s_bn, s_bn + D, s_uvar, red);
+  }
+  for (int j = tid; j < D; j += BLK) {
+    a.bn_stats[j] = s_bn[j];
+    a.bn_stats[D + j] = s_bn[D + j];
+    a.bn_rmean[j] = (1.0f - a.bn_mom) * a.bn_rmean[j] + a.bn_mom * s_bn[j];
+    a.bn_rvar[j] = (1.0f - a.bn_mom) * a.bn_rvar[j] + a.bn_mom * s_uvar[j];
+  }
+  if (tid == 0) {
+    reset_counter(a.cnt);
+    if (a.bn_nbt) *a.bn_nbt += 1;
+  }
+}
+
 // Attention + gate of one destination row (wave per row).  QB/SB/KB/VB: row bases
 // with stride ST (LDS on the fast path, global qkvs otherwise); EP/ES: CSR of the rows
 // (local indices on the fast path); eoff: offset of EP's edge indices in alpha.
@@ -709,41 +755,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
   GTR_PH(a.layer, 4);
   GTR_PH_CLK(a.layer, 7);
   if (a.cred) return;  // the consuming kernel reduces the partials
-  constexpr int PW = 1 + 2 * D;
-  const int nbk = (Gn + GTR_PART_BUCKET - 1) / GTR_PART_BUCKET;
-  if (nbk > 1) {
-    const int bk = g / GTR_PART_BUCKET, b0 = bk * GTR_PART_BUCKET;
-    if (!arrive_last(a.cnt + 4 + 2 * bk, (uint32_t)min(GTR_PART_BUCKET, Gn - b0), s_flag)) return;
-    float* row0 = a.bn_part + (size_t)b0 * PW;
-    bn_merge_parts<D, CONV_BLOCK>(row0, min(GTR_PART_BUCKET, Gn - b0), red, PW, row0);
-    if (tid == 0) reset_counter(a.cnt + 4 + 2 * bk);
-    if (!arrive_last(a.cnt, (uint32_t)nbk, s_flag)) return;
-    if (a.merge_only) {  // the buckets' rows -> ONE row (row 0, bucket 0's own row: may alias)
-      bn_merge_parts<D, CONV_BLOCK>(a.bn_part, nbk, red, (size_t)GTR_PART_BUCKET * PW, a.bn_part);
-      if (tid == 0) reset_counter(a.cnt);
-      return;
-    }
-    bn_stats_from_parts<D, CONV_BLOCK>(a.bn_part, nbk, a.bn_eps, s_bn, s_bn + D, XO, red,
-                                       (size_t)GTR_PART_BUCKET * PW);
-  } else {
-    if (!arrive_last(a.cnt, (uint32_t)Gn, s_flag)) return;
-    if (a.merge_only) {
-      bn_merge_parts<D, CONV_BLOCK>(a.bn_part, Gn, red, PW, a.bn_part);
-      if (tid == 0) reset_counter(a.cnt);
-      return;
-    }
-    bn_stats_from_parts<D, CONV_BLOCK>(a.bn_part, Gn, a.bn_eps, s_bn, s_bn + D, XO, red);
-  }
-  for (int j = tid; j < D; j += CONV_BLOCK) {
-    a.bn_stats[j] = s_bn[j];
-    a.bn_stats[D + j] = s_bn[D + j];
-    a.bn_rmean[j] = (1.0f - a.bn_mom) * a.bn_rmean[j] + a.bn_mom * s_bn[j];
-    a.bn_rvar[j] = (1.0f - a.bn_mom) * a.bn_rvar[j] + a.bn_mom * XO[j];
-  }
-  if (tid == 0) {
-    reset_counter(a.cnt);
-    if (a.bn_nbt) *a.bn_nbt += 1;
-  }
+  bn_fwd_finalize<D, CONV_BLOCK>(a, g, Gn, s_flag, red, s_bn, XO);
 }
 
 template <int D, bool SPLIT>
@@ -768,6 +780,169 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_conv_fwd(ConvFwdK a) {
 template <int D>
 __global__ __launch_bounds__(CONV_BLOCK) void k_attn_fwd(ConvFwdK a) {
   conv_fwd_body<D, false, false>(a, blockIdx.x);
+}
+
+// Split path, row-parallel attention (gtr_attn_fwd at large batches): one WAVE per
+// destination row instead of one workgroup per row group.  The fused kernels' row-group
+// fast path holds ~140 KB of LDS (one group per CU, its phases separated by barriers, no
+// overlap between groups); here a workgroup is 4 waves x 2 rows with 20 KB of LDS, so
+// several run per CU and one wave's load latency hides behind another's work.  Per row:
+// the in-edge source ids one per lane, K rows four edges in flight -> logits (LDS, per
+// head) and their maximum; the softmax denominator; V rows four in flight -> alpha,
+// dropout, the weighted sum; the beta gate -> agg / out / gate (PyG TransformerConv,
+// SURVEY.md Appendix A).  The workgroup's 8 output rows give one BatchNorm partial.
+#define AR_BLOCK 256
+#define AR_WAVES (AR_BLOCK / 64)
+#define AR_RPW 2                   // rows per wave
+#define AR_ROWS (AR_WAVES * AR_RPW)  // rows per workgroup = one BatchNorm partial
+#define AR_ECH 64                  // in-edges of a row handled with LDS logits
+#define AR_HMAX 8
+
+template <int D>
+__global__ __launch_bounds__(AR_BLOCK) void k_attn_rows(ConvFwdK a) {
+  constexpr int VPL = D >= 64 ? D / 64 : 1;
+  __shared__ __attribute__((aligned(16))) float s_out[AR_ROWS][D];
+  __shared__ float s_lg[AR_WAVES][AR_ECH][AR_HMAX];
+  __shared__ float s_red[2 * AR_BLOCK + D];
+  __shared__ float s_bn[2 * D];
+  __shared__ float s_uv[D];
+  __shared__ int s_flag;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int N = a.bt.hdr[0];
+  const int Gn = (N + AR_ROWS - 1) / AR_ROWS;
+  const int g = blockIdx.x;
+  if (g >= Gn) return;  // block-uniform: only live workgroups write partials and arrive
+  const int r0 = g * AR_ROWS, nrow = min(AR_ROWS, N - r0);
+  const uint32_t ctr = a.rng_ctr ? load_step_ctr(a.rng_ctr) + a.ctr_add : 0u;
+  const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
+  const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
+  const int d0 = lane * VPL;
+  const bool act = d0 < D;
+  const int C = a.C, H = a.H;
+  const int GL = C / VPL;
+  const int head = act ? d0 / C : 0;
+  const bool leader = act && ((lane & (GL - 1)) == 0);
+  float w1[VPL], w2[VPL], w3[VPL];
+  load_vec<VPL>(w1, a.w_beta + d0, act);
+  load_vec<VPL>(w2, a.w_beta + D + d0, act);
+  load_vec<VPL>(w3, a.w_beta + 2 * D + d0, act);
+  const float* Q = a.qkvs;
+  const float* K = a.qkvs + D;
+  const float* V = a.qkvs + 2 * D;
+  const float* S = a.qkvs + 3 * D;
+  for (int i = 0; i < AR_RPW; ++i) {
+    const int rl = wave * AR_RPW + i;
+    const int t = r0 + rl;
+    if (t >= N) break;  // wave-uniform
+    const int e0 = a.bt.in_ptr[t], e1 = a.bt.in_ptr[t + 1];
+    if (e1 - e0 > AR_ECH || H > AR_HMAX) {  // hub rows: the general wave-per-row body
+      attn_row<D>(a, t, t, Q, S, K, V, 4 * D, a.bt.in_ptr, a.bt.in_src, 0, lane, dr, st_attn, w1, w2, w3, s_out[rl]);
+      continue;
+    }
+    const int ne = e1 - e0;
+    const int my_src = lane < ne ? a.bt.in_src[e0 + lane] : 0;
+    float q[VPL], sv[VPL], ag[VPL];
+    load_vec<VPL>(q, Q + (size_t)t * (4 * D) + d0, act);
+    load_vec<VPL>(sv, S + (size_t)t * (4 * D) + d0, act);
+    // logits <Q[t], K[src]> / sqrt(C) per head, four K rows in flight
+    float m = -INFINITY;
+    for (int j = 0; j < ne; j += 4) {
+      float kv[4][VPL];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int src = __shfl(my_src, (j + u) & 63);
+        load_vec<VPL>(kv[u], K + (size_t)src * (4 * D) + d0, act && j + u < ne);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float dt = 0.0f;
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) dt += q[v] * kv[u][v];
+        const float l = group_sum(dt, GL) / a.sqrt_c;
+        if (j + u < ne) {
+          m = fmaxf(m, l);
+          if (leader) s_lg[wave][j + u][head] = l;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float z = 0.0f;
+    for (int e = 0; e < ne; ++e) z += expf(s_lg[wave][e][head] - m);
+    const float zd = z + 1e-16f;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) ag[v] = 0.0f;
+    // alpha = softmax, attention dropout, aggregate V rows (four in flight)
+    for (int j = 0; j < ne; j += 4) {
+      float vv[4][VPL];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int src = __shfl(my_src, (j + u) & 63);
+        load_vec<VPL>(vv[u], V + (size_t)src * (4 * D) + d0, act && j + u < ne);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (j + u < ne) {
+          const int eg = e0 + j + u;
+          const float al = expf(s_lg[wave][j + u][head] - m) / zd;
+          if (leader) a.alpha[(size_t)eg * H + head] = al;
+          const float ad = al * dr.mul(st_attn, (uint32_t)(eg * H + head));
+#pragma unroll
+          for (int v = 0; v < VPL; ++v) ag[v] += ad * vv[u][v];
+        }
+      }
+    }
+    float uu = 0.0f;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) uu += w1[v] * ag[v] + w2[v] * sv[v] + w3[v] * (ag[v] - sv[v]);
+    uu = wave_sum(uu);
+    const float beta = 1.0f / (1.0f + expf(-uu));
+    float o[VPL];
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) o[v] = beta * sv[v] + (1.0f - beta) * ag[v];
+    store_vec<VPL>(a.agg + (size_t)t * D + d0, ag, act);
+    store_vec<VPL>(a.out + (size_t)t * D + d0, o, act);
+    store_vec<VPL>(s_out[rl] + d0, o, act);
+    if (lane == 0) a.gate[t] = beta;
+    __builtin_amdgcn_wave_barrier();  // s_lg is reused by the wave's next row
+  }
+  if (!a.train) return;
+  // ---- this workgroup's BatchNorm partial (count, mean, M2) over its rows
+  __syncthreads();
+  constexpr int NS = AR_BLOCK / D >= 1 ? AR_BLOCK / D : 1;
+  float* part = a.bn_part + (size_t)g * (1 + 2 * D);
+  {
+    const int j = tid % D, sl = tid / D;
+    float sum = 0.0f;
+    if (sl < NS)
+      for (int i = sl; i < nrow; i += NS) sum += s_out[i][j];
+    s_red[sl * D + j] = sum;
+    __syncthreads();
+    if (tid < D) {
+      float tot = 0.0f;
+      for (int q2 = 0; q2 < NS; ++q2) tot += s_red[q2 * D + tid];
+      const float mean = tot / (float)nrow;
+      s_red[NS * D + tid] = mean;
+      part[1 + tid] = mean;
+    }
+    __syncthreads();
+    float m2 = 0.0f;
+    if (sl < NS) {
+      const float mean = s_red[NS * D + j];
+      for (int i = sl; i < nrow; i += NS) { const float d = s_out[i][j] - mean; m2 += d * d; }
+    }
+    __syncthreads();
+    s_red[sl * D + j] = m2;
+    __syncthreads();
+    if (tid < D) {
+      float tot = 0.0f;
+      for (int q2 = 0; q2 < NS; ++q2) tot += s_red[q2 * D + tid];
+      part[1 + D + tid] = tot;
+    }
+    if (tid == 0) part[0] = (float)nrow;
+  }
+  bn_fwd_finalize<D, AR_BLOCK>(a, g, Gn, &s_flag, s_red, s_bn, s_uv);
 }
 
 struct ReadoutK {
@@ -1681,10 +1856,24 @@ extern "C" int gtr_attn_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     k.merge_only = 1;
     k.sync = 0;  // no zero rows for empty groups: only live groups arrive
   }
+  hipStream_t s = (hipStream_t)stream;
+  const char* am = getenv("GTR_ATTN");  // "group": the fused kernels' row-group body (A/B)
+  if (cfg->dim <= 128 && !(am && am[0] == 'g')) {
+    // row-parallel: one BatchNorm partial per AR_ROWS rows (gtr_layer.bn_part holds
+    // max(n_cap / row_group, n_cap / 8) rows, gtr.h)
+    static_assert(AR_ROWS == 8, "gtr.h sizes bn_part for 8-row partials");
+    const int grid = (bt->n_cap + AR_ROWS - 1) / AR_ROWS;
+    switch (cfg->dim) {
+      case 32: hipLaunchKernelGGL(k_attn_rows<32>, dim3(grid), dim3(AR_BLOCK), 0, s, k); break;
+      case 64: hipLaunchKernelGGL(k_attn_rows<64>, dim3(grid), dim3(AR_BLOCK), 0, s, k); break;
+      default: hipLaunchKernelGGL(k_attn_rows<128>, dim3(grid), dim3(AR_BLOCK), 0, s, k); break;
+    }
+    GTR_HIP_CHECK_LAUNCH();
+    return GTR_OK;
+  }
   const int grid = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;
   if (grid <= 0) return GTR_OK;
   k.main_grid = grid;
-  hipStream_t s = (hipStream_t)stream;
 #define GTR_ATT(DD) set_lds_limit<DD>(k_attn_fwd<DD>, (size_t)LayerGeom<DD>::F_WORDS * 4); \
   hipLaunchKernelGGL((k_attn_fwd<DD>), dim3(grid), dim3(CONV_BLOCK), (size_t)LayerGeom<DD>::F_WORDS * 4, s, k)
   switch (cfg->dim) {

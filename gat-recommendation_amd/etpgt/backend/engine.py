@@ -172,17 +172,20 @@ class Workspace:
         n, b, e, k = caps.n_cap, caps.b_cap, caps.e_cap, max(caps.n_neg, 1)
         g = (n + R - 1) // R
         self.g_cap = g
+        # BatchNorm partial rows: one per row group, or per 8 rows on the split path's
+        # row-parallel attention (gtr_attn_fwd); arrival counters: two per bucket of 32
+        parts = max(g, (n + 7) // 8)
         self.layers = []
         self.structs = (L.GtrLayer * Lc)()
         for l in range(Lc):
             t = dict(
                 xin=_f32(n, D, device=dev), qkvs=_f32(n, 4 * D, device=dev), alpha=_f32(e, H, device=dev),
                 agg=_f32(n, D, device=dev), gate=_f32(n, device=dev), out=_f32(n, D, device=dev),
-                bn_stats=_f32(2 * D, device=dev), bn_part=_f32(g, 1 + 2 * D, device=dev),
+                bn_stats=_f32(2 * D, device=dev), bn_part=_f32(parts, 1 + 2 * D, device=dev),
                 bn_gsum=_f32(2 * D, device=dev), bn_gpart=_f32(max(g, 256), 2 * D, device=dev),
                 # arrival counters: [0..3] + two per bucket of 32 partial rows -- the row groups
                 # or the <= 256 workgroups of the split path's dX GEMM (gtr_qkvs_bwd)
-                cnt=_i32(8 + 2 * max((g + 31) // 32, 8), dev), dy=_f32(n, D, device=dev),
+                cnt=_i32(8 + 2 * max((parts + 31) // 32, 8), dev), dy=_f32(n, D, device=dev),
                 dqkvs=_f32(n, 4 * D, device=dev),
                 du=_f32(n, device=dev), dlogit=_f32(e, H, device=dev), dagg=_f32(n, D, device=dev),
             )

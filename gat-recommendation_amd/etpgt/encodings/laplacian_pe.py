@@ -39,8 +39,13 @@ def compute_laplacian_pe(edge_index, num_nodes: int, k: int = 16, normalization:
     from scipy.sparse.linalg import eigsh
 
     L = sym_laplacian(edge_index, num_nodes)
+    # fixed ARPACK start vector: without one, eigsh draws it from a generator whose state
+    # persists across calls in the process, so the result (its eigenvector signs, and on the
+    # reference's non-symmetric directed input the vectors themselves) depended on how many
+    # solves ran before -- data-parallel ranks and repeated runs must get the same table
+    v0 = np.random.default_rng(0).random(num_nodes)
     try:
-        _, vecs = eigsh(L, k=k + 1, which="SM", return_eigenvectors=True)
+        _, vecs = eigsh(L, k=k + 1, which="SM", return_eigenvectors=True, v0=v0)
     except Exception:
         _, vt = torch.linalg.eigh(torch.from_numpy(L.toarray()).float())
         vecs = vt.numpy()

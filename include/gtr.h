@@ -158,14 +158,16 @@ typedef struct gtr_layer {
   float* gate;     /* [n_cap]     beta gate                         */
   float* out;      /* [n_cap, D]  conv output (pre BatchNorm)        */
   float* bn_stats; /* [2D] batch mean, rstd                         */
-  float* bn_part;  /* [g_cap, 1+2D] forward (count, mean, M2) partials per row group.
+  float* bn_part;  /* [max(g_cap, ceil(n_cap/8)), 1+2D] forward (count, mean, M2) partials
+                      per row group (per 8 rows on the split path's gtr_attn_fwd).
                       consumer_reduce = 0 with > 32 row groups: the forward's bucket
                       mergers overwrite row 32*b with bucket b's merged row, so after
                       such a forward bn_part is NOT per-group partials any more      */
   float* bn_gsum;  /* [2D] sum(dy), sum(dy*xhat)                     */
   float* bn_gpart; /* [max(g_cap, 256), 2D] backward partials         */
-  uint32_t* cnt;   /* [4 + 2*ceil(groups/32)] arrival counters (zero-initialised once;
-                      past 32 row groups the partials are merged per bucket of 32)   */
+  uint32_t* cnt;   /* [8 + 2*max(ceil(partials/32), 8)] arrival counters (zero-initialised
+                      once; past 32 partial rows -- row groups, 8-row blocks, or the
+                      <= 256 gtr_qkvs_bwd workgroups -- they are merged per bucket of 32) */
   float* dy;       /* [n_cap, D]  grad wrt BN(out)+x_{l-1} (pre dropout) */
   float* dqkvs;    /* [n_cap, 4D]                                    */
   float* du;       /* [n_cap]     grad wrt gate logit                 */

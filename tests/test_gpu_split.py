@@ -44,6 +44,9 @@ def _step(m, loss, split, monkeypatch, **kw):
 
 @pytest.mark.parametrize("D,H,K,loss,B", CASES)
 def test_split_forward_bitwise_equals_fused(D, H, K, loss, B, monkeypatch):
+    """GTR_ATTN=group: the split path's attention on the fused kernels' row-group body --
+    bitwise the fused step (see the module docstring)."""
+    monkeypatch.setenv("GTR_ATTN", "group")
     data = small_data()
     T = data.table_rows
     m1, _ = make_pair(T, D, H, K=K, seed=61)
@@ -114,3 +117,38 @@ def test_split_eval_forward_matches_oracle(monkeypatch):
         rse = ref(R.ref_batch_from(sb))
     assert m.hip_engine().workspace(m.hip_engine().prepare(sb)[0]).split
     assert_close(se, rse, rtol=1e-3, name="session embeddings (eval)")
+
+
+@pytest.mark.parametrize("D,H,K,loss,B", CASES)
+def test_split_row_attention_equals_fused(D, H, K, loss, B, monkeypatch):
+    """The default split path: row-parallel attention kernels (one wave per destination /
+    source row, k_attn_rows*).  The projection is still bitwise the fused one; attention,
+    softmax and BatchNorm partials are summed in another order, so the rest agrees to
+    float rounding (1e-4 relative) -- and the whole step to the oracle in
+    test_split_training_matches_oracle."""
+    monkeypatch.delenv("GTR_ATTN", raising=False)
+    data = small_data()
+    T = data.table_rows
+    m1, _ = make_pair(T, D, H, K=K, seed=67)
+    m2 = copy.deepcopy(m1)
+    m1.train(); m2.train()
+    n = 100 if loss != "bpr" else 5
+    sb = batches(data, B, n, 1, seed=68)[0]
+    f1 = _step(m1, loss, False, monkeypatch)
+    l1 = float(f1(sb.to("cuda")))
+    f2 = _step(m2, loss, True, monkeypatch)
+    l2 = float(f2(sb.to("cuda")))
+    assert abs(l1 - l2) <= 1e-5 * abs(l1), (l1, l2)
+    N, E = sb.num_nodes, sb.num_edges
+    a, b = f1.ws.layers[0], f2.ws.layers[0]
+    assert torch.equal(a["xin"][:N], b["xin"][:N]) and torch.equal(a["qkvs"][:N], b["qkvs"][:N])
+    for l in range(2):
+        a, b = f1.ws.layers[l], f2.ws.layers[l]
+        for name, rows in (("xin", N), ("qkvs", N), ("agg", N), ("out", N), ("gate", N), ("alpha", E),
+                           ("dqkvs", N), ("dlogit", E), ("du", N)):
+            assert_close(b[name][:rows], a[name][:rows], rtol=1e-4, name=f"layer {l} {name}")
+    assert_close(f2.ws.dx0[:N], f1.ws.dx0[:N], rtol=1e-4, name="dx0")
+    for (n1, p1), (n2, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+        if n1.endswith("lin_key.bias"):
+            continue
+        assert_close(p2, p1, rtol=1e-3, name=n1)
