@@ -231,7 +231,9 @@ __device__ __forceinline__ bool arrive_last(uint32_t* cnt, uint32_t total, int* 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
+#ifndef GTR_PROBE_NOFENCE  // timing probe only (wrong results): what the release fences cost
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *s_flag = (prev == total - 1) ? 1 : 0;

@@ -1,0 +1,77 @@
+"""Per-kernel timing probe of one bench configuration: one step runs, then each layer /
+head / wgrad launch is re-launched alone N times between HIP events (the step's own
+stream).  usage: python scripts/dbg/kbench.py [config] [batch] [reps]"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "gat-recommendation_amd"))
+
+import ctypes as C  # noqa: E402
+
+import bench  # noqa: E402
+from etpgt.backend import _lib as L  # noqa: E402
+
+
+def timeit(fn, reps):
+    st = torch.cuda.current_stream()
+    ev = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        fn()
+        b.record(st)
+        ev.append((a, b))
+    torch.cuda.synchronize()
+    return float(np.median([a.elapsed_time(b) for a, b in ev[2:]])) * 1e3
+
+
+def main():
+    cfgname = sys.argv[1] if len(sys.argv) > 1 else "c3"
+    B = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
+    reps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+    dev = torch.device("cuda", 0)
+    w = bench.build_workload(cfgname, B, 2, dev, 0, use_graph=False, lazy=bool(bench.CONFIGS[cfgname].get("lazy")))
+    step, staged = w["step"], w["staged"]
+    for i in range(3):
+        step.load_blob(staged[i % 2])
+        step.run()
+    torch.cuda.synchronize()
+    eng, ws, cfg, bs = step.eng, step.ws, step.cfg, step.bs
+    lib = L.lib()
+    st = lambda: torch.cuda.current_stream().cuda_stream  # noqa: E731
+    emb = eng.fill_embed()
+    out = {"config": cfgname, "B": B, "split": step.split, "N": int(staged[0][0].item())}
+    t_step = timeit(lambda: step.run(), reps)
+    out["step_us"] = round(t_step, 1)
+    for l in range(eng.L):
+        if step.split:
+            out[f"qkvs_fwd{l}"] = timeit(lambda: L.check(lib.gtr_qkvs_fwd(C.byref(cfg), C.byref(bs), C.byref(emb),
+                                                                         ws.structs, l, st())), reps)
+            out[f"attn_fwd{l}"] = timeit(lambda: L.check(lib.gtr_attn_fwd(C.byref(cfg), C.byref(bs), ws.structs, l,
+                                                                         st())), reps)
+        else:
+            out[f"conv_fwd{l}"] = timeit(lambda: L.check(lib.gtr_conv_fwd(C.byref(cfg), C.byref(bs), C.byref(emb),
+                                                                         ws.structs, l, st())), reps)
+    out["head"] = timeit(lambda: eng.run_head(ws, cfg, bs, L.RO_FWD | L.RO_LOSS | L.RO_BWD, step.loss_kind,
+                                              step.temperature, step.alpha), reps)
+    for l in range(eng.L - 1, -1, -1):
+        if step.split:
+            out[f"attn_bwd{l}"] = timeit(lambda: L.check(lib.gtr_attn_bwd(C.byref(cfg), C.byref(bs), ws.structs, l,
+                                                                         st())), reps)
+            out[f"qkvs_bwd{l}"] = timeit(lambda: L.check(lib.gtr_qkvs_bwd(C.byref(cfg), C.byref(bs), ws.structs, l,
+                                                                         ws.dx0.data_ptr(), st())), reps)
+        else:
+            out[f"conv_bwd{l}"] = timeit(lambda: L.check(lib.gtr_conv_bwd(C.byref(cfg), C.byref(bs), ws.structs, l,
+                                                                         ws.dx0.data_ptr(), st())), reps)
+    out["wgrad"] = timeit(lambda: eng._wgrad(ws, cfg, bs, 0, eng.L, st()), reps)
+    out["tail"] = timeit(lambda: step._launch_b(False), reps)
+    print({k: (round(v, 1) if isinstance(v, float) else v) for k, v in out.items()}, flush=True)
+
+
+if __name__ == "__main__":
+    main()
