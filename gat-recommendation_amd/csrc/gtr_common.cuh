@@ -248,6 +248,36 @@ __device__ __forceinline__ bool arrive_last(uint32_t* cnt, uint32_t total, int* 
   return true;
 }
 
+// Write-through (sc1) store of one float: a relaxed agent-scope atomic store, visible to
+// every XCD without a release fence once the storing wave's vmcnt has drained
+// (cdna_hip_programming.md Guideline 16, R1).
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store((__attribute__((address_space(1))) uint32_t*)(p), __float_as_uint(v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// arrive_last for partials stored write-through (st_wt): every wave drains its stores, then
+// ONE relaxed agent-scope ticket per workgroup -- no release fence (an agent-scope release
+// writes back the XCD's dirty L2 lines: with ~3.5k row-group workgroups per layer launch
+// at B = 8192 those fences cost ~85 us of the launch, scripts/dbg/kbench.py + the
+// GTR_PROBE_NOFENCE build); the last arriver acquires (one buffer_inv) and reads plainly.
+__device__ __forceinline__ bool arrive_last_wt(uint32_t* cnt, uint32_t total, int* s_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_flag = (prev == total - 1) ? 1 : 0;
+  }
+  __syncthreads();
+  if (*s_flag == 0) return false;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  return true;
+}
+
 __device__ __forceinline__ void reset_counter(uint32_t* cnt) {
   __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

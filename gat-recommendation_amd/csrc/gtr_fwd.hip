@@ -123,9 +123,11 @@ __device__ __forceinline__ void bn_fwd_finalize(const ConvFwdK& a, int g, int Gn
   const int tid = threadIdx.x;
   constexpr int PW = 1 + 2 * D;
   const int nbk = (Gn + GTR_PART_BUCKET - 1) / GTR_PART_BUCKET;
+  // first level: the partial rows were stored write-through (st_wt) -- no release fence per
+  // workgroup; the bucket mergers' rows are plain stores behind arrive_last's release
   if (nbk > 1) {
     const int bk = g / GTR_PART_BUCKET, b0 = bk * GTR_PART_BUCKET;
-    if (!arrive_last(a.cnt + 4 + 2 * bk, (uint32_t)min(GTR_PART_BUCKET, Gn - b0), s_flag)) return;
+    if (!arrive_last_wt(a.cnt + 4 + 2 * bk, (uint32_t)min(GTR_PART_BUCKET, Gn - b0), s_flag)) return;
     float* row0 = a.bn_part + (size_t)b0 * PW;
     bn_merge_parts<D, BLK>(row0, min(GTR_PART_BUCKET, Gn - b0), red, PW, row0);
     if (tid == 0) reset_counter(a.cnt + 4 + 2 * bk);
@@ -137,7 +139,7 @@ __device__ __forceinline__ void bn_fwd_finalize(const ConvFwdK& a, int g, int Gn
     }
     bn_stats_from_parts<D, BLK>(a.bn_part, nbk, a.bn_eps, s_bn, s_bn + D, s_uvar, red, (size_t)GTR_PART_BUCKET * PW);
   } else {
-    if (!arrive_last(a.cnt, (uint32_t)Gn, s_flag)) return;
+    if (!arrive_last_wt(a.cnt, (uint32_t)Gn, s_flag)) return;
     if (a.merge_only) {
       bn_merge_parts<D, BLK>(a.bn_part, Gn, red, PW, a.bn_part);
       if (tid == 0) reset_counter(a.cnt);
@@ -733,7 +735,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
       for (int q = 0; q < NS; ++q) tot += red[q * D + tid];
       const float mean = nrow > 0 ? tot / (float)nrow : 0.0f;
       red[NS * D + tid] = mean;
-      part[1 + tid] = mean;
+      st_wt(part + 1 + tid, mean);  // write-through: read by another workgroup in this launch
     }
     __syncthreads();
     float m2 = 0.0f;
@@ -748,9 +750,9 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
     if (tid < D) {
       float tot = 0.0f;
       for (int q = 0; q < NS; ++q) tot += red[q * D + tid];
-      part[1 + D + tid] = tot;
+      st_wt(part + 1 + D + tid, tot);
     }
-    if (tid == 0) part[0] = (float)nrow;
+    if (tid == 0) st_wt(part, (float)nrow);
   }
   GTR_PH(a.layer, 4);
   GTR_PH_CLK(a.layer, 7);
@@ -924,7 +926,7 @@ __global__ __launch_bounds__(AR_BLOCK) void k_attn_rows(ConvFwdK a) {
       for (int q2 = 0; q2 < NS; ++q2) tot += s_red[q2 * D + tid];
       const float mean = tot / (float)nrow;
       s_red[NS * D + tid] = mean;
-      part[1 + tid] = mean;
+      st_wt(part + 1 + tid, mean);  // write-through: read by another workgroup in this launch
     }
     __syncthreads();
     float m2 = 0.0f;
@@ -938,9 +940,9 @@ __global__ __launch_bounds__(AR_BLOCK) void k_attn_rows(ConvFwdK a) {
     if (tid < D) {
       float tot = 0.0f;
       for (int q2 = 0; q2 < NS; ++q2) tot += s_red[q2 * D + tid];
-      part[1 + D + tid] = tot;
+      st_wt(part + 1 + D + tid, tot);
     }
-    if (tid == 0) part[0] = (float)nrow;
+    if (tid == 0) st_wt(part, (float)nrow);
   }
   bn_fwd_finalize<D, AR_BLOCK>(a, g, Gn, &s_flag, s_red, s_bn, s_uv);
 }
@@ -1297,18 +1299,18 @@ __device__ __forceinline__ void readout_body(const ReadoutK& a, int rb) {
   if (do_loss && tid < 2) {
     float acc = 0.0f;
     for (int w = 0; w < RO_WAVES; ++w) acc += s_loss[w][tid];
-    a.loss_part[(size_t)rb * 2 + tid] = acc;
+    st_wt(a.loss_part + (size_t)rb * 2 + tid, acc);
   }
   if (do_bwd) {
     for (int j = tid; j < 2 * D; j += RO_BLOCK) {
       float acc = 0.0f;
       for (int w = 0; w < RO_WAVES; ++w) acc += s_red[w][j];
-      a.gpart[(size_t)rb * 2 * D + j] = acc;
+      st_wt(a.gpart + (size_t)rb * 2 * D + j, acc);
     }
   }
   GTR_PH(16, 3);
   if (!a.fin) return;  // loss summed by the step tail, BN sums reduced by the consuming conv_bwd
-  if (!arrive_last(a.cnt, (uint32_t)a.main_grid, &s_flag)) return;
+  if (!arrive_last_wt(a.cnt, (uint32_t)a.main_grid, &s_flag)) return;
   if (do_loss) {
     __shared__ float s_pair[2];
     block_sum_rows<RO_BLOCK>(a.loss_part, a.main_grid, 2, 2, s_pair, &s_red[0][0]);
@@ -1634,17 +1636,17 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
   if (do_loss && tid < 2) {
     float acc = 0.0f;
     for (int w = 0; w < RW_WAVES; ++w) acc += s_loss[w][tid];
-    a.loss_part[(size_t)rb * 2 + tid] = acc;
+    st_wt(a.loss_part + (size_t)rb * 2 + tid, acc);
   }
   if (do_bwd) {
     for (int j = tid; j < 2 * D; j += RW_BLOCK) {
       float acc = 0.0f;
       for (int w = 0; w < RW_WAVES; ++w) acc += s_red[w][j];
-      a.gpart[(size_t)rb * 2 * D + j] = acc;
+      st_wt(a.gpart + (size_t)rb * 2 * D + j, acc);
     }
   }
   if (!a.fin) return;
-  if (!arrive_last(a.cnt, (uint32_t)a.main_grid, &s_flag)) return;
+  if (!arrive_last_wt(a.cnt, (uint32_t)a.main_grid, &s_flag)) return;
   if (do_loss) {
     __shared__ float s_pair[2];
     block_sum_rows<RW_BLOCK>(a.loss_part, a.main_grid, 2, 2, s_pair, s_scr);

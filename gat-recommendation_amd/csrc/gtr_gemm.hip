@@ -399,21 +399,21 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
     float acc = 0.0f;
 #pragma unroll
     for (int q = 0; q < GM_WAVES / NCT; ++q) acc += s_bnp[q][j];
-    part[j] = acc;
+    st_wt(part + j, acc);  // write-through: read by the last arriver of this launch
   }
   const int Gn = gridDim.x;
   const int nbk = (Gn + GTR_PART_BUCKET - 1) / GTR_PART_BUCKET;
   float* scr = As[0];
   if (nbk > 1) {
     const int bk = blockIdx.x / GTR_PART_BUCKET, b0 = bk * GTR_PART_BUCKET;
-    if (!arrive_last(a.p_cnt + 4 + 2 * bk, (uint32_t)min(GTR_PART_BUCKET, Gn - b0), &s_flag)) return;
+    if (!arrive_last_wt(a.p_cnt + 4 + 2 * bk, (uint32_t)min(GTR_PART_BUCKET, Gn - b0), &s_flag)) return;
     float* row0 = a.p_gpart + (size_t)b0 * 2 * D;
     block_sum_rows<GM_BLOCK>(row0, min(GTR_PART_BUCKET, Gn - b0), 2 * D, (size_t)2 * D, row0, scr);
     if (tid == 0) reset_counter(a.p_cnt + 4 + 2 * bk);
     if (!arrive_last(a.p_cnt, (uint32_t)nbk, &s_flag)) return;
     block_sum_rows<GM_BLOCK>(a.p_gpart, nbk, 2 * D, (size_t)GTR_PART_BUCKET * 2 * D, a.p_gsum, scr);
   } else {
-    if (!arrive_last(a.p_cnt, (uint32_t)Gn, &s_flag)) return;
+    if (!arrive_last_wt(a.p_cnt, (uint32_t)Gn, &s_flag)) return;
     block_sum_rows<GM_BLOCK>(a.p_gpart, Gn, 2 * D, (size_t)2 * D, a.p_gsum, scr);
   }
   if (tid == 0) reset_counter(a.p_cnt);

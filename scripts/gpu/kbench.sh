@@ -10,10 +10,8 @@ run() { echo "== $*" >> $O; env "$@" timeout -k 10 200 python3 -u scripts/dbg/kb
 run GTR_SPLIT=1
 run GTR_SPLIT=1 GTR_ATTN=group
 run GTR_SPLIT=0
-run GTR_SPLIT=1 GTR_LIB=$PWD/gat-recommendation_amd/build/probe/libgtr_hip.so
-run GTR_SPLIT=0 GTR_LIB=$PWD/gat-recommendation_amd/build/probe/libgtr_hip.so
+[ -f gat-recommendation_amd/build/probe/libgtr_hip.so ] && run GTR_SPLIT=1 GTR_LIB=$PWD/gat-recommendation_amd/build/probe/libgtr_hip.so
 run GTR_SPLIT=1 GTR_GEMM_GRID=128
-run GTR_SPLIT=1 GTR_GEMM_GRID=512
 CFG=c5 BB=1024 run GTR_SPLIT=1
 CFG=c5 BB=1024 run GTR_SPLIT=0
 grep -v "^/opt\|Warn\|warn" $O

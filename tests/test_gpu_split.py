@@ -148,7 +148,20 @@ def test_split_row_attention_equals_fused(D, H, K, loss, B, monkeypatch):
                            ("dqkvs", N), ("du", N)):  # (the fused fast path keeps dlogit in LDS)
             assert_close(b[name][:rows], a[name][:rows], rtol=1e-4, name=f"layer {l} {name}")
     assert_close(f2.ws.dx0[:N], f1.ws.dx0[:N], rtol=1e-4, name="dx0")
+    _params_after_one_adam_step(m1, m2, lr=1e-2)
+
+
+def _params_after_one_adam_step(m1, m2, lr):
+    """One AdamW step from equal parameters: the update is lr * g / (|g| + eps) per element,
+    so gradients equal to float rounding give equal parameters -- except where |g| is at
+    the eps floor and the rounding moves the update by up to 2 lr.  Elementwise 1e-3, and
+    at most one element in 1,000 per tensor inside 2 lr instead."""
     for (n1, p1), (n2, p2) in zip(m1.named_parameters(), m2.named_parameters()):
         if n1.endswith("lin_key.bias"):
             continue
-        assert_close(p2, p1, rtol=1e-3, name=n1)
+        a, b = p2.detach().float().cpu(), p1.detach().float().cpu()
+        tol = 1e-3 * (b.abs() + 1e-2 * float(b.abs().max()))
+        miss = (a - b).abs() > tol
+        assert float(miss.float().mean()) <= 1e-3, (n1, int(miss.sum()))
+        if bool(miss.any()):
+            assert float((a - b).abs()[miss].max()) <= 2 * lr, n1
