@@ -31,6 +31,12 @@ using namespace gtr;
 #define GM_BLOCK 512
 #define GM_WAVES (GM_BLOCK / 64)
 
+#ifdef GTR_PROBE_NOMFMA  // timing probe only: what the GEMM kernels cost without their MFMAs
+#define GM_MFMA4(a, b, c) (c + f32x4{(a).x, (b).y, (a).z, (b).w})
+#else
+#define GM_MFMA4(a, b, c) mfma4(a, b, c)
+#endif
+
 template <int D>
 struct ProjGeom {
   static constexpr int NCT = 4 * D / 16;          // output column tiles of qkvs
@@ -256,7 +262,7 @@ __global__ __launch_bounds__(GM_BLOCK) void k_proj(ProjK a) {
 #pragma unroll
       for (int r = 0; r < RT; ++r)
 #pragma unroll
-        for (int c = 0; c < CT; ++c) acc[r][c] = mfma4(av[r], wf[c][kb], acc[r][c]);
+        for (int c = 0; c < CT; ++c) acc[r][c] = GM_MFMA4(av[r], wf[c][kb], acc[r][c]);
     }
 #pragma unroll
     for (int r = 0; r < RT; ++r)
@@ -365,7 +371,7 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
     f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
     const float* arow = A + (rs * 16 + lr) * AS + lg * 4;
 #pragma unroll
-    for (int kb = 0; kb < K / 16; ++kb) acc = mfma4(*reinterpret_cast<const float4*>(arow + kb * 16), wb[kb], acc);
+    for (int kb = 0; kb < K / 16; ++kb) acc = GM_MFMA4(*reinterpret_cast<const float4*>(arow + kb * 16), wb[kb], acc);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = t * BM + rs * 16 + lg * 4 + i;

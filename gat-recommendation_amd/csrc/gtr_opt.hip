@@ -189,6 +189,50 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_adamw_sweep(int64_t nvec, int vpr
 // (lanes gl = 0..15 at gbase; they cover the row's float4 columns).  The per-step
 // scalars are fetched 16 steps at a time (one per lane) and broadcast by shuffles, so
 // the serial chain of updates never waits on memory.
+// Zero-gradient catch-up of one row from step old to t-1 by its 16-lane group: every
+// lane holds NP float4 columns of p / m / v in registers for the whole chain (one read
+// and one write of the row), the steps' scalars come 16 at a time from consts[] and are
+// broadcast from the lane that loaded them.
+template <int NP>
+__device__ __forceinline__ void lazy_catch_up_lanes(float4* P, float4* M, float4* V, int C4, int old, int32_t t,
+                                                    int gl, int gbase, const gtr_lazy& lz) {
+  const gtr_adam& o = lz.opt;
+  AdamStep st;
+  st.lr = o.lr; st.b1 = o.beta1; st.b2 = o.beta2; st.eps = o.eps; st.wd = o.weight_decay;
+  st.decoupled = o.decoupled;
+  st.decay_mul = (float)(1.0 - (double)o.lr * (double)o.weight_decay);
+  float4 p[NP], m[NP], v[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int c = gl + 16 * k;
+    const bool on = c < C4;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    p[k] = on ? P[c] : z;
+    m[k] = on ? M[c] : z;
+    v[k] = on ? V[c] : z;
+  }
+  for (int t0 = old + 1; t0 <= t - 1; t0 += 16) {
+    const int cnt = min(16, t - t0);
+    const float2 cc = gl < cnt ? reinterpret_cast<const float2*>(lz.consts)[t0 + gl] : make_float2(0.f, 0.f);
+    for (int q = 0; q < cnt; ++q) {
+      st.step_size = __shfl(cc.x, gbase + q);
+      st.inv_bc2 = __shfl(cc.y, gbase + q);
+#pragma unroll
+      for (int k = 0; k < NP; ++k) {
+        st.apply(p[k].x, m[k].x, v[k].x, 0.0f);
+        st.apply(p[k].y, m[k].y, v[k].y, 0.0f);
+        st.apply(p[k].z, m[k].z, v[k].z, 0.0f);
+        st.apply(p[k].w, m[k].w, v[k].w, 0.0f);
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int c = gl + 16 * k;
+    if (c < C4) { P[c] = p[k]; M[c] = m[k]; V[c] = v[k]; }
+  }
+}
+
 __device__ __forceinline__ void lazy_claim_row(int key, int T, int D, int32_t t, int gl, int gbase,
                                                int32_t* stamp, const gtr_lazy& lz) {
   int old = 0;
@@ -199,32 +243,9 @@ __device__ __forceinline__ void lazy_claim_row(int key, int T, int D, int32_t t,
   float4* P = reinterpret_cast<float4*>(lz.table) + (size_t)key * C4;
   float4* M = reinterpret_cast<float4*>(lz.m) + (size_t)key * C4;
   float4* V = reinterpret_cast<float4*>(lz.v) + (size_t)key * C4;
-  const gtr_adam& o = lz.opt;
-  AdamStep st;
-  st.lr = o.lr; st.b1 = o.beta1; st.b2 = o.beta2; st.eps = o.eps; st.wd = o.weight_decay;
-  st.decoupled = o.decoupled;
-  st.decay_mul = (float)(1.0 - (double)o.lr * (double)o.weight_decay);
-  for (int c0 = 0; c0 < C4; c0 += 16) {  // D = 256: two column passes
-    const int c = c0 + gl;
-    const bool on = c < C4;
-    float4 p, m, v;
-    if (on) { p = P[c]; m = M[c]; v = V[c]; }
-    for (int t0 = old + 1; t0 <= t - 1; t0 += 16) {
-      const int cnt = min(16, t - t0);
-      const float2 cc = gl < cnt ? reinterpret_cast<const float2*>(lz.consts)[t0 + gl] : make_float2(0.f, 0.f);
-      for (int q = 0; q < cnt; ++q) {
-        st.step_size = __shfl(cc.x, gbase + q);
-        st.bc2_sqrt = __shfl(cc.y, gbase + q);
-        if (on) {
-          st.apply(p.x, m.x, v.x, 0.0f);
-          st.apply(p.y, m.y, v.y, 0.0f);
-          st.apply(p.z, m.z, v.z, 0.0f);
-          st.apply(p.w, m.w, v.w, 0.0f);
-        }
-      }
-    }
-    if (on) { P[c] = p; M[c] = m; V[c] = v; }
-  }
+  if (C4 <= 16) lazy_catch_up_lanes<1>(P, M, V, C4, old, t, gl, gbase, lz);
+  else if (C4 <= 32) lazy_catch_up_lanes<2>(P, M, V, C4, old, t, gl, gbase, lz);
+  else lazy_catch_up_lanes<4>(P, M, V, C4, old, t, gl, gbase, lz);
 }
 
 // ---- fused step: begin (counters, stamps, sorted contribution list) -------------------
@@ -990,7 +1011,9 @@ bool dim_ok(int D) { return D == 32 || D == 64 || D == 128 || D == 256; }
 
 // ---- contribution sort (large batches): own LSD radix, 10-bit digits -------------------
 // keys < 2^20 (T <= 1M + 1) sort in two passes of three launches each: per-tile digit
-// histograms (tile = 4096 items) and digit totals, the scatter offsets of every (tile,
+// histograms (tile = 256 x rounds items, rounds = rs_rounds(n): 16 from ~1M items down to
+// 1 below 64k, so a pass keeps ~200+ workgroups busy: C5 B = 1024's 107k contributions
+// ran on 27 tiles of 4096) and digit totals, the scatter offsets of every (tile,
 // digit) from them (16 workgroups), then a stable scatter.  Inside a tile items are ranked in 16 rounds of 256 (the
 // original order): a round's items of equal digit are matched by 10 ballots within the
 // wave, waves of the round are offset by per-(wave, digit) counts in LDS, rounds by a
@@ -999,16 +1022,20 @@ bool dim_ok(int D) { return D == 32 || D == 64 || D == 128 || D == 256; }
 #define RS_BITS 10
 #define RS_RADIX (1 << RS_BITS)
 #define RS_THREADS 256
-#define RS_ROUNDS 16
-#define RS_TILE (RS_THREADS * RS_ROUNDS)
+#define RS_MAX_ROUNDS 16
+
+int rs_rounds(int n) {
+  const int r = (n + 65535) / 65536;
+  return r < 1 ? 1 : (r > RS_MAX_ROUNDS ? RS_MAX_ROUNDS : r);
+}
 
 __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const int32_t* keys, int n, int shift, int32_t* hist,
-                                                       int32_t* tot) {
+                                                       int32_t* tot, int rounds) {
   __shared__ int h[RS_RADIX];
   for (int d = threadIdx.x; d < RS_RADIX; d += RS_THREADS) h[d] = 0;
   __syncthreads();
-  const int base = blockIdx.x * RS_TILE;
-  for (int r = 0; r < RS_ROUNDS; ++r) {
+  const int base = blockIdx.x * RS_THREADS * rounds;
+  for (int r = 0; r < rounds; ++r) {
     const int i = base + r * RS_THREADS + threadIdx.x;
     if (i < n) atomicAdd(&h[((uint32_t)keys[i] >> shift) & (RS_RADIX - 1)], 1);  // integer counts
   }
@@ -1068,7 +1095,7 @@ __global__ __launch_bounds__(1024) void k_rs_offs(const int32_t* __restrict__ hi
 // pass (the workspace starts zeroed), so no memset node sits in the captured step.
 __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const int32_t* kin, const int32_t* vin, int32_t* kout,
                                                           int32_t* vout, int n, int shift, const int32_t* offs,
-                                                          int ntile, int32_t* tot) {
+                                                          int ntile, int32_t* tot, int rounds) {
   __shared__ int run[RS_RADIX];
   __shared__ int wcnt[RS_THREADS / 64][RS_RADIX];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1081,8 +1108,8 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const int32_t* kin, c
   }
   __syncthreads();
   const unsigned long long lt = (1ull << lane) - 1ull;
-  const int base = blockIdx.x * RS_TILE;
-  for (int r = 0; r < RS_ROUNDS; ++r) {
+  const int base = blockIdx.x * RS_THREADS * rounds;
+  for (int r = 0; r < rounds; ++r) {
     const int i = base + r * RS_THREADS + tid;
     const bool live = i < n;
     const int key = live ? kin[i] : 0;
@@ -1121,14 +1148,16 @@ int sort_mode() {  // 0: own radix (default), 1: hipCUB
 }
 
 size_t rs_bytes(int n) {
-  const size_t ntile = (size_t)(n + RS_TILE - 1) / RS_TILE;
+  const size_t tile = (size_t)RS_THREADS * rs_rounds(n);
+  const size_t ntile = ((size_t)n + tile - 1) / tile;
   return 4 * (size_t)n * sizeof(int32_t) + 2 * (size_t)RS_RADIX * ntile * sizeof(int32_t) +
          4 * RS_RADIX * sizeof(int32_t) + 256;
 }
 
 hipError_t rs_sort(void* tmp, const int32_t* keys, int32_t* skeys, const int32_t* vals, int32_t* svals, int n,
                    int bits, hipStream_t s) {
-  const int ntile = (n + RS_TILE - 1) / RS_TILE;
+  const int rounds = rs_rounds(n), tile = RS_THREADS * rounds;
+  const int ntile = (n + tile - 1) / tile;
   int32_t* k1 = static_cast<int32_t*>(tmp);
   int32_t* v1 = k1 + n;
   int32_t* k2 = v1 + n;
@@ -1145,10 +1174,10 @@ hipError_t rs_sort(void* tmp, const int32_t* keys, int32_t* skeys, const int32_t
     int32_t* ko = last ? skeys : (p % 2 == 0 ? k1 : k2);
     int32_t* vo = last ? svals : (p % 2 == 0 ? v1 : v2);
     int32_t* tp = tot + p * RS_RADIX;
-    hipLaunchKernelGGL(k_rs_hist, dim3(ntile), dim3(RS_THREADS), 0, s, ki, n, p * RS_BITS, hist, tp);
+    hipLaunchKernelGGL(k_rs_hist, dim3(ntile), dim3(RS_THREADS), 0, s, ki, n, p * RS_BITS, hist, tp, rounds);
     hipLaunchKernelGGL(k_rs_offs, dim3(RS_RADIX / 64), dim3(1024), 0, s, hist, tp, offs, ntile);
     hipLaunchKernelGGL(k_rs_scatter, dim3(ntile), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, n, p * RS_BITS, offs,
-                       ntile, tp);
+                       ntile, tp, rounds);
     ki = ko;
     vi = vo;
   }

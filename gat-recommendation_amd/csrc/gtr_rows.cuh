@@ -70,7 +70,7 @@ __device__ __forceinline__ void catch_up4(float4& p, float4& m, float4& v, int f
   for (int t = from + 1; t <= upto; ++t) {
     const float2 c = reinterpret_cast<const float2*>(consts)[t];
     st.step_size = c.x;
-    st.bc2_sqrt = c.y;
+    st.inv_bc2 = c.y;
     st.apply(p.x, m.x, v.x, 0.0f);
     st.apply(p.y, m.y, v.y, 0.0f);
     st.apply(p.z, m.z, v.z, 0.0f);
@@ -82,7 +82,7 @@ __device__ __forceinline__ void catch_up4(float4& p, float4& m, float4& v, int f
 __device__ __forceinline__ void lazy_consts_for(const gtr_adam& o, int64_t t, float* consts) {
   AdamStep st;
   st.init(o, t);
-  reinterpret_cast<float2*>(consts)[t] = make_float2(st.step_size, st.bc2_sqrt);
+  reinterpret_cast<float2*>(consts)[t] = make_float2(st.step_size, st.inv_bc2);
 }
 
 #define TW 128

@@ -264,9 +264,14 @@ class Engine:
         return caps.R
 
     def choose_P(self, caps: Caps) -> int:
-        # split-K of the weight gradients: <= 32 node rows per workgroup, <= 64 slabs (one
-        # chunk over ~110 rows made k_wgrad 2x slower at C2: measured 0.105 -> 0.119 ms/step)
-        rows = max(1, int(os.environ.get("GTR_WGRAD_ROWS", "32")))  # diagnostics / tuning
+        # split-K of the weight gradients: <= 32 node rows per workgroup up to 2048 rows, <= 64
+        # slabs (one chunk over ~110 rows made k_wgrad 2x slower at C2: measured 0.105 ->
+        # 0.119 ms/step); past 2048 rows chunks of >= 128 rows, where the QKVS tiles run on
+        # MFMA (GTR_WGRAD_MFMA_ROWS) -- C5 at B = 1024 (3.5k rows) had 64 VALU chunks of 55
+        rows = int(os.environ.get("GTR_WGRAD_ROWS", "0"))  # diagnostics / tuning
+        if rows <= 0 and caps.n_cap > 2048:
+            return max(1, min(64, caps.n_cap // 128))  # (floor: every chunk >= 128 rows)
+        rows = rows if rows > 0 else 32
         return max(1, min(64, (caps.n_cap + rows - 1) // rows))
 
     def workspace(self, caps: Caps, fresh: bool = False) -> Workspace:

@@ -366,7 +366,7 @@ int gtr_step_begin(const gtr_batch* bt, int num_items, int32_t* keys, int32_t* v
  * applied step by step with that step's scalars, so the floats are identical to eager
  * sweeping -- right before it is read (gtr_step_begin_lazy, gtr_dp_tail) or on demand
  * (gtr_lazy_flush: evaluation, checkpoints).  The step tail then updates only the
- * touched rows.  consts[t] = {lr / (1 - beta1^t), sqrt(1 - beta2^t)} (fp32 of the
+ * touched rows.  consts[t] = {lr / (1 - beta1^t), 1 / sqrt(1 - beta2^t)} (fp32 of the
  * double expressions, exactly as the eager kernels compute them), filled by the begin
  * kernel of step t; cap = its capacity in steps.                                      */
 typedef struct gtr_lazy {
