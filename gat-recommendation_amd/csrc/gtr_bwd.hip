@@ -50,6 +50,7 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_attn_bwd(ConvBwdK a) {
 #define BR_RPW 2
 #define BR_ECH 64
 #define BR_HMAX 8
+#define BR_VR 8   // K rows of a row pair held in registers
 
 // This layer's BatchNorm constants per lane: gamma, mean, rstd and the backward sums / N
 // (sync: every rank's gathered sums, N from the gathered counts).
@@ -110,17 +111,115 @@ __global__ __launch_bounds__(BR_BLOCK) void k_attn_rows_bwd_dst(ConvBwdK a) {
   load_vec<VPL>(w3, a.w_beta + 2 * D + d0, act);
   const float* K = a.qkvs + D;
   const float* V = a.qkvs + 2 * D;
-  for (int i = 0; i < BR_RPW; ++i) {
-    const int t = (blockIdx.x * BR_WAVES + wave) * BR_RPW + i;
-    if (t >= Nl) break;  // wave-uniform
-    const int e0 = a.bt.in_ptr[t], e1 = a.bt.in_ptr[t + 1];
-    if (e1 - e0 > BR_ECH || H > BR_HMAX) {  // hub rows: the general wave-per-row body
-      bwd_dst_row<D>(a, t, t, K, V, 4 * D, a.bt.in_ptr, a.bt.in_src, a.alpha, a.dlogit, 0, lane, dr, st_attn, k_g,
-                     k_mean, k_rstd, k_s1, k_s2);
-      continue;
-    }
-    const int ne = e1 - e0;
-    const int my_src = lane < ne ? a.bt.in_src[e0 + lane] : 0;
+  // one row of the wave alone (hub rows, wide heads: the general bodies)
+  auto one_row = [&](int i) {
+      const int t = (blockIdx.x * BR_WAVES + wave) * BR_RPW + i;
+      if (t >= Nl) return;  // wave-uniform
+      const int e0 = a.bt.in_ptr[t], e1 = a.bt.in_ptr[t + 1];
+      if (e1 - e0 > BR_ECH || H > BR_HMAX) {  // hub rows: the general wave-per-row body
+        bwd_dst_row<D>(a, t, t, K, V, 4 * D, a.bt.in_ptr, a.bt.in_src, a.alpha, a.dlogit, 0, lane, dr, st_attn, k_g,
+                       k_mean, k_rstd, k_s1, k_s2);
+        return;
+      }
+      const int ne = e1 - e0;
+      const int my_src = lane < ne ? a.bt.in_src[e0 + lane] : 0;
+      const size_t ro = (size_t)t * D + d0;
+      float dyv[VPL], ov[VPL], agv[VPL], sv[VPL];
+      load_vec<VPL>(dyv, a.dy + ro, act);
+      load_vec<VPL>(ov, a.out + ro, act);
+      load_vec<VPL>(agv, a.agg + ro, act);
+      load_vec<VPL>(sv, a.qkvs + (size_t)t * (4 * D) + 3 * D + d0, act);
+      const float beta = a.gate[t];
+      // BatchNorm backward, then the beta gate (as bwd_dst_row)
+      float gv[VPL];
+      float dbeta = 0.0f;
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) {
+        const float xh = (ov[v] - k_mean[v]) * k_rstd[v];
+        gv[v] = act ? (dyv[v] - k_s1[v] - xh * k_s2[v]) * k_rstd[v] * k_g[v] : 0.0f;
+        dbeta += gv[v] * (sv[v] - agv[v]);
+      }
+      dbeta = wave_sum(dbeta);
+      const float du = dbeta * beta * (1.0f - beta);
+      if (lane == 0) a.du[t] = du;
+      float dag[VPL], ds[VPL], dq[VPL];
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) {
+        dag[v] = gv[v] * (1.0f - beta) + du * (w1[v] + w3[v]);
+        ds[v] = gv[v] * beta + du * (w2[v] - w3[v]);
+        dq[v] = 0.0f;
+      }
+      store_vec<VPL>(a.dqkvs + (size_t)t * (4 * D) + 3 * D + d0, ds, act);
+      store_vec<VPL>(a.dagg + ro, dag, act);
+      // da = <dA[t], V[src]> * mask per edge (LDS), sdot = sum alpha * da (four V rows in flight)
+      float sdot = 0.0f;
+      for (int j = 0; j < ne; j += 4) {
+        float vv[4][VPL];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int src = __shfl(my_src, (j + u) & 63);
+          load_vec<VPL>(vv[u], V + (size_t)src * (4 * D) + d0, act && j + u < ne);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float d = 0.0f;
+#pragma unroll
+          for (int v = 0; v < VPL; ++v) d += dag[v] * vv[u][v];
+          d = group_sum(d, GL);
+          if (j + u < ne) {
+            const int eg = e0 + j + u;
+            const float da = d * dr.mul(st_attn, (uint32_t)(eg * H + head));
+            sdot += a.alpha[(size_t)eg * H + head] * da;
+            if (leader) s_da[wave][j + u][head] = da;
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // dlogit = alpha * (da - sdot); dQ += dlogit / sqrt(C) * K[src] (four K rows in flight)
+      for (int j = 0; j < ne; j += 4) {
+        float kv[4][VPL];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int src = __shfl(my_src, (j + u) & 63);
+          load_vec<VPL>(kv[u], K + (size_t)src * (4 * D) + d0, act && j + u < ne);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (j + u < ne) {
+            const int eg = e0 + j + u;
+            const float al = a.alpha[(size_t)eg * H + head];
+            const float dl = al * (s_da[wave][j + u][head] - sdot);
+            if (leader) a.dlogit[(size_t)eg * H + head] = dl;
+            const float c = dl / a.sqrt_c;
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) dq[v] += c * kv[u][v];
+          }
+        }
+      }
+      store_vec<VPL>(a.dqkvs + (size_t)t * (4 * D) + d0, dq, act);
+      __builtin_amdgcn_wave_barrier();  // s_da is reused by the wave's next row
+  };
+  // The wave's two rows together (as k_attn_rows): one id load for both rows' contiguous
+  // in-edges, every V row requested with its K row (the first BR_VR edges' K rows stay in
+  // registers for dQ).  Per row the arithmetic is the single-row body's, in the same edge
+  // order: bitwise the same outputs.
+  const int t0 = (blockIdx.x * BR_WAVES + wave) * BR_RPW;
+  if (t0 >= Nl) return;  // wave-uniform
+  const bool two = t0 + 1 < Nl;
+  const int e0 = a.bt.in_ptr[t0], em = a.bt.in_ptr[t0 + 1];
+  const int e2 = two ? a.bt.in_ptr[t0 + 2] : em;
+  const int ne0 = em - e0, ne = e2 - e0;
+  static_assert(BR_RPW == 2, "the paired body covers two rows per wave");
+  if (ne > BR_ECH || H > BR_HMAX) {
+    one_row(0);
+    one_row(1);
+    return;
+  }
+  const int my_src = lane < ne ? a.bt.in_src[e0 + lane] : 0;
+  // BatchNorm backward, then the beta gate, of one row (as bwd_dst_row) -> dA of the row
+  auto head_of = [&](int t, float (&dag)[VPL]) {
     const size_t ro = (size_t)t * D + d0;
     float dyv[VPL], ov[VPL], agv[VPL], sv[VPL];
     load_vec<VPL>(dyv, a.dy + ro, act);
@@ -128,7 +227,6 @@ __global__ __launch_bounds__(BR_BLOCK) void k_attn_rows_bwd_dst(ConvBwdK a) {
     load_vec<VPL>(agv, a.agg + ro, act);
     load_vec<VPL>(sv, a.qkvs + (size_t)t * (4 * D) + 3 * D + d0, act);
     const float beta = a.gate[t];
-    // BatchNorm backward, then the beta gate (as bwd_dst_row)
     float gv[VPL];
     float dbeta = 0.0f;
 #pragma unroll
@@ -140,65 +238,104 @@ __global__ __launch_bounds__(BR_BLOCK) void k_attn_rows_bwd_dst(ConvBwdK a) {
     dbeta = wave_sum(dbeta);
     const float du = dbeta * beta * (1.0f - beta);
     if (lane == 0) a.du[t] = du;
-    float dag[VPL], ds[VPL], dq[VPL];
+    float ds[VPL];
 #pragma unroll
     for (int v = 0; v < VPL; ++v) {
       dag[v] = gv[v] * (1.0f - beta) + du * (w1[v] + w3[v]);
       ds[v] = gv[v] * beta + du * (w2[v] - w3[v]);
-      dq[v] = 0.0f;
     }
     store_vec<VPL>(a.dqkvs + (size_t)t * (4 * D) + 3 * D + d0, ds, act);
     store_vec<VPL>(a.dagg + ro, dag, act);
-    // da = <dA[t], V[src]> * mask per edge (LDS), sdot = sum alpha * da (four V rows in flight)
-    float sdot = 0.0f;
-    for (int j = 0; j < ne; j += 4) {
+  };
+  float dag0[VPL], dag1[VPL], dq0[VPL], dq1[VPL];
+  head_of(t0, dag0);
+  if (two) head_of(t0 + 1, dag1);
+  else {
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) dag1[v] = 0.0f;
+  }
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) { dq0[v] = 0.0f; dq1[v] = 0.0f; }
+  // da = <dA[t], V[src]> * mask per edge (LDS), sdot = sum alpha * da
+  float sdot0 = 0.0f, sdot1 = 0.0f;
+  auto dot_v = [&](int e, const float (&vr)[VPL]) {
+    const bool r1 = e >= ne0;  // wave-uniform
+    float d = 0.0f;
+#pragma unroll
+    for (int v = 0; v < VPL; ++v) d += (r1 ? dag1[v] : dag0[v]) * vr[v];
+    d = group_sum(d, GL);
+    if (e < ne) {
+      const int eg = e0 + e;
+      const float da = d * dr.mul(st_attn, (uint32_t)(eg * H + head));
+      // explicit fma: the single-row body's contracted `sdot += alpha * da` (the two
+      // accumulators' branches must not share one rounded product)
+      const float al = a.alpha[(size_t)eg * H + head];
+      if (r1) sdot1 = __builtin_fmaf(al, da, sdot1);
+      else sdot0 = __builtin_fmaf(al, da, sdot0);
+      if (leader) s_da[wave][e][head] = da;
+    }
+  };
+  float kh[BR_VR][VPL];
+#pragma unroll
+  for (int jj = 0; jj < BR_VR; jj += 4) {
+    if (jj < ne) {  // wave-uniform
       float vv[4][VPL];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int src = __shfl(my_src, (j + u) & 63);
-        load_vec<VPL>(vv[u], V + (size_t)src * (4 * D) + d0, act && j + u < ne);
+        const int src = __shfl(my_src, (jj + u) & 63);
+        const bool ok = act && jj + u < ne;
+        load_vec<VPL>(vv[u], V + (size_t)src * (4 * D) + d0, ok);
+        load_vec<VPL>(kh[jj + u], K + (size_t)src * (4 * D) + d0, ok);
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        float d = 0.0f;
-#pragma unroll
-        for (int v = 0; v < VPL; ++v) d += dag[v] * vv[u][v];
-        d = group_sum(d, GL);
-        if (j + u < ne) {
-          const int eg = e0 + j + u;
-          const float da = d * dr.mul(st_attn, (uint32_t)(eg * H + head));
-          sdot += a.alpha[(size_t)eg * H + head] * da;
-          if (leader) s_da[wave][j + u][head] = da;
-        }
-      }
+      for (int u = 0; u < 4; ++u) dot_v(jj + u, vv[u]);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // dlogit = alpha * (da - sdot); dQ += dlogit / sqrt(C) * K[src] (four K rows in flight)
-    for (int j = 0; j < ne; j += 4) {
-      float kv[4][VPL];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int src = __shfl(my_src, (j + u) & 63);
-        load_vec<VPL>(kv[u], K + (size_t)src * (4 * D) + d0, act && j + u < ne);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (j + u < ne) {
-          const int eg = e0 + j + u;
-          const float al = a.alpha[(size_t)eg * H + head];
-          const float dl = al * (s_da[wave][j + u][head] - sdot);
-          if (leader) a.dlogit[(size_t)eg * H + head] = dl;
-          const float c = dl / a.sqrt_c;
-#pragma unroll
-          for (int v = 0; v < VPL; ++v) dq[v] += c * kv[u][v];
-        }
-      }
-    }
-    store_vec<VPL>(a.dqkvs + (size_t)t * (4 * D) + d0, dq, act);
-    __builtin_amdgcn_wave_barrier();  // s_da is reused by the wave's next row
   }
+  for (int j = BR_VR; j < ne; j += 4) {
+    float vv[4][VPL];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int src = __shfl(my_src, (j + u) & 63);
+      load_vec<VPL>(vv[u], V + (size_t)src * (4 * D) + d0, act && j + u < ne);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) dot_v(j + u, vv[u]);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // dlogit = alpha * (da - sdot); dQ += dlogit / sqrt(C) * K[src]
+  auto acc_q = [&](int e, const float (&kr)[VPL]) {
+    const bool r1 = e >= ne0;  // wave-uniform
+    const int eg = e0 + e;
+    const float al = a.alpha[(size_t)eg * H + head];
+    const float dl = al * (s_da[wave][e][head] - (r1 ? sdot1 : sdot0));
+    if (leader) a.dlogit[(size_t)eg * H + head] = dl;
+    const float c = dl / a.sqrt_c;
+    if (r1) {
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) dq1[v] = __builtin_fmaf(c, kr[v], dq1[v]);
+    } else {
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) dq0[v] = __builtin_fmaf(c, kr[v], dq0[v]);
+    }
+  };
+#pragma unroll
+  for (int e = 0; e < BR_VR; ++e)
+    if (e < ne) acc_q(e, kh[e]);
+  for (int j = BR_VR; j < ne; j += 4) {
+    float kv[4][VPL];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int src = __shfl(my_src, (j + u) & 63);
+      load_vec<VPL>(kv[u], K + (size_t)src * (4 * D) + d0, act && j + u < ne);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (j + u < ne) acc_q(j + u, kv[u]);
+  }
+  store_vec<VPL>(a.dqkvs + (size_t)t0 * (4 * D) + d0, dq0, act);
+  if (two) store_vec<VPL>(a.dqkvs + (size_t)(t0 + 1) * (4 * D) + d0, dq1, act);
 }
 
 template <int D>
@@ -214,9 +351,9 @@ __global__ __launch_bounds__(BR_BLOCK) void k_attn_rows_bwd_src(ConvBwdK a) {
   const int C = a.C, H = a.H;
   const int head = act ? d0 / C : 0;
   const float isc = 1.0f / a.sqrt_c;
-  for (int i = 0; i < BR_RPW; ++i) {
+  auto one_row = [&](int i) {
     const int s = (blockIdx.x * BR_WAVES + wave) * BR_RPW + i;
-    if (s >= Nl) break;
+    if (s >= Nl) return;
     const int i0 = a.bt.out_ptr[s], i1 = a.bt.out_ptr[s + 1];
     float dk[VPL], dv[VPL];
 #pragma unroll
@@ -242,8 +379,8 @@ __global__ __launch_bounds__(BR_BLOCK) void k_attn_rows_bwd_src(ConvBwdK a) {
             const float ad = a.alpha[(size_t)p[u] * H + head] * dr.mul(st_attn, (uint32_t)(p[u] * H + head));
 #pragma unroll
             for (int v = 0; v < VPL; ++v) {
-              dk[v] += dl * qv[u][v];
-              dv[v] += ad * gv[u][v];
+              dk[v] = __builtin_fmaf(dl, qv[u][v], dk[v]);
+              dv[v] = __builtin_fmaf(ad, gv[u][v], dv[v]);
             }
           }
         }
@@ -251,6 +388,62 @@ __global__ __launch_bounds__(BR_BLOCK) void k_attn_rows_bwd_src(ConvBwdK a) {
     }
     store_vec<VPL>(a.dqkvs + (size_t)s * (4 * D) + D + d0, dk, act);
     store_vec<VPL>(a.dqkvs + (size_t)s * (4 * D) + 2 * D + d0, dv, act);
+  };
+  // The wave's two source rows together: their out-edges are contiguous (CSR by source),
+  // so one id load covers both and every edge's Q / dA rows are requested in one round;
+  // per row the same edge order and arithmetic as one_row (bitwise the same dK / dV).
+  const int s0 = (blockIdx.x * BR_WAVES + wave) * BR_RPW;
+  if (s0 >= Nl) return;  // wave-uniform
+  const bool two = s0 + 1 < Nl;
+  const int i0 = a.bt.out_ptr[s0], im = a.bt.out_ptr[s0 + 1];
+  const int i2 = two ? a.bt.out_ptr[s0 + 2] : im;
+  const int n0 = im - i0, n = i2 - i0;
+  if (n > 64) {
+    one_row(0);
+    one_row(1);
+    return;
+  }
+  const int my_p = lane < n ? a.bt.out_edge[i0 + lane] : 0;
+  const int my_t = lane < n ? a.bt.out_dst[i0 + lane] : 0;
+  float dk0[VPL], dv0[VPL], dk1[VPL], dv1[VPL];
+#pragma unroll
+  for (int v = 0; v < VPL; ++v) { dk0[v] = 0.0f; dv0[v] = 0.0f; dk1[v] = 0.0f; dv1[v] = 0.0f; }
+  for (int j = 0; j < n; j += 4) {
+    float qv[4][VPL], gv[4][VPL];
+    int p[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      p[u] = __shfl(my_p, (j + u) & 63);
+      const int t = __shfl(my_t, (j + u) & 63);
+      load_vec<VPL>(qv[u], a.qkvs + (size_t)t * (4 * D) + d0, act && j + u < n);
+      load_vec<VPL>(gv[u], a.dagg + (size_t)t * D + d0, act && j + u < n);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (j + u < n) {  // wave-uniform
+        const float dl = a.dlogit[(size_t)p[u] * H + head] * isc;
+        const float ad = a.alpha[(size_t)p[u] * H + head] * dr.mul(st_attn, (uint32_t)(p[u] * H + head));
+        if (j + u >= n0) {
+#pragma unroll
+          for (int v = 0; v < VPL; ++v) {
+            dk1[v] = __builtin_fmaf(dl, qv[u][v], dk1[v]);
+            dv1[v] = __builtin_fmaf(ad, gv[u][v], dv1[v]);
+          }
+        } else {
+#pragma unroll
+          for (int v = 0; v < VPL; ++v) {
+            dk0[v] = __builtin_fmaf(dl, qv[u][v], dk0[v]);
+            dv0[v] = __builtin_fmaf(ad, gv[u][v], dv0[v]);
+          }
+        }
+      }
+    }
+  }
+  store_vec<VPL>(a.dqkvs + (size_t)s0 * (4 * D) + D + d0, dk0, act);
+  store_vec<VPL>(a.dqkvs + (size_t)s0 * (4 * D) + 2 * D + d0, dv0, act);
+  if (two) {
+    store_vec<VPL>(a.dqkvs + (size_t)(s0 + 1) * (4 * D) + D + d0, dk1, act);
+    store_vec<VPL>(a.dqkvs + (size_t)(s0 + 1) * (4 * D) + 2 * D + d0, dv1, act);
   }
 }
 

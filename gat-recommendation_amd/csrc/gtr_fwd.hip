@@ -346,9 +346,10 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
   const float* bn_part = a.sync ? a.p_part_all : a.p_part;
   BnParts<D, CONV_BLOCK> bnr;
   if (pre_bn) bn_parts_load<D, CONV_BLOCK>(bn_part, bn_G, 1 + 2 * D, bnr);
-  if (PROJ && pe_lds) {  // LapPE projection weight [D][KPE], zero-padded past pe_k (stored right away)
+  if (PROJ && pe_lds) {  // LapPE projection weight, transposed [KPE][D] (k-major, conflict-free
+                         // reads), zero-padded past pe_k (stored right away)
     for (int idx = tid; idx < D * KPE; idx += CONV_BLOCK) {
-      const int j = idx / KPE, k = idx - j * KPE;
+      const int k = idx / D, j = idx - k * D;
       PEs[idx] = k < a.pe_k ? a.wpe[j * a.pe_k + k] : 0.0f;
     }
   }
@@ -454,14 +455,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
           if (pe_lds && (a.pe_k & 3) == 0) {
             for (int k = 0; k < a.pe_k; k += 4) {
               const float4 p4 = *reinterpret_cast<const float4*>(pr + k);
-#pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                const float4 w4 = *reinterpret_cast<const float4*>(PEs + (j + q) * KPE + k);
-                acc[q] += p4.x * w4.x;
-                acc[q] += p4.y * w4.y;
-                acc[q] += p4.z * w4.z;
-                acc[q] += p4.w * w4.w;
-              }
+              pe_fma4(acc, p4, PEs + k * D + j, D);
             }
           } else {
             for (int k = 0; k < a.pe_k; ++k) {
@@ -799,9 +793,10 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_attn_fwd(ConvFwdK a) {
 #define AR_ROWS (AR_WAVES * AR_RPW)  // rows per workgroup = one BatchNorm partial
 #define AR_ECH 64                  // in-edges of a row handled with LDS logits
 #define AR_HMAX 8
+#define AR_VR 8                    // V rows of a row pair held in registers
 
 template <int D>
-__global__ __launch_bounds__(AR_BLOCK) void k_attn_rows(ConvFwdK a) {
+__global__ __launch_bounds__(AR_BLOCK) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_attn_rows(ConvFwdK a) {
   constexpr int VPL = D >= 64 ? D / 64 : 1;
   __shared__ __attribute__((aligned(16))) float s_out[AR_ROWS][D];
   __shared__ float s_lg[AR_WAVES][AR_ECH][AR_HMAX];
@@ -832,82 +827,200 @@ __global__ __launch_bounds__(AR_BLOCK) void k_attn_rows(ConvFwdK a) {
   const float* K = a.qkvs + D;
   const float* V = a.qkvs + 2 * D;
   const float* S = a.qkvs + 3 * D;
-  for (int i = 0; i < AR_RPW; ++i) {
-    const int rl = wave * AR_RPW + i;
-    const int t = r0 + rl;
-    if (t >= N) break;  // wave-uniform
-    const int e0 = a.bt.in_ptr[t], e1 = a.bt.in_ptr[t + 1];
-    if (e1 - e0 > AR_ECH || H > AR_HMAX) {  // hub rows: the general wave-per-row body
-      attn_row<D>(a, t, t, Q, S, K, V, 4 * D, a.bt.in_ptr, a.bt.in_src, 0, lane, dr, st_attn, w1, w2, w3, s_out[rl]);
-      continue;
-    }
-    const int ne = e1 - e0;
-    const int my_src = lane < ne ? a.bt.in_src[e0 + lane] : 0;
-    float q[VPL], sv[VPL], ag[VPL];
-    load_vec<VPL>(q, Q + (size_t)t * (4 * D) + d0, act);
-    load_vec<VPL>(sv, S + (size_t)t * (4 * D) + d0, act);
-    // logits <Q[t], K[src]> / sqrt(C) per head, four K rows in flight
-    float m = -INFINITY;
-    for (int j = 0; j < ne; j += 4) {
-      float kv[4][VPL];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int src = __shfl(my_src, (j + u) & 63);
-        load_vec<VPL>(kv[u], K + (size_t)src * (4 * D) + d0, act && j + u < ne);
+  // one row of the wave alone (hub rows, wide heads: the general bodies)
+  auto one_row = [&](int i) {
+      const int rl = wave * AR_RPW + i;
+      const int t = r0 + rl;
+      if (t >= N) return;  // wave-uniform
+      const int e0 = a.bt.in_ptr[t], e1 = a.bt.in_ptr[t + 1];
+      if (e1 - e0 > AR_ECH || H > AR_HMAX) {  // hub rows: the general wave-per-row body
+        attn_row<D>(a, t, t, Q, S, K, V, 4 * D, a.bt.in_ptr, a.bt.in_src, 0, lane, dr, st_attn, w1, w2, w3, s_out[rl]);
+        return;
       }
+      const int ne = e1 - e0;
+      const int my_src = lane < ne ? a.bt.in_src[e0 + lane] : 0;
+      float q[VPL], sv[VPL], ag[VPL];
+      load_vec<VPL>(q, Q + (size_t)t * (4 * D) + d0, act);
+      load_vec<VPL>(sv, S + (size_t)t * (4 * D) + d0, act);
+      // logits <Q[t], K[src]> / sqrt(C) per head, four K rows in flight
+      float m = -INFINITY;
+      for (int j = 0; j < ne; j += 4) {
+        float kv[4][VPL];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 4; ++u) {
+          const int src = __shfl(my_src, (j + u) & 63);
+          load_vec<VPL>(kv[u], K + (size_t)src * (4 * D) + d0, act && j + u < ne);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          float dt = 0.0f;
+#pragma unroll
+          for (int v = 0; v < VPL; ++v) dt += q[v] * kv[u][v];
+          const float l = group_sum(dt, GL) / a.sqrt_c;
+          if (j + u < ne) {
+            m = fmaxf(m, l);
+            if (leader) s_lg[wave][j + u][head] = l;
+          }
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      float z = 0.0f;
+      for (int e = 0; e < ne; ++e) z += expf(s_lg[wave][e][head] - m);
+      const float zd = z + 1e-16f;
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) ag[v] = 0.0f;
+      // alpha = softmax, attention dropout, aggregate V rows (four in flight)
+      for (int j = 0; j < ne; j += 4) {
+        float vv[4][VPL];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int src = __shfl(my_src, (j + u) & 63);
+          load_vec<VPL>(vv[u], V + (size_t)src * (4 * D) + d0, act && j + u < ne);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (j + u < ne) {
+            const int eg = e0 + j + u;
+            const float al = expf(s_lg[wave][j + u][head] - m) / zd;
+            if (leader) a.alpha[(size_t)eg * H + head] = al;
+            const float ad = al * dr.mul(st_attn, (uint32_t)(eg * H + head));
+#pragma unroll
+            for (int v = 0; v < VPL; ++v) ag[v] += ad * vv[u][v];
+          }
+        }
+      }
+      float uu = 0.0f;
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) uu += w1[v] * ag[v] + w2[v] * sv[v] + w3[v] * (ag[v] - sv[v]);
+      uu = wave_sum(uu);
+      const float beta = 1.0f / (1.0f + expf(-uu));
+      float o[VPL];
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) o[v] = beta * sv[v] + (1.0f - beta) * ag[v];
+      store_vec<VPL>(a.agg + (size_t)t * D + d0, ag, act);
+      store_vec<VPL>(a.out + (size_t)t * D + d0, o, act);
+      store_vec<VPL>(s_out[rl] + d0, o, act);
+      if (lane == 0) a.gate[t] = beta;
+      __builtin_amdgcn_wave_barrier();  // s_lg is reused by the wave's next row
+  };
+  // The wave's two rows together: their in-edges are contiguous (CSR by destination), so
+  // ONE id load covers both rows, and every K row is requested together with its V row
+  // (the first AR_VR edges' V rows stay in registers for the aggregation) -- three
+  // dependent memory rounds per wave instead of four per row.  Per row the arithmetic is
+  // the single-row body's, operation for operation (same edge order for the maximum, the
+  // denominator and the weighted sum): bitwise the same outputs.
+  const int t0 = r0 + wave * AR_RPW;
+  if (t0 < N) {  // wave-uniform
+    const bool two = t0 + 1 < N;
+    const int e0 = a.bt.in_ptr[t0], em = a.bt.in_ptr[t0 + 1];
+    const int e2 = two ? a.bt.in_ptr[t0 + 2] : em;
+    const int ne0 = em - e0, ne = e2 - e0;
+    static_assert(AR_RPW == 2, "the paired body covers two rows per wave");
+    if (ne > AR_ECH || H > AR_HMAX) {
+      one_row(0);
+      one_row(1);
+    } else {
+      const int my_src = lane < ne ? a.bt.in_src[e0 + lane] : 0;
+      float q0[VPL], s0[VPL], q1[VPL], s1[VPL], ag0[VPL], ag1[VPL];
+      load_vec<VPL>(q0, Q + (size_t)t0 * (4 * D) + d0, act);
+      load_vec<VPL>(s0, S + (size_t)t0 * (4 * D) + d0, act);
+      load_vec<VPL>(q1, Q + (size_t)(t0 + 1) * (4 * D) + d0, act && two);
+      load_vec<VPL>(s1, S + (size_t)(t0 + 1) * (4 * D) + d0, act && two);
+      float m0 = -INFINITY, m1 = -INFINITY;
+      float vh[AR_VR][VPL];
+      auto logit = [&](int e, const float (&kr)[VPL]) {
+        const bool r1 = e >= ne0;  // wave-uniform
         float dt = 0.0f;
 #pragma unroll
-        for (int v = 0; v < VPL; ++v) dt += q[v] * kv[u][v];
+        for (int v = 0; v < VPL; ++v) dt += (r1 ? q1[v] : q0[v]) * kr[v];
         const float l = group_sum(dt, GL) / a.sqrt_c;
-        if (j + u < ne) {
-          m = fmaxf(m, l);
-          if (leader) s_lg[wave][j + u][head] = l;
+        if (e < ne) {
+          if (r1) m1 = fmaxf(m1, l);
+          else m0 = fmaxf(m0, l);
+          if (leader) s_lg[wave][e][head] = l;
+        }
+      };
+#pragma unroll
+      for (int jj = 0; jj < AR_VR; jj += 4) {
+        if (jj < ne) {  // wave-uniform
+          float kv[4][VPL];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int src = __shfl(my_src, (jj + u) & 63);
+            const bool ok = act && jj + u < ne;
+            load_vec<VPL>(kv[u], K + (size_t)src * (4 * D) + d0, ok);
+            load_vec<VPL>(vh[jj + u], V + (size_t)src * (4 * D) + d0, ok);
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) logit(jj + u, kv[u]);
         }
       }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    float z = 0.0f;
-    for (int e = 0; e < ne; ++e) z += expf(s_lg[wave][e][head] - m);
-    const float zd = z + 1e-16f;
+      for (int j = AR_VR; j < ne; j += 4) {
+        float kv[4][VPL];
 #pragma unroll
-    for (int v = 0; v < VPL; ++v) ag[v] = 0.0f;
-    // alpha = softmax, attention dropout, aggregate V rows (four in flight)
-    for (int j = 0; j < ne; j += 4) {
-      float vv[4][VPL];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int src = __shfl(my_src, (j + u) & 63);
-        load_vec<VPL>(vv[u], V + (size_t)src * (4 * D) + d0, act && j + u < ne);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (j + u < ne) {
-          const int eg = e0 + j + u;
-          const float al = expf(s_lg[wave][j + u][head] - m) / zd;
-          if (leader) a.alpha[(size_t)eg * H + head] = al;
-          const float ad = al * dr.mul(st_attn, (uint32_t)(eg * H + head));
-#pragma unroll
-          for (int v = 0; v < VPL; ++v) ag[v] += ad * vv[u][v];
+        for (int u = 0; u < 4; ++u) {
+          const int src = __shfl(my_src, (j + u) & 63);
+          load_vec<VPL>(kv[u], K + (size_t)src * (4 * D) + d0, act && j + u < ne);
         }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) logit(j + u, kv[u]);
       }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      float z0 = 0.0f, z1 = 0.0f;
+      for (int e = 0; e < ne0; ++e) z0 += expf(s_lg[wave][e][head] - m0);
+      for (int e = ne0; e < ne; ++e) z1 += expf(s_lg[wave][e][head] - m1);
+      const float zd0 = z0 + 1e-16f, zd1 = z1 + 1e-16f;
+#pragma unroll
+      for (int v = 0; v < VPL; ++v) { ag0[v] = 0.0f; ag1[v] = 0.0f; }
+      auto accum = [&](int e, const float (&vr)[VPL]) {
+        const bool r1 = e >= ne0;  // wave-uniform
+        const int eg = e0 + e;
+        const float al = expf(s_lg[wave][e][head] - (r1 ? m1 : m0)) / (r1 ? zd1 : zd0);
+        if (leader) a.alpha[(size_t)eg * H + head] = al;
+        const float ad = al * dr.mul(st_attn, (uint32_t)(eg * H + head));
+        if (r1) {
+#pragma unroll
+          for (int v = 0; v < VPL; ++v) ag1[v] = __builtin_fmaf(ad, vr[v], ag1[v]);  // the contracted `ag += ad * v`
+        } else {
+#pragma unroll
+          for (int v = 0; v < VPL; ++v) ag0[v] = __builtin_fmaf(ad, vr[v], ag0[v]);
+        }
+      };
+#pragma unroll
+      for (int e = 0; e < AR_VR; ++e)
+        if (e < ne) accum(e, vh[e]);
+      for (int j = AR_VR; j < ne; j += 4) {
+        float vv[4][VPL];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int src = __shfl(my_src, (j + u) & 63);
+          load_vec<VPL>(vv[u], V + (size_t)src * (4 * D) + d0, act && j + u < ne);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (j + u < ne) accum(j + u, vv[u]);
+      }
+      auto finish = [&](int t, int rl, const float (&ag)[VPL], const float (&sv)[VPL]) {
+        float uu = 0.0f;
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) uu += w1[v] * ag[v] + w2[v] * sv[v] + w3[v] * (ag[v] - sv[v]);
+        uu = wave_sum(uu);
+        const float beta = 1.0f / (1.0f + expf(-uu));
+        float o[VPL];
+#pragma unroll
+        for (int v = 0; v < VPL; ++v) o[v] = beta * sv[v] + (1.0f - beta) * ag[v];
+        store_vec<VPL>(a.agg + (size_t)t * D + d0, ag, act);
+        store_vec<VPL>(a.out + (size_t)t * D + d0, o, act);
+        store_vec<VPL>(s_out[rl] + d0, o, act);
+        if (lane == 0) a.gate[t] = beta;
+      };
+      finish(t0, wave * AR_RPW, ag0, s0);
+      if (two) finish(t0 + 1, wave * AR_RPW + 1, ag1, s1);
     }
-    float uu = 0.0f;
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) uu += w1[v] * ag[v] + w2[v] * sv[v] + w3[v] * (ag[v] - sv[v]);
-    uu = wave_sum(uu);
-    const float beta = 1.0f / (1.0f + expf(-uu));
-    float o[VPL];
-#pragma unroll
-    for (int v = 0; v < VPL; ++v) o[v] = beta * sv[v] + (1.0f - beta) * ag[v];
-    store_vec<VPL>(a.agg + (size_t)t * D + d0, ag, act);
-    store_vec<VPL>(a.out + (size_t)t * D + d0, o, act);
-    store_vec<VPL>(s_out[rl] + d0, o, act);
-    if (lane == 0) a.gate[t] = beta;
-    __builtin_amdgcn_wave_barrier();  // s_lg is reused by the wave's next row
   }
   if (!a.train) return;
   // ---- this workgroup's BatchNorm partial (count, mean, M2) over its rows

@@ -85,12 +85,12 @@ struct ProjIn {
   float4 pe[4];
 };
 
-template <int D>
-__global__ __launch_bounds__(GM_BLOCK) void k_proj(ProjK a) {
+template <int D, bool FIRST>
+__global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 64 ? 4 : 2))) void k_proj(ProjK a) {
   using G = ProjGeom<D>;
   constexpr int CT = G::CT, RT = G::RT, BM = G::BM, XS = G::XS, C4 = G::C4, KPE = G::KPE;
   __shared__ __attribute__((aligned(16))) float Xs[2][BM * XS];
-  __shared__ __attribute__((aligned(16))) float s_pw[D * KPE];  // W_pe [D][KPE] (layer 0)
+  __shared__ __attribute__((aligned(16))) float s_pw[KPE * D];  // W_pe^T [KPE][D] (layer 0)
   __shared__ __attribute__((aligned(16))) float s_c[4 * D];     // bpe | mean | rstd | gamma | beta
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
   const int N = a.bt.hdr[0];
@@ -108,11 +108,13 @@ __global__ __launch_bounds__(GM_BLOCK) void k_proj(ProjK a) {
     for (int kb = 0; kb < D / 16; ++kb) wf[c][kb] = *reinterpret_cast<const float4*>(wrow + kb * 16 + lg * 4);
     bias[c] = a.b_all[ct * 16 + lr];
   }
-  const bool pe_lds = a.first && a.pe_k > 0 && a.pe_k <= KPE;
-  if (a.first) {
+  const bool pe_lds = FIRST && a.pe_k > 0 && a.pe_k <= KPE;
+  if (FIRST) {
+    // transposed (k-major): a thread's four output columns of one k are one float4, and a
+    // wave's reads of one k are consecutive (no LDS bank conflicts)
     if (pe_lds)
       for (int idx = tid; idx < D * KPE; idx += GM_BLOCK) {
-        const int j = idx / KPE, k = idx - j * KPE;
+        const int k = idx / D, j = idx - k * D;
         s_pw[idx] = k < a.pe_k ? a.wpe[j * a.pe_k + k] : 0.0f;
       }
     if (a.pe_k > 0)
@@ -148,7 +150,7 @@ __global__ __launch_bounds__(GM_BLOCK) void k_proj(ProjK a) {
   const uint32_t st_prev = drop_stream(1, (uint32_t)(a.layer - 1), ctr);
   const int xi = tid / C4, xj = (tid - (tid / C4) * C4) * 4;  // this thread's row / column of X
   float4 pg = make_float4(0.f, 0.f, 0.f, 0.f), pb = pg, mu = pg, rs = pg;
-  if (!a.first) {
+  if (!FIRST) {
     mu = *reinterpret_cast<const float4*>(s_c + D + xj);
     rs = *reinterpret_cast<const float4*>(s_c + 2 * D + xj);
     pg = *reinterpret_cast<const float4*>(s_c + 3 * D + xj);
@@ -157,7 +159,7 @@ __global__ __launch_bounds__(GM_BLOCK) void k_proj(ProjK a) {
 
   auto item_of = [&](int t) -> int {
     const int r = t * BM + xi;
-    return (a.first && t < ntile && r < N) ? a.bt.node_item[r] : 0;
+    return (FIRST && t < ntile && r < N) ? a.bt.node_item[r] : 0;
   };
   auto fetch = [&](int t, int item, ProjIn& in) {
     const int r = t * BM + xi;
@@ -168,7 +170,7 @@ __global__ __launch_bounds__(GM_BLOCK) void k_proj(ProjK a) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) in.pe[q] = z;
     if (!live) return;
-    if (a.first) {
+    if (FIRST) {
       in.u = *reinterpret_cast<const float4*>(a.table + (size_t)item * D + xj);
       if (pe_lds && (a.pe_k & 3) == 0) {
         const float* pr = a.bt.node_pe ? a.bt.node_pe + (size_t)r * a.pe_k : a.pe_tab + (size_t)item * a.pe_k;
@@ -189,7 +191,7 @@ __global__ __launch_bounds__(GM_BLOCK) void k_proj(ProjK a) {
     float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
     if (r < N) {
       const size_t o = (size_t)r * D + xj;
-      if (a.first) {
+      if (FIRST) {
         val = in.u;
         if (a.pe_k > 0) {
           float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -198,15 +200,7 @@ __global__ __launch_bounds__(GM_BLOCK) void k_proj(ProjK a) {
             for (int kq = 0; kq < 4; ++kq) {  // k = 0, 4, .. < pe_k: the fused loop's order
               if (4 * kq >= a.pe_k) break;
               const int k = 4 * kq;
-              const float4 p4 = in.pe[kq];
-#pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                const float4 w4 = *reinterpret_cast<const float4*>(s_pw + (xj + q) * KPE + k);
-                acc[q] += p4.x * w4.x;
-                acc[q] += p4.y * w4.y;
-                acc[q] += p4.z * w4.z;
-                acc[q] += p4.w * w4.w;
-              }
+              pe_fma4(acc, in.pe[kq], s_pw + k * D + xj, D);
             }
           } else {
             const float* pr = a.bt.node_pe ? a.bt.node_pe + (size_t)r * a.pe_k : a.pe_tab + (size_t)item * a.pe_k;
@@ -233,21 +227,24 @@ __global__ __launch_bounds__(GM_BLOCK) void k_proj(ProjK a) {
     *reinterpret_cast<float4*>(X + xi * XS + xj) = val;
   };
 
+  // two tiles in flight behind the one being multiplied (its rows were requested two
+  // tiles earlier, its item ids three): one workgroup per CU needs the depth to cover the
+  // gather latency
+  const int GS = gridDim.x;
   int t = blockIdx.x;
-  int it = item_of(t);
-  ProjIn cur;
+  int it = item_of(t), it_next = item_of(t + GS);
+  ProjIn cur, nxt;
   fetch(t, it, cur);
-  int it_next = item_of(t + gridDim.x);
+  fetch(t + GS, it_next, nxt);
+  int it_nn = item_of(t + 2 * GS);
   int buf = 0;
-  for (; t < ntile; t += gridDim.x) {
+  for (; t < ntile; t += GS) {
     float* X = Xs[buf];
     produce(t, it, cur, X);
     __syncthreads();
-    // the next tile's rows (its ids were requested one tile earlier) and the ids after it
-    const int t2 = t + gridDim.x;
-    ProjIn nxt;
-    fetch(t2, it_next, nxt);  // past the last tile: zeros, nothing loaded
-    const int it2 = item_of(t2 + gridDim.x);
+    ProjIn nn;
+    fetch(t + 2 * GS, it_nn, nn);  // past the last tile: zeros, nothing loaded
+    const int it3 = item_of(t + 3 * GS);
     // ---- QKVS = X . W_all^T (f32 MFMA, k order of the fused kernel)
     f32x4 acc[RT][CT];
 #pragma unroll
@@ -276,8 +273,10 @@ __global__ __launch_bounds__(GM_BLOCK) void k_proj(ProjK a) {
         }
       }
     cur = nxt;
+    nxt = nn;
     it = it_next;
-    it_next = it2;
+    it_next = it_nn;
+    it_nn = it3;
     buf ^= 1;
   }
 }
@@ -355,8 +354,9 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
     }
   };
   int t = blockIdx.x;
-  float4 cur[PER];
+  float4 cur[PER], nxt[PER];
   fetch(t, cur);
+  fetch(t + gridDim.x, nxt);  // two tiles in flight behind the one being multiplied
   int buf = 0;
   for (; t < ntile; t += gridDim.x) {
     float* A = As[buf];
@@ -367,7 +367,9 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
       *reinterpret_cast<float4*>(A + i * AS + c) = cur[u];
     }
     __syncthreads();
-    fetch(t + gridDim.x, cur);  // the next tile's rows, in flight during the MFMAs
+#pragma unroll
+    for (int u = 0; u < PER; ++u) cur[u] = nxt[u];
+    fetch(t + 2 * gridDim.x, nxt);  // in flight during the MFMAs
     f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
     const float* arow = A + (rs * 16 + lr) * AS + lg * 4;
 #pragma unroll
@@ -498,8 +500,13 @@ extern "C" int gtr_qkvs_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   const int bm = D == 64 ? ProjGeom<64>::BM : ProjGeom<128>::BM;
   const int grid = gemm_grid((bt->n_cap + bm - 1) / bm, D == 64 ? 2 : 1);
   hipStream_t s = (hipStream_t)stream;
-  if (D == 64) hipLaunchKernelGGL(k_proj<64>, dim3(grid), dim3(GM_BLOCK), 0, s, k);
-  else hipLaunchKernelGGL(k_proj<128>, dim3(grid), dim3(GM_BLOCK), 0, s, k);
+  if (D == 64) {
+    if (l == 0) hipLaunchKernelGGL((k_proj<64, true>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
+    else hipLaunchKernelGGL((k_proj<64, false>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
+  } else {
+    if (l == 0) hipLaunchKernelGGL((k_proj<128, true>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
+    else hipLaunchKernelGGL((k_proj<128, false>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
+  }
   GTR_HIP_CHECK_LAUNCH();
   return GTR_OK;
 }

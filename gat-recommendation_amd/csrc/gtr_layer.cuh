@@ -94,6 +94,25 @@ __device__ __forceinline__ f32x4 mfma4(const float4 a, const float4 b, f32x4 acc
   return acc;
 }
 
+// LapPE projection of four pe values k..k+3 into a thread's four output columns j..j+3:
+// w points at W_pe^T[k][j] in LDS (k-major, row stride `ld`).  Explicit fmas in k order, so
+// every kernel that projects the PE rows (k_conv_fwd, k_proj) rounds identically.
+__device__ __forceinline__ void pe_fma4(float (&acc)[4], const float4 p4, const float* w, int ld) {
+  const float4 w0 = *reinterpret_cast<const float4*>(w);
+  const float4 w1 = *reinterpret_cast<const float4*>(w + ld);
+  const float4 w2 = *reinterpret_cast<const float4*>(w + 2 * ld);
+  const float4 w3 = *reinterpret_cast<const float4*>(w + 3 * ld);
+  const float wq[4][4] = {{w0.x, w1.x, w2.x, w3.x}, {w0.y, w1.y, w2.y, w3.y},
+                          {w0.z, w1.z, w2.z, w3.z}, {w0.w, w1.w, w2.w, w3.w}};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    acc[q] = __builtin_fmaf(p4.x, wq[q][0], acc[q]);
+    acc[q] = __builtin_fmaf(p4.y, wq[q][1], acc[q]);
+    acc[q] = __builtin_fmaf(p4.z, wq[q][2], acc[q]);
+    acc[q] = __builtin_fmaf(p4.w, wq[q][3], acc[q]);
+  }
+}
+
 template <int VPL>
 __device__ __forceinline__ void load_vec(float (&x)[VPL], const float* p, bool act) {
   if constexpr (VPL == 4) {

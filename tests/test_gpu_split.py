@@ -52,6 +52,7 @@ def test_split_forward_bitwise_equals_fused(D, H, K, loss, B, monkeypatch):
     m1, _ = make_pair(T, D, H, K=K, seed=61)
     m2 = copy.deepcopy(m1)
     m1.train(); m2.train()
+    p0 = {k: v.detach().clone() for k, v in m1.named_parameters()}
     n = 100 if loss != "bpr" else 5
     sb = batches(data, B, n, 1, seed=62)[0]
     f1 = _step(m1, loss, False, monkeypatch)
@@ -70,12 +71,18 @@ def test_split_forward_bitwise_equals_fused(D, H, K, loss, B, monkeypatch):
     assert torch.equal(*top)  # its BatchNorm sums come from the readout in both paths
     assert_close(f2.ws.layers[0]["dqkvs"][:N], f1.ws.layers[0]["dqkvs"][:N], rtol=1e-4, name="dqkvs layer 0")
     assert_close(f2.ws.dx0[:N], f1.ws.dx0[:N], rtol=1e-4, name="dx0")
-    # one AdamW step (lr 1e-2) on gradients that differ by rounding only: Adam moves an
-    # element whose gradient nearly cancels by a visible fraction of lr, so 1e-3 here
+    # one AdamW step (lr 1e-2) on gradients that differ by rounding only.  A first Adam
+    # step moves an element by lr * g / (|g| + eps): by lr exactly unless |g| is near eps,
+    # i.e. a gradient that cancels to rounding noise, whose update then depends on that
+    # noise -- such elements (fused update visibly shorter than lr) are bounded by 2 lr,
+    # every other element is held to 1e-3
     for (n1, p1), (n2, p2) in zip(m1.named_parameters(), m2.named_parameters()):
         if n1.endswith("lin_key.bias"):
             continue
-        assert_close(p2, p1, rtol=1e-3, name=n1)
+        step = (p1.detach() - p0[n1] * (1.0 - 1e-2 * 1e-2)).abs()
+        noise = step < 0.99e-2
+        assert float((p2.detach() - p1.detach())[noise].abs().max()) <= 2e-2 + 1e-7 if bool(noise.any()) else True
+        assert_close(p2.detach()[~noise], p1.detach()[~noise], rtol=1e-3, name=n1)
 
 
 @pytest.mark.parametrize("D,H,K,loss,B", CASES[:2])
