@@ -342,7 +342,8 @@ template <int D>
 __global__ __launch_bounds__(BR_BLOCK) void k_attn_rows_bwd_src(ConvBwdK a) {
   constexpr int VPL = LayerGeom<D>::VPL;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int Nl = a.bt.hdr[0];
+  // source rows: the batch rows, plus the ghost rows of a halo batch (hdr[6], gtr.h)
+  const int Nl = max(a.bt.hdr[0], a.bt.hdr[6]);
   const uint32_t ctr = a.rng_ctr ? load_step_ctr(a.rng_ctr) + a.ctr_add : 0u;
   const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
   const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);

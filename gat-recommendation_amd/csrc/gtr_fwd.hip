@@ -1094,6 +1094,7 @@ struct ReadoutK {
   const float* part_all;
   uint32_t ctr_add;
   int xpack;            // XCD-packed roles (role_block)
+  float loss_b;         // > 0: the loss means' session count (gtr_config.loss_batch)
 };
 
 // Block per session (grid-strided): RO_WAVES waves split the session's node rows and
@@ -1129,8 +1130,9 @@ __device__ __forceinline__ void readout_body(const ReadoutK& a, int rb) {
   const bool use_bpr = a.loss_kind == GTR_LOSS_BPR || a.loss_kind == GTR_LOSS_DUAL;
   const float w_lw = a.loss_kind == GTR_LOSS_DUAL ? a.dual_alpha : 1.0f;
   const float w_bpr = a.loss_kind == GTR_LOSS_DUAL ? 1.0f - a.dual_alpha : 1.0f;
-  const float inv_bn = 1.0f / ((float)B * (float)n);  // BPR mean over B*n
-  const float inv_b = 1.0f / (float)B;                // listwise mean over B
+  const float Bm = a.loss_b > 0.0f ? a.loss_b : (float)B;  // gtr_config.loss_batch
+  const float inv_bn = 1.0f / (Bm * (float)n);  // BPR mean over B*n
+  const float inv_b = 1.0f / Bm;                // listwise mean over B
   const float inv_t = 1.0f / a.temperature;
   const int nchunk = do_loss ? (n + CHN - 1) / CHN : 0;
 
@@ -1578,8 +1580,9 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
   const bool use_bpr = a.loss_kind == GTR_LOSS_BPR || a.loss_kind == GTR_LOSS_DUAL;
   const float w_lw = a.loss_kind == GTR_LOSS_DUAL ? a.dual_alpha : 1.0f;
   const float w_bpr = a.loss_kind == GTR_LOSS_DUAL ? 1.0f - a.dual_alpha : 1.0f;
-  const float inv_bn = 1.0f / ((float)B * (float)n);
-  const float inv_b = 1.0f / (float)B;
+  const float Bm = a.loss_b > 0.0f ? a.loss_b : (float)B;  // gtr_config.loss_batch
+  const float inv_bn = 1.0f / (Bm * (float)n);
+  const float inv_b = 1.0f / Bm;
   const float inv_t = 1.0f / a.temperature;
 
   if (do_fwd) {
@@ -1893,6 +1896,7 @@ int make_readout_args(const gtr_config* cfg, const gtr_batch* bt, const float* t
   k.sync = cfg->sync_bn;
   k.part_all = L.bn_part_all;
   k.nparts = L.nparts_fwd;
+  k.loss_b = cfg->loss_batch;
   if (cfg->sync_bn && ((head->flags & GTR_RO_FWD) && cfg->training) && (!L.bn_part_all || L.nparts_fwd <= 0 || !cfg->consumer_reduce)) {
     set_error("gtr_readout_loss: sync_bn needs consumer_reduce and the gathered partials of the last layer");
     return GTR_E_ARG;

@@ -37,7 +37,7 @@ class GtrConfig(C.Structure):
         ("num_items", i32), ("dim", i32), ("heads", i32), ("pe_k", i32), ("num_layers", i32),
         ("row_group", i32), ("training", i32), ("dropout", f32), ("bn_eps", f32),
         ("bn_momentum", f32), ("seed", u32), ("rng_ctr", P), ("consumer_reduce", i32), ("sync_bn", i32),
-        ("sweep", P), ("begin", P), ("ctr_add", i32), ("split_sync", i32),
+        ("sweep", P), ("begin", P), ("ctr_add", i32), ("split_sync", i32), ("loss_batch", f32),
     ]
 
 
@@ -92,7 +92,7 @@ class GtrTail(C.Structure):
 
 
 SWEEP_SLOTS = 8
-ABI_VERSION = 4  # GTR_ABI_VERSION of include/gtr.h
+ABI_VERSION = 5  # GTR_ABI_VERSION of include/gtr.h
 
 
 class GtrLazy(C.Structure):

@@ -165,7 +165,7 @@ def split_default(D: int, g_cap: int) -> bool:
 class Workspace:
     """Capacity-sized activations + gradient buffers for one in-flight batch."""
 
-    def __init__(self, eng: "Engine", caps: Caps, R: int, P: int):
+    def __init__(self, eng: "Engine", caps: Caps, R: int, P: int, split: bool | None = None):
         dev = eng.device
         D, H, Lc = eng.D, eng.H, eng.L
         self.caps, self.R, self.P = caps, R, P
@@ -193,7 +193,7 @@ class Workspace:
         # large batches: each layer as GEMM + attention launches (gtr_qkvs_* / gtr_attn_*)
         # instead of one fused launch -- from more row groups than the chip has CUs / 2
         # (the fused kernels re-fetch W_all per 16-row group), D in {64, 128}
-        self.split = split_default(D, g)
+        self.split = split_default(D, g) if split is None else (bool(split) and D in (64, 128))
         self.dx0 = _f32(n, D, device=dev)
         self.se = _f32(b, D, device=dev)
         self.dse_in = _f32(b, D, device=dev)
@@ -274,13 +274,16 @@ class Engine:
         rows = rows if rows > 0 else 32
         return max(1, min(64, (caps.n_cap + rows - 1) // rows))
 
-    def workspace(self, caps: Caps, fresh: bool = False) -> Workspace:
+    def workspace(self, caps: Caps, fresh: bool = False, split: bool | None = None) -> Workspace:
+        """Workspace of these capacities; ``split`` forces the split (GEMM + attention) layer
+        path on or off (None: split_default)."""
         if fresh:
-            return Workspace(self, caps, self.choose_R(caps), self.choose_P(caps))
-        ws = self._ws_cache.pop(caps, None)
+            return Workspace(self, caps, self.choose_R(caps), self.choose_P(caps), split)
+        key = caps if split is None else (caps, bool(split))
+        ws = self._ws_cache.pop(key, None)
         if ws is None:
-            ws = Workspace(self, caps, self.choose_R(caps), self.choose_P(caps))
-        self._ws_cache[caps] = ws  # most recently used last
+            ws = Workspace(self, caps, self.choose_R(caps), self.choose_P(caps), split)
+        self._ws_cache[key] = ws  # most recently used last
         while len(self._ws_cache) > 8:
             self._ws_cache.pop(next(iter(self._ws_cache)))
         return ws

@@ -101,6 +101,8 @@ class FusedTrainStep:
 
             self.shard_state = ShardState(self, process_group)
             model.__dict__["_lazy_sync"] = self._shard_guard
+        self._force_split = None  # the halo step (etpgt.train.halo) runs the split layer path
+        self._loss_batch = 0.0    # gtr_config.loss_batch (halo cuts: global B / P)
         self.caps = None
         self.graph = None
         self.builder = None
@@ -157,7 +159,7 @@ class FusedTrainStep:
         eng = self.eng
         caps = self._agree(caps)
         self.caps = caps
-        self.ws = eng.workspace(caps)
+        self.ws = eng.workspace(caps, split=self._force_split)
         from etpgt.data.batch import blob_layout
 
         self.blob = torch.zeros(blob_layout(caps)["_total"], dtype=torch.int32, device=self.dev)
@@ -177,6 +179,7 @@ class FusedTrainStep:
         self.sort_tmp = torch.zeros(max(int(nb.value), 16), dtype=torch.uint8, device=self.dev)
         self.segs, self.nseg = eng.segments(self.ws)
         self.cfg = eng.config(self.ws, True)
+        self.cfg.loss_batch = float(self._loss_batch)
         # large batches: every layer as projection GEMM + attention launches (Engine.layer_fwd /
         # layer_bwd); under SyncBN one merged BatchNorm row per rank and layer is gathered
         # (gtr_config.split_sync) instead of every row group's partials

@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GTR_ABI_VERSION 4 /* 4: gtr_step_tail_wgrad on split-K slabs; 3: gtr_config.begin / ctr_add, gtr_tail.rng_inc */
+#define GTR_ABI_VERSION 5 /* 5: gtr_config.loss_batch, hdr[6] halo source rows; 4: gtr_step_tail_wgrad on split-K slabs; 3: gtr_config.begin / ctr_add, gtr_tail.rng_inc */
 
 #define GTR_OK 0
 #define GTR_E_ARG 1001      /* bad argument / unsupported shape */
@@ -67,7 +67,11 @@ typedef void* gtr_stream_t; /* hipStream_t */
 
 /* Batch in HBM: fixed-capacity arrays, live sizes in hdr[] on device.
  * hdr[0] = N (nodes), hdr[1] = B (sessions), hdr[2] = E (edges),
- * hdr[4] = G (row groups), hdr[5] = R (row-group width, == gtr_config.row_group).
+ * hdr[4] = G (row groups), hdr[5] = R (row-group width, == gtr_config.row_group),
+ * hdr[6] = source rows of a halo batch (0: N; etpgt.train.halo): rows [N, hdr[6]) are
+ * ghost copies of other ranks' nodes -- sources of local edges (their K / V rows arrive
+ * by the halo exchange, gtr_attn_bwd writes their dK / dV for the owner) and the tail of
+ * a session that straddles the cut (read by the readout).
  * Row group g owns every session whose first node lies in [g*R, (g+1)*R):
  * rows [grp_row[g], grp_row[g+1]) and dst-ordered edges [grp_edge[g], grp_edge[g+1]).  */
 typedef struct gtr_batch {
@@ -135,6 +139,10 @@ typedef struct gtr_config {
                               bn_part_all is [P][1 + 2D] and bn_gpart_all [P][2D]
                               (nparts_fwd = nparts_bwd = P), and the consumers
                               (gtr_qkvs_fwd, the readout, gtr_attn_bwd) fold P rows     */
+  float loss_batch;        /* > 0: the loss means divide by this many sessions instead of
+                              the batch's own B (a halo cut gives ranks unequal session
+                              counts: loss_batch = global B / P makes the rank average of
+                              the gradients the global batch's mean)                      */
 } gtr_config;
 
 
