@@ -42,6 +42,9 @@ struct ConvBwdK {
   const float* part_all;
   uint32_t ctr_add;
   int xpack;            // XCD-packed roles (role_block)
+  float* wslab;         // gtr_layer.wfold: this layer's per-row-group weight-gradient partials
+  int64_t wstride;      //   (null: the weight gradients run in gtr_wgrad)
+  const float* xin;     //   the layer input rows (dW_all = dQKVS^T . X)
 };
 
 // Destination-row backward: BatchNorm backward, beta gate, softmax backward, dQ, dS.
@@ -236,6 +239,35 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
       for (int q = 0; q < GPR; ++q) gpr[q] = q < np ? gp[(size_t)q * 2 * D + tid] : 0.0f;
     }
   }
+  // ---- phase W operands (folded weight gradients), requested now so that their latency
+  //      hides behind the attention phases: the group's first 8 X rows (MFMA B operands of
+  //      k-steps 0 and 1) and this thread's gate-slice rows of agg and S
+  //      (compiled for D <= 64 only: at D = 128 the extra registers spill).  Issued once
+  //      the staging loads have been consumed (vector loads retire in order), so they wait
+  //      behind nothing and arrive during the attention phases.
+  constexpr bool WF = DX && D <= 64;
+  constexpr int WTK = WF ? D / 16 : 1;                              // dW_all k-tiles (X columns)
+  constexpr int NGT = 3 * D / 16;                                   // gate-weight column tiles
+  constexpr int GPW = WF ? (NGT + CONV_WAVES - 1) / CONV_WAVES : 1; // per wave (waves 0 .. NGT/GPW-1)
+  float wx[2][WTK], wga[2][GPW], wgs[2][GPW];
+  float* s_du = sm + G::B_DU;
+  auto wprefetch = [&]() {
+    if (!(WF && a.wslab)) return;
+    const int wlr = lane & 15, wlg = lane >> 4;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int rr = ks * 4 + wlg;
+#pragma unroll
+      for (int t = 0; t < WTK; ++t) wx[ks][t] = rr < nrow ? a.xin[(size_t)(r0 + rr) * D + t * 16 + wlr] : 0.0f;
+#pragma unroll
+      for (int q = 0; q < GPW; ++q) {
+        const int gt = wave * GPW + q, c = (gt * 16 + wlr) % D;
+        const bool ok = rr < nrow && gt < NGT;
+        wga[ks][q] = ok ? a.agg[(size_t)(r0 + rr) * D + c] : 0.0f;
+        wgs[ks][q] = ok ? a.qkvs[(size_t)(r0 + rr) * (4 * D) + 3 * D + c] : 0.0f;
+      }
+    }
+  };
   auto reduce_gsum = [&]() {
     if (!a.cred) return;
     if constexpr (GPR > 0) {
@@ -361,6 +393,7 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
     reduce_gsum();
     __syncthreads();
     GTR_PH(a.layer, 1);
+    wprefetch();
 
     // ---- (D1) BatchNorm backward, beta gate: TPR lanes per destination row, CH features each
     const bool live = prow < nrow;
@@ -402,7 +435,10 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
     dbeta = group_sum_c<TPR>(dbeta);
     if (live) {
       const float du = dbeta * beta * (1.0f - beta);
-      if (pchunk == 0) a.du[t] = du;
+      if (pchunk == 0) {
+        a.du[t] = du;
+        if (WF) s_du[prow] = du;  // the folded gate-weight gradient (phase W)
+      }
 #pragma unroll
       for (int c = 0; c < CH; c += 4) {
         float dag[4], ds[4];
@@ -571,6 +607,7 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
   }
     __syncthreads();
     GTR_PH(a.layer, 1);
+    wprefetch();
     // ---- general path: wave per row against global memory (any group size / dim)
     const int d0 = lane * VPL;
     const bool act = d0 < D;
@@ -759,6 +796,115 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
     }
   }
 
+  // ---- phase W (gtr_config.wfold_stride): this group's split-K partial of the layer's
+  //      weight gradients -- the gtr_wgrad jobs of the layer over the group's rows, at the
+  //      gtr_wgrad slab offsets (w_all [4D][D] | b_all [4D] | w_beta [3D]); the optimizer
+  //      tail sums the live groups' partials (gtr_segment.live_groups) in group order.
+  //      dW_all = dQKVS^T . X on f32 MFMA 16x16x4 (A: a dQKVS row's 16 output units, B: an X
+  //      row's 16 input columns; 4 rows per step); wave w owns j-tiles [w*TJW, (w+1)*TJW) x
+  //      every k-tile, JB j-tiles (16 accumulator tiles) at a time.
+  GTR_PH(a.layer, 9);
+  if (WF && a.wslab) {
+    // Everything on f32 MFMA 16x16x4 over the group's rows (4 per step), each sum complete
+    // in one accumulator (no cross-wave reduction):
+    //   dW_all[j][k] = sum_r dQKVS[r][j] X[r][k]   A: a dQKVS row's 16 output units,
+    //                                              B: an X row's 16 input columns;
+    //   b_all[j]     = sum_r dQKVS[r][j]           one more B tile: a ones column;
+    //   w_beta[c]    = sum_r du[r] G[r][c]         A: du in unit 0, B: [agg | S | agg - S].
+    // Wave w owns dW j-tiles [w*TJW, (w+1)*TJW) x every k-tile (+ the ones tile), JB j-tiles
+    // at a time, and gate tiles [w*GPW, (w+1)*GPW).
+    constexpr int TJ = 4 * D / 16, TK = D / 16;
+    constexpr int TJW = TJ / CONV_WAVES > 0 ? TJ / CONV_WAVES : 1;
+    constexpr int JB = (16 / (TK + 1)) < 1 ? 1 : ((16 / (TK + 1)) < TJW ? 16 / (TK + 1) : TJW);
+    static_assert(TJ % CONV_WAVES == 0 && TJW % JB == 0, "phase W tiling");
+    float* slab = a.wslab + (size_t)g * a.wstride;
+    float* bias = slab + (size_t)4 * D * D;
+    float* gw = bias + 4 * D;
+    const float* Xb = a.xin + (size_t)r0 * D;
+    const int nks = (nrow + 3) / 4;
+    // Ab: the group's dQKVS rows (stride astr), dU its du values -- LDS on the fast path,
+    // global rows otherwise.  One body per memory kind (called in two branches, never
+    // through one pointer that could be either): a generic (flat) load would make its
+    // waits wait for every outstanding global store of the dX phase as well.
+    auto body = [&](const float* Ab, int astr, const float* dU, bool lds) {
+      auto arow = [&](int rr, int col) {  // LDS rows up to RMAX exist: no branch needed
+        if (lds) { const float t = Ab[(size_t)rr * astr + col]; return rr < nrow ? t : 0.0f; }
+        return rr < nrow ? Ab[(size_t)rr * astr + col] : 0.0f;
+      };
+      for (int jb = 0; jb < TJW; jb += JB) {
+        const int j0 = (wave * TJW + jb) * 16;
+        f32x4 acc[JB][TK + 1];
+#pragma unroll
+        for (int u = 0; u < JB; ++u)
+#pragma unroll
+          for (int t = 0; t <= TK; ++t) acc[u][t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int ks = 0; ks < nks; ++ks) {
+          const int rr = ks * 4 + lg;
+          const bool live = rr < nrow;
+          float bv[TK + 1], av[JB];
+          if (ks < 2) {  // prefetched after the staging
+#pragma unroll
+            for (int t = 0; t < TK; ++t) bv[t] = ks == 0 ? wx[0][t] : wx[1][t];
+          } else {
+#pragma unroll
+            for (int t = 0; t < TK; ++t) bv[t] = live ? Xb[(size_t)rr * D + t * 16 + lr] : 0.0f;
+          }
+          bv[TK] = (live && lr == 0) ? 1.0f : 0.0f;
+#pragma unroll
+          for (int u = 0; u < JB; ++u) av[u] = arow(rr, j0 + u * 16 + lr);
+#pragma unroll
+          for (int u = 0; u < JB; ++u)
+#pragma unroll
+            for (int t = 0; t <= TK; ++t)
+              acc[u][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[t], acc[u][t], 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < JB; ++u) {
+#pragma unroll
+          for (int t = 0; t < TK; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) slab[(size_t)(j0 + u * 16 + lg * 4 + i) * D + t * 16 + lr] = acc[u][t][i];
+          if (lr == 0) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) bias[j0 + u * 16 + lg * 4 + i] = acc[u][TK][i];
+          }
+        }
+      }
+      if (wave * GPW < NGT) {  // wave-uniform
+        f32x4 gacc[GPW];
+#pragma unroll
+        for (int q = 0; q < GPW; ++q) gacc[q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        for (int ks = 0; ks < nks; ++ks) {
+          const int rr = ks * 4 + lg;
+          const bool live = rr < nrow;
+          float du = 0.0f;
+          if (lr == 0 && live) du = dU[rr];
+#pragma unroll
+          for (int q = 0; q < GPW; ++q) {
+            const int gt = wave * GPW + q, c = gt * 16 + lr, sel = c / D, col = c % D;
+            float x, y;
+            if (ks < 2) {
+              x = ks == 0 ? wga[0][q] : wga[1][q];
+              y = ks == 0 ? wgs[0][q] : wgs[1][q];
+            } else {
+              const bool ok = live && gt < NGT;
+              x = ok ? a.agg[(size_t)(r0 + rr) * D + col] : 0.0f;
+              y = ok ? a.qkvs[(size_t)(r0 + rr) * (4 * D) + 3 * D + col] : 0.0f;
+            }
+            const float bvg = sel == 0 ? x : (sel == 1 ? y : x - y);
+            gacc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(du, bvg, gacc[q], 0, 0, 0);
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < GPW; ++q) {
+          const int gt = wave * GPW + q;
+          if (lg == 0 && gt < NGT) gw[gt * 16 + lr] = gacc[q][0];  // row 0 of the tile: unit du
+        }
+      }
+    };
+    if (fast && !SPLIT) body(sm + G::B_R, AS32, s_du, true);  // fp32 dQKVS rows and du in LDS
+    else body(a.dqkvs + (size_t)r0 * (4 * D), 4 * D, a.du + r0, false);
+  }
   GTR_PH(a.layer, 4);
   if (!a.has_prev) return;
   // ---- previous layer's BatchNorm backward partials: reduce the 4 row quads of each
@@ -847,6 +993,19 @@ inline int make_bwd_args(const gtr_config* cfg, const gtr_batch* bt, const gtr_l
   k.nparts_bwd = L.nparts_bwd;
   k.part_all = L.bn_part_all;
   k.nparts_fwd = L.nparts_fwd;
+  if (cfg->wfold_stride > 0 && L.wfold) {  // weight gradients folded into the row groups
+    if (D > 64) {
+      set_error("gtr_conv_bwd: folded weight gradients cover D <= 64 (gtr_wgrad otherwise)");
+      return GTR_E_ARG;
+    }
+    if ((reinterpret_cast<uintptr_t>(L.wfold) & 15) || cfg->wfold_stride < (int64_t)4 * D * D + 7 * D) {
+      set_error("gtr_conv_bwd: wfold slab misaligned or its stride below 4D^2 + 7D");
+      return GTR_E_ARG;
+    }
+    k.wslab = L.wfold;
+    k.wstride = cfg->wfold_stride;
+    k.xin = L.xin;
+  }
   if (cfg->sync_bn && (!cfg->consumer_reduce || !L.bn_gpart_all || !L.bn_part_all || L.nparts_bwd <= 0 ||
                        L.nparts_fwd <= 0)) {
     set_error("gtr_conv_bwd: sync_bn needs consumer_reduce and the gathered partials of layer %d", l);

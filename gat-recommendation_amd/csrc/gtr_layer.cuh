@@ -55,7 +55,8 @@ struct LayerGeom {
   static constexpr int B_ODST = B_OEDGE + EMAX;               // [EMAX] local dst row
   static constexpr int B_GS = B_ODST + EMAX;                  // [2D] reduced BN backward sums
   static constexpr int B_BNP = B_GS + 2 * D;                  // [CONV_WAVES][2D] dX-epilogue BN partials
-  static constexpr int B_FLAG = B_BNP + CONV_WAVES * 2 * D;
+  static constexpr int B_DU = B_BNP + CONV_WAVES * 2 * D;    // [RMAX] du of the group's rows (fast path)
+  static constexpr int B_FLAG = B_DU + RMAX;
   static constexpr int B_WORDS = B_FLAG + 4;
 };
 

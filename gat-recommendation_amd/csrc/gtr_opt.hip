@@ -56,7 +56,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_adamw_small(SmallK a) {
   if (a.grad_out == nullptr && threadIdx.x == 0) s_st.init(a.opt, *a.opt.step_dev + a.opt.step_offset);
   __syncthreads();
   const AdamStep st = s_st;
-  small_body(e, a.segs, a.nseg, a.param, a.m, a.v, a.grad_out, st);
+  small_body(e, a.segs, a.nseg, nullptr, a.param, a.m, a.v, a.grad_out, st);
 }
 
 __global__ __launch_bounds__(GTR_BLOCK) void k_contrib_prep(gtr_batch bt, int T, int32_t* keys, int32_t* vals,
@@ -571,8 +571,8 @@ __global__ __launch_bounds__(DEFER ? GTR_TAIL_BLOCK : GTR_BLOCK) void k_step_tai
   }
   if (blk < a.nb_rows + a.nb_small) {
     const int sb = blk - a.nb_rows;
-    small_body((int64_t)sb * GTR_BLOCK + tid, a.segs, a.nseg, a.tl.flat, a.tl.flat_m, a.tl.flat_v, nullptr, s_st,
-               wait);
+    small_body((int64_t)sb * GTR_BLOCK + tid, a.segs, a.nseg, a.bt.hdr, a.tl.flat, a.tl.flat_m, a.tl.flat_v, nullptr,
+               s_st, wait);
     if (sb == 0 && a.tl.loss_part) {  // loss of the step: the readout's partials, fixed order
       float acc = 0.0f;
       for (int q = tid; q < a.tl.loss_nparts; q += GTR_BLOCK)
@@ -839,7 +839,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_dp_pack(DpPackK a) {
   }
   const int sb = blk - a.nb_rows;
   const AdamStep unused{};
-  small_body((int64_t)sb * GTR_BLOCK + tid, a.segs, a.nseg, nullptr, nullptr, nullptr, a.pack, unused);
+  small_body((int64_t)sb * GTR_BLOCK + tid, a.segs, a.nseg, a.bt.hdr, nullptr, nullptr, nullptr, a.pack, unused);
   if (sb == 0) {  // local loss
     float acc = 0.0f;
     if (a.tl.loss_part)
@@ -1240,6 +1240,11 @@ int gtr_adamw_small(float* param, float* m, float* v, float* grad_out, int64_t t
     set_error("gtr_adamw_small: missing optimizer state");
     return GTR_E_ARG;
   }
+  for (int i = 0; i < nseg; ++i)
+    if (segs[i].live_groups) {  // per-row-group partials need the batch's group count
+      set_error("gtr_adamw_small: segment %d sums live row groups (gtr_conv_bwd wfold partials)", i);
+      return GTR_E_ARG;
+    }
   SmallK k{};
   k.param = param; k.m = m; k.v = v; k.grad_out = grad_out; k.total = total; k.nseg = nseg;
   if (opt) k.opt = *opt;
@@ -1569,7 +1574,11 @@ int gtr_step_tail_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_la
   k.nb_wg = wblocks;
   k.nb_rows = (int)(((int64_t)m_cap * (D / 4) + GTR_BLOCK - 1) / GTR_BLOCK);
   int64_t tot = 0;
-  for (int i = 0; i < nseg; ++i) { k.segs[i] = segs[i]; tot += segs[i].len; }
+  for (int i = 0; i < nseg; ++i) {
+    if (segs[i].live_groups) { set_error("gtr_step_tail_wgrad: folded (per row group) weight gradients"); return GTR_E_ARG; }
+    k.segs[i] = segs[i];
+    tot += segs[i].len;
+  }
   k.nseg = nseg;
   k.small_total = (int)tot;
   k.nb_small = (int)((tot + GTR_BLOCK - 1) / GTR_BLOCK);

@@ -33,10 +33,12 @@ struct NoWait {
 };
 
 // Small parameters: element e of the flat buffer; its segment's gradient partials summed.
-// wait(): called after every load is issued, before `st` is first read.
+// hdr: the batch header (segments with live_groups sum only its hdr[4] row groups' partials;
+// null: no such segment).  wait(): called after every load is issued, before `st` is first read.
 template <class Wait = NoWait>
-__device__ __forceinline__ void small_body(int64_t e, const gtr_segment* segs, int nseg, float* param, float* m,
-                                           float* v, float* grad_out, const AdamStep& st, Wait wait = Wait{}) {
+__device__ __forceinline__ void small_body(int64_t e, const gtr_segment* segs, int nseg, const int32_t* hdr,
+                                           float* param, float* m, float* v, float* grad_out, const AdamStep& st,
+                                           Wait wait = Wait{}) {
   int s = -1;
   for (int i = 0; i < nseg; ++i)
     if (e >= segs[i].begin && e < segs[i].begin + segs[i].len) s = i;
@@ -44,7 +46,18 @@ __device__ __forceinline__ void small_body(int64_t e, const gtr_segment* segs, i
   const gtr_segment& sg = segs[s];
   const int64_t off = e - sg.begin;
   float g = 0.0f;
-  for (int p = 0; p < sg.nparts; ++p) g += sg.src[(int64_t)p * sg.pstride + off];
+  const int np = sg.nparts;
+  // live row groups (wfold partials): the count is loaded beside the partials, not before
+  // them (every partial slot is allocated; dead groups' slots are read and skipped)
+  const int live = (sg.live_groups && hdr) ? hdr[4] : np;
+  for (int p0 = 0; p0 < np; p0 += 8) {
+    float pv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) pv[u] = p0 + u < np ? sg.src[(int64_t)(p0 + u) * sg.pstride + off] : 0.0f;
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (p0 + u < live) g += pv[u];
+  }
   if (grad_out) {
     grad_out[e] = g;
     return;

@@ -271,7 +271,8 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_shard_pack(PackK a) {
   }
   const int sb = blockIdx.x - a.nb_rows;
   const AdamStep unused{};
-  small_body((int64_t)sb * GTR_BLOCK + tid, a.segs, a.nseg, nullptr, nullptr, nullptr, a.small_pack, unused);
+  small_body((int64_t)sb * GTR_BLOCK + tid, a.segs, a.nseg, a.bt.hdr, nullptr, nullptr, nullptr, a.small_pack,
+             unused);
   if (sb == 0) {  // local loss after the flat gradient
     float acc = 0.0f;
     if (a.tl.loss_part)

@@ -38,6 +38,7 @@ class GtrConfig(C.Structure):
         ("row_group", i32), ("training", i32), ("dropout", f32), ("bn_eps", f32),
         ("bn_momentum", f32), ("seed", u32), ("rng_ctr", P), ("consumer_reduce", i32), ("sync_bn", i32),
         ("sweep", P), ("begin", P), ("ctr_add", i32), ("split_sync", i32), ("loss_batch", f32),
+        ("wfold_stride", i64),
     ]
 
 
@@ -52,7 +53,7 @@ class GtrLayer(C.Structure):
         ("xin", P), ("qkvs", P), ("alpha", P), ("agg", P), ("gate", P), ("out", P),
         ("bn_stats", P), ("bn_part", P), ("bn_gsum", P), ("bn_gpart", P), ("cnt", P),
         ("dy", P), ("dqkvs", P), ("du", P), ("dlogit", P), ("dagg", P),
-        ("bn_part_all", P), ("bn_gpart_all", P), ("nparts_fwd", i32), ("nparts_bwd", i32),
+        ("bn_part_all", P), ("bn_gpart_all", P), ("nparts_fwd", i32), ("nparts_bwd", i32), ("wfold", P),
     ]
 
 
@@ -70,7 +71,7 @@ class GtrHead(C.Structure):
 
 class GtrSegment(C.Structure):
     _fields_ = [
-        ("begin", i64), ("len", i64), ("src", P), ("pstride", i64), ("nparts", i32), ("pad", i32),
+        ("begin", i64), ("len", i64), ("src", P), ("pstride", i64), ("nparts", i32), ("live_groups", i32),
     ]
 
 

@@ -207,8 +207,19 @@ class Workspace:
         self.slabs = _f32(Lc, P, lay.slab_stride, device=dev)
         self.pe_slab = _f32(P, lay.slab_stride, device=dev) if eng.K > 0 else None
         self.slab_ptrs = (C.c_void_p * Lc)(*[self.slabs[l].data_ptr() for l in range(Lc)])
+        self.wfold = None  # [Lc, g_cap, slab_stride]: per-row-group weight-gradient partials
         self.head = L.GtrHead()
         self._fill_layer_structs(eng)
+
+    def enable_wfold(self, eng) -> int:
+        """Per-row-group weight-gradient partials for the fused backward (gtr_layer.wfold);
+        returns the slab stride for gtr_config.wfold_stride."""
+        lay = eng.flat.layout
+        if self.wfold is None:
+            self.wfold = _f32(eng.L, self.g_cap, lay.slab_stride, device=eng.device)
+        for l in range(eng.L):
+            self.structs[l].wfold = self.wfold[l].data_ptr()
+        return lay.slab_stride
 
     def _fill_layer_structs(self, eng):
         for l, t in enumerate(self.layers):
@@ -395,6 +406,8 @@ class Engine:
         return h, tab
 
     def _wgrad(self, ws, cfg, bs, l0, l1, st):
+        if cfg.wfold_stride > 0:  # the layer jobs ran in gtr_conv_bwd (wfold): the PE job only
+            l1 = l0
         pe_tab = None
         if self.K > 0 and self.model.laplacian_pe._cached_pe is not None:
             pe_tab = self.model.laplacian_pe._cached_pe.data_ptr()
@@ -423,28 +436,32 @@ class Engine:
         else:
             self._wgrad(ws, cfg, bs, 0, self.L, st)
 
-    def segments(self, ws: Workspace):
-        """Segment table mapping each flat parameter segment to its gradient source."""
+    def segments(self, ws: Workspace, wfold: bool = False):
+        """Segment table mapping each flat parameter segment to its gradient source;
+        ``wfold``: the layer weights' partials are the fused backward's per-row-group slabs
+        (Workspace.enable_wfold), summed over the batch's live groups."""
         lay = self.flat.layout
         segs = []
         D, K = self.D, self.K
         stride = lay.slab_stride
         for l in range(self.L):
-            base = ws.slabs[l].data_ptr()
+            base = ws.wfold[l].data_ptr() if wfold else ws.slabs[l].data_ptr()
+            n, live = (ws.g_cap, 1) if wfold else (ws.P, 0)
             g = ws.layers[l]["bn_gsum"].data_ptr()
-            for name, src, n in ((f"{l}.w_all", base, ws.P), (f"{l}.b_all", base + 4 * (4 * D * D), ws.P),
-                                 (f"{l}.w_beta", base + 4 * (4 * D * D + 4 * D), ws.P),
-                                 (f"{l}.gamma", g + 4 * D, 1), (f"{l}.beta", g, 1)):
+            for name, src, np_, lv in ((f"{l}.w_all", base, n, live), (f"{l}.b_all", base + 4 * (4 * D * D), n, live),
+                                       (f"{l}.w_beta", base + 4 * (4 * D * D + 4 * D), n, live),
+                                       (f"{l}.gamma", g + 4 * D, 1, 0), (f"{l}.beta", g, 1, 0)):
                 s = lay.seg(name)
-                segs.append((s.begin, s.numel, src, stride, n))
+                segs.append((s.begin, s.numel, src, stride, np_, lv))
         if K > 0:
             base = ws.pe_slab.data_ptr()
             for name, src in (("pe.w", base), ("pe.b", base + 4 * D * K)):
                 s = lay.seg(name)
-                segs.append((s.begin, s.numel, src, stride, ws.P))
+                segs.append((s.begin, s.numel, src, stride, ws.P, 0))
         arr = (L.GtrSegment * len(segs))()
-        for i, (b, n, src, ps, npart) in enumerate(segs):
+        for i, (b, n, src, ps, npart, lv) in enumerate(segs):
             arr[i].begin, arr[i].len, arr[i].src, arr[i].pstride, arr[i].nparts = b, n, src, ps, npart
+            arr[i].live_groups = lv
         return arr, len(segs)
 
     def reduce_small_grads(self, ws: Workspace, flat_grad: torch.Tensor):

@@ -177,9 +177,21 @@ class FusedTrainStep:
         nb = C.c_size_t(0)
         L.check(L.lib().gtr_contrib_sort_bytes(m_cap, eng.T, C.byref(nb)), "sort_bytes")
         self.sort_tmp = torch.zeros(max(int(nb.value), 16), dtype=torch.uint8, device=self.dev)
-        self.segs, self.nseg = eng.segments(self.ws)
+        # opt-in (GTR_WFOLD=1): weight gradients folded into the fused backward (each row
+        # group writes its split-K partial; no gtr_wgrad launch for the layers) -- the fused
+        # layer path at D <= 64, not with GTR_TAILW=1.  Measured neutral at C2 (0.0794 ms both
+        # ways): the gtr_wgrad launch (7.9 us) goes, but each gtr_conv_bwd grows by 4 us
+        # (1.5 us of MFMA phase, the rest draining its 64 KB of partials at the kernel's end)
+        self.wfold = (not bool(self.ws.split) and eng.D <= 64 and os.environ.get("GTR_TAILW", "0") != "1"
+                      and os.environ.get("GTR_WFOLD", "0") == "1")
+        wstride = self.ws.enable_wfold(eng) if self.wfold else 0
+        if not self.wfold:
+            for l in range(eng.L):
+                self.ws.structs[l].wfold = None
+        self.segs, self.nseg = eng.segments(self.ws, wfold=self.wfold)
         self.cfg = eng.config(self.ws, True)
         self.cfg.loss_batch = float(self._loss_batch)
+        self.cfg.wfold_stride = wstride
         # large batches: every layer as projection GEMM + attention launches (Engine.layer_fwd /
         # layer_bwd); under SyncBN one merged BatchNorm row per rank and layer is gathered
         # (gtr_config.split_sync) instead of every row group's partials

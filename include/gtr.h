@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GTR_ABI_VERSION 5 /* 5: gtr_config.loss_batch, hdr[6] halo source rows; 4: gtr_step_tail_wgrad on split-K slabs; 3: gtr_config.begin / ctr_add, gtr_tail.rng_inc */
+#define GTR_ABI_VERSION 5 /* 5: gtr_config.loss_batch / wfold_stride, gtr_layer.wfold, gtr_segment.live_groups, hdr[6] halo source rows; 4: gtr_step_tail_wgrad on split-K slabs; 3: gtr_config.begin / ctr_add, gtr_tail.rng_inc */
 
 #define GTR_OK 0
 #define GTR_E_ARG 1001      /* bad argument / unsupported shape */
@@ -143,6 +143,8 @@ typedef struct gtr_config {
                               the batch's own B (a halo cut gives ranks unequal session
                               counts: loss_batch = global B / P makes the rank average of
                               the gradients the global batch's mean)                      */
+  int64_t wfold_stride;    /* > 0: weight gradients folded into gtr_conv_bwd (gtr_layer.wfold;
+                              the segments read them with live_groups = 1); 0: gtr_wgrad    */
 } gtr_config;
 
 
@@ -185,6 +187,9 @@ typedef struct gtr_layer {
   const float* bn_gpart_all; /* sync_bn: every rank's backward partials [nparts_bwd][2D]   */
   int32_t nparts_fwd;
   int32_t nparts_bwd;
+  float* wfold;              /* gtr_config.wfold_stride > 0: gtr_conv_bwd writes each row group's
+                                split-K partial of this layer's weight gradients (w_all | b_all |
+                                w_beta at the gtr_wgrad slab offsets) at wfold + g * stride     */
 } gtr_layer;
 
 /* Embedding + LapPE inputs of layer 0. */
@@ -284,7 +289,8 @@ typedef struct gtr_segment {
   const float* src;   /* gradient partials                                  */
   int64_t pstride;    /* distance between partials                           */
   int32_t nparts;
-  int32_t pad;
+  int32_t live_groups; /* 1: sum only the batch's live row groups (min(nparts, hdr[4])):
+                          partials written per row group by gtr_conv_bwd (wfold)     */
 } gtr_segment;
 
 typedef struct gtr_adam {

@@ -83,6 +83,9 @@ def main():
                 rec["span"].append((end.max() - start.min()) * 10e-3)
                 rec["skew"].append((start.max() - start.min()) * 10e-3)
                 rec["ph"].append(np.diff(st, axis=1).mean(0) * 10e-3)
+                if kind == "b":  # dX then the folded weight gradients (stamp 9 between them)
+                    sub = arr[kid, :ng][:, [3, 9, 4]].astype(np.int64)
+                    detail.setdefault(name, []).append(np.diff(sub, axis=1).mean(0) * 10e-3)
                 if kind == "f" and kid != 16:
                     cols = [0, 10, 12, 13, 14, 15, 1, 11, 2, 5, 8, 3, 4]
                     sub = arr[kid, :ng][:, cols].astype(np.int64)
@@ -92,6 +95,9 @@ def main():
                (3, "bnpart"), (4, None)]
         for name, d in detail.items():
             m = np.median(np.stack(d), axis=0)
+            if "bwd" in name:
+                print(f"{name:14s} detail: dX={m[0]:.2f} wfold={m[1]:.2f}")
+                continue
             print(f"{name:14s} detail: " + " ".join(f"{seq[i][1]}={m[i]:.2f}" for i in range(len(seq) - 1)))
     print(f"{'kernel':14s} {'begin_us':>9s} {'span_us':>8s} {'skew_us':>8s}  phases (mean us per workgroup)")
     order = sorted(rows, key=lambda n: np.median(rows[n]["begin"]))

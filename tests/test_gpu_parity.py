@@ -196,6 +196,7 @@ def test_tail_wgrad_bitwise_equals_separate_launches(D, H, K, loss, wgrad, monke
     (GTR_TAILW=0): losses, parameters, buffers and moments bit for bit, dropout on."""
     if wgrad != "default":
         monkeypatch.setenv("GTR_WGRAD", wgrad)
+    monkeypatch.setenv("GTR_WFOLD", "0")  # the reference: gtr_wgrad's split-K chunks
     T = data().table_rows
     n = 100 if loss == "listwise" else 5
     m1, _ = make_pair(T, D, H, K=K, dropout=0.1, seed=9)
