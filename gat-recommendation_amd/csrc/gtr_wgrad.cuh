@@ -231,13 +231,17 @@ __device__ __forceinline__ void wgrad_tile_mfma(const WJob& J, int tile, int t0,
   // wide tiles with n0 == 0 also sum the A columns (the bias gradient: a ones column of B)
   const bool colsum = !NARROW && n0 == 0;
   float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
-  float4 a0, b0, a1, b1;
+  // rows 16 ahead in flight (4 row quads): at 2 waves per SIMD one 8-row round of MFMAs
+  // (~1k cycles) is shorter than a load's latency from MALL under a full-chip stream
+  float4 a0, b0, a1, b1, a2, b2, a3, b3;
   ld(r0 + kq, a0, b0);
   ld(r0 + 4 + kq, a1, b1);
+  ld(r0 + 8 + kq, a2, b2);
+  ld(r0 + 12 + kq, a3, b3);
   for (int t = r0; t < r1; t += 8) {
-    float4 a2, b2, a3, b3;
-    ld(t + 8 + kq, a2, b2);
-    ld(t + 12 + kq, a3, b3);
+    float4 a4, b4, a5, b5;
+    ld(t + 16 + kq, a4, b4);
+    ld(t + 20 + kq, a5, b5);
     mma(a0, b0);
     mma(a1, b1);
     if (colsum) {
@@ -245,6 +249,7 @@ __device__ __forceinline__ void wgrad_tile_mfma(const WJob& J, int tile, int t0,
       cs.x += a1.x; cs.y += a1.y; cs.z += a1.z; cs.w += a1.w;
     }
     a0 = a2; b0 = b2; a1 = a3; b1 = b3;
+    a2 = a4; b2 = b4; a3 = a5; b3 = b5;
   }
   if (colsum) {  // the four row lanes of a column, then the row splits in order
     cs.x = bfly_add<32>(bfly_add<16>(cs.x)); cs.y = bfly_add<32>(bfly_add<16>(cs.y));

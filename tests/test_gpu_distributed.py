@@ -353,3 +353,54 @@ def test_collective_capture_refusal_falls_back_per_instance():
     assert same
     for l1, l2 in out:
         assert l1 == l2
+
+
+def _resident_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from etpgt.data.batch import Caps
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        data = small_data()
+        T = data.table_rows
+        m1, _ = make_pair(T, D, H, K=0, dropout=0.1, seed=31)
+        m2 = copy.deepcopy(m1)
+        m1.train(); m2.train()
+        bl = batches(data, B, NNEG, 3 * world, seed=32)[rank::world]
+        caps = Caps(max(b.num_nodes for b in bl) * 2, B, max(b.num_edges for b in bl) * 2, NNEG)
+        f1 = FusedTrainStep(m1, loss="bpr", caps=caps, data_parallel=True, lagged=True)
+        f2 = FusedTrainStep(m2, loss="bpr", caps=caps, data_parallel=True, lagged=True)
+        staged = [torch.from_numpy(b.packed(f2.caps)[1]).cuda() for b in bl]
+        f2.bind_resident(staged)
+        same = True
+        for i in [0, 1, 2, 1, 0]:
+            same = same and float(f1(bl[i].to("cuda"))) == float(f2.run_resident(i))
+        f1.flush()
+        f2.flush()
+        same = same and all(torch.equal(a, b) for a, b in zip(m1.parameters(), m2.parameters()))
+        q.put((rank, same))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_resident_images_equal_copied_blob():
+    """The data-parallel step (2 ranks sharing the GPU over gloo, lagged sweep, dropout on)
+    launched on resident batch images (bind_resident / run_resident: one graph per image,
+    no copy into the step's blob; bench.py's default at N > 1) trains bit for bit like
+    load + run, images reused included."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_resident_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(collect(q, procs, world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert res[0] and res[1]
