@@ -1035,10 +1035,16 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const int32_t* keys, int
   for (int d = threadIdx.x; d < RS_RADIX; d += RS_THREADS) h[d] = 0;
   __syncthreads();
   const int base = blockIdx.x * RS_THREADS * rounds;
-  for (int r = 0; r < rounds; ++r) {
+  // every round's key requested before the first count (the loads are independent)
+  int kk[RS_MAX_ROUNDS];
+#pragma unroll
+  for (int r = 0; r < RS_MAX_ROUNDS; ++r) {
     const int i = base + r * RS_THREADS + threadIdx.x;
-    if (i < n) atomicAdd(&h[((uint32_t)keys[i] >> shift) & (RS_RADIX - 1)], 1);  // integer counts
+    kk[r] = (r < rounds && i < n) ? keys[i] : -1;
   }
+#pragma unroll
+  for (int r = 0; r < RS_MAX_ROUNDS; ++r)
+    if (kk[r] >= 0) atomicAdd(&h[((uint32_t)kk[r] >> shift) & (RS_RADIX - 1)], 1);  // integer counts
   __syncthreads();
   for (int d = threadIdx.x; d < RS_RADIX; d += RS_THREADS) {
     hist[(size_t)blockIdx.x * RS_RADIX + d] = h[d];  // tile-major, coalesced
@@ -1109,11 +1115,19 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const int32_t* kin, c
   __syncthreads();
   const unsigned long long lt = (1ull << lane) - 1ull;
   const int base = blockIdx.x * RS_THREADS * rounds;
+  // the next round's (key, value) are requested while this round is ranked and written
+  int key_n = base + tid < n ? kin[base + tid] : 0;
+  int val_n = base + tid < n ? vin[base + tid] : 0;
   for (int r = 0; r < rounds; ++r) {
     const int i = base + r * RS_THREADS + tid;
     const bool live = i < n;
-    const int key = live ? kin[i] : 0;
-    const int val = live ? vin[i] : 0;
+    const int key = key_n;
+    const int val = val_n;
+    if (r + 1 < rounds) {
+      const int i2 = i + RS_THREADS;
+      key_n = i2 < n ? kin[i2] : 0;
+      val_n = i2 < n ? vin[i2] : 0;
+    }
     const int d = ((uint32_t)key >> shift) & (RS_RADIX - 1);
     unsigned long long match = __ballot(live);
 #pragma unroll
