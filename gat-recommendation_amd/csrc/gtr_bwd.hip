@@ -485,6 +485,10 @@ extern "C" int gtr_conv_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     set_error("gtr_conv_bwd: bad arguments");
     return GTR_E_ARG;
   }
+  if (layers[l].ffn || (l > 0 && layers[l - 1].ffn)) {
+    set_error("gtr_conv_bwd: a feed-forward block runs on the split layer path (gtr_qkvs_* / gtr_attn_* / gtr_ffn_*)");
+    return GTR_E_ARG;
+  }
   const int D = cfg->dim;
   ConvBwdK k;
   if (const int rc = make_bwd_args(cfg, bt, layers, l, dx0, k)) return rc;

@@ -1914,6 +1914,10 @@ extern "C" int gtr_conv_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     set_error("gtr_conv_fwd: bad arguments");
     return GTR_E_ARG;
   }
+  if (layers[l].ffn || (l > 0 && layers[l - 1].ffn)) {
+    set_error("gtr_conv_fwd: a feed-forward block runs on the split layer path (gtr_qkvs_* / gtr_attn_* / gtr_ffn_*)");
+    return GTR_E_ARG;
+  }
   ConvFwdK k;
   if (const int rc = make_fwd_args(cfg, bt, emb, layers, l, k)) return rc;
   int grid = (bt->n_cap + cfg->row_group - 1) / cfg->row_group;

@@ -13,6 +13,16 @@
 //   k_dx<D>    dX = dQKVS . W_all + dy (the residual), the previous layer's dropout mask,
 //              -> that layer's dy (or dx0 at layer 0), and its BatchNorm backward sums.
 //
+// The feed-forward block of the use_ffn=True variant (graph_transformer.py:88-100,160-170)
+// runs on the same two kernels, by mode:
+//   k_proj<PJ_FOLD>     y = dropout(BN(out) + x) -> ffn.y, a = y W1^T + b1 -> ffn.a (W1 is
+//                       [4D, D] like W_all: the conv projection with other pointers);
+//   k_dx<DX_FFN_DOWN>   z = y + dropout(dropout(GELU(a)) W2^T + b2) -> ffn.z (K = 4D);
+//   k_proj<PJ_FFN_DH>   g2 = dz * mask -> ffn.g2, da = (g2 W2) * mask * GELU'(a) -> ffn.da;
+//   k_dx<DX_CONV>       dy = (dz + da W1) * the layer's output mask -> layers[l].dy + sums;
+//   k_proj<PJ_READY>    the next layer's X = ffn.z as it is (no BatchNorm fold);
+// and k_ffn_wgrad reduces dW1 / db1 / dW2 / db2 over row chunks on f32 MFMA.
+//
 // One workgroup per CU, 8 waves, persistent over 16- (D = 128) or 32-row (D = 64) tiles.
 // Each wave keeps ITS column tiles of W_all in registers for the whole launch (128 VGPRs
 // at D = 128: loaded once per CU instead of once per row group), the row tile is staged
@@ -36,6 +46,18 @@ using namespace gtr;
 #else
 #define GM_MFMA4(a, b, c) mfma4(a, b, c)
 #endif
+
+// k_proj modes: layer 0 (item row + LapPE), layer >= 1 (BatchNorm fold of the previous
+// layer), rows taken as they are (after a feed-forward block), FFN hidden-gradient GEMM
+enum { PJ_FIRST = 0, PJ_FOLD = 1, PJ_READY = 2, PJ_FFN_DH = 3 };
+// k_dx modes: the conv dX GEMM (+ previous layer's mask and BatchNorm sums), FFN down-projection
+enum { DX_CONV = 0, DX_FFN_DOWN = 1 };
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  return cdf + x * (0.39894228040143268f * expf(-0.5f * x * x));
+}
 
 template <int D>
 struct ProjGeom {
@@ -76,6 +98,7 @@ struct ProjK {
   int sync, p_nparts;        // split_sync: fold the ranks' merged rows of the previous layer
   const float* p_part_all;   // [p_nparts][1 + 2D] (count, mean, M2)
   float bn_mom;
+  const float* fa;           // PJ_FFN_DH: the saved pre-activation a [n, 4D]
 };
 
 // Inputs of one thread's float4 of X for one tile: layer 0 the item row (+ its LapPE row),
@@ -85,8 +108,9 @@ struct ProjIn {
   float4 pe[4];
 };
 
-template <int D, bool FIRST>
+template <int D, int MODE>
 __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 64 ? 4 : 2))) void k_proj(ProjK a) {
+  constexpr bool FIRST = MODE == PJ_FIRST, FOLD = MODE == PJ_FOLD, DH = MODE == PJ_FFN_DH;
   using G = ProjGeom<D>;
   constexpr int CT = G::CT, RT = G::RT, BM = G::BM, XS = G::XS, C4 = G::C4, KPE = G::KPE;
   __shared__ __attribute__((aligned(16))) float Xs[2][BM * XS];
@@ -103,10 +127,20 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
 #pragma unroll
   for (int c = 0; c < CT; ++c) {
     const int ct = wave + c * GM_WAVES;
-    const float* wrow = a.w_all + (size_t)(ct * 16 + lr) * D;
+    if (DH) {  // B[k][col] = W2[k][col], W2 = [D, 4D] row-major
+      const float* wcol = a.w_all + (size_t)(lg * 4) * (4 * D) + ct * 16 + lr;
 #pragma unroll
-    for (int kb = 0; kb < D / 16; ++kb) wf[c][kb] = *reinterpret_cast<const float4*>(wrow + kb * 16 + lg * 4);
-    bias[c] = a.b_all[ct * 16 + lr];
+      for (int kb = 0; kb < D / 16; ++kb) {
+        const float* wp = wcol + (size_t)(kb * 16) * (4 * D);
+        wf[c][kb] = make_float4(wp[0], wp[4 * D], wp[8 * D], wp[12 * D]);
+      }
+      bias[c] = 0.0f;
+    } else {
+      const float* wrow = a.w_all + (size_t)(ct * 16 + lr) * D;
+#pragma unroll
+      for (int kb = 0; kb < D / 16; ++kb) wf[c][kb] = *reinterpret_cast<const float4*>(wrow + kb * 16 + lg * 4);
+      bias[c] = a.b_all[ct * 16 + lr];
+    }
   }
   const bool pe_lds = FIRST && a.pe_k > 0 && a.pe_k <= KPE;
   if (FIRST) {
@@ -119,6 +153,8 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
       }
     if (a.pe_k > 0)
       for (int j = tid; j < D; j += GM_BLOCK) s_c[j] = a.bpe[j];
+  } else if (!FOLD) {
+    // PJ_READY / PJ_FFN_DH: no BatchNorm of a previous layer
   } else if (a.sync && a.train) {
     // SyncBN (split_sync): every rank's merged (count, mean, M2) row of the previous layer,
     // folded in rank order; workgroup 0 publishes the statistics (read by the backward) and
@@ -147,10 +183,12 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
   __syncthreads();
   const uint32_t ctr = a.rng_ctr ? load_step_ctr(a.rng_ctr) + a.ctr_add : 0u;
   const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
-  const uint32_t st_prev = drop_stream(1, (uint32_t)(a.layer - 1), ctr);
+  // FOLD: the previous layer's output mask; FFN_DH: this layer's FFN output mask (kind 3)
+  const uint32_t st_prev = DH ? drop_stream(3, (uint32_t)a.layer, ctr) : drop_stream(1, (uint32_t)(a.layer - 1), ctr);
+  const uint32_t st_h = drop_stream(2, (uint32_t)a.layer, ctr);  // FFN_DH: the hidden mask
   const int xi = tid / C4, xj = (tid - (tid / C4) * C4) * 4;  // this thread's row / column of X
   float4 pg = make_float4(0.f, 0.f, 0.f, 0.f), pb = pg, mu = pg, rs = pg;
-  if (!FIRST) {
+  if (FOLD) {
     mu = *reinterpret_cast<const float4*>(s_c + D + xj);
     rs = *reinterpret_cast<const float4*>(s_c + 2 * D + xj);
     pg = *reinterpret_cast<const float4*>(s_c + 3 * D + xj);
@@ -181,7 +219,7 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
     } else {
       const size_t o = (size_t)r * D + xj;
       in.u = *reinterpret_cast<const float4*>(a.p_out + o);
-      in.v = *reinterpret_cast<const float4*>(a.p_xin + o);
+      if (FOLD) in.v = *reinterpret_cast<const float4*>(a.p_xin + o);
     }
   };
   // X of one tile -> LDS (rows past N: zero) and xin; the arithmetic of k_conv_fwd's
@@ -215,6 +253,13 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
           val.z = val.z + (acc[2] + s_c[xj + 2]);
           val.w = val.w + (acc[3] + s_c[xj + 3]);
         }
+      } else if (MODE == PJ_READY) {
+        val = in.u;
+      } else if (DH) {
+        val.x = in.u.x * dr.mul(st_prev, (uint32_t)o);
+        val.y = in.u.y * dr.mul(st_prev, (uint32_t)(o + 1));
+        val.z = in.u.z * dr.mul(st_prev, (uint32_t)(o + 2));
+        val.w = in.u.w * dr.mul(st_prev, (uint32_t)(o + 3));
       } else {
         const float4 po = in.u, px = in.v;
         val.x = (((po.x - mu.x) * rs.x * pg.x + pb.x) + px.x) * dr.mul(st_prev, (uint32_t)o);
@@ -269,7 +314,11 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int row = t * BM + r * 16 + lg * 4 + i;
-          if (row < N) a.qkvs[(size_t)row * (4 * D) + col] = acc[r][c][i] + bias[c];
+          if (row < N) {
+            const size_t o = (size_t)row * (4 * D) + col;
+            if (DH) a.qkvs[o] = acc[r][c][i] * dr.mul(st_h, (uint32_t)o) * gelu_erf_grad(a.fa[o]);
+            else a.qkvs[o] = acc[r][c][i] + bias[c];
+          }
         }
       }
     cur = nxt;
@@ -311,10 +360,12 @@ struct DxK {
   float* p_gsum;
   uint32_t* p_cnt;
   float* dx0;
+  const float* b2;  // DX_FFN_DOWN: the second Linear's bias
 };
 
-template <int D>
+template <int D, int MODE>
 __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
+  constexpr bool DOWN = MODE == DX_FFN_DOWN;
   using G = DxGeom<D>;
   constexpr int NCT = G::NCT, BM = G::BM, K = G::K, AS = G::AS, PER = G::PER;
   __shared__ __attribute__((aligned(16))) float As[2][BM * AS];
@@ -328,7 +379,11 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
   // ---- W_all column fragments (B[k][col] = W_all[k][col], k = kb*16 + lg*4 + j): the
   //      fused kernel's bv, held in registers for every tile
   float4 wb[K / 16];
-  {
+  if (DOWN) {  // B[k][col] = W2[col][k], W2 = [D, 4D] row-major: contiguous in k
+    const float* brow = a.w_all + (size_t)col * K + lg * 4;
+#pragma unroll
+    for (int kb = 0; kb < K / 16; ++kb) wb[kb] = *reinterpret_cast<const float4*>(brow + kb * 16);
+  } else {
     const float* bcol = a.w_all + (size_t)(lg * 4) * D + col;
 #pragma unroll
     for (int kb = 0; kb < K / 16; ++kb) {
@@ -339,6 +394,9 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
   const uint32_t ctr = a.rng_ctr ? load_step_ctr(a.rng_ctr) + a.ctr_add : 0u;
   const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
   const uint32_t st_prev = drop_stream(1, (uint32_t)(a.layer - 1), ctr);
+  // DX_FFN_DOWN: the hidden mask (kind 2) and the block-output mask (kind 3) of layer a.layer
+  const uint32_t st_h = drop_stream(2, (uint32_t)a.layer, ctr), st_o = drop_stream(3, (uint32_t)a.layer, ctr);
+  const float b2c = DOWN ? a.b2[col] : 0.0f;
   float pm = 0.0f, pr = 0.0f;
   if (a.has_prev) { pm = a.p_stats[col]; pr = a.p_stats[D + col]; }
   float s1 = 0.0f, s2 = 0.0f;
@@ -364,7 +422,15 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
     for (int u = 0; u < PER; ++u) {
       const int idx = tid + u * GM_BLOCK;
       const int i = idx / (K / 4), c = (idx - i * (K / 4)) * 4;
-      *reinterpret_cast<float4*>(A + i * AS + c) = cur[u];
+      float4 v = cur[u];
+      if (DOWN) {  // h = dropout(GELU(a)) (rows past N are zero: GELU(0) = 0)
+        const uint32_t e = (uint32_t)((size_t)(t * BM + i) * K + c);
+        v.x = gelu_erf(v.x) * dr.mul(st_h, e);
+        v.y = gelu_erf(v.y) * dr.mul(st_h, e + 1);
+        v.z = gelu_erf(v.z) * dr.mul(st_h, e + 2);
+        v.w = gelu_erf(v.w) * dr.mul(st_h, e + 3);
+      }
+      *reinterpret_cast<float4*>(A + i * AS + c) = v;
     }
     __syncthreads();
 #pragma unroll
@@ -379,6 +445,10 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
       const int row = t * BM + rs * 16 + lg * 4 + i;
       if (row < N) {
         const size_t o = (size_t)row * D + col;
+        if (DOWN) {  // z = y + dropout(h W2^T + b2)
+          a.dx0[o] = a.dy[o] + (acc[i] + b2c) * dr.mul(st_o, (uint32_t)o);
+          continue;
+        }
         const float dx = a.dy[o] + acc[i];
         if (a.has_prev) {
           const float d = dx * dr.mul(st_prev, (uint32_t)o);
@@ -392,7 +462,7 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
     }
     buf ^= 1;
   }
-  if (!a.has_prev) return;
+  if (DOWN || !a.has_prev) return;
   // ---- the previous layer's BatchNorm backward sums: one partial row per workgroup (its
   //      tiles in order), reduced by the bucketed last arrivers (fixed order: deterministic)
   s1 = bfly_add<32>(bfly_add<16>(s1));
@@ -427,6 +497,102 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
   if (tid == 0) reset_counter(a.p_cnt);
 }
 
+// ---- FFN weight gradients: workgroup (p, prod) reduces row chunk p of
+//   prod 0: dW1[f][d] = sum_n da[n][f] y[n][d]   and db1[f] = sum_n da[n][f]
+//   prod 1: dW2[d][f] = sum_n g2[n][d] h[n][f]   and db2[d] = sum_n g2[n][d],  h = dropout(GELU(a))
+// into its slab (adamw_small sums the chunks).  16-row blocks of both operands are staged in
+// LDS (h recomputed from a); each wave owns a contiguous run of the 16x16 output tiles and
+// accumulates them on f32 MFMA with k = the node rows.
+struct FfnWK {
+  gtr_batch bt;
+  int layer, n_chunks;
+  float scale;
+  uint32_t seed, thresh;
+  int drop_on;
+  uint32_t ctr_add;
+  const uint32_t* rng_ctr;
+  const float* y;
+  const float* fa;
+  const float* g2;
+  const float* da;
+  float* slab;
+  int64_t stride;
+};
+
+template <int D>
+__global__ __launch_bounds__(GM_BLOCK) void k_ffn_wgrad(FfnWK a) {
+  constexpr int F = 4 * D, WA = F + 4, WB = F + 4;  // padded LDS rows (bank-conflict free)
+  constexpr int TILES = (F / 16) * (D / 16), TW = TILES / GM_WAVES;
+  static_assert(TW * GM_WAVES == TILES, "tiles split evenly over the waves");
+  __shared__ __attribute__((aligned(16))) float As[16 * WA];
+  __shared__ __attribute__((aligned(16))) float Bs[16 * WB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
+  const int prod = blockIdx.y;
+  const int N = a.bt.hdr[0];
+  const int per = (((N + a.n_chunks - 1) / a.n_chunks) + 15) & ~15;
+  const int r0 = blockIdx.x * per, r1 = min(N, r0 + per);
+  // prod 0: A = da [16][F] (M = F), B = y [16][D] (N' = D); prod 1: A = g2 [16][D], B = h [16][F]
+  const int MA = prod == 0 ? F : D, NB = prod == 0 ? D : F;
+  const int NT = NB / 16;
+  const uint32_t ctr = a.rng_ctr ? load_step_ctr(a.rng_ctr) + a.ctr_add : 0u;
+  const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
+  const uint32_t st_h = drop_stream(2, (uint32_t)a.layer, ctr);
+  f32x4 acc[TW];
+#pragma unroll
+  for (int q = 0; q < TW; ++q) acc[q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+  float bsum = 0.0f;  // bias gradient of column tid (tid < MA)
+  for (int rb = r0; rb < r1; rb += 16) {
+    __syncthreads();
+    // stage A (16 x MA) and B (16 x NB); rows past r1 are zero
+    for (int idx = tid; idx < 16 * (MA / 4); idx += GM_BLOCK) {
+      const int i = idx / (MA / 4), c = (idx - i * (MA / 4)) * 4, r = rb + i;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < r1) v = *reinterpret_cast<const float4*>((prod == 0 ? a.da : a.g2) + (size_t)r * MA + c);
+      *reinterpret_cast<float4*>(As + i * WA + c) = v;
+    }
+    for (int idx = tid; idx < 16 * (NB / 4); idx += GM_BLOCK) {
+      const int i = idx / (NB / 4), c = (idx - i * (NB / 4)) * 4, r = rb + i;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (r < r1) {
+        if (prod == 0) {
+          v = *reinterpret_cast<const float4*>(a.y + (size_t)r * D + c);
+        } else {
+          const size_t e = (size_t)r * F + c;
+          v = *reinterpret_cast<const float4*>(a.fa + e);
+          v.x = gelu_erf(v.x) * dr.mul(st_h, (uint32_t)e);
+          v.y = gelu_erf(v.y) * dr.mul(st_h, (uint32_t)(e + 1));
+          v.z = gelu_erf(v.z) * dr.mul(st_h, (uint32_t)(e + 2));
+          v.w = gelu_erf(v.w) * dr.mul(st_h, (uint32_t)(e + 3));
+        }
+      }
+      *reinterpret_cast<float4*>(Bs + i * WB + c) = v;
+    }
+    __syncthreads();
+    if (tid < MA) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) bsum += As[i * WA + tid];
+    }
+#pragma unroll
+    for (int q = 0; q < TW; ++q) {
+      const int tile = wave * TW + q, m0 = (tile / NT) * 16, n0 = (tile - (tile / NT) * NT) * 16;
+      const float* ap = As + (lg * 4) * WA + m0 + lr;
+      const float* bp = Bs + (lg * 4) * WB + n0 + lr;
+      const float4 av = make_float4(ap[0], ap[WA], ap[2 * WA], ap[3 * WA]);
+      const float4 bv = make_float4(bp[0], bp[WB], bp[2 * WB], bp[3 * WB]);
+      acc[q] = mfma4(av, bv, acc[q]);
+    }
+  }
+  // slab: [dW1 F*D | db1 F | dW2 D*F | db2 D]
+  float* out = a.slab + (size_t)blockIdx.x * a.stride + (prod == 0 ? 0 : (size_t)F * D + F);
+#pragma unroll
+  for (int q = 0; q < TW; ++q) {
+    const int tile = wave * TW + q, m0 = (tile / NT) * 16, n0 = (tile - (tile / NT) * NT) * 16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[(size_t)(m0 + lg * 4 + i) * NB + n0 + lr] = acc[q][i];
+  }
+  if (tid < MA) out[(size_t)F * D + tid] = bsum;
+}
+
 // Persistent grid: `per_cu` workgroups per CU (the register / LDS budget: 2 at D = 64,
 // 1 at D = 128), never more than the tiles.
 int gemm_grid(int tiles, int per_cu) {
@@ -457,7 +623,8 @@ extern "C" int gtr_qkvs_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     return GTR_E_ARG;
   }
   if (cfg->pe_k < 0 || cfg->pe_k > 256) { set_error("gtr_qkvs_fwd: pe_k out of range"); return GTR_E_ARG; }
-  if (l > 0 && cfg->training && (cfg->sync_bn ? !cfg->split_sync : cfg->consumer_reduce)) {
+  const bool ready = l > 0 && layers[l - 1].ffn;  // input rows = the previous layer's FFN output
+  if (l > 0 && !ready && cfg->training && (cfg->sync_bn ? !cfg->split_sync : cfg->consumer_reduce)) {
     set_error("gtr_qkvs_fwd: the split path reads producer-finalized BatchNorm statistics (consumer_reduce 0) "
               "or, under sync_bn, the ranks' merged rows (split_sync)");
     return GTR_E_ARG;
@@ -481,6 +648,9 @@ extern "C" int gtr_qkvs_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   k.ctr_add = (uint32_t)cfg->ctr_add;
   if (l == 0) {
     k.table = emb->table; k.pe_tab = emb->pe_tab; k.wpe = emb->wpe; k.bpe = emb->bpe;
+  } else if (ready) {
+    if (!layers[l - 1].ffn->z) { set_error("gtr_qkvs_fwd: layer %d's FFN has no output rows", l - 1); return GTR_E_ARG; }
+    k.p_out = layers[l - 1].ffn->z;
   } else {
     const gtr_layer& P = layers[l - 1];
     k.p_out = P.out; k.p_xin = P.xin; k.p_stats = P.bn_stats; k.p_rmean = P.bn_rmean; k.p_rvar = P.bn_rvar;
@@ -501,11 +671,13 @@ extern "C" int gtr_qkvs_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   const int grid = gemm_grid((bt->n_cap + bm - 1) / bm, D == 64 ? 2 : 1);
   hipStream_t s = (hipStream_t)stream;
   if (D == 64) {
-    if (l == 0) hipLaunchKernelGGL((k_proj<64, true>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
-    else hipLaunchKernelGGL((k_proj<64, false>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
+    if (l == 0) hipLaunchKernelGGL((k_proj<64, PJ_FIRST>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
+    else if (ready) hipLaunchKernelGGL((k_proj<64, PJ_READY>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
+    else hipLaunchKernelGGL((k_proj<64, PJ_FOLD>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
   } else {
-    if (l == 0) hipLaunchKernelGGL((k_proj<128, true>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
-    else hipLaunchKernelGGL((k_proj<128, false>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
+    if (l == 0) hipLaunchKernelGGL((k_proj<128, PJ_FIRST>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
+    else if (ready) hipLaunchKernelGGL((k_proj<128, PJ_READY>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
+    else hipLaunchKernelGGL((k_proj<128, PJ_FOLD>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
   }
   GTR_HIP_CHECK_LAUNCH();
   return GTR_OK;
@@ -522,9 +694,11 @@ extern "C" int gtr_qkvs_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   if (!cfg->training) { set_error("gtr_qkvs_bwd: backward requires training mode"); return GTR_E_ARG; }
   if (cfg->sync_bn && !cfg->split_sync) { set_error("gtr_qkvs_bwd: sync_bn needs split_sync"); return GTR_E_ARG; }
   const gtr_layer& L = layers[l];
+  const bool ffn_prev = l > 0 && layers[l - 1].ffn;  // dX is d/dz of the previous layer's FFN
+  if (ffn_prev && !layers[l - 1].ffn->dz) { set_error("gtr_qkvs_bwd: layer %d's FFN has no dz rows", l - 1); return GTR_E_ARG; }
   DxK k{};
   k.bt = *bt;
-  k.has_prev = l > 0;
+  k.has_prev = l > 0 && !ffn_prev;
   k.layer = l;
   k.drop_on = (cfg->dropout > 0.0f) ? 1 : 0;
   {
@@ -535,8 +709,8 @@ extern "C" int gtr_qkvs_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   k.seed = cfg->seed;
   k.rng_ctr = cfg->rng_ctr;
   k.ctr_add = (uint32_t)cfg->ctr_add;
-  k.dqkvs = L.dqkvs; k.w_all = L.w_all; k.dy = L.dy; k.dx0 = dx0;
-  if (l > 0) {
+  k.dqkvs = L.dqkvs; k.w_all = L.w_all; k.dy = L.dy; k.dx0 = ffn_prev ? layers[l - 1].ffn->dz : dx0;
+  if (k.has_prev) {
     const gtr_layer& P = layers[l - 1];
     k.p_out = P.out; k.p_stats = P.bn_stats; k.p_dy = P.dy; k.p_gpart = P.bn_gpart; k.p_gsum = P.bn_gsum;
     k.p_cnt = P.cnt + 1;
@@ -545,8 +719,147 @@ extern "C" int gtr_qkvs_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   const int grid = gemm_grid((bt->n_cap + bm - 1) / bm, 1);
   if (grid > 256) { set_error("gtr_qkvs_bwd: more than 256 partial rows"); return GTR_E_ARG; }
   hipStream_t s = (hipStream_t)stream;
-  if (D == 64) hipLaunchKernelGGL(k_dx<64>, dim3(grid), dim3(GM_BLOCK), 0, s, k);
-  else hipLaunchKernelGGL(k_dx<128>, dim3(grid), dim3(GM_BLOCK), 0, s, k);
+  if (D == 64) hipLaunchKernelGGL((k_dx<64, DX_CONV>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
+  else hipLaunchKernelGGL((k_dx<128, DX_CONV>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+namespace {
+
+// Shared argument checks of the FFN entry points; fills the dropout parameters.
+int ffn_check(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l, const char* fn,
+              bool need_train, uint32_t& thresh, float& scale, int& drop_on) {
+  if (!cfg || !bt || !layers || l < 0 || l >= cfg->num_layers || !layers[l].ffn) {
+    set_error("%s: bad arguments (layer %d needs gtr_layer.ffn)", fn, l);
+    return GTR_E_ARG;
+  }
+  const gtr_ffn& f = *layers[l].ffn;
+  if (cfg->dim != 64 && cfg->dim != 128) { set_error("%s: dim %d (the FFN GEMMs cover 64 / 128)", fn, cfg->dim); return GTR_E_ARG; }
+  if (f.expansion != 4) { set_error("%s: ffn_expansion %d (4 supported)", fn, f.expansion); return GTR_E_ARG; }
+  if (!f.w1 || !f.b1 || !f.w2 || !f.b2 || !f.y || !f.a || !f.z) { set_error("%s: missing FFN buffers", fn); return GTR_E_ARG; }
+  if (need_train && !cfg->training) { set_error("%s: backward requires training mode", fn); return GTR_E_ARG; }
+  if (cfg->training && (cfg->sync_bn || cfg->consumer_reduce)) {
+    set_error("%s: the FFN variant reads producer-finalized BatchNorm statistics (consumer_reduce 0, no sync_bn)", fn);
+    return GTR_E_ARG;
+  }
+  drop_on = (cfg->training && cfg->dropout > 0.0f) ? 1 : 0;
+  const double p = cfg->dropout >= 1.0f ? 0.999999 : cfg->dropout;
+  thresh = (uint32_t)(p * 4294967296.0);
+  scale = drop_on ? (float)(1.0 / (1.0 - p)) : 1.0f;
+  return GTR_OK;
+}
+
+}  // namespace
+
+extern "C" int gtr_ffn_fwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l,
+                           gtr_stream_t stream) {
+  uint32_t thresh;
+  float scale;
+  int drop_on;
+  if (const int rc = ffn_check(cfg, bt, layers, l, "gtr_ffn_fwd", false, thresh, scale, drop_on)) return rc;
+  const int D = cfg->dim;
+  const gtr_layer& L = layers[l];
+  const gtr_ffn& f = *L.ffn;
+  hipStream_t s = (hipStream_t)stream;
+  // y = dropout(BN(out) + xin) and a = y W1^T + b1: the conv projection of a "layer l + 1"
+  ProjK k{};
+  k.bt = *bt;
+  k.first = 0;
+  k.train = cfg->training;
+  k.layer = l + 1;
+  k.bn_eps = cfg->bn_eps;
+  k.drop_on = drop_on; k.thresh = thresh; k.scale = scale;
+  k.seed = cfg->seed; k.rng_ctr = cfg->rng_ctr; k.ctr_add = (uint32_t)cfg->ctr_add;
+  k.p_out = L.out; k.p_xin = L.xin; k.p_stats = L.bn_stats; k.p_rmean = L.bn_rmean; k.p_rvar = L.bn_rvar;
+  k.p_nbt = L.bn_nbt; k.p_gamma = L.bn_gamma; k.p_beta = L.bn_beta; k.bn_mom = cfg->bn_momentum;
+  k.w_all = f.w1; k.b_all = f.b1; k.xin = f.y; k.qkvs = f.a;
+  const int bm = D == 64 ? ProjGeom<64>::BM : ProjGeom<128>::BM;
+  const int grid = gemm_grid((bt->n_cap + bm - 1) / bm, D == 64 ? 2 : 1);
+  if (D == 64) hipLaunchKernelGGL((k_proj<64, PJ_FOLD>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
+  else hipLaunchKernelGGL((k_proj<128, PJ_FOLD>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
+  GTR_HIP_CHECK_LAUNCH();
+  // z = y + dropout(dropout(GELU(a)) W2^T + b2)
+  DxK d{};
+  d.bt = *bt;
+  d.has_prev = 0;
+  d.layer = l;
+  d.drop_on = drop_on; d.thresh = thresh; d.scale = scale;
+  d.seed = cfg->seed; d.rng_ctr = cfg->rng_ctr; d.ctr_add = (uint32_t)cfg->ctr_add;
+  d.dqkvs = f.a; d.w_all = f.w2; d.dy = f.y; d.dx0 = f.z; d.b2 = f.b2;
+  const int bmd = D == 64 ? DxGeom<64>::BM : DxGeom<128>::BM;
+  const int gd = gemm_grid((bt->n_cap + bmd - 1) / bmd, 1);
+  if (D == 64) hipLaunchKernelGGL((k_dx<64, DX_FFN_DOWN>), dim3(gd), dim3(GM_BLOCK), 0, s, d);
+  else hipLaunchKernelGGL((k_dx<128, DX_FFN_DOWN>), dim3(gd), dim3(GM_BLOCK), 0, s, d);
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+extern "C" int gtr_ffn_bwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l,
+                           gtr_stream_t stream) {
+  uint32_t thresh;
+  float scale;
+  int drop_on;
+  if (const int rc = ffn_check(cfg, bt, layers, l, "gtr_ffn_bwd", true, thresh, scale, drop_on)) return rc;
+  const int D = cfg->dim;
+  const gtr_layer& L = layers[l];
+  const gtr_ffn& f = *L.ffn;
+  if (!f.dz || !f.g2 || !f.da) { set_error("gtr_ffn_bwd: missing FFN gradient buffers"); return GTR_E_ARG; }
+  hipStream_t s = (hipStream_t)stream;
+  // g2 = dz * mask3 -> ffn.g2; da = (g2 W2) * mask2 * GELU'(a) -> ffn.da
+  ProjK k{};
+  k.bt = *bt;
+  k.train = 1;
+  k.layer = l;
+  k.drop_on = drop_on; k.thresh = thresh; k.scale = scale;
+  k.seed = cfg->seed; k.rng_ctr = cfg->rng_ctr; k.ctr_add = (uint32_t)cfg->ctr_add;
+  k.p_out = f.dz; k.w_all = f.w2; k.xin = f.g2; k.qkvs = f.da; k.fa = f.a;
+  const int bm = D == 64 ? ProjGeom<64>::BM : ProjGeom<128>::BM;
+  const int grid = gemm_grid((bt->n_cap + bm - 1) / bm, D == 64 ? 2 : 1);
+  if (D == 64) hipLaunchKernelGGL((k_proj<64, PJ_FFN_DH>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
+  else hipLaunchKernelGGL((k_proj<128, PJ_FFN_DH>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
+  GTR_HIP_CHECK_LAUNCH();
+  // dy = (dz + da W1) * the layer's output mask -> layers[l].dy, + its BatchNorm backward sums
+  DxK d{};
+  d.bt = *bt;
+  d.has_prev = 1;
+  d.layer = l + 1;
+  d.drop_on = drop_on; d.thresh = thresh; d.scale = scale;
+  d.seed = cfg->seed; d.rng_ctr = cfg->rng_ctr; d.ctr_add = (uint32_t)cfg->ctr_add;
+  d.dqkvs = f.da; d.w_all = f.w1; d.dy = f.dz;
+  d.p_out = L.out; d.p_stats = L.bn_stats; d.p_dy = L.dy; d.p_gpart = L.bn_gpart; d.p_gsum = L.bn_gsum;
+  d.p_cnt = L.cnt + 1;
+  const int bmd = D == 64 ? DxGeom<64>::BM : DxGeom<128>::BM;
+  const int gd = gemm_grid((bt->n_cap + bmd - 1) / bmd, 1);
+  if (gd > 256) { set_error("gtr_ffn_bwd: more than 256 partial rows"); return GTR_E_ARG; }
+  if (D == 64) hipLaunchKernelGGL((k_dx<64, DX_CONV>), dim3(gd), dim3(GM_BLOCK), 0, s, d);
+  else hipLaunchKernelGGL((k_dx<128, DX_CONV>), dim3(gd), dim3(GM_BLOCK), 0, s, d);
+  GTR_HIP_CHECK_LAUNCH();
+  return GTR_OK;
+}
+
+extern "C" int gtr_ffn_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l,
+                             float* slab, int n_chunks, int64_t slab_stride, gtr_stream_t stream) {
+  uint32_t thresh;
+  float scale;
+  int drop_on;
+  if (const int rc = ffn_check(cfg, bt, layers, l, "gtr_ffn_wgrad", true, thresh, scale, drop_on)) return rc;
+  const int D = cfg->dim;
+  const gtr_ffn& f = *layers[l].ffn;
+  if (!slab || n_chunks <= 0 || slab_stride < (int64_t)8 * D * D + 5 * D || !f.g2 || !f.da) {
+    set_error("gtr_ffn_wgrad: bad slab / chunks");
+    return GTR_E_ARG;
+  }
+  FfnWK k{};
+  k.bt = *bt;
+  k.layer = l;
+  k.n_chunks = n_chunks;
+  k.drop_on = drop_on; k.thresh = thresh; k.scale = scale;
+  k.seed = cfg->seed; k.rng_ctr = cfg->rng_ctr; k.ctr_add = (uint32_t)cfg->ctr_add;
+  k.y = f.y; k.fa = f.a; k.g2 = f.g2; k.da = f.da; k.slab = slab; k.stride = slab_stride;
+  hipStream_t s = (hipStream_t)stream;
+  if (D == 64) hipLaunchKernelGGL(k_ffn_wgrad<64>, dim3(n_chunks, 2), dim3(GM_BLOCK), 0, s, k);
+  else hipLaunchKernelGGL(k_ffn_wgrad<128>, dim3(n_chunks, 2), dim3(GM_BLOCK), 0, s, k);
   GTR_HIP_CHECK_LAUNCH();
   return GTR_OK;
 }

@@ -54,6 +54,14 @@ class GtrLayer(C.Structure):
         ("bn_stats", P), ("bn_part", P), ("bn_gsum", P), ("bn_gpart", P), ("cnt", P),
         ("dy", P), ("dqkvs", P), ("du", P), ("dlogit", P), ("dagg", P),
         ("bn_part_all", P), ("bn_gpart_all", P), ("nparts_fwd", i32), ("nparts_bwd", i32), ("wfold", P),
+        ("ffn", P),
+    ]
+
+
+class GtrFfn(C.Structure):
+    _fields_ = [
+        ("w1", P), ("b1", P), ("w2", P), ("b2", P), ("y", P), ("a", P), ("z", P), ("dz", P), ("g2", P), ("da", P),
+        ("expansion", i32), ("pad", i32),
     ]
 
 
@@ -93,7 +101,7 @@ class GtrTail(C.Structure):
 
 
 SWEEP_SLOTS = 8
-ABI_VERSION = 5  # GTR_ABI_VERSION of include/gtr.h
+ABI_VERSION = 6  # GTR_ABI_VERSION of include/gtr.h
 
 
 class GtrLazy(C.Structure):
@@ -148,6 +156,9 @@ _SIGS = {
     "gtr_attn_fwd": (C.c_int, [P, P, P, C.c_int, P]),
     "gtr_attn_bwd": (C.c_int, [P, P, P, C.c_int, P]),
     "gtr_qkvs_bwd": (C.c_int, [P, P, P, C.c_int, P, P]),
+    "gtr_ffn_fwd": (C.c_int, [P, P, P, C.c_int, P]),
+    "gtr_ffn_bwd": (C.c_int, [P, P, P, C.c_int, P]),
+    "gtr_ffn_wgrad": (C.c_int, [P, P, P, C.c_int, P, C.c_int, i64, P]),
     "gtr_wgrad": (C.c_int, [P, P, P, P, P, P, P, C.c_int, i64, C.c_int, C.c_int, P]),
     "gtr_adamw_small": (C.c_int, [P, P, P, P, i64, P, C.c_int, P, P]),
     "gtr_contrib_prep": (C.c_int, [P, C.c_int, P, P, P, P, P]),

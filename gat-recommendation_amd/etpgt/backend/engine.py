@@ -45,8 +45,8 @@ class Seg:
 class ParamLayout:
     """Flat layout of the dense (non-table) parameters of a GraphTransformer."""
 
-    def __init__(self, D: int, L_: int, pe_k: int):
-        self.D, self.L, self.K = D, L_, pe_k
+    def __init__(self, D: int, L_: int, pe_k: int, ffn: bool = False):
+        self.D, self.L, self.K, self.ffn = D, L_, pe_k, ffn
         self.segs: dict[str, Seg] = {}
         off = 0
 
@@ -62,6 +62,11 @@ class ParamLayout:
             add(f"{l}.w_beta", (1, 3 * D))
             add(f"{l}.gamma", (D,))
             add(f"{l}.beta", (D,))
+            if ffn:  # ffns.{l}.0 / ffns.{l}.3 (graph_transformer.py:88-100), F = 4 D
+                add(f"{l}.ffn_w1", (4 * D, D))
+                add(f"{l}.ffn_b1", (4 * D,))
+                add(f"{l}.ffn_w2", (D, 4 * D))
+                add(f"{l}.ffn_b2", (D,))
         if pe_k > 0:
             add("pe.w", (D, pe_k))
             add("pe.b", (D,))
@@ -69,6 +74,9 @@ class ParamLayout:
         self.layer_block = 4 * D * D + 4 * D + 3 * D   # slab layout of one layer
         self.pe_block = D * pe_k + D if pe_k > 0 else 0
         self.slab_stride = _al(max(self.layer_block, self.pe_block))
+        # gtr_ffn_wgrad slab of one layer: [dW1 F*D | db1 F | dW2 D*F | db2 D]
+        self.ffn_block = 8 * D * D + 5 * D if ffn else 0
+        self.ffn_stride = _al(self.ffn_block) if ffn else 0
 
     def seg(self, name: str) -> Seg:
         return self.segs[name]
@@ -87,6 +95,10 @@ def model_param_map(model) -> list[tuple[str, torch.nn.Parameter, int]]:
             (f"{l}.w_beta", conv.lin_beta.weight, 0),
             (f"{l}.gamma", bn.weight, 0), (f"{l}.beta", bn.bias, 0),
         ]
+        if getattr(model, "use_ffn", False):
+            ffn = model.ffns[l]
+            out += [(f"{l}.ffn_w1", ffn[0].weight, 0), (f"{l}.ffn_b1", ffn[0].bias, 0),
+                    (f"{l}.ffn_w2", ffn[3].weight, 0), (f"{l}.ffn_b2", ffn[3].bias, 0)]
     if model.use_laplacian_pe:
         out += [("pe.w", model.laplacian_pe.projection.weight, 0), ("pe.b", model.laplacian_pe.projection.bias, 0)]
     return out
@@ -97,7 +109,8 @@ class FlatParams:
 
     def __init__(self, model, device):
         self.model = model
-        self.layout = ParamLayout(model.hidden_dim, model.num_layers, model.laplacian_k if model.use_laplacian_pe else 0)
+        self.layout = ParamLayout(model.hidden_dim, model.num_layers, model.laplacian_k if model.use_laplacian_pe else 0,
+                                  bool(getattr(model, "use_ffn", False)))
         self.device = device
         self.flat = torch.zeros(self.layout.total, dtype=torch.float32, device=device)
         self.map = model_param_map(model)
@@ -194,6 +207,8 @@ class Workspace:
         # instead of one fused launch -- from more row groups than the chip has CUs / 2
         # (the fused kernels re-fetch W_all per 16-row group), D in {64, 128}
         self.split = split_default(D, g) if split is None else (bool(split) and D in (64, 128))
+        if eng.ffn:  # the feed-forward blocks run on the split layer path only
+            self.split = True
         self.dx0 = _f32(n, D, device=dev)
         self.se = _f32(b, D, device=dev)
         self.dse_in = _f32(b, D, device=dev)
@@ -209,7 +224,61 @@ class Workspace:
         self.slab_ptrs = (C.c_void_p * Lc)(*[self.slabs[l].data_ptr() for l in range(Lc)])
         self.wfold = None  # [Lc, g_cap, slab_stride]: per-row-group weight-gradient partials
         self.head = L.GtrHead()
+        self.ffns = None
+        if eng.ffn:
+            self._alloc_ffn(eng, n, parts, g)
         self._fill_layer_structs(eng)
+
+    def _alloc_ffn(self, eng, n, parts, g):
+        """Feed-forward blocks (gtr_ffn per layer), their weight-gradient slabs, and the
+        readout's view of the last layer: an identity BatchNorm layer over ffn.z (statistics
+        0 / 1, gamma 1, beta 0, zero residual; run with dropout 0 and eps 0), so the mean
+        readout reads z as it is and writes d/dz into ffn.dz."""
+        dev = eng.device
+        D, Lc = eng.D, eng.L
+        F = 4 * D
+        self.ffns = []
+        self.ffn_structs = []
+        for l in range(Lc):
+            t = dict(y=_f32(n, D, device=dev), a=_f32(n, F, device=dev), z=_f32(n, D, device=dev),
+                     dz=_f32(n, D, device=dev), g2=_f32(n, D, device=dev), da=_f32(n, F, device=dev))
+            self.ffns.append(t)
+            fs = L.GtrFfn()
+            for f in ("y", "a", "z", "dz", "g2", "da"):
+                setattr(fs, f, t[f].data_ptr())
+            fs.expansion = 4
+            self.ffn_structs.append(fs)
+        self.ffn_slabs = _f32(Lc, self.P, eng.flat.layout.ffn_stride, device=dev)
+        last = self.ffns[Lc - 1]
+        self.ro_ident = dict(
+            xin=_f32(n, D, device=dev),
+            stats=torch.cat([torch.zeros(D), torch.ones(D)]).to(dev),
+            gamma=torch.ones(D, device=dev), beta=torch.zeros(D, device=dev),
+            rmean=torch.zeros(D, device=dev), rvar=torch.ones(D, device=dev),
+            nbt=torch.zeros(1, dtype=torch.int64, device=dev),
+            part=_f32(parts, 1 + 2 * D, device=dev), gsum=_f32(2 * D, device=dev),
+            gpart=_f32(max(g, 512), 2 * D, device=dev),
+            cnt=_i32(8 + 2 * max((parts + 31) // 32, 8), dev),
+        )
+        r = self.ro_ident
+        self.ro_structs = (L.GtrLayer * Lc)()
+        s = self.ro_structs[Lc - 1]
+        s.out, s.xin, s.bn_stats = last["z"].data_ptr(), r["xin"].data_ptr(), r["stats"].data_ptr()
+        s.bn_gamma, s.bn_beta = r["gamma"].data_ptr(), r["beta"].data_ptr()
+        s.bn_rmean, s.bn_rvar, s.bn_nbt = r["rmean"].data_ptr(), r["rvar"].data_ptr(), r["nbt"].data_ptr()
+        s.bn_part, s.bn_gsum, s.bn_gpart, s.cnt = (r["part"].data_ptr(), r["gsum"].data_ptr(),
+                                                   r["gpart"].data_ptr(), r["cnt"].data_ptr())
+        s.dy = last["dz"].data_ptr()
+
+    def readout_args(self, cfg):
+        """(config, layer structs) of the readout: with FFN blocks the identity view of the
+        last block's output (dropout 0, eps 0)."""
+        if self.ffns is None:
+            return cfg, self.structs
+        c = type(cfg).from_buffer_copy(cfg)
+        c.dropout = 0.0
+        c.bn_eps = 0.0
+        return c, self.ro_structs
 
     def enable_wfold(self, eng) -> int:
         """Per-row-group weight-gradient partials for the fused backward (gtr_layer.wfold);
@@ -241,6 +310,11 @@ class Workspace:
             s.bn_rmean = bn.running_mean.data_ptr()
             s.bn_rvar = bn.running_var.data_ptr()
             s.bn_nbt = bn.num_batches_tracked.data_ptr()
+            if self.ffns is not None:
+                fs = self.ffn_structs[l]
+                fs.w1, fs.b1 = eng.flat.seg_ptr(f"{l}.ffn_w1"), eng.flat.seg_ptr(f"{l}.ffn_b1")
+                fs.w2, fs.b2 = eng.flat.seg_ptr(f"{l}.ffn_w2"), eng.flat.seg_ptr(f"{l}.ffn_b2")
+                s.ffn = C.addressof(fs)
 
 
 class Engine:
@@ -259,6 +333,7 @@ class Engine:
         self.L = model.num_layers
         self.K = model.laplacian_k if model.use_laplacian_pe else 0
         self.T = model.num_items
+        self.ffn = bool(getattr(model, "use_ffn", False))
         self.flat = FlatParams(model, device)
         self.rng_ctr = torch.zeros(1, dtype=torch.int32, device=device)
         self.seed = int(torch.randint(0, 2**31 - 1, (1,), generator=torch.Generator().manual_seed(0x5EED)).item())
@@ -380,11 +455,14 @@ class Engine:
         emb = self.fill_embed()
         for l in range(self.L):
             self.layer_fwd(ws, cfg, bs, l, emb, st, split)
+            if ws.ffns is not None:
+                L.check(L.lib().gtr_ffn_fwd(C.byref(cfg), C.byref(bs), ws.structs, l, st), "ffn_fwd")
         self.run_head(ws, cfg, bs, flags, loss_kind, temperature, alpha)
 
     def run_head(self, ws, cfg, bs, flags, loss_kind=0, temperature=1.0, alpha=0.7, dse_out=False, table=None):
         h, tab = self.fill_head(ws, flags, loss_kind, temperature, alpha, dse_out, table)
-        L.check(L.lib().gtr_readout_loss(C.byref(cfg), C.byref(bs), tab, ws.structs, C.byref(h), self.stream()),
+        rcfg, structs = ws.readout_args(cfg)
+        L.check(L.lib().gtr_readout_loss(C.byref(rcfg), C.byref(bs), tab, structs, C.byref(h), self.stream()),
                 "readout_loss")
 
     def fill_head(self, ws, flags, loss_kind=0, temperature=1.0, alpha=0.7, dse_out=False, table=None):
@@ -424,7 +502,14 @@ class Engine:
         lib = L.lib()
         main = torch.cuda.current_stream(self.device)
         st = main.cuda_stream
+        if ws.ffns is not None:
+            side = None  # FFN blocks: every gradient kernel on the main stream
         for l in range(self.L - 1, -1, -1):
+            if ws.ffns is not None:
+                L.check(lib.gtr_ffn_bwd(C.byref(cfg), C.byref(bs), ws.structs, l, st), "ffn_bwd")
+                if wgrad:
+                    L.check(lib.gtr_ffn_wgrad(C.byref(cfg), C.byref(bs), ws.structs, l, ws.ffn_slabs[l].data_ptr(),
+                                              ws.P, self.flat.layout.ffn_stride, st), "ffn_wgrad")
             self.layer_bwd(ws, cfg, bs, l, st, split)
             if wgrad and side is not None and l >= 1:
                 side.wait_stream(main)
@@ -453,6 +538,12 @@ class Engine:
                                        (f"{l}.gamma", g + 4 * D, 1, 0), (f"{l}.beta", g, 1, 0)):
                 s = lay.seg(name)
                 segs.append((s.begin, s.numel, src, stride, np_, lv))
+            if ws.ffns is not None:
+                fb, F = ws.ffn_slabs[l].data_ptr(), 4 * D
+                for name, off in ((f"{l}.ffn_w1", 0), (f"{l}.ffn_b1", F * D), (f"{l}.ffn_w2", F * D + F),
+                                  (f"{l}.ffn_b2", 2 * F * D + F)):
+                    s = lay.seg(name)
+                    segs.append((s.begin, s.numel, fb + 4 * off, lay.ffn_stride, ws.P, 0))
         if K > 0:
             base = ws.pe_slab.data_ptr()
             for name, src in (("pe.w", base), ("pe.b", base + 4 * D * K)):

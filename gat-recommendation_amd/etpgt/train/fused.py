@@ -37,6 +37,9 @@ class FusedTrainStep:
                  lazy: bool = False, sync_bn: bool = False, lagged: bool = False, shard_table: bool = False):
         if loss not in ("bpr", "listwise", "dual", "sampled_softmax"):
             raise ValueError(f"Unknown loss type: {loss}")
+        if getattr(model, "use_ffn", False):
+            raise NotImplementedError("the fused training step covers the optimized model (use_ffn=False); "
+                                      "FFN models train through autograd on the HIP layer kernels (Trainer does this)")
         self.model = model
         self.eng: Engine = model.hip_engine()
         self.dev = self.eng.device

@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GTR_ABI_VERSION 5 /* 5: gtr_config.loss_batch / wfold_stride, gtr_layer.wfold, gtr_segment.live_groups, hdr[6] halo source rows; 4: gtr_step_tail_wgrad on split-K slabs; 3: gtr_config.begin / ctr_add, gtr_tail.rng_inc */
+#define GTR_ABI_VERSION 6 /* 6: gtr_layer.ffn + gtr_ffn_fwd / gtr_ffn_bwd / gtr_ffn_wgrad (the FFN variant); 5: gtr_config.loss_batch / wfold_stride, gtr_layer.wfold, gtr_segment.live_groups, hdr[6] halo source rows; 4: gtr_step_tail_wgrad on split-K slabs; 3: gtr_config.begin / ctr_add, gtr_tail.rng_inc */
 
 #define GTR_OK 0
 #define GTR_E_ARG 1001      /* bad argument / unsupported shape */
@@ -190,7 +190,31 @@ typedef struct gtr_layer {
   float* wfold;              /* gtr_config.wfold_stride > 0: gtr_conv_bwd writes each row group's
                                 split-K partial of this layer's weight gradients (w_all | b_all |
                                 w_beta at the gtr_wgrad slab offsets) at wfold + g * stride     */
+  const struct gtr_ffn* ffn; /* NULL, or this layer's feed-forward block (use_ffn=True; split
+                                layer path only): the next layer's gtr_qkvs_fwd then takes its
+                                input rows from ffn->z as they are, and its gtr_qkvs_bwd writes
+                                d/dz into ffn->dz (no dropout mask, no BatchNorm sums)         */
 } gtr_layer;
+
+/* Feed-forward block of one layer (graph_transformer.py:88-100 _make_ffn, applied at
+ * :160-170): with y = dropout(BN(conv out) + x) the layer's output rows,
+ *   a = y W1^T + b1,  h = dropout(GELU(a)),  z = y + dropout(h W2^T + b2)   (F = 4 D).
+ * GELU is the exact (erf) form of nn.GELU().  Dropout streams: kind 2 = h (element
+ * row*F + j), kind 3 = the block output (row*D + j), per layer and step counter.       */
+typedef struct gtr_ffn {
+  const float* w1;  /* [F, D] ffns.{l}.0.weight  */
+  const float* b1;  /* [F]    ffns.{l}.0.bias    */
+  const float* w2;  /* [D, F] ffns.{l}.3.weight  */
+  const float* b2;  /* [D]    ffns.{l}.3.bias    */
+  float* y;         /* [n_cap, D] block input (saved)                         */
+  float* a;         /* [n_cap, F] pre-activation (saved)                      */
+  float* z;         /* [n_cap, D] block output                                */
+  float* dz;        /* [n_cap, D] d loss / d z                                */
+  float* g2;        /* [n_cap, D] dz * output dropout mask (d / d(h W2^T + b2)) */
+  float* da;        /* [n_cap, F] d loss / d a                                */
+  int32_t expansion; /* F / D: 4 (the factory default)                       */
+  int32_t pad;
+} gtr_ffn;
 
 /* Embedding + LapPE inputs of layer 0. */
 typedef struct gtr_embed {
@@ -272,6 +296,24 @@ int gtr_attn_bwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* la
  * BatchNorm backward sums (bn_gsum), or dx0 at l == 0.                                */
 int gtr_qkvs_bwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l,
                  float* dx0, gtr_stream_t stream);
+
+/* ---- feed-forward block (gtr_layer.ffn; D in {64, 128}, F = 4 D).  Order per layer l:
+ *   forward   gtr_qkvs_fwd(l) -> gtr_attn_fwd(l) -> gtr_ffn_fwd(l)
+ *   backward  gtr_ffn_bwd(l) -> gtr_attn_bwd(l) -> gtr_qkvs_bwd(l)
+ * The readout of a model whose last layer has an FFN reads ffn->z through an identity
+ * BatchNorm layer struct (statistics 0 / 1, gamma 1, beta 0, zero residual, dropout 0). */
+/* y = dropout(BN(out) + xin) of layer l -> ffn->y; a = y W1^T + b1 -> ffn->a;
+ * z = y + dropout(dropout(GELU(a)) W2^T + b2) -> ffn->z.                               */
+int gtr_ffn_fwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l,
+                gtr_stream_t stream);
+/* From ffn->dz: g2 -> ffn->g2, da -> ffn->da, and dy = (dz + da W1) * the layer's output
+ * dropout mask -> layers[l].dy with its BatchNorm backward sums (bn_gsum).              */
+int gtr_ffn_bwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l,
+                gtr_stream_t stream);
+/* Weight-gradient partials of layer l's FFN over n_chunks row chunks:
+ * slab[p * slab_stride + ...] = [dW1 F*D | db1 F | dW2 D*F | db2 D].                    */
+int gtr_ffn_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l,
+                  float* slab, int n_chunks, int64_t slab_stride, gtr_stream_t stream);
 
 /* Weight-gradient partial slabs for layers [l_begin, l_end) (+ LapPE projection
  * when l_begin == 0).

@@ -274,11 +274,20 @@ class RefGraphTransformer(nn.Module):
             pe = getattr(batch, "laplacian_pe", None)
             x = x + (self.laplacian_pe.project(pe) if pe is not None else self.laplacian_pe(batch.x))
         if self.use_ffn:
-            for conv, bn, ffn in zip(self.convs, self.batch_norms, self.ffns):
+            masks = getattr(self, "drop_masks", None) if self.training else None
+            for l, (conv, bn, ffn) in enumerate(zip(self.convs, self.batch_norms, self.ffns)):
                 r = x
-                x = self.dropout_layer(bn(conv(x, edge_index)) + r)
-                r = x
-                x = ffn(x) + r
+                if masks is not None:  # graph_transformer.py:160-170 with the HIP path's masks
+                    conv.attn_mask = masks["attn"][l]
+                    x = (bn(conv(x, edge_index)) + r) * masks["out"][l]
+                    conv.attn_mask = None
+                    r = x
+                    h = ffn[1](ffn[0](x)) * masks["ffn_h"][l]
+                    x = ffn[3](h) * masks["ffn_o"][l] + r
+                else:
+                    x = self.dropout_layer(bn(conv(x, edge_index)) + r)
+                    r = x
+                    x = ffn(x) + r
         else:
             masks = getattr(self, "drop_masks", None) if self.training else None
             for l, (conv, bn) in enumerate(zip(self.convs, self.batch_norms)):
@@ -342,19 +351,22 @@ def hip_mix3(a, b, c) -> np.ndarray:
 
 def hip_drop_stream(kind: int, layer: int, ctr: int) -> int:
     """gtr_common.cuh ``drop_stream``: kind 0 = attention probabilities of a layer,
-    kind 1 = the layer's output (BN + residual)."""
+    kind 1 = the layer's output (BN + residual), kind 2 / 3 = its feed-forward block's
+    hidden / output dropout (gtr.h gtr_ffn)."""
     return int(((kind << 28) ^ (layer << 20) ^ ((ctr * 0x632BE5AB) & 0xFFFFFFFF)) & 0xFFFFFFFF)
 
 
 def hip_dropout_masks(seed: int, ctr: int, p: float, num_layers: int, edge_index, num_nodes: int, dim: int,
-                      heads: int) -> dict:
+                      heads: int, ffn_expansion: int = 0) -> dict:
     """The masks (0 or 1/(1-p)) the HIP step applies at dropout ``p`` with stream counter
     ``ctr``: {"attn": [L] x [E, H] in edge_index order, "out": [L] x [N, D]}.
 
     Element indices follow the kernels: attention (edge, head) pairs are numbered in the
     packed batch's destination order (a stable sort of edge_index by destination,
     etpgt/data/batch.py build_csr) as e*H + h; output elements as row*D + j.  Keep iff
-    mix3(seed, stream, idx) >= uint32(p * 2^32) (p as the fp32 config value)."""
+    mix3(seed, stream, idx) >= uint32(p * 2^32) (p as the fp32 config value).
+    ``ffn_expansion`` > 0 adds the feed-forward blocks' masks: "ffn_h" [N, F] (kind 2,
+    row*F + j, after GELU) and "ffn_o" [N, D] (kind 3, row*D + j, after the second Linear)."""
     pf = float(np.float32(p))
     thresh = np.uint64(int(pf * 4294967296.0))
     scale = float(np.float32(1.0 / (1.0 - pf)))
@@ -371,6 +383,13 @@ def hip_dropout_masks(seed: int, ctr: int, p: float, num_layers: int, edge_index
         ho = hip_mix3(seed, hip_drop_stream(1, l, ctr), idx_out)
         out["attn"].append(torch.from_numpy(np.where(ha >= thresh, scale, 0.0).astype(np.float32)))
         out["out"].append(torch.from_numpy(np.where(ho >= thresh, scale, 0.0).astype(np.float32)))
+        if ffn_expansion > 0:
+            F = ffn_expansion * dim
+            idx_h = np.arange(num_nodes * F, dtype=np.int64).reshape(num_nodes, F)
+            hh = hip_mix3(seed, hip_drop_stream(2, l, ctr), idx_h)
+            hf = hip_mix3(seed, hip_drop_stream(3, l, ctr), idx_out)
+            out.setdefault("ffn_h", []).append(torch.from_numpy(np.where(hh >= thresh, scale, 0.0).astype(np.float32)))
+            out.setdefault("ffn_o", []).append(torch.from_numpy(np.where(hf >= thresh, scale, 0.0).astype(np.float32)))
     return out
 
 

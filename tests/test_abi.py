@@ -46,7 +46,7 @@ def test_python_binding_matches_header(libpath):
 
     assert set(_lib.EXPORTS) == set(header_functions())
     lib = _lib.lib()
-    assert lib.gtr_abi_version() == _lib.ABI_VERSION == 5
+    assert lib.gtr_abi_version() == _lib.ABI_VERSION == 6
     assert lib.gtr_version() >= 100
 
 
@@ -55,7 +55,7 @@ def test_struct_layouts_match_header():
     from etpgt.backend import _lib
 
     src = open(HEADER).read()
-    for cname, py in (("gtr_batch", _lib.GtrBatch), ("gtr_config", _lib.GtrConfig), ("gtr_layer", _lib.GtrLayer),
+    for cname, py in (("gtr_batch", _lib.GtrBatch), ("gtr_config", _lib.GtrConfig), ("gtr_layer", _lib.GtrLayer), ("gtr_ffn", _lib.GtrFfn),
                       ("gtr_embed", _lib.GtrEmbed), ("gtr_head", _lib.GtrHead), ("gtr_segment", _lib.GtrSegment),
                       ("gtr_adam", _lib.GtrAdam), ("gtr_tail", _lib.GtrTail), ("gtr_dp_layout", _lib.GtrDpLayout),
                       ("gtr_sweep", _lib.GtrSweep), ("gtr_sessions", _lib.GtrSessions),
