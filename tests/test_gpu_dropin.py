@@ -120,3 +120,23 @@ def test_train_baseline_counterpart_one_epoch_matches_oracle(tmp_path):
     r10 = compute_recall_at_k(torch.cat(preds)[:, :10], torch.cat(tg), k=10)
     got = hist["val_metrics"][0]["recall@10"]
     assert abs(got - r10) <= 1.0 / Sv + 1e-9, (got, r10)
+
+
+def test_train_baseline_ffn_model_trains_one_epoch(tmp_path):
+    """``--model graph_transformer`` (the FFN variant, create_graph_transformer defaults
+    apart from the dimensions) trains through the Trainer's autograd path on the HIP
+    layer + FFN kernels: one epoch, finite loss, a checkpoint with the reference keys."""
+    d = write_csvs(tmp_path)
+    args = ["--model", "graph_transformer", "--train-sessions", str(d / "train.csv"),
+            "--val-sessions", str(d / "val.csv"), "--graph-edges", str(d / "graph_edges.csv"),
+            "--embedding-dim", "64", "--hidden-dim", "64", "--num-layers", "2", "--num-heads", "2",
+            "--batch-size", "16", "--num-negatives", "5", "--max-epochs", "1",
+            "--num-workers", "0", "--output-dir", str(tmp_path / "out")]
+    trainer = _script().main(args)
+    assert trainer._fused is None and trainer.model.use_ffn
+    with open(tmp_path / "out" / "graph_transformer" / "history.json") as f:
+        hist = json.load(f)
+    assert len(hist["train_loss"]) == 1 and np.isfinite(hist["train_loss"][0])
+    ck = torch.load(tmp_path / "out" / "graph_transformer" / "checkpoint_latest.pt", map_location="cpu",
+                    weights_only=True)
+    assert "ffns.1.3.weight" in ck["model_state_dict"]
