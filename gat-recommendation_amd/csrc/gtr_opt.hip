@@ -159,10 +159,10 @@ __device__ __forceinline__ void sweep_body(int blk, int nblk, int64_t nvec, int 
     const int64_t row = i >> vpr_log2;
     if (stamp[row] == t) continue;
     float4 p = sw_ld(table + i), mm = sw_ld(m + i), vv = sw_ld(v + i);  // streaming: spare L2
-    st.apply(p.x, mm.x, vv.x, 0.0f);
-    st.apply(p.y, mm.y, vv.y, 0.0f);
-    st.apply(p.z, mm.z, vv.z, 0.0f);
-    st.apply(p.w, mm.w, vv.w, 0.0f);
+    st.apply_zero(p.x, mm.x, vv.x);
+    st.apply_zero(p.y, mm.y, vv.y);
+    st.apply_zero(p.z, mm.z, vv.z);
+    st.apply_zero(p.w, mm.w, vv.w);
     sw_st(table + i, p);
     sw_st(m + i, mm);
     sw_st(v + i, vv);
@@ -219,10 +219,10 @@ __device__ __forceinline__ void lazy_catch_up_lanes(float4* P, float4* M, float4
       st.inv_bc2 = __shfl(cc.y, gbase + q);
 #pragma unroll
       for (int k = 0; k < NP; ++k) {
-        st.apply(p[k].x, m[k].x, v[k].x, 0.0f);
-        st.apply(p[k].y, m[k].y, v[k].y, 0.0f);
-        st.apply(p[k].z, m[k].z, v[k].z, 0.0f);
-        st.apply(p[k].w, m[k].w, v[k].w, 0.0f);
+        st.apply_zero(p[k].x, m[k].x, v[k].x);
+        st.apply_zero(p[k].y, m[k].y, v[k].y);
+        st.apply_zero(p[k].z, m[k].z, v[k].z);
+        st.apply_zero(p[k].w, m[k].w, v[k].w);
       }
     }
   }
@@ -355,14 +355,97 @@ __global__ __launch_bounds__(GTR_BEGIN_BLOCK) void k_step_begin_lazy(gtr_batch b
   }
 }
 
-// Lazy catch-up for the large-batch (radix) path: 16 lanes per contribution slot.
+// Zero-gradient catch-up of a row by a whole wave: lane holds EPL consecutive floats of
+// p / m / v (D = 64 * EPL; D = 32: the upper lanes idle).  Every lane of the wave follows
+// the same row, so the chain of missed steps is wave-uniform: no lane waits on another
+// row's longer gap, and the per-step scalars (64 steps per load, one per lane) reach the
+// update through v_readlane into scalar registers instead of LDS shuffles.
+template <int EPL>
+struct RowRegs {
+  float p[EPL], m[EPL], v[EPL];
+};
+
+template <int EPL>
+__device__ __forceinline__ void row_load(RowRegs<EPL>& r, const gtr_lazy& lz, int key, int D, int lane) {
+  const int c = lane * EPL;
+  const size_t o = (size_t)key * D + c;
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) {
+    r.p[k] = c < D ? lz.table[o + k] : 0.0f;
+    r.m[k] = c < D ? lz.m[o + k] : 0.0f;
+    r.v[k] = c < D ? lz.v[o + k] : 0.0f;
+  }
+}
+
+template <int EPL>
+__device__ __forceinline__ void row_catch_up_store(RowRegs<EPL>& r, const gtr_lazy& lz, int key, int D, int old,
+                                                   int32_t t, int lane, AdamStep st) {
+  for (int t0 = old + 1; t0 <= t - 1; t0 += 64) {
+    const int cnt = min(64, t - t0);
+    const float2 cc = lane < cnt ? reinterpret_cast<const float2*>(lz.consts)[t0 + lane] : make_float2(0.f, 0.f);
+    for (int q = 0; q < cnt; ++q) {
+      st.step_size = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cc.x), q));
+      st.inv_bc2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cc.y), q));
+#pragma unroll
+      for (int k = 0; k < EPL; ++k) st.apply_zero(r.p[k], r.m[k], r.v[k]);
+    }
+  }
+  const int c = lane * EPL;
+  if (c < D) {
+    const size_t o = (size_t)key * D + c;
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) { lz.table[o + k] = r.p[k]; lz.m[o + k] = r.m[k]; lz.v[o + k] = r.v[k]; }
+  }
+}
+
+// Lazy catch-up for the large-batch (radix) path.  A wave takes `spw` (<= 64) contribution
+// slots at a time (grid-strided): each lane claims its slot's row (stamp exchange, all in
+// flight together), then the wave brings the claimed rows forward one after the other,
+// loading the next claimed row while the current one runs its chain of missed steps.
+// spw trades claim parallelism against the rows a wave walks serially (host: ~2 tasks per
+// resident wave).
+template <int EPL>
 __global__ __launch_bounds__(GTR_BLOCK) void k_lazy_catchup(gtr_batch bt, int T, int D, int32_t* stamp,
-                                                            const int64_t* step_dev, gtr_lazy lz) {
-  const int gid = blockIdx.x * GTR_BLOCK + threadIdx.x;
+                                                            const int64_t* step_dev, gtr_lazy lz, int spw) {
+  const int lane = threadIdx.x & 63;
   const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
-  const int slot = gid / 16;
-  const int key = slot < m_cap ? contrib_key(bt, T, slot, bt.hdr[0], bt.hdr[1]) : T;
-  lazy_claim_row(key, T, D, (int32_t)(*step_dev + 1), threadIdx.x & 15, (threadIdx.x & 63) & ~15, stamp, lz);
+  const int N = bt.hdr[0], B = bt.hdr[1];
+  const int32_t t = (int32_t)(*step_dev + 1);
+  const gtr_adam& o = lz.opt;
+  AdamStep st;
+  st.lr = o.lr; st.b1 = o.beta1; st.b2 = o.beta2; st.eps = o.eps; st.wd = o.weight_decay;
+  st.decoupled = o.decoupled;
+  st.decay_mul = (float)(1.0 - (double)o.lr * (double)o.weight_decay);
+  st.step_size = 0.0f;
+  st.inv_bc2 = 0.0f;
+  const int nw = gridDim.x * (GTR_BLOCK / 64);
+  for (int base = (blockIdx.x * (GTR_BLOCK / 64) + (threadIdx.x >> 6)) * spw; base < m_cap; base += nw * spw) {
+    const int slot = base + lane;
+    const int key = (lane < spw && slot < m_cap) ? contrib_key(bt, T, slot, N, B) : T;
+    int old = t - 1;
+    if (key > 0 && key < T) old = atomicExch(stamp + key, t - 1);
+    uint64_t todo = __ballot(old < t - 1);
+    if (!todo) continue;
+    int i = __builtin_ctzll(todo);
+    int k_cur = __builtin_amdgcn_readlane(key, i);
+    RowRegs<EPL> cur, nxt;
+    row_load<EPL>(cur, lz, k_cur, D, lane);
+    while (true) {
+      const int o_cur = __builtin_amdgcn_readlane(old, i);
+      todo &= todo - 1;
+      int i_n = 0, k_n = 0;
+      if (todo) {  // the next claimed row's loads fly during this row's chain
+        i_n = __builtin_ctzll(todo);
+        k_n = __builtin_amdgcn_readlane(key, i_n);
+        row_load<EPL>(nxt, lz, k_n, D, lane);
+      }
+      row_catch_up_store<EPL>(cur, lz, k_cur, D, o_cur, t, lane, st);
+      if (!todo) break;
+      cur = nxt;
+      i = i_n;
+      k_cur = k_n;
+    }
+  }
 }
 
 __global__ void k_counters_lazy(int64_t* step_dev, uint32_t* rng_ctr, gtr_lazy lz) {
@@ -1416,6 +1499,19 @@ int gtr_dp_union_stamp(const int32_t* keys_all, int64_t n, int num_items, int32_
   return GTR_OK;
 }
 
+// Grid of k_lazy_catchup: 8 workgroups (32 waves) per CU; GTR_CATCHUP_BLOCKS overrides.
+static int lazy_catchup_blocks() {
+  static int blocks = 0;
+  if (blocks <= 0) {
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    const char* e = getenv("GTR_CATCHUP_BLOCKS");
+    blocks = e && atoi(e) > 0 ? atoi(e) : 8 * cus;
+  }
+  return blocks;
+}
+
 int gtr_step_begin_lazy(const gtr_batch* bt, int num_items, int dim, int32_t* keys, int32_t* vals, int32_t* skeys,
                         int32_t* svals, int32_t* stamp, int64_t* step_dev, uint32_t* rng_ctr, void* tmp,
                         size_t tmp_bytes, const gtr_lazy* lazy, gtr_stream_t stream) {
@@ -1437,9 +1533,19 @@ int gtr_step_begin_lazy(const gtr_batch* bt, int num_items, int dim, int32_t* ke
   if (rc) return rc;
   rc = gtr_contrib_sort(keys, vals, skeys, svals, m_cap, num_items, tmp, tmp_bytes, stream);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_lazy_catchup, dim3((unsigned)(((int64_t)m_cap * 16 + GTR_BLOCK - 1) / GTR_BLOCK)),
-                     dim3(GTR_BLOCK), 0, s, *bt, num_items, dim, stamp, step_dev, *lazy);
-  GTR_HIP_CHECK_LAUNCH();
+  {
+    const int blocks = lazy_catchup_blocks();
+    const int64_t tasks_per_wave = 2, waves = (int64_t)blocks * (GTR_BLOCK / 64);
+    int spw = 1;
+    while (spw < 64 && (int64_t)spw * 2 * waves * tasks_per_wave <= m_cap) spw *= 2;
+    if (const char* e = getenv("GTR_CATCHUP_SPW")) spw = std::max(1, std::min(64, atoi(e)));
+    const int spb = spw * (GTR_BLOCK / 64);
+    const int grid = std::max(1, std::min((m_cap + spb - 1) / spb, blocks));
+    if (dim <= 64) hipLaunchKernelGGL(k_lazy_catchup<1>, dim3(grid), dim3(GTR_BLOCK), 0, s, *bt, num_items, dim, stamp, step_dev, *lazy, spw);
+    else if (dim == 128) hipLaunchKernelGGL(k_lazy_catchup<2>, dim3(grid), dim3(GTR_BLOCK), 0, s, *bt, num_items, dim, stamp, step_dev, *lazy, spw);
+    else hipLaunchKernelGGL(k_lazy_catchup<4>, dim3(grid), dim3(GTR_BLOCK), 0, s, *bt, num_items, dim, stamp, step_dev, *lazy, spw);
+    GTR_HIP_CHECK_LAUNCH();
+  }
   hipLaunchKernelGGL(k_counters_lazy, dim3(1), dim3(1), 0, s, step_dev, rng_ctr, *lazy);
   GTR_HIP_CHECK_LAUNCH();
   return GTR_OK;
