@@ -324,6 +324,7 @@ def main():
             "vs_baseline": None,
             "dtype": "fp32",
             "gemm_precision": gemm_mode(D),
+            "build": build_provenance(),
             "data": ("synthetic Yoochoose-scale" if cfg.get("scale") else "synthetic RetailRocket-shaped")
                     + " sessions/graph (seed 42), random-init weights",
             "config": {
@@ -736,6 +737,17 @@ def recall_parity(cfg, data, T, dev, steps, n_val, B=32):
     }
     out["abs_diff_recall@10"] = round(abs(out["gpu"]["recall@10"] - out["oracle"]["recall@10"]), 5)
     return out
+
+
+def build_provenance() -> dict:
+    """Which binary ran: the source hash compiled into the loaded libgtr_hip.so, this
+    tree's source hash, and the library's path and modification time."""
+    from etpgt.backend import _lib
+
+    lib_hash, tree_hash = _lib.library_source_hash(), _lib.source_hash()
+    return {"lib": os.path.relpath(_lib.LIB_PATH, os.path.dirname(os.path.abspath(__file__))),
+            "lib_source_hash": lib_hash, "tree_source_hash": tree_hash, "built_from_tree": lib_hash == tree_hash,
+            "lib_mtime_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(os.path.getmtime(_lib.LIB_PATH)))}
 
 
 def c1_quick(dev, reps: int) -> dict:

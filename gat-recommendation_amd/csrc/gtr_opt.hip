@@ -1311,6 +1311,10 @@ int gtr_tail_carry_floats(int m_cap, int dim) {
 int gtr_version(void) { return 100; }
 int gtr_readout_grid(int b_cap) { return b_cap < 1 ? 1 : (b_cap > 256 ? 256 : b_cap); }
 int gtr_abi_version(void) { return GTR_ABI_VERSION; }
+#ifndef GTR_SRC_HASH
+#define GTR_SRC_HASH "unknown"
+#endif
+const char* gtr_source_hash(void) { return GTR_SRC_HASH; }
 const char* gtr_last_error(void) { return gtr::g_err; }
 
 int gtr_device_check(int device) {

@@ -147,6 +147,7 @@ SMALL_MAX_SEG = 48
 _SIGS = {
     "gtr_version": (C.c_int, []),
     "gtr_abi_version": (C.c_int, []),
+    "gtr_source_hash": (C.c_char_p, []),
     "gtr_last_error": (C.c_char_p, []),
     "gtr_device_check": (C.c_int, [C.c_int]),
     "gtr_conv_fwd": (C.c_int, [P, P, P, P, C.c_int, P]),
@@ -230,18 +231,16 @@ def lib():
 
 def source_hash() -> str:
     """Hash of the library's sources (csrc/*.hip, *.cuh, include/gtr.h).  Profiles
-    record it, so a measurement taken on other kernels is recognisable as stale."""
-    import glob
-    import hashlib
+    record it, so a measurement taken on other kernels is recognisable as stale; the
+    library carries the hash of the sources it was built from (gtr_source_hash)."""
+    from etpgt.backend._srchash import source_hash as _h
 
-    h = hashlib.sha256()
-    files = sorted(glob.glob(os.path.join(PKG_ROOT, "csrc", "*.hip")) + glob.glob(os.path.join(PKG_ROOT, "csrc", "*.cuh"))
-                   + [os.path.join(os.path.dirname(PKG_ROOT), "include", "gtr.h")])
-    for f in files:
-        h.update(os.path.basename(f).encode())
-        with open(f, "rb") as fh:
-            h.update(fh.read())
-    return h.hexdigest()[:16]
+    return _h()
+
+
+def library_source_hash() -> str:
+    """The source hash compiled into the loaded libgtr_hip.so."""
+    return lib().gtr_source_hash().decode()
 
 
 def check(status: int, what: str = "") -> None:

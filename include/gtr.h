@@ -250,6 +250,8 @@ typedef struct gtr_head {
 
 int gtr_version(void);
 int gtr_abi_version(void);
+/* Hash of the sources the library was built from (etpgt/backend/_srchash.py). */
+const char* gtr_source_hash(void);
 const char* gtr_last_error(void);
 /* 0 if `device` is a gfx950 (MI355X) device. */
 int gtr_device_check(int device);

@@ -116,3 +116,12 @@ def test_lap_plan_is_nnz_balanced(libpath):
     bad = np.array([0, 5, 3], np.int32)
     assert lib.gtr_lap_plan(bad.ctypes.data, 2, 128, None, ctypes.byref(ni), None, ctypes.byref(ns),
                             ctypes.byref(npart)) != 0
+
+
+def test_library_built_from_this_tree(libpath):
+    """The loaded libgtr_hip.so carries the hash of the sources it was compiled from
+    (Makefile -> gtr_source_hash): it must be this tree's, so a stale binary never runs
+    the tests or the bench (rebuild: make -C gat-recommendation_amd/csrc)."""
+    from etpgt.backend import _lib
+
+    assert _lib.library_source_hash() == _lib.source_hash()
