@@ -104,7 +104,7 @@ class GraphTransformerFn(torch.autograd.Function):
     def forward(ctx, eng, caps, blob, node_pe, B, training, need_grad, table, *params):
         eng.check_intact()
         need_grad = bool(need_grad) and training
-        ws = eng.workspace(caps, fresh=need_grad)
+        ws = eng.acquire_workspace(caps) if need_grad else eng.workspace(caps)
         rng = torch.empty(1, dtype=torch.int32, device=eng.device)
         rng.copy_(eng.rng_ctr)
         if training:
@@ -115,6 +115,7 @@ class GraphTransformerFn(torch.autograd.Function):
         eng.run_forward(ws, cfg, bs, L.RO_FWD)
         se = ws.se[:B].clone()
         ctx.eng = None
+        ctx.done = False
         if need_grad:
             ctx.eng, ctx.ws, ctx.cfg, ctx.bs, ctx.B = eng, ws, cfg, bs, B
             ctx.keep = (blob, node_pe, rng)
@@ -122,6 +123,9 @@ class GraphTransformerFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dse):
+        if ctx.done:
+            raise RuntimeError("the GraphTransformer's saved activations were released after the first backward "
+                               "(backward twice / retain_graph is not supported on the HIP path)")
         if ctx.eng is None:
             raise RuntimeError("backward through the GraphTransformer requires train() mode "
                                "(BatchNorm batch statistics) and grad mode at forward time")
@@ -136,6 +140,8 @@ class GraphTransformerFn(torch.autograd.Function):
         L.check(L.lib().gtr_scatter_rows(C.byref(bs), eng.D, 0, ws.dx0.data_ptr(), None, None, dtab.data_ptr(),
                                          eng.stream()), "scatter_rows")
         grads = eng.flat.grad_views(flat_grad)
+        ctx.done = True
+        eng.release_workspace(ws)  # the gradients above are fresh tensors; ws may serve the next forward
         return (None, None, None, None, None, None, None, dtab, *grads)
 
 
