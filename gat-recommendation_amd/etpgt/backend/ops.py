@@ -24,6 +24,23 @@ def _dev_i32(t: torch.Tensor, device) -> torch.Tensor:
     return t.to(device=device, dtype=torch.int32).contiguous()
 
 
+_HDR: dict = {}
+
+
+def _score_hdr(B: int, n: int, device) -> tuple[torch.Tensor, torch.Tensor]:
+    """Batch header + zero session pointers of a scoring-only launch, cached per shape: a
+    fresh torch.tensor(..., device=cuda) every step is a host-to-device copy that waits
+    for the stream (the host would stall behind every queued kernel)."""
+    key = (str(device), int(B), int(n))
+    t = _HDR.get(key)
+    if t is None:
+        if len(_HDR) > 64:
+            _HDR.clear()
+        hdr = torch.tensor([0, B, 0, n, 0, 0, 0, 0], dtype=torch.int32).to(device)
+        t = _HDR[key] = (hdr, torch.zeros(B + 1, dtype=torch.int32, device=device))
+    return t
+
+
 class _ScoreLossFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, se, table, target, negatives, kind, temperature, alpha):
@@ -38,8 +55,7 @@ class _ScoreLossFn(torch.autograd.Function):
         se_c = se.detach().float().contiguous()
         tgt = _dev_i32(target.reshape(-1), dev)
         neg = _dev_i32(negatives.reshape(-1), dev)
-        hdr = torch.tensor([0, B, 0, n, 0, 0, 0, 0], dtype=torch.int32, device=dev)
-        node_ptr = torch.zeros(B + 1, dtype=torch.int32, device=dev)
+        hdr, node_ptr = _score_hdr(B, n, dev)
         bs = L.GtrBatch()
         bs.hdr, bs.node_ptr, bs.target, bs.negatives = hdr.data_ptr(), node_ptr.data_ptr(), tgt.data_ptr(), neg.data_ptr()
         bs.n_cap, bs.b_cap, bs.e_cap, bs.n_neg = 1, B, 1, n
