@@ -38,8 +38,12 @@ class FusedTrainStep:
         if loss not in ("bpr", "listwise", "dual", "sampled_softmax"):
             raise ValueError(f"Unknown loss type: {loss}")
         if getattr(model, "use_ffn", False):
-            raise NotImplementedError("the fused training step covers the optimized model (use_ffn=False); "
-                                      "FFN models train through autograd on the HIP layer kernels (Trainer does this)")
+            from etpgt.train.distributed import world_info as _wi
+
+            multi = bool(data_parallel) if data_parallel is not None else _wi(process_group)[1] > 1
+            if multi or shard_table or sync_bn or os.environ.get("GTR_TAILW") == "1":
+                raise NotImplementedError("the FFN variant (use_ffn=True) trains on one GPU: no data-parallel / "
+                                          "row-sharded / SyncBN step, no GTR_TAILW")
         self.model = model
         self.eng: Engine = model.hip_engine()
         self.dev = self.eng.device
@@ -61,6 +65,7 @@ class FusedTrainStep:
             raise ValueError("the row-sharded table keeps its own lazy stamps (no lazy/lagged option)")
         self.data_parallel = (self.world > 1) if data_parallel is None else bool(data_parallel)
         self.data_parallel = self.data_parallel or self.shard_table
+
         # SyncBN: BatchNorm statistics over every rank's batch (all-gathered partials per
         # BatchNorm), so N ranks train exactly like one GPU on the concatenated batch
         self.sync_bn = bool(sync_bn)

@@ -46,9 +46,27 @@ def run(data, D, H, L, B, n_neg, steps, warmup):
         loss = step(batches[i % len(batches)])
     torch.cuda.synchronize()
     ms = 1e3 * (time.perf_counter() - t0) / steps
-    return {"model": "graph_transformer (use_ffn=True, ffn_expansion=4)", "dim": D, "heads": H, "layers": L,
-            "batch": B, "negatives": n_neg, "ms_per_step": round(ms, 4), "sessions_per_s": round(B / ms * 1e3, 1),
-            "final_loss": round(float(loss), 5), "path": "autograd (GraphTransformerFn) + torch.optim.AdamW"}
+    out = {"model": "graph_transformer (use_ffn=True, ffn_expansion=4)", "dim": D, "heads": H, "layers": L,
+           "batch": B, "negatives": n_neg, "ms_per_step": round(ms, 4), "sessions_per_s": round(B / ms * 1e3, 1),
+           "final_loss": round(float(loss), 5), "path": "autograd (GraphTransformerFn) + torch.optim.AdamW"}
+    # the fused step (one captured hipGraph per step, the batch built inside it: the Trainer's
+    # path with a DeviceSessionLoader)
+    from etpgt.train.fused import FusedTrainStep
+
+    fs = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5, loss="bpr")
+    fbld = GpuBatchBuilder(GpuSessionStore.from_synthetic(data, "cuda"), B, n_neg, seed=6)
+    fs.attach_builder(fbld, num_batches=steps + warmup)
+    for _ in range(warmup):
+        fs.run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fl = fs.run()
+    torch.cuda.synchronize()
+    fms = 1e3 * (time.perf_counter() - t0) / steps
+    out["fused"] = {"ms_per_step": round(fms, 4), "sessions_per_s": round(B / fms * 1e3, 1),
+                    "final_loss": round(float(fl), 5), "path": "FusedTrainStep (captured step, device-built batches)"}
+    return out
 
 
 def main():

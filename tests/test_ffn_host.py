@@ -65,12 +65,14 @@ def test_oracle_ffn_masks_shapes_and_rate():
     assert "ffn_h" not in R.hip_dropout_masks(987654321, 3, p, 2, ei, N, D, H)
 
 
-def test_ffn_models_refuse_the_fused_step_and_unsupported_shapes():
+def test_ffn_models_refuse_multi_gpu_fused_steps_and_unsupported_shapes():
     from etpgt.train.fused import FusedTrainStep
 
     m = create_graph_transformer(50, embedding_dim=64, hidden_dim=64, num_layers=2, num_heads=2, use_ffn=True)
     with pytest.raises(NotImplementedError, match="use_ffn"):
-        FusedTrainStep(m)
+        FusedTrainStep(m, data_parallel=True)
+    with pytest.raises(NotImplementedError, match="use_ffn"):
+        FusedTrainStep(m, shard_table=True)
     bad = create_graph_transformer(50, embedding_dim=256, hidden_dim=256, num_layers=2, num_heads=4, use_ffn=True)
     with pytest.raises(NotImplementedError, match="hidden_dim 64 / 128"):
         bad._check_supported()

@@ -164,8 +164,34 @@ def test_ffn_adamw_steps_match_oracle():
         assert_close(p, rp[name], rtol=1e-3, name=name, floor=2e-3 * 5)
 
 
+@pytest.mark.parametrize("D,H,K,B,loss", [(64, 2, 0, 32, "bpr"), (128, 4, 16, 300, "listwise")])
+def test_ffn_fused_step_matches_oracle(D, H, K, B, loss):
+    """The fused (captured) training step on an FFN model: five steps of the whole step
+    (forward, loss, backward, dense-equivalent AdamW on the table, the FFN weights among
+    the small parameters) against the oracle trainer, losses every step and every trained
+    parameter."""
+    from etpgt.train.fused import FusedTrainStep
+
+    T = data().table_rows
+    n = 5 if loss == "bpr" else 20
+    m, ref = make_ffn_pair(T, D, H, K=K, seed=21)
+    m.train(); ref.train()
+    step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5, loss=loss)
+    ropt = torch.optim.AdamW(ref.parameters(), lr=1e-3, weight_decay=1e-5)
+    for i, sb in enumerate(batches(data(), B, n, 5, seed=37)):
+        hl = float(step(sb.to("cuda")))
+        rl = R.ref_train_step(ref, ref_batch(sb), ropt, loss)
+        assert abs(hl - float(rl)) <= 1e-4 * max(1.0, abs(float(rl))), (i, hl, float(rl))
+    step.sync_table() if hasattr(step, "sync_table") else None
+    rp = dict(ref.named_parameters())
+    for name, p in m.named_parameters():
+        assert_close_norm(p, rp[name], rtol=1e-3, name=name)
+        assert_close(p, rp[name], rtol=1e-3, name=name, floor=2e-3 * 5)
+
+
 def test_ffn_trainer_runs_autograd_path(tmp_path):
-    """The drop-in Trainer trains an FFN model: no fused step, one epoch on device."""
+    """The drop-in Trainer trains an FFN model on the autograd path (fused=False) for one
+    epoch on device."""
     from etpgt.train.trainer import Trainer
 
     data_ = data()
@@ -173,7 +199,7 @@ def test_ffn_trainer_runs_autograd_path(tmp_path):
     m, _ = make_ffn_pair(T, 64, 2, seed=17)
     loader = [sb for sb in batches(data_, 32, 5, 4, seed=31)]
     opt = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-5)
-    tr = Trainer(m, loader, loader, opt, device="cuda", output_dir=tmp_path, max_epochs=1)
+    tr = Trainer(m, loader, loader, opt, device="cuda", output_dir=tmp_path, max_epochs=1, fused=False)
     loss = tr.train_epoch()
     assert tr._fused is None
     assert loss == loss and loss > 0
