@@ -82,7 +82,7 @@ class Trainer:
         spec = _fused_loss_spec(self.loss_fn)
         opt = self.optimizer
         ok = (isinstance(self.model, GraphTransformer) and torch.device(self.device).type == "cuda"
-              and not self.model.use_ffn
+              and not (self.model.use_ffn and self.world > 1)
               and spec is not None and type(opt) in (torch.optim.AdamW, torch.optim.Adam)
               and len(opt.param_groups) == 1 and not opt.state
               and not opt.param_groups[0].get("amsgrad", False)

@@ -124,7 +124,7 @@ def test_train_baseline_counterpart_one_epoch_matches_oracle(tmp_path):
 
 def test_train_baseline_ffn_model_trains_one_epoch(tmp_path):
     """``--model graph_transformer`` (the FFN variant, create_graph_transformer defaults
-    apart from the dimensions) trains through the Trainer's autograd loop on the HIP split
+    apart from the dimensions) trains through the Trainer's fused step on the HIP split
     layer + FFN kernels: one epoch, finite loss, a checkpoint with the reference keys."""
     d = write_csvs(tmp_path)
     args = ["--model", "graph_transformer", "--train-sessions", str(d / "train.csv"),
@@ -133,7 +133,7 @@ def test_train_baseline_ffn_model_trains_one_epoch(tmp_path):
             "--batch-size", "16", "--num-negatives", "5", "--max-epochs", "1",
             "--num-workers", "0", "--output-dir", str(tmp_path / "out")]
     trainer = _script().main(args)
-    assert trainer._fused is None and trainer.model.use_ffn
+    assert trainer._fused is not None and trainer.model.use_ffn
     with open(tmp_path / "out" / "graph_transformer" / "history.json") as f:
         hist = json.load(f)
     assert len(hist["train_loss"]) == 1 and np.isfinite(hist["train_loss"][0])
