@@ -339,7 +339,7 @@ class Engine:
         self.seed = int(torch.randint(0, 2**31 - 1, (1,), generator=torch.Generator().manual_seed(0x5EED)).item())
         self.embed = L.GtrEmbed()
         self._ws_cache: dict[Caps, Workspace] = {}
-        self._ws_free: dict[Caps, list[Workspace]] = {}  # autograd workspaces whose backward has run
+        self._ws_free: dict[Caps, list] = {}  # (workspace, release event) whose backward has run
 
     # ------------------------------------------------------------------ helpers
     def check_intact(self):
@@ -378,15 +378,23 @@ class Engine:
     def acquire_workspace(self, caps: Caps) -> Workspace:
         """A workspace owned by one autograd forward until its backward has run: reused
         from the free list (release_workspace) instead of allocating ~40 buffers per step.
-        Kernels of the next forward queue behind the released workspace's last use on the
-        same stream."""
+        The release recorded an event on the stream of the backward that last used the
+        workspace; the acquiring stream waits on it, so a forward on another stream (or
+        under another ``torch.cuda.stream`` context) cannot overwrite buffers a queued
+        backward still reads."""
         free = self._ws_free.get(caps)
-        return free.pop() if free else self.workspace(caps, fresh=True)
+        if not free:
+            return self.workspace(caps, fresh=True)
+        ws, ev = free.pop()
+        torch.cuda.current_stream(self.device).wait_event(ev)
+        return ws
 
     def release_workspace(self, ws: Workspace) -> None:
         free = self._ws_free.setdefault(ws.caps, [])
         if len(free) < 2:
-            free.append(ws)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self.device))
+            free.append((ws, ev))
 
     def config(self, ws: Workspace, training: bool) -> L.GtrConfig:
         m = self.model

@@ -134,12 +134,19 @@ class GpuBatchBuilder:
         sess = self.order_h[idx]
         return self.store.nodes[sess].sum(1), self.store.edges[sess].sum(1)
 
-    def plan_caps(self, num_batches: int | None = None, position: int = 0) -> Caps:
-        """Capacities covering the next ``num_batches`` batches (default: one epoch)."""
+    def plan_caps(self, num_batches: int | None = None, position: int = 0, extra=()) -> Caps:
+        """Capacities covering the next ``num_batches`` batches (default: one epoch) and
+        every ``(position, sessions)`` window in ``extra`` (e.g. a data-parallel rank's
+        last, partial batch, which starts at ``i*P*B + rank*b`` rather than on the
+        stride grid)."""
         if num_batches is None:
             num_batches = max(1, -(-self.order_h.size // self.stride))
         N, E = self.batch_sizes(num_batches, position)
-        return Caps.bucket(int(N.max()), self.B, max(int(E.max()), 1), self.n_neg)
+        n_max, e_max = int(N.max()), int(E.max())
+        for pos, b in extra:
+            n, e = self._sizes_at(int(pos), int(b))
+            n_max, e_max = max(n_max, n), max(e_max, e)
+        return Caps.bucket(n_max, self.B, max(e_max, 1), self.n_neg)
 
     def launch(self, bs: L.GtrBatch, caps: Caps, stream: int, B: int | None = None) -> None:
         """Build the next batch (``B`` sessions, default the builder's batch size) into the
@@ -158,10 +165,20 @@ class GpuBatchBuilder:
                 "build_batch")
         self.pos += stride
 
-    def check_status(self) -> None:
-        """Raise if any batch built since the last check failed (host sync)."""
+    def check_status(self, group=None) -> None:
+        """Raise if any batch built since the last check failed (host sync).  Under a
+        process group of more than one rank the sticky code is MAX-all-reduced first, so
+        every rank raises at the same point (a rank-local raise would leave the others
+        blocked in the step's next collective)."""
         code = int(self.status[1].item())
         self.status.zero_()
+        import torch.distributed as dist
+
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+            dev = self.store.device if dist.get_backend(group) != "gloo" else "cpu"
+            t = torch.tensor([code], dtype=torch.int32, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+            code = int(t.item())
         if code & 2:
             raise RuntimeError("negative sampling: a session holds (nearly) every catalog item, so no "
                                "negative outside it exists (the reference would loop forever)")

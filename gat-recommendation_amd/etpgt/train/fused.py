@@ -352,35 +352,36 @@ class FusedTrainStep:
         """D2D copy of a pre-staged packed blob of the same capacities."""
         self.blob.copy_(blob, non_blocking=True)
 
-    def attach_builder(self, builder, num_batches: int | None = None):
+    def attach_builder(self, builder, num_batches: int | None = None, extra=()):
         """Build every batch on the device inside the step (etpgt.data.gpu_batch): each
         ``run()`` first writes the builder's next batch into the batch image, and the
         build is captured in the step's hipGraph with the rest.  Capacities cover the
-        builder's next ``num_batches`` batches (default: one epoch of its order)."""
-        caps = self._planned_caps(builder, num_batches)
+        builder's next ``num_batches`` batches (default: one epoch of its order) and the
+        ``(position, sessions)`` windows of ``extra``."""
+        caps = self._planned_caps(builder, num_batches, extra)
         if self.caps is None or not self.caps.fits(caps.n_cap, caps.b_cap, caps.e_cap, caps.n_neg):
             self._bind(caps if self.caps is None else self.caps.grow(caps.n_cap, caps.b_cap, caps.e_cap, caps.n_neg))
         self.builder = builder
         self.graph = self.graph_pe = self.graph_b = None
         self.resident_graphs = None
 
-    def _planned_caps(self, builder, num_batches: int | None) -> Caps:
+    def _planned_caps(self, builder, num_batches: int | None, extra=()) -> Caps:
         """Capacities of the builder's next batches; data parallel: agreed over the ranks
         FIRST, so that every rank takes the same rebind decision (a rank-local one would
         leave the others waiting in _bind's collective)."""
-        caps = builder.plan_caps(num_batches, int(builder.cursor.item()))
+        caps = builder.plan_caps(num_batches, int(builder.cursor.item()), extra)
         if caps.n_neg != (self.caps.n_neg if self.caps is not None else caps.n_neg):
             raise ValueError("the number of negatives per session must stay fixed")
         return self._agree(caps)
 
-    def refresh_builder_caps(self, num_batches: int | None = None):
+    def refresh_builder_caps(self, num_batches: int | None = None, extra=()):
         """Grow the capacities if the attached builder's next ``num_batches`` batches need it
         (collective in data parallel); the captured graphs survive when nothing grows."""
         if self.builder is None:
             raise RuntimeError("no device batch builder attached")
-        caps = self._planned_caps(self.builder, num_batches)
+        caps = self._planned_caps(self.builder, num_batches, extra)
         if not self.caps.fits(caps.n_cap, caps.b_cap, caps.e_cap, caps.n_neg):
-            self.attach_builder(self.builder, num_batches)
+            self.attach_builder(self.builder, num_batches, extra)
 
     def detach_builder(self):
         self.builder = None

@@ -116,10 +116,14 @@ class Trainer:
         loader.start_epoch()
         sizes = loader.batch_sizes()
         bld = loader.builder
+        # the last, partial batch of rank r starts at i*P*B + r*b, off the stride grid the
+        # full batches follow: plan its window explicitly, before the ranks agree on caps
+        full = sum(1 for b in sizes if b == loader.batch_size)
+        extra = [(loader.batch_start(i), b) for i, b in enumerate(sizes) if b != loader.batch_size]
         if fused.builder is not bld:
-            fused.attach_builder(bld, num_batches=len(sizes))
+            fused.attach_builder(bld, num_batches=max(full, 1), extra=extra)
         else:  # capacities for this epoch's order (rebinds only if they grew; agreed over ranks)
-            fused.refresh_builder_caps(len(sizes))
+            fused.refresh_builder_caps(max(full, 1), extra=extra)
         total = torch.zeros((), dtype=torch.float64, device=self.device)
         for i, b in enumerate(sizes):
             if b == loader.batch_size:
@@ -128,12 +132,18 @@ class Trainer:
                 bld.seek(loader.batch_start(i))  # last, partial batch: this rank's even share
                 loss = fused.run_partial(b)
             total += loss
-        bld.check_status()
+        bld.check_status(fused.group)  # collective under a process group: every rank raises together
         return float(total.item()) / max(len(sizes), 1)
 
     def train_epoch(self) -> float:
         self.model.train()
         fused = self._fused_step()
+        if fused is None and self.world > 1:
+            # the generic autograd loop averages nothing across ranks: each rank would train
+            # its own replica on its own shard of the data and the replicas would drift apart
+            raise RuntimeError(f"data-parallel training ({self.world} ranks) needs the fused HIP step; this "
+                               "model / optimizer / loss takes the single-process autograd loop (the FFN "
+                               "variant, fused=False, or an unsupported optimizer or loss)")
         from etpgt.train.dataloader import DeviceSessionLoader
 
         if fused is not None and isinstance(self.train_loader, DeviceSessionLoader):

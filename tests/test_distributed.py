@@ -248,3 +248,47 @@ def test_shard_capacity_bounds():
     assert shard_capacity(100, 10**6, 8) == 1 + 19 + 64       # 1.5 x the even share + 64 ...
     assert shard_capacity(40, 10**6, 8) == 1 + 40             # ... never above the batch's rows
     assert shard_capacity(107_000, 10**6, 8, slack=1.5) == 1 + 20_063 + 64  # 1.5 x the even share
+
+
+def _trainer_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import tempfile
+
+    import torch.distributed as dist
+
+    from etpgt.model import create_graph_transformer
+    from etpgt.train import Trainer
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        model = create_graph_transformer(T, embedding_dim=64, hidden_dim=64)  # use_ffn=True
+        opt = torch.optim.AdamW(model.parameters(), lr=1e-3)
+        with tempfile.TemporaryDirectory() as d:
+            tr = Trainer(model, [], [], opt, device="cpu", output_dir=d, max_epochs=1)
+            try:
+                tr.train_epoch()
+                q.put((rank, "no error"))
+            except RuntimeError as e:
+                q.put((rank, str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_trainer_refuses_the_autograd_loop_under_data_parallel():
+    """under a process group of more than one rank the generic autograd loop
+    averages nothing across ranks (the replicas would drift apart), so Trainer raises
+    instead of silently training P independent models (here: the FFN variant, which has
+    no data-parallel fused step)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_trainer_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    msgs = dict(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(world):
+        assert "data-parallel training (2 ranks) needs the fused HIP step" in msgs[r], msgs[r]

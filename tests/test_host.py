@@ -427,3 +427,29 @@ def test_device_loader_epoch_order_matches_torch_dataloader():
         got.append(va._epoch_order().tolist())
     assert got == ref
     assert got[0] != got[2]  # fresh permutation per epoch
+
+
+def test_plan_caps_covers_a_ranks_partial_batch_off_the_stride_grid():
+    """a data-parallel rank r >= 1 builds its last, partial batch at
+    i*P*B + r*b (b < B), off the stride grid [pos + i*P*B, +B) the full batches follow.
+    ``plan_caps(..., extra=[(position, b)])`` must cover that window too; here rank 1's
+    partial batch holds the longest sessions, which the grid windows never see."""
+    import types
+
+    from etpgt.data.gpu_batch import GpuBatchBuilder
+
+    S, B, P = 37, 8, 2  # 2 full global batches (32 sessions) + 5 left: last batch b = 2 per rank
+    nodes = np.full(S, 3, np.int64)
+    edges = np.full(S, 4, np.int64)
+    b_last = (S % (B * P)) // P
+    pos1 = 2 * B * P + 1 * b_last          # rank 1's partial batch
+    nodes[pos1: pos1 + b_last] = 50        # the longest sessions of the epoch
+    edges[pos1: pos1 + b_last] = 400
+    bld = GpuBatchBuilder.__new__(GpuBatchBuilder)
+    bld.store = types.SimpleNamespace(nodes=nodes, edges=edges)
+    bld.B, bld.stride, bld.n_neg = B, B * P, 5
+    bld.order_h = np.arange(S, dtype=np.int64)
+    grid_only = bld.plan_caps(2, position=1 * B)  # rank 1's full batches
+    assert grid_only.n_cap < 100  # the grid windows miss the long sessions
+    caps = bld.plan_caps(2, position=1 * B, extra=[(pos1, b_last)])
+    assert caps.n_cap >= 100 and caps.e_cap >= 800 and caps.b_cap >= B
