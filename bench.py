@@ -148,6 +148,12 @@ def main():
     ap.add_argument("--gather-batch", type=int, default=8192,
                     help="embedding-gather roofline legs: C5 (512 MB table, HBM) and C3 (42 MB, Infinity Cache) "
                          "shapes (d=128, 100 negatives) at this batch (0 = skip)")
+    ap.add_argument("--strong-batches", default="8192,65536",
+                    help="strong-scaling legs (comma-separated global batches; '0' = skip): the C4 mode -- C3 model, "
+                         "82k table row-sharded, SyncBN, global batch split over the same N GPUs -- run after the "
+                         "main line as a child launch (its own process group) and reported under strong_scaling")
+    ap.add_argument("--strong-steps", type=int, default=0, help="timed steps per strong leg (0: 40 up to B=16384, "
+                                                                 "else 10)")
     ap.add_argument("--c1-reps", type=int, default=5,
                     help="config C1 quick-validation leg (run_full_pipeline.py: model + 3 Adam steps), HIP and CPU "
                          "oracle, median of this many runs (0 = skip)")
@@ -384,10 +390,93 @@ def main():
             "recall_parity": recall,
             "c1_quick_validation": c1,
         }
-        sys.stdout.flush()
-        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if world > 1:
         torch.distributed.destroy_process_group()
+    if rank == 0:
+        legs = [int(x) for x in args.strong_batches.split(",") if x.strip() and int(x) > 0]
+        if legs and not cfg.get("shard") and os.environ.get("GTR_STRONG_CHILD") != "1":
+            del w, step, staged
+            torch.cuda.empty_cache()
+            out["strong_scaling"] = strong_scaling_legs(world, legs, args.strong_steps)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
+
+
+def _child_line(cmd: list, env: dict, timeout: float) -> dict:
+    """Run one bench child (its stdout: ONE JSON line) with a time limit; errors are
+    returned, not raised, so the main line is always printed."""
+    import subprocess
+
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out after {timeout:.0f} s"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"exit {r.returncode}: {r.stderr.strip()[-600:]}"}
+    return json.loads(lines[-1])
+
+
+def strong_scaling_legs(world: int, global_batches: list, steps: int = 0) -> dict:
+    """North star: ">= 6x strong scaling at 8 GPUs".  The C4 mode (configs[3]: the C3 model
+    on the RetailRocket table, the table row-sharded across the ranks, rows / row
+    gradients by RCCL all-to-all, SyncBN) at each fixed global batch, split over the SAME
+    N GPUs as this run: one child launch per batch (``torch.distributed.run`` with N
+    ranks, or one process at N = 1) after this run's process group is gone, so a failure
+    there cannot take the main line with it.  At N = 1 the unsharded single-GPU step at
+    the same batch (C3 at B = G) is reported beside it.  The driver's N = 1 / 2 / 4 / 8
+    lines together give the curve: value(N) / value(1) per global batch."""
+    import socket
+
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "GTR_BENCH_SPAWNED")
+           and not k.startswith("TORCHELASTIC")}
+    env["GTR_STRONG_CHILD"] = "1"
+    lean = ["--cpu-seconds", "0", "--gather-batch", "0", "--recall-steps", "0", "--e2e-steps", "0", "--c1-reps", "0",
+            "--tail-probe", "0", "--strong-batches", "0"]
+    res = {"config": "c4", "workload": CONFIGS["c4"]["name"], "n_gpus": world, "legs": []}
+    for G in global_batches:
+        st = steps or (40 if G <= 16384 else 10)
+        wu = 5 if G <= 16384 else 3
+        nb = 4 if G // world <= 16384 else 2
+        args = [os.path.abspath(__file__), "--config", "c4", "--gpus", str(world), "--global-batch", str(G),
+                "--steps", str(st), "--warmup", str(wu), "--num-batches", str(nb), *lean]
+        if G % world:
+            res["legs"].append({"global_batch": G, "error": "global batch does not divide by the GPUs"})
+            continue
+        if world > 1:
+            sock = socket.socket()
+            sock.bind(("127.0.0.1", 0))
+            port = sock.getsockname()[1]
+            sock.close()
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+                   "--master-addr", "127.0.0.1", "--master-port", str(port), *args]
+        else:
+            cmd = [sys.executable, *args]
+        log(f"strong scaling leg: C4 global batch {G} over {world} GPU(s)")
+        t0 = time.time()
+        line = _child_line(cmd, env, 600.0)
+        leg = {"global_batch": G, "per_gpu_batch": G // world, "wall_s": round(time.time() - t0, 1)}
+        if "error" in line:
+            leg["error"] = line["error"]
+        else:
+            c = line["config"]
+            leg.update({"value": line["value"], "unit": line["unit"], "ms_per_step": line["ms_per_step"],
+                        "gpu_ms_per_step_events": c["gpu_ms_per_step_events"], "steps": line["steps"],
+                        "parallelism": c["parallelism"], "process_group_world": c["process_group_world"],
+                        "transport": c["transport"], "graph_collectives": c["graph_collectives"],
+                        "sync_bn": c["sync_bn"], "replicas_identical": c["replicas_identical"],
+                        "exchange": c["dp_exchange"], "final_loss": c["final_loss"]})
+        if world == 1 and "error" not in leg:  # the plain single-GPU step at the same batch, beside it
+            one = _child_line([sys.executable, os.path.abspath(__file__), "--config", "c3", "--batch-size", str(G),
+                               "--steps", str(st), "--warmup", str(wu), "--num-batches", str(nb), *lean], env, 600.0)
+            leg["unsharded_single_gpu"] = ({"error": one["error"]} if "error" in one else
+                                           {"value": one["value"], "ms_per_step": one["ms_per_step"],
+                                            "config": "c3 (same model and table, no row sharding)"})
+        log(f"  -> {leg}")
+        res["legs"].append(leg)
+    return res
 
 
 def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, use_graph: bool = True,

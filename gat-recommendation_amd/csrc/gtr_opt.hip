@@ -496,45 +496,11 @@ struct TailK {
 };
 
 
-// ---- large batches: windowed segmented sums -----------------------------------------
-// The sorted contribution list is cut into windows of TW slots.  A row's segment that
-// starts in window w is summed by window w's block over its in-window part; the part
-// lying in each following window w' (it can span many: hot Zipf items collect thousands
-// of node contributions) is a "carry" summed beforehand by k_tail_carry, so no thread
-// walks a long segment serially.  Sums run in slot order inside a piece and pieces are
-// added in window order: deterministic.
-// Carry of window w (>= 1) whose first slot continues the previous window's segment:
-// the sum over [w*TW, first key change in w), split over the block's groups in fixed
-// contiguous pieces and combined in group order.  carry: [nwin][D].
+// ---- large batches: windowed segmented sums (gtr_rows.cuh) ----------------------------
 template <int D>
 __global__ __launch_bounds__(GTR_BLOCK) void k_tail_carry(gtr_batch bt, int T, gtr_tail tl) {
-  constexpr int C4 = D / 4, NG = GTR_BLOCK / C4;
-  __shared__ int s_end;
-  __shared__ __attribute__((aligned(16))) float4 s_part[NG][C4];
-  const int tid = threadIdx.x;
-  const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
-  const int w = blockIdx.x + 1;
-  const int w0 = w * TW, w1 = min(w0 + TW, m_cap);
-  const int key = tl.skeys[w0];
-  if (key <= 0 || key >= T || tl.skeys[w0 - 1] != key) return;  // block-uniform
-  if (tid == 0) s_end = w1;
-  __syncthreads();
-  if (tid < TW && w0 + tid < w1 && tl.skeys[w0 + tid] != key) atomicMin(&s_end, w0 + tid);
-  __syncthreads();
-  const int e = s_end;
-  const int grp = tid / C4, gl = tid % C4;
-  const int len = e - w0, per = (len + NG - 1) / NG;
-  const int ps = min(e, w0 + grp * per), pe = min(e, ps + per);
-  s_part[grp][gl] = piece_sum<D>(bt, tl.svals, ps, pe, tl.dx0, tl.se, tl.coef_tgt, tl.coef_neg, gl, grp * C4 % 64);
-  __syncthreads();
-  if (tid < C4) {
-    float4 g = s_part[0][tid];
-    for (int q = 1; q < NG; ++q) {
-      const float4 t = s_part[q][tid];
-      g.x += t.x; g.y += t.y; g.z += t.z; g.w += t.w;
-    }
-    reinterpret_cast<float4*>(tl.carry)[(size_t)w * C4 + tid] = g;
-  }
+  tail_carry_body<D, GTR_BLOCK>(blockIdx.x + 1, bt, T, tl.skeys, tl.svals, tl.dx0, tl.se, tl.coef_tgt, tl.coef_neg,
+                                tl.carry);
 }
 
 // Rows part of the tail for window w = blk: every segment starting in the window is
@@ -544,30 +510,10 @@ __device__ __forceinline__ void window_rows(int w, const gtr_batch& bt, int T, c
                                             int32_t* lazy_stamp, int32_t lazy_t) {
   constexpr int C4 = D / 4, NG = GTR_BLOCK / C4;
   __shared__ int s_bnd[TW + 1];
-  __shared__ int s_nb;
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = threadIdx.x;
   const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
   const int w0 = w * TW, w1 = min(w0 + TW, m_cap);
-  // boundaries (key changes) of the window in slot order: ballot + prefix per wave
-  if (tid == 0) s_nb = 0;
-  __syncthreads();
-  const int i = w0 + tid;
-  bool bnd = false;
-  if (tid < TW && i < w1) bnd = (i == 0) || tl.skeys[i] != tl.skeys[i - 1];
-  __shared__ int s_wcnt[GTR_WAVES];
-  const unsigned long long bal = __ballot(bnd);
-  if (lane == 0) s_wcnt[tid >> 6] = __popcll(bal);
-  __syncthreads();
-  int off = 0;
-  for (int q = 0; q < (tid >> 6); ++q) off += s_wcnt[q];
-  if (bnd) s_bnd[off + __popcll(bal & ((1ull << lane) - 1ull))] = i;
-  if (tid == 0) {
-    int tot = 0;
-    for (int q = 0; q < GTR_WAVES; ++q) tot += s_wcnt[q];
-    s_nb = tot;
-  }
-  __syncthreads();
-  const int nb = s_nb;
+  const int nb = window_bounds<GTR_BLOCK>(tl.skeys, w0, w1, s_bnd);
   const int grp = tid / C4, gl = tid % C4, gb = grp * C4 % 64;
   for (int q = grp; q < nb; q += NG) {
     const int s0 = s_bnd[q];
@@ -580,14 +526,8 @@ __device__ __forceinline__ void window_rows(int w, const gtr_batch& bt, int T, c
     float4 pv = sw_ld(reinterpret_cast<const float4*>(tl.table) + base);
     float4 mv = sw_ld(reinterpret_cast<const float4*>(tl.table_m) + base);
     float4 vv = sw_ld(reinterpret_cast<const float4*>(tl.table_v) + base);
-    float4 g = piece_sum<D>(bt, tl.svals, s0, e, tl.dx0, tl.se, tl.coef_tgt, tl.coef_neg, gl, gb);
-    if (e == w1) {  // the segment may continue: add the carries in window order
-      for (int w2 = w + 1; w2 * TW < m_cap && tl.skeys[w2 * TW] == key; ++w2) {
-        const float4 c = reinterpret_cast<const float4*>(tl.carry)[(size_t)w2 * C4 + gl];
-        g.x += c.x; g.y += c.y; g.z += c.z; g.w += c.w;
-        if (tl.skeys[min((w2 + 1) * TW, m_cap) - 1] != key) break;
-      }
-    }
+    const float4 g = window_segment_sum<D>(bt, tl.skeys, tl.svals, tl.dx0, tl.se, tl.coef_tgt, tl.coef_neg, tl.carry,
+                                           w, s0, e, w1, m_cap, key, gl, gb);
     st.apply(pv.x, mv.x, vv.x, g.x);
     st.apply(pv.y, mv.y, vv.y, g.y);
     st.apply(pv.z, mv.z, vv.z, g.z);
@@ -873,8 +813,40 @@ struct DpPackK {
   gtr_dp_layout lay;
   float* pack;
   int T, nb_rows, nb_small, nseg;
+  int windowed, pad0;  // 1 (m_cap > GTR_BEGIN_MCAP): rows part = one block per TW-slot window
   gtr_segment segs[GTR_SMALL_MAX_SEG];
 };
+
+// Windowed rows part of the pack (large batches): window w's keys, its segment sums (the
+// single-GPU tail's windowed order: bitwise its gradient rows) at the segments' first
+// slots, zero rows at every other slot.
+template <int D>
+__device__ __forceinline__ void dp_pack_window(int w, const DpPackK& a, int32_t* keys, float* rows) {
+  constexpr int C4 = D / 4, NG = GTR_BLOCK / C4;
+  __shared__ int s_bnd[TW + 1];
+  const int tid = threadIdx.x;
+  const int m_cap = a.lay.m_cap;
+  const int w0 = w * TW, w1 = min(w0 + TW, m_cap);
+  const int32_t* sk = a.tl.skeys;
+  if (tid < TW && w0 + tid < w1) keys[w0 + tid] = sk[w0 + tid];
+  for (int idx = tid; idx < (w1 - w0) * C4; idx += GTR_BLOCK) {
+    const int i = w0 + idx / C4;
+    if (i > 0 && sk[i - 1] == sk[i])
+      reinterpret_cast<float4*>(rows + (size_t)i * D)[idx % C4] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const int nb = window_bounds<GTR_BLOCK>(sk, w0, w1, s_bnd);
+  const int grp = tid / C4, gl = tid % C4, gb = grp * C4 % 64;
+  for (int q = grp; q < nb; q += NG) {
+    const int s0 = s_bnd[q];
+    const int key = sk[s0];
+    const int e = q + 1 < nb ? s_bnd[q + 1] : w1;
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (key > 0 && key < a.T)
+      g = window_segment_sum<D>(a.bt, sk, a.tl.svals, a.tl.dx0, a.tl.se, a.tl.coef_tgt, a.tl.coef_neg, a.tl.carry, w,
+                                s0, e, w1, m_cap, key, gl, gb);
+    reinterpret_cast<float4*>(rows + (size_t)s0 * D)[gl] = g;
+  }
+}
 
 template <int D>
 __global__ __launch_bounds__(GTR_BLOCK) void k_dp_pack(DpPackK a) {
@@ -885,6 +857,10 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_dp_pack(DpPackK a) {
   const int m_cap = a.lay.m_cap;
   int32_t* keys = reinterpret_cast<int32_t*>(a.pack + a.lay.keys_off);
   float* rows = a.pack + a.lay.rows_off;
+  if (blk < a.nb_rows && a.windowed) {
+    dp_pack_window<D>(blk, a, keys, rows);
+    return;
+  }
   if (blk < a.nb_rows) {
     const int gid = blk * GTR_BLOCK + tid;
     const int i = gid / C4, c = gid - i * C4;
@@ -1739,13 +1715,30 @@ int gtr_dp_pack(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tai
   k.lay = *lay;
   k.pack = pack;
   k.T = num_items;
-  k.nb_rows = (int)(((int64_t)lay->m_cap * (dim / 4) + GTR_BLOCK - 1) / GTR_BLOCK);
+  hipStream_t s = (hipStream_t)stream;
+  // large batches: segment sums in window pieces + carries, as the single-GPU tail sums them
+  k.windowed = lay->m_cap > GTR_BEGIN_MCAP ? 1 : 0;
+  if (k.windowed) {
+    if (!tail->carry) { set_error("gtr_dp_pack: large batch (m_cap > %d) needs the carry scratch", GTR_BEGIN_MCAP); return GTR_E_ARG; }
+    const int nwin = (lay->m_cap + TW - 1) / TW;
+    k.nb_rows = nwin;
+    if (nwin > 1) {
+      switch (dim) {
+        case 32: hipLaunchKernelGGL(k_tail_carry<32>, dim3(nwin - 1), dim3(GTR_BLOCK), 0, s, *bt, num_items, *tail); break;
+        case 64: hipLaunchKernelGGL(k_tail_carry<64>, dim3(nwin - 1), dim3(GTR_BLOCK), 0, s, *bt, num_items, *tail); break;
+        case 128: hipLaunchKernelGGL(k_tail_carry<128>, dim3(nwin - 1), dim3(GTR_BLOCK), 0, s, *bt, num_items, *tail); break;
+        default: hipLaunchKernelGGL(k_tail_carry<256>, dim3(nwin - 1), dim3(GTR_BLOCK), 0, s, *bt, num_items, *tail); break;
+      }
+      GTR_HIP_CHECK_LAUNCH();
+    }
+  } else {
+    k.nb_rows = (int)(((int64_t)lay->m_cap * (dim / 4) + GTR_BLOCK - 1) / GTR_BLOCK);
+  }
   k.nb_small = (int)((lay->flat_total + GTR_BLOCK - 1) / GTR_BLOCK);
   if (k.nb_small == 0) k.nb_small = 1;
   k.nseg = nseg;
   for (int i = 0; i < nseg; ++i) k.segs[i] = segs[i];
   const int grid = k.nb_rows + k.nb_small;
-  hipStream_t s = (hipStream_t)stream;
   switch (dim) {
     case 32: hipLaunchKernelGGL(k_dp_pack<32>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;
     case 64: hipLaunchKernelGGL(k_dp_pack<64>, dim3(grid), dim3(GTR_BLOCK), 0, s, k); break;

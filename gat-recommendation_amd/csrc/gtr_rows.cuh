@@ -98,7 +98,7 @@ __device__ __forceinline__ void lazy_consts_for(const gtr_adam& o, int64_t t, fl
   reinterpret_cast<float2*>(consts)[t] = make_float2(st.step_size, st.inv_bc2);
 }
 
-#define TW 128
+#define TW 128  // slots per window of the large-batch segmented sums (below)
 
 // Sum of contributions in slots [s, e) for column float4 `gl` by the C4 = D/4 lanes of
 // one group (group base lane gb): slot ids are fetched one per lane, decoded to a source
@@ -145,6 +145,95 @@ __device__ __forceinline__ float4 piece_sum(const gtr_batch& bt, const int32_t* 
           g.x += f[u] * v[u].x; g.y += f[u] * v[u].y; g.z += f[u] * v[u].z; g.w += f[u] * v[u].w;
         }
       }
+    }
+  }
+  return g;
+}
+
+// ---- large batches (m_cap > GTR_BEGIN_MCAP): windowed segmented sums ------------------
+// The sorted contribution list is cut into windows of TW slots.  A row's segment that
+// starts in window w is summed by window w's block over its in-window part; the part
+// lying in each following window w' (it can span many: hot Zipf items collect thousands
+// of node contributions) is a "carry" summed beforehand (tail_carry_body), so no thread
+// walks a long segment serially.  Sums run in slot order inside a piece and pieces are
+// added in window order: deterministic.  The single-GPU tail, the data-parallel pack and
+// the row-sharded pack all sum this way, so their segment sums are bitwise equal.
+
+// Carry of window w (>= 1) whose first slot continues the previous window's segment:
+// the sum over [w*TW, first key change in w), split over the block's groups in fixed
+// contiguous pieces and combined in group order.  carry: [nwin][D].  Block-uniform exit.
+template <int D, int BLOCK>
+__device__ __forceinline__ void tail_carry_body(int w, const gtr_batch& bt, int T, const int32_t* skeys,
+                                                const int32_t* svals, const float* dx0, const float* se,
+                                                const float* coef_tgt, const float* coef_neg, float* carry) {
+  constexpr int C4 = D / 4, NG = BLOCK / C4;
+  __shared__ int s_end;
+  __shared__ __attribute__((aligned(16))) float4 s_part[NG][C4];
+  const int tid = threadIdx.x;
+  const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
+  const int w0 = w * TW, w1 = min(w0 + TW, m_cap);
+  const int key = skeys[w0];
+  if (key <= 0 || key >= T || skeys[w0 - 1] != key) return;  // block-uniform
+  if (tid == 0) s_end = w1;
+  __syncthreads();
+  if (tid < TW && w0 + tid < w1 && skeys[w0 + tid] != key) atomicMin(&s_end, w0 + tid);
+  __syncthreads();
+  const int e = s_end;
+  const int grp = tid / C4, gl = tid % C4;
+  const int len = e - w0, per = (len + NG - 1) / NG;
+  const int ps = min(e, w0 + grp * per), pe = min(e, ps + per);
+  s_part[grp][gl] = piece_sum<D>(bt, svals, ps, pe, dx0, se, coef_tgt, coef_neg, gl, grp * C4 % 64);
+  __syncthreads();
+  if (tid < C4) {
+    float4 g = s_part[0][tid];
+    for (int q = 1; q < NG; ++q) {
+      const float4 t = s_part[q][tid];
+      g.x += t.x; g.y += t.y; g.z += t.z; g.w += t.w;
+    }
+    reinterpret_cast<float4*>(carry)[(size_t)w * C4 + tid] = g;
+  }
+}
+
+// Segment starts (key changes) of window [w0, w1) in slot order -> s_bnd[0..nb), returns
+// nb.  Every thread of the block calls it (barriers inside); BLOCK >= TW.
+template <int BLOCK>
+__device__ __forceinline__ int window_bounds(const int32_t* skeys, int w0, int w1, int* s_bnd) {
+  __shared__ int s_nb;
+  __shared__ int s_wcnt[BLOCK / 64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int i = w0 + tid;
+  bool bnd = false;
+  if (tid < TW && i < w1) bnd = (i == 0) || skeys[i] != skeys[i - 1];
+  const unsigned long long bal = __ballot(bnd);
+  if (lane == 0) s_wcnt[tid >> 6] = __popcll(bal);
+  __syncthreads();
+  int off = 0;
+  for (int q = 0; q < (tid >> 6); ++q) off += s_wcnt[q];
+  if (bnd) s_bnd[off + __popcll(bal & ((1ull << lane) - 1ull))] = i;
+  if (tid == 0) {
+    int tot = 0;
+    for (int q = 0; q < BLOCK / 64; ++q) tot += s_wcnt[q];
+    s_nb = tot;
+  }
+  __syncthreads();
+  return s_nb;
+}
+
+// Sum of the segment of `key` that starts at s0 inside window w (in-window end e): the
+// in-window piece, then -- if the segment reaches the window's end -- the carries of the
+// following windows in window order.
+template <int D>
+__device__ __forceinline__ float4 window_segment_sum(const gtr_batch& bt, const int32_t* skeys, const int32_t* svals,
+                                                     const float* dx0, const float* se, const float* coef_tgt,
+                                                     const float* coef_neg, const float* carry, int w, int s0, int e,
+                                                     int w1, int m_cap, int key, int gl, int gb) {
+  constexpr int C4 = D / 4;
+  float4 g = piece_sum<D>(bt, svals, s0, e, dx0, se, coef_tgt, coef_neg, gl, gb);
+  if (e == w1) {  // the segment may continue: add the carries in window order
+    for (int w2 = w + 1; w2 * TW < m_cap && skeys[w2 * TW] == key; ++w2) {
+      const float4 c = reinterpret_cast<const float4*>(carry)[(size_t)w2 * C4 + gl];
+      g.x += c.x; g.y += c.y; g.z += c.z; g.w += c.w;
+      if (skeys[min((w2 + 1) * TW, m_cap) - 1] != key) break;
     }
   }
   return g;

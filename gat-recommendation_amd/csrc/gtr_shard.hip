@@ -9,8 +9,8 @@
 //   gtr_shard_route  unique requested rows per owner -> send_ids [P][cap]; the batch's
 //                    ids remapped to "compact" rows q*cap + 1 + j of the fetched-row buffer
 //   all-to-all ids   (RCCL)
-//   gtr_shard_serve  owner: requested rows brought up to step t-1 (lazy zero-gradient
-//                    AdamW, bitwise the dense update) -> send_rows [P][cap][D]
+//   gtr_shard_serve  owner: requested rows as of step t-1 (lazy zero-gradient AdamW applied
+//                    in registers, bitwise the dense update) -> send_rows [P][cap][D]
 //   all-to-all rows  == the "halo" fetch of source embeddings at layer 0
 //   forward / loss / backward on the compact rows (unchanged layer kernels)
 //   gtr_shard_pack   per requested row the summed table-gradient row -> send_grads
@@ -174,43 +174,21 @@ __global__ __launch_bounds__(RB_THREADS) void k_route_write(RouteK a) {
   }
 }
 
-// Owner side, step t: claim each requested local row (first claimer gets the old stamp)
-// and bring it to step t-1 with the zero-gradient update of every missed step (the
-// consts chain of the lazy table, bitwise the dense sweep).  16 lanes per entry.
-__device__ __forceinline__ void shard_claim_row(int local, const gtr_shard& sh, int32_t t, int gl, int gbase) {
-  int old = 0;
-  const bool ok = local >= 0 && local < sh.local_rows;
-  if (gl == 0 && ok) old = atomicExch(sh.stamp + local, t - 1);
-  old = __shfl(old, gbase);
-  if (!ok || old >= t - 1) return;
-  const int C4 = sh.dim / 4;
-  float4* P = reinterpret_cast<float4*>(sh.table) + (size_t)local * C4;
-  float4* M = reinterpret_cast<float4*>(sh.m) + (size_t)local * C4;
-  float4* V = reinterpret_cast<float4*>(sh.v) + (size_t)local * C4;
-  for (int c = gl; c < C4; c += 16) {
-    float4 p = P[c], m = M[c], v = V[c];
-    catch_up4(p, m, v, old, t - 1, sh.opt, sh.consts);
-    P[c] = p; M[c] = m; V[c] = v;
-  }
-}
-
 __device__ __forceinline__ int peer_count(const int32_t* ids, int r, int cap) {
   const int c = ids[(size_t)r * cap];
   return c < 0 ? 0 : (c > cap - 1 ? cap - 1 : c);
 }
 
-__global__ __launch_bounds__(GTR_BLOCK) void k_shard_claim(gtr_shard sh, const int32_t* recv_ids,
-                                                           const int64_t* step_dev) {
-  const int64_t gid = (int64_t)blockIdx.x * GTR_BLOCK + threadIdx.x;
-  const int64_t e = gid / 16;
-  const int r = (int)(e / sh.cap), j = (int)(e - (int64_t)r * sh.cap);
-  int local = -1;
-  if (r < sh.world && j >= 1 && j <= peer_count(recv_ids, r, sh.cap)) local = recv_ids[e] / sh.world;
-  shard_claim_row(local, sh, (int32_t)(*step_dev + sh.opt.step_offset), threadIdx.x & 15, (threadIdx.x & 63) & ~15);
-}
-
+// Owner side, step t: every requested row as it stands after step t-1, into its slot of
+// send_rows.  A row whose stamp lags (< t-1) is brought forward IN REGISTERS with the
+// zero-gradient update of every missed step (the consts chain of the lazy table, bitwise
+// the dense sweep); the table itself is not written here.  The owner's update
+// (k_shard_update) recomputes the same chain and writes p / m / v once, together with the
+// step-t update: one read-modify-write of a touched row per step, and no write in this
+// kernel, so several ranks' requests of one row need no claim (one launch, read-only on
+// the table).  C4 lanes per entry.
 template <int D>
-__global__ __launch_bounds__(GTR_BLOCK) void k_shard_copy(gtr_shard sh, const int32_t* recv_ids, float* send_rows) {
+__global__ __launch_bounds__(GTR_BLOCK) void k_shard_serve(gtr_shard sh, const int32_t* recv_ids, float* send_rows) {
   constexpr int C4 = D / 4;
   const int64_t gid = (int64_t)blockIdx.x * GTR_BLOCK + threadIdx.x;
   const int64_t e = gid / C4;
@@ -218,7 +196,16 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_shard_copy(gtr_shard sh, const in
   const int r = (int)(e / sh.cap), j = (int)(e - (int64_t)r * sh.cap);
   if (r >= sh.world || j < 1 || j > peer_count(recv_ids, r, sh.cap)) return;
   const int local = recv_ids[e] / sh.world;
-  reinterpret_cast<float4*>(send_rows)[e * C4 + c] = reinterpret_cast<const float4*>(sh.table)[(size_t)local * C4 + c];
+  const int32_t t = (int32_t)(*sh.opt.step_dev + sh.opt.step_offset);
+  const int old = sh.stamp[local];
+  const size_t at = (size_t)local * C4 + c;
+  float4 p = reinterpret_cast<const float4*>(sh.table)[at];
+  if (old < t - 1) {
+    float4 m = reinterpret_cast<const float4*>(sh.m)[at];
+    float4 v = reinterpret_cast<const float4*>(sh.v)[at];
+    catch_up4(p, m, v, old, t - 1, sh.opt, sh.consts);
+  }
+  reinterpret_cast<float4*>(send_rows)[e * C4 + c] = p;
 }
 
 struct PackK {
@@ -229,8 +216,43 @@ struct PackK {
   float* small_pack;
   const int32_t* status;  // this rank's overflow flag of the step (status[0]) -> small_pack[F + 1]
   int T, nb_rows, nseg, m_cap;
+  int windowed, pad0;  // 1 (m_cap > GTR_BEGIN_MCAP): rows part = one block per TW-slot window
   gtr_segment segs[GTR_SMALL_MAX_SEG];
 };
+
+// Large batches: carries of the windows (gtr_rows.cuh), summed before k_shard_pack.
+template <int D>
+__global__ __launch_bounds__(GTR_BLOCK) void k_shard_carry(gtr_batch bt, int T, gtr_tail tl) {
+  tail_carry_body<D, GTR_BLOCK>(blockIdx.x + 1, bt, T, tl.skeys, tl.svals, tl.dx0, tl.se, tl.coef_tgt, tl.coef_neg,
+                                tl.carry);
+}
+
+// Windowed rows part (large batches): the segments starting in window w, each summed as
+// the single-GPU tail sums it (in-window piece + carries of the following windows), so no
+// thread walks a hot row's thousands of contributions serially.
+template <int D>
+__device__ __forceinline__ void shard_pack_window(int w, const PackK& a) {
+  constexpr int C4 = D / 4, NG = GTR_BLOCK / C4;
+  __shared__ int s_bnd[TW + 1];
+  const int tid = threadIdx.x;
+  const int w0 = w * TW, w1 = min(w0 + TW, a.m_cap);
+  const int32_t* sk = a.tl.skeys;
+  const int nb = window_bounds<GTR_BLOCK>(sk, w0, w1, s_bnd);
+  const int grp = tid / C4, gl = tid % C4, gb = grp * C4 % 64;
+  for (int q = grp; q < nb; q += NG) {
+    const int s0 = s_bnd[q];
+    const int key = sk[s0];
+    if (key < 0 || key >= a.T) continue;
+    const int ck = a.ckeys[s0];
+    if (ck < 0) continue;
+    const int e = q + 1 < nb ? s_bnd[q + 1] : w1;
+    float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (key > 0)  // padding_idx = 0: no gradient (the owner still applies g = 0)
+      g = window_segment_sum<D>(a.bt, sk, a.tl.svals, a.tl.dx0, a.tl.se, a.tl.coef_tgt, a.tl.coef_neg, a.tl.carry, w,
+                                s0, e, w1, a.m_cap, key, gl, gb);
+    reinterpret_cast<float4*>(a.send_grads)[(size_t)ck * C4 + gl] = g;
+  }
+}
 
 // Requester side: the summed gradient row of every requested row (segment of the sorted
 // contribution list, summed in slot order like the single-GPU tail) -> its compact slot;
@@ -240,6 +262,10 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_shard_pack(PackK a) {
   constexpr int C4 = D / 4, NG = GTR_BLOCK / C4;
   __shared__ float s_acc[GTR_BLOCK];
   const int tid = threadIdx.x, lane = tid & 63;
+  if ((int)blockIdx.x < a.nb_rows && a.windowed) {
+    shard_pack_window<D>(blockIdx.x, a);
+    return;
+  }
   if ((int)blockIdx.x < a.nb_rows) {
     const int grp = tid / C4, gl = tid % C4, gb = grp * C4 % 64;
     const int i = blockIdx.x * NG + grp;
@@ -360,9 +386,11 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_shard_update(UpdateK a) {
     g.x *= inv_w; g.y *= inv_w; g.z *= inv_w; g.w *= inv_w;
     const int local = key / W;
     const size_t base = (size_t)local * C4 + c;
+    const int old = sh.stamp[local];
     float4 pv = reinterpret_cast<const float4*>(sh.table)[base];
     float4 mv = reinterpret_cast<const float4*>(sh.m)[base];
     float4 vv = reinterpret_cast<const float4*>(sh.v)[base];
+    catch_up4(pv, mv, vv, old, t - 1, sh.opt, sh.consts);  // the chain k_shard_serve applied in registers
     st.apply(pv.x, mv.x, vv.x, g.x);
     st.apply(pv.y, mv.y, vv.y, g.y);
     st.apply(pv.z, mv.z, vv.z, g.z);
@@ -370,6 +398,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_shard_update(UpdateK a) {
     reinterpret_cast<float4*>(sh.table)[base] = pv;
     reinterpret_cast<float4*>(sh.m)[base] = mv;
     reinterpret_cast<float4*>(sh.v)[base] = vv;
+    __builtin_amdgcn_wave_barrier();  // the row's column lanes (one wave) read the stamp above
     if (c == 0) sh.stamp[local] = t;
     return;
   }
@@ -451,16 +480,13 @@ int gtr_shard_serve(const gtr_shard* sh, const int32_t* recv_ids, float* send_ro
   }
   hipStream_t s = (hipStream_t)stream;
   const int64_t entries = (int64_t)sh->world * sh->cap;
-  hipLaunchKernelGGL(k_shard_claim, dim3((unsigned)((entries * 16 + GTR_BLOCK - 1) / GTR_BLOCK)), dim3(GTR_BLOCK), 0,
-                     s, *sh, recv_ids, sh->opt.step_dev);
-  GTR_HIP_CHECK_LAUNCH();
   const int64_t threads = entries * (sh->dim / 4);
   const dim3 grid((unsigned)((threads + GTR_BLOCK - 1) / GTR_BLOCK));
   switch (sh->dim) {
-    case 32: hipLaunchKernelGGL(k_shard_copy<32>, grid, dim3(GTR_BLOCK), 0, s, *sh, recv_ids, send_rows); break;
-    case 64: hipLaunchKernelGGL(k_shard_copy<64>, grid, dim3(GTR_BLOCK), 0, s, *sh, recv_ids, send_rows); break;
-    case 128: hipLaunchKernelGGL(k_shard_copy<128>, grid, dim3(GTR_BLOCK), 0, s, *sh, recv_ids, send_rows); break;
-    default: hipLaunchKernelGGL(k_shard_copy<256>, grid, dim3(GTR_BLOCK), 0, s, *sh, recv_ids, send_rows); break;
+    case 32: hipLaunchKernelGGL(k_shard_serve<32>, grid, dim3(GTR_BLOCK), 0, s, *sh, recv_ids, send_rows); break;
+    case 64: hipLaunchKernelGGL(k_shard_serve<64>, grid, dim3(GTR_BLOCK), 0, s, *sh, recv_ids, send_rows); break;
+    case 128: hipLaunchKernelGGL(k_shard_serve<128>, grid, dim3(GTR_BLOCK), 0, s, *sh, recv_ids, send_rows); break;
+    default: hipLaunchKernelGGL(k_shard_serve<256>, grid, dim3(GTR_BLOCK), 0, s, *sh, recv_ids, send_rows); break;
   }
   GTR_HIP_CHECK_LAUNCH();
   return GTR_OK;
@@ -483,14 +509,36 @@ int gtr_shard_pack(const gtr_batch* bt, const gtr_shard* sh, const gtr_tail* tai
   k.status = sh->status;
   k.T = sh->num_items;
   k.m_cap = bt->n_cap + bt->b_cap * (1 + bt->n_neg);
-  const int NG = GTR_BLOCK / (sh->dim / 4);
-  k.nb_rows = (k.m_cap + NG - 1) / NG;
+  hipStream_t s = (hipStream_t)stream;
+  // large batches: windowed segment sums (one block per window + carries), bitwise the
+  // single-GPU tail's and the data-parallel pack's order
+  k.windowed = k.m_cap > GTR_BEGIN_MCAP ? 1 : 0;
+  if (k.windowed) {
+    if (!tail->carry) {
+      set_error("gtr_shard_pack: large batch (m_cap > %d) needs the carry scratch", GTR_BEGIN_MCAP);
+      return GTR_E_ARG;
+    }
+    const int nwin = (k.m_cap + TW - 1) / TW;
+    k.nb_rows = nwin;
+    if (nwin > 1) {
+      const dim3 cg(nwin - 1);
+      switch (sh->dim) {
+        case 32: hipLaunchKernelGGL(k_shard_carry<32>, cg, dim3(GTR_BLOCK), 0, s, *bt, sh->num_items, *tail); break;
+        case 64: hipLaunchKernelGGL(k_shard_carry<64>, cg, dim3(GTR_BLOCK), 0, s, *bt, sh->num_items, *tail); break;
+        case 128: hipLaunchKernelGGL(k_shard_carry<128>, cg, dim3(GTR_BLOCK), 0, s, *bt, sh->num_items, *tail); break;
+        default: hipLaunchKernelGGL(k_shard_carry<256>, cg, dim3(GTR_BLOCK), 0, s, *bt, sh->num_items, *tail); break;
+      }
+      GTR_HIP_CHECK_LAUNCH();
+    }
+  } else {
+    const int NG = GTR_BLOCK / (sh->dim / 4);
+    k.nb_rows = (k.m_cap + NG - 1) / NG;
+  }
   k.nseg = nseg;
   for (int i = 0; i < nseg; ++i) k.segs[i] = segs[i];
   int nb_small = (int)((tail->flat_total + GTR_BLOCK - 1) / GTR_BLOCK);
   if (nb_small == 0) nb_small = 1;
   const dim3 grid(k.nb_rows + nb_small);
-  hipStream_t s = (hipStream_t)stream;
   switch (sh->dim) {
     case 32: hipLaunchKernelGGL(k_shard_pack<32>, grid, dim3(GTR_BLOCK), 0, s, k); break;
     case 64: hipLaunchKernelGGL(k_shard_pack<64>, grid, dim3(GTR_BLOCK), 0, s, k); break;

@@ -171,12 +171,16 @@ class ShardExchange:
         slots = P * self.cap
         i32 = dict(dtype=torch.int32, device=dev)
         f32 = dict(dtype=torch.float32, device=dev)
+        # one rank: nothing crosses a link, so every receive buffer IS its send buffer and
+        # the exchanges are no-ops (no 2 x slots x D copies per step; the kernels never read
+        # and write the same buffer of a pair in one launch)
+        self.alias = P == 1
         self.send_ids = torch.zeros(slots, **i32)
-        self.recv_ids = torch.zeros(slots, **i32)
+        self.recv_ids = self.send_ids if self.alias else torch.zeros(slots, **i32)
         self.send_rows = torch.zeros(slots, D, **f32)
-        self.recv_rows = torch.zeros(slots, D, **f32)  # the compact "table" the layer kernels read
+        self.recv_rows = self.send_rows if self.alias else torch.zeros(slots, D, **f32)  # the compact "table"
         self.send_grads = torch.zeros(slots, D, **f32)
-        self.recv_grads = torch.zeros(slots, D, **f32)
+        self.recv_grads = self.send_grads if self.alias else torch.zeros(slots, D, **f32)
         self.ckeys = torch.zeros(self.m_cap, **i32)
         self.node_item_c = torch.zeros(caps.n_cap, **i32)
         self.target_c = torch.zeros(caps.b_cap, **i32)
@@ -187,8 +191,8 @@ class ShardExchange:
         self.scratch = torch.zeros(max(int(nb.value), 16), dtype=torch.uint8, device=dev)
         F = eng.flat.layout.total
         self.small_words = (F + 2 + 3) & ~3  # flat gradient | loss | overflow flag
-        self.small_pack = torch.zeros(self.small_words, **f32)
         self.small_all = torch.zeros(P, self.small_words, **f32)
+        self.small_pack = self.small_all[0] if self.alias else torch.zeros(self.small_words, **f32)
         self.bs_c = self._compact(step.bs)
         self.bs_c_pe = self._compact(step.bs_pe) if step.bs_pe is not None else None
 
@@ -223,14 +227,16 @@ class ShardExchange:
                                         self.scratch.data_ptr(), self.scratch.numel(), stream), "shard_route")
 
     def exchange_ids(self):
-        all_to_all(self.recv_ids, self.send_ids, self.state.group)
+        if not self.alias:
+            all_to_all(self.recv_ids, self.send_ids, self.state.group)
 
     def serve(self, stream):
         L.check(L.lib().gtr_shard_serve(C.byref(self.state.s), self.recv_ids.data_ptr(), self.send_rows.data_ptr(),
                                         stream), "shard_serve")
 
     def exchange_rows(self):
-        all_to_all(self.recv_rows, self.send_rows, self.state.group)
+        if not self.alias:
+            all_to_all(self.recv_rows, self.send_rows, self.state.group)
 
     def pack(self, bs, stream):
         st = self.step
@@ -239,8 +245,9 @@ class ShardExchange:
                                        stream), "shard_pack")
 
     def exchange_grads(self):
-        all_to_all(self.recv_grads, self.send_grads, self.state.group)
-        all_gather_packs(self.small_all, self.small_pack, self.state.group)
+        if not self.alias:
+            all_to_all(self.recv_grads, self.send_grads, self.state.group)
+            all_gather_packs(self.small_all, self.small_pack, self.state.group)
 
     def update(self, stream):
         st = self.step

@@ -573,15 +573,17 @@ int gtr_shard_route(const gtr_batch* bt, const int32_t* skeys, const int32_t* sv
                     int32_t* send_ids, int32_t* ckeys, int32_t* node_item_c, int32_t* target_c, int32_t* negatives_c,
                     const float* pe_tab, int pe_k, float* node_pe, void* scratch, size_t scratch_bytes,
                     gtr_stream_t stream);
-/* Owner: the rows every peer requested (recv_ids = the all-to-all of send_ids), brought
- * to step t-1, into send_rows [P][cap][D] (row j of block r = recv_ids[r][j]).       */
+/* Owner: the rows every peer requested (recv_ids = the all-to-all of send_ids) as they
+ * stand after step t-1 (a lagging row's zero-gradient steps applied in registers; the
+ * table is only read), into send_rows [P][cap][D] (row j of block r = recv_ids[r][j]). */
 int gtr_shard_serve(const gtr_shard* sh, const int32_t* recv_ids, float* send_rows, gtr_stream_t stream);
 /* Requester: summed table-gradient row of every requested row -> send_grads [P][cap][D]
  * at its compact slot; summed small-parameter gradient [flat_total] + local loss +
  * this step's overflow flag -> small_pack [flat_total + 2].                           */
 int gtr_shard_pack(const gtr_batch* bt, const gtr_shard* sh, const gtr_tail* tail, const int32_t* ckeys,
                    const gtr_segment* segs, int nseg, float* send_grads, float* small_pack, gtr_stream_t stream);
-/* Owner: AdamW at step t of every requested row with the rank-averaged gradient (peers
+/* Owner: every requested row caught up from its stamp to step t-1 and AdamW-updated at
+ * step t in ONE read-modify-write, with the rank-averaged gradient (peers
  * summed in rank order), stamps t, consts[t]; small parameters from small_all
  * [P][small_words >= flat_total + 2] (rank-averaged) and the rank-averaged loss ->
  * tail->loss_out.  If any rank's pack carries the overflow flag, the step is applied

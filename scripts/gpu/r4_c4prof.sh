@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-LEAN="--cpu-seconds 0 --gather-batch 0 --recall-steps 0 --e2e-steps 0 --c1-reps 0 --tail-probe 0"
+LEAN="--cpu-seconds 0 --gather-batch 0 --recall-steps 0 --e2e-steps 0 --c1-reps 0 --tail-probe 0 --strong-batches 0"
 timeout -k 10 300 python -u -m pytest tests/test_gpu_dropin.py -m gpu -x -v --timeout 200 --timeout-method thread \
   -p no:cacheprovider -k ffn > gpurun_out/t_ffn.log 2>&1 || { tail -30 gpurun_out/t_ffn.log; exit 1; }
 tail -3 gpurun_out/t_ffn.log

@@ -32,6 +32,7 @@ from gpu_helpers import collect, assert_close_norm  # noqa: E402
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LEAN = ["--cpu-seconds", "0", "--gather-batch", "0", "--recall-steps", "0", "--e2e-steps", "0", "--c1-reps", "0",
         "--tail-probe", "0"]
+NO_STRONG = ["--strong-batches", "0"]
 
 
 def _bench(args, timeout=420):
@@ -46,18 +47,38 @@ def _bench(args, timeout=420):
 
 
 def test_bench_gpus2_launches_two_ranks():
-    out = _bench(["--gpus", "2", "--steps", "4", "--warmup", "2", "--num-batches", "4"])
+    """The default line at N = 2, with its strong-scaling leg: the C4 mode (row-sharded
+    table, SyncBN) at a fixed global batch over the same two ranks, launched as a child
+    after the main line's process group is gone."""
+    out = _bench(["--gpus", "2", "--steps", "4", "--warmup", "2", "--num-batches", "4", "--strong-batches", "512",
+                  "--strong-steps", "3"])
     assert out["n_gpus"] == 2
     cfg = out["config"]
     assert cfg["process_group_world"] == 2 and cfg["launcher"].startswith("bench.py --gpus")
     assert cfg["replicas_identical"] is True
     assert cfg["parallelism"] == "dp2" and cfg["global_batch"] == 64 and out["scaling"] == "weak"
     assert out["value"] > 0
+    ss = out["strong_scaling"]
+    assert ss["config"] == "c4" and ss["n_gpus"] == 2 and len(ss["legs"]) == 1
+    leg = ss["legs"][0]
+    assert "error" not in leg, leg
+    assert leg["global_batch"] == 512 and leg["per_gpu_batch"] == 256 and leg["process_group_world"] == 2
+    assert leg["parallelism"] == "dp2+rowshard" and leg["sync_bn"] is True and leg["replicas_identical"] is True
+    assert leg["value"] > 0
+
+
+def test_bench_one_gpu_strong_leg_reports_the_unsharded_step_beside_it():
+    out = _bench(["--steps", "3", "--warmup", "1", "--num-batches", "2", "--strong-batches", "256",
+                  "--strong-steps", "3"])
+    leg = out["strong_scaling"]["legs"][0]
+    assert "error" not in leg, leg
+    assert leg["parallelism"] == "dp1+rowshard" and leg["process_group_world"] is None
+    assert leg["unsharded_single_gpu"]["value"] > 0
 
 
 def test_bench_c4_gpus2_sharded_strong():
     out = _bench(["--config", "c4", "--gpus", "2", "--global-batch", "512", "--steps", "3", "--warmup", "1",
-                  "--num-batches", "2"])
+                  "--num-batches", "2", *NO_STRONG])
     assert out["n_gpus"] == 2 and out["scaling"] == "strong"
     cfg = out["config"]
     assert cfg["global_batch"] == 512 and cfg["per_gpu_batch"] == 256
@@ -67,7 +88,8 @@ def test_bench_c4_gpus2_sharded_strong():
 
 def test_bench_c4_one_gpu_line():
     """N = 1 of the C4 mode: the same sharded step at world 1 (the curve's first point)."""
-    out = _bench(["--config", "c4", "--global-batch", "256", "--steps", "3", "--warmup", "1", "--num-batches", "2"])
+    out = _bench(["--config", "c4", "--global-batch", "256", "--steps", "3", "--warmup", "1", "--num-batches", "2",
+                  *NO_STRONG])
     assert out["n_gpus"] == 1 and out["config"]["parallelism"] == "dp1+rowshard"
     assert out["config"]["process_group_world"] is None
 
