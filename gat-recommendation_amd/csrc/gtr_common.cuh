@@ -231,9 +231,7 @@ __device__ __forceinline__ bool arrive_last(uint32_t* cnt, uint32_t total, int* 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-#ifndef GTR_PROBE_NOFENCE  // timing probe only (wrong results): what the release fences cost
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t prev = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *s_flag = (prev == total - 1) ? 1 : 0;
@@ -259,8 +257,8 @@ __device__ __forceinline__ void st_wt(float* p, float v) {
 // arrive_last for partials stored write-through (st_wt): every wave drains its stores, then
 // ONE relaxed agent-scope ticket per workgroup -- no release fence (an agent-scope release
 // writes back the XCD's dirty L2 lines: with ~3.5k row-group workgroups per layer launch
-// at B = 8192 those fences cost ~85 us of the launch, scripts/dbg/kbench.py + the
-// GTR_PROBE_NOFENCE build); the last arriver acquires (one buffer_inv) and reads plainly.
+// at B = 8192 those fences cost ~85 us of the launch, measured in round 2 with
+// scripts/dbg/kbench.py); the last arriver acquires (one buffer_inv) and reads plainly.
 __device__ __forceinline__ bool arrive_last_wt(uint32_t* cnt, uint32_t total, int* s_flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -326,13 +324,8 @@ struct AdamStep {
   __device__ __forceinline__ void init(const gtr_adam& o, int64_t t) {
     lr = o.lr; b1 = o.beta1; b2 = o.beta2; eps = o.eps; wd = o.weight_decay;
     decoupled = o.decoupled;
-#ifdef GTR_PROBE_NOPOW  // timing probe only: what the step-scalar computation costs
-    double bc1 = 1.0 - (double)o.beta1 * (double)t * 1e-3;
-    double bc2 = 1.0 - (double)o.beta2 * (double)t * 1e-3;
-#else
     double bc1 = 1.0 - pow((double)o.beta1, (double)t);
     double bc2 = 1.0 - pow((double)o.beta2, (double)t);
-#endif
     step_size = (float)((double)o.lr / bc1);
     inv_bc2 = (float)(1.0 / sqrt(bc2));
     decay_mul = (float)(1.0 - (double)o.lr * (double)o.weight_decay);

@@ -41,11 +41,7 @@ using namespace gtr;
 #define GM_BLOCK 512
 #define GM_WAVES (GM_BLOCK / 64)
 
-#ifdef GTR_PROBE_NOMFMA  // timing probe only: what the GEMM kernels cost without their MFMAs
-#define GM_MFMA4(a, b, c) (c + f32x4{(a).x, (b).y, (a).z, (b).w})
-#else
 #define GM_MFMA4(a, b, c) mfma4(a, b, c)
-#endif
 
 // k_proj modes: layer 0 (item row + LapPE), layer >= 1 (BatchNorm fold of the previous
 // layer), rows taken as they are (after a feed-forward block), FFN hidden-gradient GEMM
