@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 if not torch.cuda.is_available():  # pragma: no cover - collected only on the GPU box
     pytest.skip("no GPU", allow_module_level=True)
 
-from gpu_helpers import collect, assert_close_norm, batches, make_pair, ref_batch, small_data  # noqa: E402
+from gpu_helpers import OracleTrio, collect, assert_close_norm, batches, make_pair, ref_batch, small_data  # noqa: E402
 
 from etpgt.train.fused import FusedTrainStep  # noqa: E402
 
@@ -100,29 +100,32 @@ def test_dp_two_ranks_match_oracle_average():
     data = small_data()
     T = data.table_rows
     _, ref = make_pair(T, D, H, K=0, seed=23)
-    opt = torch.optim.AdamW(ref.parameters(), lr=1e-2, weight_decay=1e-2)
+    lr = 1e-2
+    trio = OracleTrio(ref, lambda ps: torch.optim.AdamW(ps, lr=lr, weight_decay=1e-2))
     bl = batches(data, B, NNEG, STEPS * world, seed=24)
     for s in range(STEPS):
-        gsum, ls = {}, []
-        for r in range(world):
-            rb = ref_batch(bl[s * world + r])
-            ref.train()
-            ref.zero_grad()
-            se = ref(rb)
-            loss = R.ref_loss("bpr", se, rb.target_item, rb.negative_items.view(B, NNEG), ref.item_embedding)
-            loss.backward()
-            ls.append(float(loss))
-            for n, p in ref.named_parameters():
-                gsum[n] = gsum.get(n, 0) + p.grad.clone()
-        for n, p in ref.named_parameters():
-            p.grad = gsum[n] / world
-        opt.step()
-        assert abs(res[0][0][s] - sum(ls) / world) <= 1e-3 * abs(sum(ls) / world)
-    for n, p in ref.named_parameters():
-        if n.endswith("lin_key.bias"):  # softmax-invariant: zero gradient, Adam-amplified rounding
-            assert float((res[0][1][n] - p.detach()).abs().max()) <= 2 * 1e-2 * STEPS + 1e-6
-            continue
-        assert_close_norm(res[0][1][n], p, rtol=1e-3, name=n)
+        rbs = [ref_batch(bl[s * world + r]) for r in range(world)]
+
+        def dp_step(model, opt):
+            gsum, ls = {}, []
+            for rb in rbs:
+                model.train()
+                model.zero_grad()
+                se = model(rb)
+                loss = R.ref_loss("bpr", se, rb.target_item, rb.negative_items.view(B, NNEG), model.item_embedding)
+                loss.backward()
+                ls.append(float(loss))
+                for n, p in model.named_parameters():
+                    gsum[n] = gsum.get(n, 0) + p.grad.clone()
+            for n, p in model.named_parameters():
+                p.grad = gsum[n] / world
+            opt.step()
+            return sum(ls) / world
+
+        lavg = trio.step(dp_step)
+        assert abs(res[0][0][s] - lavg) <= 1e-3 * abs(lavg)
+    # every parameter ELEMENTWISE against the oracle trio (fp32 / fp32 one thread / fp64)
+    trio.compare(res[0][1], lr=lr)
 
 
 def _concat(b0, b1):

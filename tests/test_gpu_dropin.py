@@ -46,9 +46,13 @@ def _script():
     return tb
 
 
-def test_train_baseline_counterpart_one_epoch_matches_oracle(tmp_path):
+@pytest.mark.parametrize("D,H,L,B", [(32, 2, 2, 16), (256, 4, 3, 32)])
+def test_train_baseline_counterpart_one_epoch_matches_oracle(tmp_path, D, H, L, B):
+    """(256, 4, 3, 32): the reference script's own defaults -- embedding / hidden 256, 3
+    layers, 4 heads, batch 32, 5 negatives (train_baseline.py:39-42,63-64) -- with
+    dropout 0 so that the oracle can replay the epoch."""
     d = write_csvs(tmp_path)
-    D, H, L, B, n = 32, 2, 2, 16, 5
+    n = 5
     args = ["--model", "graph_transformer_optimized", "--train-sessions", str(d / "train.csv"),
             "--val-sessions", str(d / "val.csv"), "--graph-edges", str(d / "graph_edges.csv"),
             "--embedding-dim", str(D), "--hidden-dim", str(D), "--num-layers", str(L), "--num-heads", str(H),
@@ -120,6 +124,31 @@ def test_train_baseline_counterpart_one_epoch_matches_oracle(tmp_path):
     r10 = compute_recall_at_k(torch.cat(preds)[:, :10], torch.cat(tg), k=10)
     got = hist["val_metrics"][0]["recall@10"]
     assert abs(got - r10) <= 1.0 / Sv + 1e-9, (got, r10)
+
+
+def test_train_baseline_reference_default_flags_one_epoch(tmp_path):
+    """``train_baseline.py --model graph_transformer_optimized`` with NO model / training
+    flags: the reference defaults (d = 256, 3 layers, 4 heads, dropout 0.1, batch 32, 5
+    negatives, AdamW 1e-3 / 1e-5).  One epoch through the fused step: finite loss, the
+    validation metrics, a checkpoint with the reference's state-dict keys."""
+    d = write_csvs(tmp_path)
+    args = ["--model", "graph_transformer_optimized", "--train-sessions", str(d / "train.csv"),
+            "--val-sessions", str(d / "val.csv"), "--graph-edges", str(d / "graph_edges.csv"), "--max-epochs", "1",
+            "--num-workers", "0", "--output-dir", str(tmp_path / "out")]
+    trainer = _script().main(args)
+    m = trainer.model
+    assert trainer._fused is not None
+    assert m.item_embedding.weight.shape[1] == 256 and m.num_layers == 3 and m.num_heads == 4
+    with open(tmp_path / "out" / "graph_transformer_optimized" / "history.json") as f:
+        hist = json.load(f)
+    assert len(hist["train_loss"]) == 1 and np.isfinite(hist["train_loss"][0])
+    assert 0.0 <= hist["val_metrics"][0]["recall@10"] <= 1.0
+    ck = torch.load(tmp_path / "out" / "graph_transformer_optimized" / "checkpoint_latest.pt", map_location="cpu",
+                    weights_only=True)
+    sd = ck["model_state_dict"]
+    for k in ("item_embedding.weight", "laplacian_pe.projection.weight", "convs.2.lin_query.weight",
+              "convs.2.lin_beta.weight", "batch_norms.2.running_var"):
+        assert k in sd, k
 
 
 def test_train_baseline_ffn_model_trains_one_epoch(tmp_path):

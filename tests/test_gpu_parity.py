@@ -452,3 +452,35 @@ def test_row_group_widths_match_oracle(rg, monkeypatch):
     monkeypatch.setenv("GTR_ROW_GROUP", rg)
     _fused_vs_reference(64, 1, 0, "bpr", "adamw", True, B=32, steps=3)
     _fused_vs_reference(128, 4, 16, "listwise", "adamw", True, B=32, steps=3)
+
+
+@pytest.mark.parametrize("B", [32, 700])
+def test_dropin_default_config_fused_steps(B):
+    """The drop-in's default model: ``train_baseline.py --model graph_transformer_optimized``
+    at its default flags builds create_graph_transformer_optimized with d = 256, 3 layers,
+    4 heads and LapPE k = 16 (train_baseline.py:39-42,220-232), trained by the Trainer's
+    default BPR loss with 5 negatives.  Five fused steps against the oracle trainer, every
+    trained parameter ELEMENTWISE (gpu_helpers.close_trained), at B = 32 and at B = 700
+    (> 128 row groups at d = 256)."""
+    from gpu_helpers import OracleTrio
+
+    T = data().table_rows
+    m, ref = make_pair(T, 256, 4, L=3, K=16, seed=41)
+    m.train(); ref.train()
+    fused = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5, loss="bpr")
+    trio = OracleTrio(ref, lambda ps: torch.optim.AdamW(ps, lr=1e-3, weight_decay=1e-5))
+    for i, sb in enumerate(batches(data(), B, 5, 5, seed=43)):
+        hl = float(fused(sb.to("cuda")))
+        rb = ref_batch(sb)
+        rl = trio.step(lambda mod, o: R.ref_train_step(mod, rb, o, "bpr"))
+        assert abs(hl - float(rl)) <= 1e-3 * max(1.0, abs(float(rl))), (i, hl, float(rl))
+    if B == 700:
+        assert fused.ws.g_cap > 128, fused.ws.g_cap
+    trio.compare(dict(m.named_parameters()), lr=1e-3)
+    bufs = dict(m.named_buffers())
+    from gpu_helpers import close_trained
+
+    b64, b1 = dict(trio.ref64.named_buffers()), dict(trio.ref1.named_buffers())
+    for name, b in ref.named_buffers():
+        if "running" in name:
+            close_trained(bufs[name], b, b64[name], torch.zeros_like(b, dtype=torch.bool), 0.0, name, b1[name])
