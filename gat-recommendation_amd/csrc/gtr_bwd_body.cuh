@@ -935,9 +935,9 @@ __device__ __forceinline__ void conv_bwd_body(const ConvBwdK& a, int rb) {
     const int bk = g / GTR_PART_BUCKET, b0 = bk * GTR_PART_BUCKET;
     if (!arrive_last_wt(a.p_cnt + 4 + 2 * bk, (uint32_t)min(GTR_PART_BUCKET, Gn - b0), s_flag)) return;
     float* row0 = a.p_gpart + (size_t)b0 * 2 * D;
-    block_sum_rows<CONV_BLOCK>(row0, min(GTR_PART_BUCKET, Gn - b0), 2 * D, (size_t)2 * D, row0, sm);
+    block_sum_rows<CONV_BLOCK>(row0, min(GTR_PART_BUCKET, Gn - b0), 2 * D, (size_t)2 * D, row0, sm, true);
     if (tid == 0) reset_counter(a.p_cnt + 4 + 2 * bk);
-    if (!arrive_last(a.p_cnt, (uint32_t)nbk, s_flag)) return;
+    if (!arrive_last_wt(a.p_cnt, (uint32_t)nbk, s_flag)) return;
     block_sum_rows<CONV_BLOCK>(a.p_gpart, nbk, 2 * D, (size_t)GTR_PART_BUCKET * 2 * D, a.p_gsum, sm);
   } else {
     if (!arrive_last_wt(a.p_cnt, (uint32_t)Gn, s_flag)) return;

@@ -281,20 +281,25 @@ __device__ __forceinline__ void reset_counter(uint32_t* cnt) {
 }
 
 // Column sums of a [G][stride] partial array (columns [0, W)) with the whole block, in a
-// fixed order: slice sl of NSL = BLK / W sums rows sl, sl + NSL, ... with 8 loads in
+// fixed order: slice sl of NSL = BLK / W sums rows sl, sl + NSL, ... with 32 loads in
 // flight, then the slices are combined through LDS (scr: >= BLK floats).  Used by the
 // last-arriving workgroup of a launch, where hundreds of partial rows (large batches)
-// summed by one thread per column were a serial chain of L2 round trips.
+// summed by one thread per column were a serial chain of L2 round trips: the partial rows
+// sit in the Infinity Cache (written through by the producers), ~1 us away, so the launch's
+// tail is one such latency per unrolled round (round 4: 8 -> 32 in flight, the readout's
+// 256-row sum from 16 rounds to 4; the same order of additions, so the same sums).
+// wt: `out` written through (st_wt) -- a bucket's merged row read by the launch's final
+// last arriver on another XCD after arrive_last_wt (no agent-scope release fence).
 template <int BLK>
 __device__ __forceinline__ void block_sum_rows(const float* p, int G, int W, size_t stride, float* out,
-                                               float* scr) {
+                                               float* scr, bool wt = false) {
   const int tid = threadIdx.x;
   if (W >= BLK) {
     for (int j = tid; j < W; j += BLK) {
       float acc = 0.0f;
-#pragma unroll 8
+#pragma unroll 32
       for (int q = 0; q < G; ++q) acc += p[(size_t)q * stride + j];
-      out[j] = acc;
+      if (wt) st_wt(out + j, acc); else out[j] = acc;
     }
     __syncthreads();
     return;
@@ -303,7 +308,7 @@ __device__ __forceinline__ void block_sum_rows(const float* p, int G, int W, siz
   const int j = tid % W, sl = tid / W;
   if (sl < NSL) {
     float acc = 0.0f;
-#pragma unroll 8
+#pragma unroll 32
     for (int q = sl; q < G; q += NSL) acc += p[(size_t)q * stride + j];
     scr[sl * W + j] = acc;
   }
@@ -311,7 +316,7 @@ __device__ __forceinline__ void block_sum_rows(const float* p, int G, int W, siz
   if (tid < W) {
     float t = 0.0f;
     for (int q = 0; q < NSL; ++q) t += scr[q * W + tid];
-    out[tid] = t;
+    if (wt) st_wt(out + tid, t); else out[tid] = t;
   }
   __syncthreads();
 }

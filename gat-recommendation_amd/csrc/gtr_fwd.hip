@@ -123,21 +123,26 @@ __device__ __forceinline__ void bn_fwd_finalize(const ConvFwdK& a, int g, int Gn
   const int tid = threadIdx.x;
   constexpr int PW = 1 + 2 * D;
   const int nbk = (Gn + GTR_PART_BUCKET - 1) / GTR_PART_BUCKET;
-  // first level: the partial rows were stored write-through (st_wt) -- no release fence per
-  // workgroup; the bucket mergers' rows are plain stores behind arrive_last's release
+  // both levels: the partial rows and the bucket mergers' rows are stored write-through
+  // (st_wt) -- no agent-scope release fence anywhere (round 4: the bucket level's fence was
+  // part of the ~10 us tail a last arriver added to k_attn_rows)
   if (nbk > 1) {
     const int bk = g / GTR_PART_BUCKET, b0 = bk * GTR_PART_BUCKET;
     if (!arrive_last_wt(a.cnt + 4 + 2 * bk, (uint32_t)min(GTR_PART_BUCKET, Gn - b0), s_flag)) return;
+    GTR_PH(20 + a.layer, 4);
     float* row0 = a.bn_part + (size_t)b0 * PW;
-    bn_merge_parts<D, BLK>(row0, min(GTR_PART_BUCKET, Gn - b0), red, PW, row0);
+    bn_merge_parts<D, BLK>(row0, min(GTR_PART_BUCKET, Gn - b0), red, PW, row0, true);
     if (tid == 0) reset_counter(a.cnt + 4 + 2 * bk);
-    if (!arrive_last(a.cnt, (uint32_t)nbk, s_flag)) return;
+    GTR_PH(20 + a.layer, 5);
+    if (!arrive_last_wt(a.cnt, (uint32_t)nbk, s_flag)) return;
+    GTR_PH(20 + a.layer, 6);
     if (a.merge_only) {  // the buckets' rows -> ONE row (row 0, bucket 0's own row: may alias)
       bn_merge_parts<D, BLK>(a.bn_part, nbk, red, (size_t)GTR_PART_BUCKET * PW, a.bn_part);
       if (tid == 0) reset_counter(a.cnt);
       return;
     }
     bn_stats_from_parts<D, BLK>(a.bn_part, nbk, a.bn_eps, s_bn, s_bn + D, s_uvar, red, (size_t)GTR_PART_BUCKET * PW);
+    GTR_PH(20 + a.layer, 7);
   } else {
     if (!arrive_last_wt(a.cnt, (uint32_t)Gn, s_flag)) return;
     if (a.merge_only) {
@@ -810,6 +815,7 @@ __global__ __launch_bounds__(AR_BLOCK) __attribute__((amdgpu_waves_per_eu(6, 8))
   const int g = blockIdx.x;
   if (g >= Gn) return;  // block-uniform: only live workgroups write partials and arrive
   const int r0 = g * AR_ROWS, nrow = min(AR_ROWS, N - r0);
+  GTR_PH(20 + a.layer, 0);
   const uint32_t ctr = a.rng_ctr ? load_step_ctr(a.rng_ctr) + a.ctr_add : 0u;
   const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
   const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
@@ -1025,6 +1031,7 @@ __global__ __launch_bounds__(AR_BLOCK) __attribute__((amdgpu_waves_per_eu(6, 8))
   if (!a.train) return;
   // ---- this workgroup's BatchNorm partial (count, mean, M2) over its rows
   __syncthreads();
+  GTR_PH(20 + a.layer, 1);
   constexpr int NS = AR_BLOCK / D >= 1 ? AR_BLOCK / D : 1;
   float* part = a.bn_part + (size_t)g * (1 + 2 * D);
   {
@@ -1057,7 +1064,9 @@ __global__ __launch_bounds__(AR_BLOCK) __attribute__((amdgpu_waves_per_eu(6, 8))
     }
     if (tid == 0) st_wt(part, (float)nrow);
   }
+  GTR_PH(20 + a.layer, 2);
   bn_fwd_finalize<D, AR_BLOCK>(a, g, Gn, &s_flag, s_red, s_bn, s_uv);
+  GTR_PH(20 + a.layer, 3);
 }
 
 struct ReadoutK {
@@ -1501,6 +1510,23 @@ __device__ __forceinline__ void issue_round(float (&rv)[KQ][D / 16], const float
   }
 }
 
+// The same round from the session's negative ids preloaded into registers (nid[i] holds id
+// i * 64 + lane; n <= 256): a round is 16 consecutive ids, all in one register, so the
+// round's row loads need no id load of their own (round 4: every round used to wait for its
+// ids before its rows -- one memory latency per 16 rows on the wave's serial path).
+template <int D, int KQ>
+__device__ __forceinline__ void issue_round_pre(float (&rv)[KQ][D / 16], const float* table, const int (&nid)[4],
+                                                int n, int r, int rg, int c0) {
+  static_assert(4 * KQ == 16, "16 ids per round: a round never straddles two id registers");
+  const int blk = r >> 2;  // wave-uniform
+  const int src = blk == 0 ? nid[0] : blk == 1 ? nid[1] : blk == 2 ? nid[2] : nid[3];
+#pragma unroll
+  for (int q = 0; q < KQ; ++q) {
+    const int id = __shfl(src, (r & 3) * 16 + q * 4 + rg);
+    ld_row<D / 16>(rv[q], table + (size_t)id * D + c0, r * 16 + q * 4 + rg < n);
+  }
+}
+
 // Per-session scoring accumulators of one wave (row group rg's share until combined).
 template <int EPL>
 struct ScoreAcc {
@@ -1584,6 +1610,7 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
   const float inv_bn = 1.0f / (Bm * (float)n);
   const float inv_b = 1.0f / Bm;
   const float inv_t = 1.0f / a.temperature;
+  GTR_PH(26, 0);
 
   if (do_fwd) {
     prev_bn_stats<D, RW_BLOCK>(a.train, a.cred, a.sync ? a.nparts : a.bt.hdr[4], a.sync ? a.part_all : a.part,
@@ -1596,18 +1623,29 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
     for (int j = tid; j < D; j += RW_BLOCK) { s_gb[j] = a.gamma[j]; s_gb[D + j] = a.beta[j]; }
   for (int j = lane; j < 2 * D; j += 64) s_red[wave][j] = 0.0f;  // this wave's BN-backward sums
   __syncthreads();
+  GTR_PH(26, 1);
 
   float lw_sum = 0.0f, bpr_sum = 0.0f;
 
+  // sessions interleaved over the workgroups first (b = wave * grid + rb): at B below
+  // grid * RW_WAVES every CU gets B / grid busy waves instead of half the CUs getting 8
 #pragma unroll 1
-  for (int b = rb * RW_WAVES + wave; b < B; b += a.main_grid * RW_WAVES) {
+  for (int b = wave * a.main_grid + rb; b < B; b += a.main_grid * RW_WAVES) {
     const int n0 = a.bt.node_ptr[b], n1 = a.bt.node_ptr[b + 1];
     const float cnt = (float)(n1 - n0);
     const int* negs = a.bt.negatives + (size_t)b * n;
     float tv[EPL], rv[KQ][EPL], rv2[KQ][EPL];
+    const bool pre = n <= RW_NMAX;  // all of the session's negative ids in registers
+    int nid[4] = {0, 0, 0, 0};
     if (do_loss) {
+      if (pre) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (i * 64 < n) nid[i] = i * 64 + lane < n ? negs[i * 64 + lane] : 0;
+      }
       ld_row<EPL>(tv, a.table + (size_t)a.bt.target[b] * D + c0, true);
-      issue_round<D, KQ>(rv, a.table, negs, n, 0, lane, rg, c0);
+      if (pre) issue_round_pre<D, KQ>(rv, a.table, nid, n, 0, rg, c0);
+      else issue_round<D, KQ>(rv, a.table, negs, n, 0, lane, rg, c0);
     }
     // ---- session embedding: mean over node rows of drop(bn(out) + xin)
     float se[EPL];
@@ -1631,6 +1669,7 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
 #pragma unroll
       for (int e = 0; e < EPL; ++e) se[e] = sum_groups(acc[e]) / cnt;
       if (rg == 0) st_row<EPL>(a.se + (size_t)b * D + c0, se);
+      if (b == rb) GTR_PH(26, 6);
     } else {
       ld_row<EPL>(se, a.se + (size_t)b * D + c0, true);
     }
@@ -1656,14 +1695,21 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
       // double-buffered rounds: round r+1's rows are in flight while round r is scored
 #pragma unroll 1
       for (int r = 0; r < nr; r += 2) {
-        if (r + 1 < nr) issue_round<D, KQ>(rv2, a.table, negs, n, r + 1, lane, rg, c0);
+        if (r + 1 < nr) {
+          if (pre) issue_round_pre<D, KQ>(rv2, a.table, nid, n, r + 1, rg, c0);
+          else issue_round<D, KQ>(rv2, a.table, negs, n, r + 1, lane, rg, c0);
+        }
         consume_round<D, KQ>(A, rv, se, pos, r, n, rg, lead, use_bpr, use_lw, inv_bn, w_bpr, inv_t, sc, coef_row);
         if (r + 1 < nr) {
-          if (r + 2 < nr) issue_round<D, KQ>(rv, a.table, negs, n, r + 2, lane, rg, c0);
+          if (r + 2 < nr) {
+            if (pre) issue_round_pre<D, KQ>(rv, a.table, nid, n, r + 2, rg, c0);
+            else issue_round<D, KQ>(rv, a.table, negs, n, r + 2, lane, rg, c0);
+          }
           consume_round<D, KQ>(A, rv2, se, pos, r + 1, n, rg, lead, use_bpr, use_lw, inv_bn, w_bpr, inv_t, sc,
                                coef_row);
         }
       }
+      if (b == rb) GTR_PH(26, 7);
       bpr_sum += A.bpr_sum;
       float dpos = sum_groups(A.dpos);
 #pragma unroll
@@ -1711,6 +1757,7 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
       for (int e = 0; e < EPL; ++e) dse[e] += dpos * tv[e];
       if (lane == 0) a.coef_tgt[b] = dpos;
       if (rg == 0 && a.dse_out) st_row<EPL>(a.dse_out + (size_t)b * D + c0, dse);
+      if (b == rb) GTR_PH(26, 8);
     } else if (do_bwd) {
       ld_row<EPL>(dse, a.dse_in + (size_t)b * D + c0, true);
     }
@@ -1741,9 +1788,11 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
         const float g1 = sum_groups(gs[e]), g2 = sum_groups(gx[e]);
         if (rg == 0) { s_red[wave][c0 + e] += g1; s_red[wave][D + c0 + e] += g2; }
       }
+      if (b == rb) GTR_PH(26, 9);
     }
   }
 
+  GTR_PH(26, 2);
   if (!(do_loss || do_bwd)) return;
   // ---- block partials in fixed order (waves)
   const float bsum = wave_sum(bpr_sum);
@@ -1761,8 +1810,10 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
       st_wt(a.gpart + (size_t)rb * 2 * D + j, acc);
     }
   }
+  GTR_PH(26, 3);
   if (!a.fin) return;
   if (!arrive_last_wt(a.cnt, (uint32_t)a.main_grid, &s_flag)) return;
+  GTR_PH(26, 4);
   if (do_loss) {
     __shared__ float s_pair[2];
     block_sum_rows<RW_BLOCK>(a.loss_part, a.main_grid, 2, 2, s_pair, s_scr);
@@ -1770,6 +1821,7 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
   }
   if (do_bwd) block_sum_rows<RW_BLOCK>(a.gpart, a.main_grid, 2 * D, (size_t)2 * D, a.gsum, s_scr);
   if (tid == 0) reset_counter(a.cnt);
+  GTR_PH(26, 5);
 }
 
 

@@ -156,10 +156,13 @@ __device__ __forceinline__ void store_vec(float* p, const float (&x)[VPL], bool 
 // by bn_parts_load -- which a caller may issue early, before loads whose wait it must not
 // join (vector loads retire in order) -- and kept for both passes of bn_fold_parts_ (same
 // summation order as re-reading them).
+// QR covers a whole GTR_PART_BUCKET of rows per slice up to 16 rows (3 x 16 VGPRs): a
+// bucket merge at 2 slices is then ONE round of loads, and past QR the loops keep 16 in
+// flight (the same order of additions either way).
 template <int D, int BLK>
 struct BnParts {
   static constexpr int NSL = BLK / D >= 1 ? BLK / D : 1;
-  static constexpr int QR = (32 + NSL - 1) / NSL < 8 ? (32 + NSL - 1) / NSL : 8;
+  static constexpr int QR = (32 + NSL - 1) / NSL < 16 ? (32 + NSL - 1) / NSL : 16;
   float rc[QR], rmu[QR], rm2[QR];
 };
 
@@ -189,7 +192,7 @@ __device__ __forceinline__ void bn_parts_load(const float* part, int G, size_t r
 template <int D, int BLK>
 __device__ __forceinline__ void bn_fold_parts_(const float* part, int G, float eps, float* s_mean,
                                                float* s_rstd, float* s_uvar, float* scr, size_t rstride,
-                                               float* merged, const BnParts<D, BLK>& r) {
+                                               float* merged, const BnParts<D, BLK>& r, bool wt = false) {
   constexpr int NSL = BnParts<D, BLK>::NSL, QR = BnParts<D, BLK>::QR;
   const int tid = threadIdx.x;
   const int j = tid % D, sl = tid / D;
@@ -204,7 +207,7 @@ __device__ __forceinline__ void bn_fold_parts_(const float* part, int G, float e
         n += r.rc[u];
         sum += r.rc[u] * r.rmu[u];
       }
-#pragma unroll 8
+#pragma unroll 16
     for (int q = sl + QR * NSL; q < G; q += NSL) {
       const float* pp = part + (size_t)q * rstride;
       const float c = pp[0];
@@ -227,7 +230,7 @@ __device__ __forceinline__ void bn_fold_parts_(const float* part, int G, float e
         const float d = r.rmu[u] - mean;
         m2 += r.rm2[u] + r.rc[u] * d * d;
       }
-#pragma unroll 8
+#pragma unroll 16
     for (int q = sl + QR * NSL; q < G; q += NSL) {
       const float* pp = part + (size_t)q * rstride;
       const float d = pp[1 + j] - mean;
@@ -239,7 +242,11 @@ __device__ __forceinline__ void bn_fold_parts_(const float* part, int G, float e
   if (tid < D) {  // slice 0's threads: tid == j, n_tot and mean already formed
     float m2 = 0.0f;
     for (int q = 0; q < NSL; ++q) m2 += s_m2[q * D + tid];
-    if (merged) {  // the G partials combined into one (count, mean, M2) row (may alias row 0)
+    if (merged && wt) {  // written through: read on another XCD after arrive_last_wt
+      st_wt(merged + 1 + tid, mean);
+      st_wt(merged + 1 + D + tid, m2);
+      if (tid == 0) st_wt(merged, n_tot);
+    } else if (merged) {  // the G partials combined into one (count, mean, M2) row (may alias row 0)
       merged[1 + tid] = mean;
       merged[1 + D + tid] = m2;
       if (tid == 0) merged[0] = n_tot;
@@ -272,10 +279,10 @@ __device__ __forceinline__ void bn_stats_from_loaded(const float* part, int G, f
 
 template <int D, int BLK>
 __device__ __forceinline__ void bn_merge_parts(const float* part, int G, float* scr, size_t rstride,
-                                               float* merged) {
+                                               float* merged, bool wt = false) {
   BnParts<D, BLK> r;
   bn_parts_load<D, BLK>(part, G, rstride, r);
-  bn_fold_parts_<D, BLK>(part, G, 0.0f, nullptr, nullptr, nullptr, scr, rstride, merged, r);
+  bn_fold_parts_<D, BLK>(part, G, 0.0f, nullptr, nullptr, nullptr, scr, rstride, merged, r, wt);
 }
 
 // Row groups whose partials one last-arriving workgroup combines; past that the groups

@@ -163,22 +163,26 @@ def readout_grid(b_cap: int) -> int:
     return int(L.lib().gtr_readout_grid(int(b_cap)))
 
 
-def split_default(D: int, g_cap: int) -> bool:
+def split_default(D: int, g_cap: int, sync: bool = False) -> bool:
     """The split (GEMM + attention) layer path: GTR_SPLIT=1 / 0 forces it on / off (tests,
-    A/B); by default from 129 row groups on -- where the chain sweep is off too -- at
-    D in {64, 128}."""
+    A/B); by default at D in {64, 128} from 513 row groups on (measured, scripts/dbg/kbench.py
+    full steps: the fused row-group kernels win up to B = 2048 -- C3 B = 1024 315 vs 363 us,
+    B = 2048 414 vs 433; C2 B = 1024 187 vs 248, B = 2048 231 vs 264 -- and the split path
+    from B = 3072 / 4096 on).  Under SyncBN across ranks (``sync``) from 129 groups on: the
+    split path gathers ONE merged BatchNorm row per rank where the fused kernels gather
+    every row group's partials and each consumer workgroup reduces all of them."""
     if D not in (64, 128):
         return False
     e = os.environ.get("GTR_SPLIT")
     if e is not None:
         return e == "1"
-    return g_cap > 128
+    return g_cap > (128 if sync else 512)
 
 
 class Workspace:
     """Capacity-sized activations + gradient buffers for one in-flight batch."""
 
-    def __init__(self, eng: "Engine", caps: Caps, R: int, P: int, split: bool | None = None):
+    def __init__(self, eng: "Engine", caps: Caps, R: int, P: int, split: bool | None = None, sync: bool = False):
         dev = eng.device
         D, H, Lc = eng.D, eng.H, eng.L
         self.caps, self.R, self.P = caps, R, P
@@ -206,7 +210,7 @@ class Workspace:
         # large batches: each layer as GEMM + attention launches (gtr_qkvs_* / gtr_attn_*)
         # instead of one fused launch -- from more row groups than the chip has CUs / 2
         # (the fused kernels re-fetch W_all per 16-row group), D in {64, 128}
-        self.split = split_default(D, g) if split is None else (bool(split) and D in (64, 128))
+        self.split = split_default(D, g, sync) if split is None else (bool(split) and D in (64, 128))
         if eng.ffn:  # the feed-forward blocks run on the split layer path only
             self.split = True
         self.dx0 = _f32(n, D, device=dev)
@@ -361,15 +365,15 @@ class Engine:
         rows = rows if rows > 0 else 32
         return max(1, min(64, (caps.n_cap + rows - 1) // rows))
 
-    def workspace(self, caps: Caps, fresh: bool = False, split: bool | None = None) -> Workspace:
+    def workspace(self, caps: Caps, fresh: bool = False, split: bool | None = None, sync: bool = False) -> Workspace:
         """Workspace of these capacities; ``split`` forces the split (GEMM + attention) layer
-        path on or off (None: split_default)."""
+        path on or off (None: split_default; ``sync``: SyncBN across ranks)."""
         if fresh:
-            return Workspace(self, caps, self.choose_R(caps), self.choose_P(caps), split)
-        key = caps if split is None else (caps, bool(split))
+            return Workspace(self, caps, self.choose_R(caps), self.choose_P(caps), split, sync)
+        key = (caps, split, bool(sync))
         ws = self._ws_cache.pop(key, None)
         if ws is None:
-            ws = Workspace(self, caps, self.choose_R(caps), self.choose_P(caps), split)
+            ws = Workspace(self, caps, self.choose_R(caps), self.choose_P(caps), split, sync)
         self._ws_cache[key] = ws  # most recently used last
         while len(self._ws_cache) > 8:
             self._ws_cache.pop(next(iter(self._ws_cache)))

@@ -136,6 +136,12 @@ class GraphTransformer(BaseRecommendationModel):
         params = eng.flat.params()
         need_grad = torch.is_grad_enabled() and (self.item_embedding.weight.requires_grad
                                                   or any(p.requires_grad for p in params))
+        if not self.training and not need_grad:  # inference: the registered op etpgt::graph_transformer_eval
+            from etpgt.backend.ops import engine_handle
+
+            return torch.ops.etpgt.graph_transformer_eval(blob, node_pe, self.item_embedding.weight, list(params),
+                                                          engine_handle(eng), caps.n_cap, caps.b_cap, caps.e_cap,
+                                                          caps.n_neg, B)
         return GraphTransformerFn.apply(eng, caps, blob, node_pe, B, self.training, need_grad,
                                         self.item_embedding.weight, *params)
 

@@ -167,7 +167,7 @@ class FusedTrainStep:
         eng = self.eng
         caps = self._agree(caps)
         self.caps = caps
-        self.ws = eng.workspace(caps, split=self._force_split)
+        self.ws = eng.workspace(caps, split=self._force_split, sync=self.sync_bn and self.world > 1)
         from etpgt.data.batch import blob_layout
 
         self.blob = torch.zeros(blob_layout(caps)["_total"], dtype=torch.int32, device=self.dev)

@@ -125,3 +125,27 @@ def test_library_built_from_this_tree(libpath):
     from etpgt.backend import _lib
 
     assert _lib.library_source_hash() == _lib.source_hash()
+
+
+def test_kernels_are_registered_torch_library_ops():
+    """the HIP entry points are torch.library ops of the ``etpgt`` namespace
+    (FX / torch.compile / fake-tensor tracing see them), each with a fake implementation
+    for shape inference -- checked here without a GPU (no kernel runs under FakeTensorMode)."""
+    import torch
+    from torch._subclasses.fake_tensor import FakeTensorMode
+
+    from etpgt.backend import ops  # noqa: F401  (registers the ops)
+
+    for name in ("score_loss", "score_rows_grad", "score_topk", "graph_transformer_eval"):
+        assert hasattr(torch.ops.etpgt, name), name
+    with FakeTensorMode():
+        se, tab = torch.empty(4, 64), torch.empty(100, 64)
+        t, n = torch.zeros(4, dtype=torch.long), torch.zeros(4, 5, dtype=torch.long)
+        loss, dse, ct, cn = torch.ops.etpgt.score_loss(se, tab, t, n, 2, 1.0, 0.7)
+        assert loss.shape == () and dse.shape == (4, 64) and ct.shape == (4,) and cn.shape == (20,)
+        assert torch.ops.etpgt.score_rows_grad(se, ct, cn, t, n, 100).shape == (100, 64)
+        idx, sc = torch.ops.etpgt.score_topk(se, tab, 10, None, None)
+        assert idx.shape == (4, 10) and idx.dtype == torch.int64 and sc.shape == (4, 10)
+        blob = torch.zeros(64, dtype=torch.int32)
+        out = torch.ops.etpgt.graph_transformer_eval(blob, None, tab, [tab], 0, 16, 4, 16, 5, 4)
+        assert out.shape == (4, 64)

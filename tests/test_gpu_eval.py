@@ -250,3 +250,19 @@ def test_recommender_k_past_the_unmasked_items(tmp_path):
     assert all(s == float("-inf") for s in scores[live:])
     short, _ = rec.recommend(ValidatedRequest(session, live))
     assert short == ids[:live]
+
+
+def test_registered_ops_pass_opcheck():
+    """torch.library.opcheck of the registered HIP ops (schema, fake implementation vs the
+    real kernel, autograd registration) on device tensors."""
+    from etpgt.backend import ops  # noqa: F401
+
+    g = torch.Generator().manual_seed(5)
+    se = torch.randn(8, 64, generator=g).cuda().requires_grad_()
+    tab = torch.randn(300, 64, generator=g).cuda().requires_grad_()
+    t = torch.randint(1, 300, (8,), generator=g).cuda()
+    n = torch.randint(1, 300, (8, 5), generator=g).cuda()
+    torch.library.opcheck(torch.ops.etpgt.score_loss.default, (se, tab, t, n, 2, 1.0, 0.7),
+                          test_utils=("test_schema", "test_faketensor", "test_autograd_registration"))
+    torch.library.opcheck(torch.ops.etpgt.score_topk.default, (se.detach(), tab.detach(), 10, None, None),
+                          test_utils=("test_schema", "test_faketensor"))
