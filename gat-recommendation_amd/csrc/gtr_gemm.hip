@@ -34,6 +34,17 @@
 
 #include "gtr_layer.cuh"
 
+namespace gtr {  // gtr_gemm_gen.hip: the LDS-staged GEMMs for D = 256 and FFN expansions != 4
+int gen_qkvs_fwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_embed* emb, const gtr_layer* layers, int l,
+                 hipStream_t s);
+int gen_qkvs_bwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l, float* dx0,
+                 hipStream_t s);
+int gen_ffn_fwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l, hipStream_t s);
+int gen_ffn_bwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l, hipStream_t s);
+int gen_ffn_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l, float* slab,
+                  int n_chunks, int64_t slab_stride, hipStream_t s);
+}  // namespace gtr
+
 namespace {
 
 using namespace gtr;
@@ -612,7 +623,10 @@ extern "C" int gtr_qkvs_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     return GTR_E_ARG;
   }
   const int D = cfg->dim;
-  if (D != 64 && D != 128) { set_error("gtr_qkvs_fwd: dim %d (the split layer path covers 64 / 128)", D); return GTR_E_ARG; }
+  if (D != 64 && D != 128 && D != 256) {
+    set_error("gtr_qkvs_fwd: dim %d (the split layer path covers 64 / 128 / 256)", D);
+    return GTR_E_ARG;
+  }
   if (l == 0 && (!emb || !emb->table)) { set_error("gtr_qkvs_fwd: layer 0 needs the table"); return GTR_E_ARG; }
   if (l == 0 && cfg->pe_k > 0 && (!emb->wpe || !emb->bpe || (!emb->pe_tab && !bt->node_pe))) {
     set_error("gtr_qkvs_fwd: Laplacian PE not precomputed");
@@ -624,6 +638,11 @@ extern "C" int gtr_qkvs_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     set_error("gtr_qkvs_fwd: the split path reads producer-finalized BatchNorm statistics (consumer_reduce 0) "
               "or, under sync_bn, the ranks' merged rows (split_sync)");
     return GTR_E_ARG;
+  }
+  if (D == 256) {  // LDS-staged GEMM (gtr_gemm_gen.hip): no SyncBN merged-row mode there
+    if (cfg->sync_bn && cfg->training) { set_error("gtr_qkvs_fwd: dim 256 on the split path has no SyncBN"); return GTR_E_ARG; }
+    if (l == 0 && cfg->pe_k > 0 && (!emb->wpe || !emb->bpe)) { set_error("gtr_qkvs_fwd: Laplacian PE not precomputed"); return GTR_E_ARG; }
+    return gen_qkvs_fwd(cfg, bt, emb, layers, l, (hipStream_t)stream);
   }
   const gtr_layer& L = layers[l];
   ProjK k{};
@@ -686,9 +705,17 @@ extern "C" int gtr_qkvs_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     return GTR_E_ARG;
   }
   const int D = cfg->dim;
-  if (D != 64 && D != 128) { set_error("gtr_qkvs_bwd: dim %d (the split layer path covers 64 / 128)", D); return GTR_E_ARG; }
+  if (D != 64 && D != 128 && D != 256) {
+    set_error("gtr_qkvs_bwd: dim %d (the split layer path covers 64 / 128 / 256)", D);
+    return GTR_E_ARG;
+  }
   if (!cfg->training) { set_error("gtr_qkvs_bwd: backward requires training mode"); return GTR_E_ARG; }
   if (cfg->sync_bn && !cfg->split_sync) { set_error("gtr_qkvs_bwd: sync_bn needs split_sync"); return GTR_E_ARG; }
+  if (D == 256) {
+    if (cfg->sync_bn) { set_error("gtr_qkvs_bwd: dim 256 on the split path has no SyncBN"); return GTR_E_ARG; }
+    if (l > 0 && layers[l - 1].ffn && !layers[l - 1].ffn->dz) { set_error("gtr_qkvs_bwd: layer %d's FFN has no dz rows", l - 1); return GTR_E_ARG; }
+    return gen_qkvs_bwd(cfg, bt, layers, l, dx0, (hipStream_t)stream);
+  }
   const gtr_layer& L = layers[l];
   const bool ffn_prev = l > 0 && layers[l - 1].ffn;  // dX is d/dz of the previous layer's FFN
   if (ffn_prev && !layers[l - 1].ffn->dz) { set_error("gtr_qkvs_bwd: layer %d's FFN has no dz rows", l - 1); return GTR_E_ARG; }
@@ -731,8 +758,14 @@ int ffn_check(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layer
     return GTR_E_ARG;
   }
   const gtr_ffn& f = *layers[l].ffn;
-  if (cfg->dim != 64 && cfg->dim != 128) { set_error("%s: dim %d (the FFN GEMMs cover 64 / 128)", fn, cfg->dim); return GTR_E_ARG; }
-  if (f.expansion != 4) { set_error("%s: ffn_expansion %d (4 supported)", fn, f.expansion); return GTR_E_ARG; }
+  if (cfg->dim != 64 && cfg->dim != 128 && cfg->dim != 256) {
+    set_error("%s: dim %d (the FFN GEMMs cover 64 / 128 / 256)", fn, cfg->dim);
+    return GTR_E_ARG;
+  }
+  if (f.expansion != 1 && f.expansion != 2 && f.expansion != 4) {
+    set_error("%s: ffn_expansion %d (1 / 2 / 4 supported)", fn, f.expansion);
+    return GTR_E_ARG;
+  }
   if (!f.w1 || !f.b1 || !f.w2 || !f.b2 || !f.y || !f.a || !f.z) { set_error("%s: missing FFN buffers", fn); return GTR_E_ARG; }
   if (need_train && !cfg->training) { set_error("%s: backward requires training mode", fn); return GTR_E_ARG; }
   if (cfg->training && (cfg->sync_bn || cfg->consumer_reduce)) {
@@ -746,6 +779,12 @@ int ffn_check(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layer
   return GTR_OK;
 }
 
+// The register-resident kernels above cover D = 64 / 128 with F = 4 D; every other FFN
+// shape runs on the LDS-staged GEMMs of gtr_gemm_gen.hip.
+bool ffn_generic(const gtr_config* cfg, const gtr_ffn& f) {
+  return !((cfg->dim == 64 || cfg->dim == 128) && f.expansion == 4);
+}
+
 }  // namespace
 
 extern "C" int gtr_ffn_fwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l,
@@ -754,6 +793,7 @@ extern "C" int gtr_ffn_fwd(const gtr_config* cfg, const gtr_batch* bt, const gtr
   float scale;
   int drop_on;
   if (const int rc = ffn_check(cfg, bt, layers, l, "gtr_ffn_fwd", false, thresh, scale, drop_on)) return rc;
+  if (ffn_generic(cfg, *layers[l].ffn)) return gen_ffn_fwd(cfg, bt, layers, l, (hipStream_t)stream);
   const int D = cfg->dim;
   const gtr_layer& L = layers[l];
   const gtr_ffn& f = *L.ffn;
@@ -801,6 +841,7 @@ extern "C" int gtr_ffn_bwd(const gtr_config* cfg, const gtr_batch* bt, const gtr
   const gtr_layer& L = layers[l];
   const gtr_ffn& f = *L.ffn;
   if (!f.dz || !f.g2 || !f.da) { set_error("gtr_ffn_bwd: missing FFN gradient buffers"); return GTR_E_ARG; }
+  if (ffn_generic(cfg, f)) return gen_ffn_bwd(cfg, bt, layers, l, (hipStream_t)stream);
   hipStream_t s = (hipStream_t)stream;
   // g2 = dz * mask3 -> ffn.g2; da = (g2 W2) * mask2 * GELU'(a) -> ffn.da
   ProjK k{};
@@ -842,10 +883,12 @@ extern "C" int gtr_ffn_wgrad(const gtr_config* cfg, const gtr_batch* bt, const g
   if (const int rc = ffn_check(cfg, bt, layers, l, "gtr_ffn_wgrad", true, thresh, scale, drop_on)) return rc;
   const int D = cfg->dim;
   const gtr_ffn& f = *layers[l].ffn;
-  if (!slab || n_chunks <= 0 || slab_stride < (int64_t)8 * D * D + 5 * D || !f.g2 || !f.da) {
+  const int64_t F = (int64_t)f.expansion * D;
+  if (!slab || n_chunks <= 0 || slab_stride < 2 * F * D + F + D || !f.g2 || !f.da) {
     set_error("gtr_ffn_wgrad: bad slab / chunks");
     return GTR_E_ARG;
   }
+  if (ffn_generic(cfg, f)) return gen_ffn_wgrad(cfg, bt, layers, l, slab, n_chunks, slab_stride, (hipStream_t)stream);
   FfnWK k{};
   k.bt = *bt;
   k.layer = l;

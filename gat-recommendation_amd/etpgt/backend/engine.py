@@ -45,8 +45,10 @@ class Seg:
 class ParamLayout:
     """Flat layout of the dense (non-table) parameters of a GraphTransformer."""
 
-    def __init__(self, D: int, L_: int, pe_k: int, ffn: bool = False):
+    def __init__(self, D: int, L_: int, pe_k: int, ffn: bool = False, ffn_expansion: int = 4):
         self.D, self.L, self.K, self.ffn = D, L_, pe_k, ffn
+        F = ffn_expansion * D
+        self.F = F if ffn else 0
         self.segs: dict[str, Seg] = {}
         off = 0
 
@@ -62,10 +64,10 @@ class ParamLayout:
             add(f"{l}.w_beta", (1, 3 * D))
             add(f"{l}.gamma", (D,))
             add(f"{l}.beta", (D,))
-            if ffn:  # ffns.{l}.0 / ffns.{l}.3 (graph_transformer.py:88-100), F = 4 D
-                add(f"{l}.ffn_w1", (4 * D, D))
-                add(f"{l}.ffn_b1", (4 * D,))
-                add(f"{l}.ffn_w2", (D, 4 * D))
+            if ffn:  # ffns.{l}.0 / ffns.{l}.3 (graph_transformer.py:88-100), F = ffn_expansion * D
+                add(f"{l}.ffn_w1", (F, D))
+                add(f"{l}.ffn_b1", (F,))
+                add(f"{l}.ffn_w2", (D, F))
                 add(f"{l}.ffn_b2", (D,))
         if pe_k > 0:
             add("pe.w", (D, pe_k))
@@ -75,7 +77,7 @@ class ParamLayout:
         self.pe_block = D * pe_k + D if pe_k > 0 else 0
         self.slab_stride = _al(max(self.layer_block, self.pe_block))
         # gtr_ffn_wgrad slab of one layer: [dW1 F*D | db1 F | dW2 D*F | db2 D]
-        self.ffn_block = 8 * D * D + 5 * D if ffn else 0
+        self.ffn_block = 2 * F * D + F + D if ffn else 0
         self.ffn_stride = _al(self.ffn_block) if ffn else 0
 
     def seg(self, name: str) -> Seg:
@@ -110,7 +112,7 @@ class FlatParams:
     def __init__(self, model, device):
         self.model = model
         self.layout = ParamLayout(model.hidden_dim, model.num_layers, model.laplacian_k if model.use_laplacian_pe else 0,
-                                  bool(getattr(model, "use_ffn", False)))
+                                  bool(getattr(model, "use_ffn", False)), int(getattr(model, "ffn_expansion", 4)))
         self.device = device
         self.flat = torch.zeros(self.layout.total, dtype=torch.float32, device=device)
         self.map = model_param_map(model)
@@ -240,7 +242,7 @@ class Workspace:
         readout reads z as it is and writes d/dz into ffn.dz."""
         dev = eng.device
         D, Lc = eng.D, eng.L
-        F = 4 * D
+        F = eng.flat.layout.F
         self.ffns = []
         self.ffn_structs = []
         for l in range(Lc):
@@ -250,7 +252,7 @@ class Workspace:
             fs = L.GtrFfn()
             for f in ("y", "a", "z", "dz", "g2", "da"):
                 setattr(fs, f, t[f].data_ptr())
-            fs.expansion = 4
+            fs.expansion = F // D
             self.ffn_structs.append(fs)
         self.ffn_slabs = _f32(Lc, self.P, eng.flat.layout.ffn_stride, device=dev)
         last = self.ffns[Lc - 1]
@@ -565,7 +567,7 @@ class Engine:
                 s = lay.seg(name)
                 segs.append((s.begin, s.numel, src, stride, np_, lv))
             if ws.ffns is not None:
-                fb, F = ws.ffn_slabs[l].data_ptr(), 4 * D
+                fb, F = ws.ffn_slabs[l].data_ptr(), lay.F
                 for name, off in ((f"{l}.ffn_w1", 0), (f"{l}.ffn_b1", F * D), (f"{l}.ffn_w2", F * D + F),
                                   (f"{l}.ffn_b2", 2 * F * D + F)):
                     s = lay.seg(name)

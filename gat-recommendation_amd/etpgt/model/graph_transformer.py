@@ -12,8 +12,9 @@ TransformerConv(beta=True)).  There is no CPU path: a
 model on the CPU raises.  Scope: the optimized variant
 (use_ffn=False) with the mean readout is the hot path.  use_ffn=True (the
 feed-forward block of graph_transformer.py:88-100,160-170) runs on the split layer
-kernels plus gtr_ffn_fwd / gtr_ffn_bwd / gtr_ffn_wgrad at hidden_dim 64 / 128 with
-ffn_expansion 4; other FFN shapes and the max/last/attention readouts raise
+kernels plus gtr_ffn_fwd / gtr_ffn_bwd / gtr_ffn_wgrad at hidden_dim 64 / 128 / 256 with
+ffn_expansion 1 / 2 / 4 (the reference's create_graph_transformer default d = 256, x 4 and
+the optimized factory's x 2 included); the max/last/attention readouts raise
 NotImplementedError.
 """
 
@@ -112,9 +113,9 @@ class GraphTransformer(BaseRecommendationModel):
     def _check_supported(self):
         if self.embedding_dim != self.hidden_dim:
             raise ValueError("embedding_dim must equal hidden_dim (residual at graph_transformer.py:176)")
-        if self.use_ffn and (self.hidden_dim not in (64, 128) or self.ffn_expansion != 4):
-            raise NotImplementedError("use_ffn=True runs on the split-layer FFN kernels: hidden_dim 64 / 128 with "
-                                      "ffn_expansion 4 (gtr_ffn_fwd / gtr_ffn_bwd)")
+        if self.use_ffn and (self.hidden_dim not in (64, 128, 256) or self.ffn_expansion not in (1, 2, 4)):
+            raise NotImplementedError(f"use_ffn=True runs on the split-layer FFN kernels: hidden_dim 64 / 128 / 256 "
+                                      f"with ffn_expansion 1 / 2 / 4 (got {self.hidden_dim}, {self.ffn_expansion})")
         if self.readout_type != "mean":
             raise NotImplementedError(f"readout '{self.readout_type}' is outside the HIP hot path (mean only)")
 

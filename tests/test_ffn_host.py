@@ -73,12 +73,17 @@ def test_ffn_models_refuse_multi_gpu_fused_steps_and_unsupported_shapes():
         FusedTrainStep(m, data_parallel=True)
     with pytest.raises(NotImplementedError, match="use_ffn"):
         FusedTrainStep(m, shard_table=True)
-    bad = create_graph_transformer(50, embedding_dim=256, hidden_dim=256, num_layers=2, num_heads=4, use_ffn=True)
-    with pytest.raises(NotImplementedError, match="hidden_dim 64 / 128"):
+    # the reference's create_graph_transformer defaults (d = 256, FFN x 4) and the optimized
+    # factory's FFN x 2 are supported (gtr_gemm_gen.hip); other widths / expansions refuse
+    create_graph_transformer(50)._check_supported()
+    create_graph_transformer(50, embedding_dim=64, hidden_dim=64, num_layers=2, num_heads=2, use_ffn=True,
+                             ffn_expansion=2)._check_supported()
+    bad = create_graph_transformer(50, embedding_dim=96, hidden_dim=96, num_layers=2, num_heads=4, use_ffn=True)
+    with pytest.raises(NotImplementedError, match="hidden_dim 64 / 128 / 256"):
         bad._check_supported()
     odd = create_graph_transformer(50, embedding_dim=64, hidden_dim=64, num_layers=2, num_heads=2, use_ffn=True,
-                                   ffn_expansion=2)
-    with pytest.raises(NotImplementedError, match="ffn_expansion 4"):
+                                   ffn_expansion=3)
+    with pytest.raises(NotImplementedError, match="ffn_expansion 1 / 2 / 4"):
         odd._check_supported()
     ok = create_graph_transformer(50, embedding_dim=128, hidden_dim=128, num_layers=2, num_heads=4, use_ffn=True)
     ok._check_supported()

@@ -169,3 +169,24 @@ def test_train_baseline_ffn_model_trains_one_epoch(tmp_path):
     ck = torch.load(tmp_path / "out" / "graph_transformer" / "checkpoint_latest.pt", map_location="cpu",
                     weights_only=True)
     assert "ffns.1.3.weight" in ck["model_state_dict"]
+
+
+def test_train_baseline_graph_transformer_reference_default_flags(tmp_path):
+    """``train_baseline.py --model graph_transformer`` with NO model flags: the reference
+    defaults build create_graph_transformer with d = 256, 3 layers, 4 heads, FFN x 4 and
+    LapPE (train_baseline.py:39-42,198-208; graph_transformer.py:185-197).  One epoch
+    through the Trainer's fused step on the LDS-staged d = 256 GEMMs."""
+    d = write_csvs(tmp_path)
+    args = ["--model", "graph_transformer", "--train-sessions", str(d / "train.csv"),
+            "--val-sessions", str(d / "val.csv"), "--graph-edges", str(d / "graph_edges.csv"), "--max-epochs", "1",
+            "--num-workers", "0", "--output-dir", str(tmp_path / "out")]
+    trainer = _script().main(args)
+    m = trainer.model
+    assert trainer._fused is not None and m.use_ffn and m.ffn_expansion == 4
+    assert m.item_embedding.weight.shape[1] == 256 and m.num_layers == 3 and m.num_heads == 4
+    with open(tmp_path / "out" / "graph_transformer" / "history.json") as f:
+        hist = json.load(f)
+    assert len(hist["train_loss"]) == 1 and np.isfinite(hist["train_loss"][0])
+    ck = torch.load(tmp_path / "out" / "graph_transformer" / "checkpoint_latest.pt", map_location="cpu",
+                    weights_only=True)
+    assert ck["model_state_dict"]["ffns.2.0.weight"].shape == (1024, 256)

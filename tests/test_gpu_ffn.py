@@ -38,11 +38,12 @@ def data():
     return _DATA
 
 
-def make_ffn_pair(T, D, H, L=2, K=0, dropout=0.0, seed=0):
+def make_ffn_pair(T, D, H, L=2, K=0, dropout=0.0, seed=0, expansion=4):
     """HIP FFN model (cuda) + oracle FFN model (cpu) with identical parameters."""
     torch.manual_seed(seed)
     m = create_graph_transformer(T, embedding_dim=D, hidden_dim=D, num_layers=L, num_heads=H, dropout=dropout,
-                                 use_laplacian_pe=K > 0, laplacian_k=max(K, 1), use_ffn=True, ffn_expansion=4)
+                                 use_laplacian_pe=K > 0, laplacian_k=max(K, 1), use_ffn=True,
+                                 ffn_expansion=expansion)
     if K > 0:
         m.laplacian_pe._cached_pe = torch.rand(T, K)
     with torch.no_grad():
@@ -50,7 +51,7 @@ def make_ffn_pair(T, D, H, L=2, K=0, dropout=0.0, seed=0):
             bn.weight.uniform_(0.5, 1.5)
             bn.bias.uniform_(-0.2, 0.2)
     ref = R.RefGraphTransformer(T, embedding_dim=D, hidden_dim=D, num_layers=L, num_heads=H, dropout=dropout,
-                                use_laplacian_pe=K > 0, laplacian_k=max(K, 1), use_ffn=True, ffn_expansion=4)
+                                use_laplacian_pe=K > 0, laplacian_k=max(K, 1), use_ffn=True, ffn_expansion=expansion)
     if K > 0:
         ref.laplacian_pe._cached_pe = torch.zeros(T, K)
     sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
@@ -96,6 +97,59 @@ def test_ffn_train_grads(D, H, K, B):
     m.train(); ref.train()
     sb = batches(data(), B, 5, 1, seed=11 + D)[0]
     _grads_vs_oracle(m, ref, sb, 5)
+
+
+@pytest.mark.parametrize("D,H,K,B,E,L", [(256, 4, 16, 32, 4, 3), (256, 4, 16, 300, 4, 2), (128, 4, 16, 200, 2, 2),
+                                         (64, 2, 0, 64, 2, 3), (256, 4, 0, 48, 2, 2)])
+def test_ffn_reference_default_shapes_train_grads(D, H, K, B, E, L):
+    """The FFN shapes the register-resident GEMMs do not cover, on the LDS-staged GEMMs
+    (gtr_gemm_gen.hip): create_graph_transformer's own defaults -- d = 256, 4 heads, FFN x 4,
+    LapPE k = 16, 3 layers (graph_transformer.py:185-197) -- and ffn_expansion = 2 (the
+    optimized factory's default when its FFN is on, :231-280).  Train mode, dropout 0: the
+    loss, the session embeddings, every gradient and the running statistics."""
+    T = data().table_rows
+    m, ref = make_ffn_pair(T, D, H, L=L, K=K, seed=3 + D + E, expansion=E)
+    m.train(); ref.train()
+    sb = batches(data(), B, 5, 1, seed=13 + D)[0]
+    _grads_vs_oracle(m, ref, sb, 5)
+
+
+def test_ffn_reference_defaults_fused_steps_match_oracle():
+    """create_graph_transformer(num_items) at its defaults (d = 256, L = 3, H = 4, FFN x 4,
+    LapPE k = 16) through the fused step: five steps against the oracle trainer, every
+    trained parameter elementwise (gpu_helpers.close_trained)."""
+    from etpgt.train.fused import FusedTrainStep
+
+    T = data().table_rows
+    m, ref = make_ffn_pair(T, 256, 4, L=3, K=16, seed=23)
+    m.train(); ref.train()
+    step = FusedTrainStep(m, lr=1e-3, weight_decay=1e-5, loss="bpr")
+    trio = OracleTrio(ref, lambda ps: torch.optim.AdamW(ps, lr=1e-3, weight_decay=1e-5))
+    for i, sb in enumerate(batches(data(), 32, 5, 5, seed=41)):
+        hl = float(step(sb.to("cuda")))
+        rb_ = ref_batch(sb)
+        rl = trio.step(lambda mod, o: R.ref_train_step(mod, rb_, o, "bpr"))
+        assert abs(hl - float(rl)) <= 1e-3 * max(1.0, abs(float(rl))), (i, hl, float(rl))
+    trio.compare(dict(m.named_parameters()), lr=1e-3)
+
+
+def test_ffn_eval_forward_d256():
+    """Eval forward of the reference-default FFN model (the registered op
+    etpgt::graph_transformer_eval)."""
+    T = data().table_rows
+    m, ref = make_ffn_pair(T, 256, 4, L=3, K=16, dropout=0.1, seed=9)
+    with torch.no_grad():
+        for bn, rb_ in zip(m.batch_norms, ref.batch_norms):
+            bn.running_mean.uniform_(-0.1, 0.1)
+            bn.running_var.uniform_(0.5, 2.0)
+            rb_.running_mean.copy_(bn.running_mean.cpu())
+            rb_.running_var.copy_(bn.running_var.cpu())
+    m.eval(); ref.eval()
+    sb = batches(data(), 40, 5, 1, seed=27)[0]
+    with torch.no_grad():
+        se = m(sb.to("cuda"))
+        se_ref = ref(ref_batch(sb))
+    assert_close(se, se_ref, name="se eval d256")
 
 
 def test_ffn_three_layers_edge_cases():
