@@ -361,12 +361,18 @@ struct AdamStep {
   //   v*b2 + ((1-b2)*0)*0 == v*b2 + (+0) == v*b2, since v >= +0 (exp_avg_sq starts at +0 and
   //     only grows by squares), so v*b2 is never -0.
   // Plain Adam (L2 into the gradient) has g = wd*p != 0: the general update.
+  // the moments' part of apply_zero alone (decoupled AdamW: m and v do not depend on p):
+  // the lazy table's tail re-derives a lagging row's m / v with it (gtr_rows.cuh)
+  __device__ __forceinline__ void apply_zero_mv(float& m, float& v) const {
+#pragma clang fp contract(off)
+    m = m - (1.0f - b1) * m;
+    v = v * b2;
+  }
   __device__ __forceinline__ void apply_zero(float& p, float& m, float& v) const {
 #pragma clang fp contract(off)
     if (!decoupled) { apply(p, m, v, 0.0f); return; }
     p = p * decay_mul;
-    m = m - (1.0f - b1) * m;
-    v = v * b2;
+    apply_zero_mv(m, v);
     const float denom = __builtin_amdgcn_sqrtf(v) * inv_bc2 + eps;
     p = p + (-step_size) * (m * __builtin_amdgcn_rcpf(denom));
   }

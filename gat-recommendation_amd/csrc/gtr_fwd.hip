@@ -798,10 +798,15 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_attn_fwd(ConvFwdK a) {
 #define AR_ROWS (AR_WAVES * AR_RPW)  // rows per workgroup = one BatchNorm partial
 #define AR_ECH 64                  // in-edges of a row handled with LDS logits
 #define AR_HMAX 8
+#ifndef AR_VR
 #define AR_VR 8                    // V rows of a row pair held in registers
+#endif
+#ifndef GTR_AR_WAVES_EU
+#define GTR_AR_WAVES_EU 6
+#endif
 
 template <int D>
-__global__ __launch_bounds__(AR_BLOCK) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_attn_rows(ConvFwdK a) {
+__global__ __launch_bounds__(AR_BLOCK) __attribute__((amdgpu_waves_per_eu(GTR_AR_WAVES_EU, 8))) void k_attn_rows(ConvFwdK a) {
   constexpr int VPL = D >= 64 ? D / 64 : 1;
   __shared__ __attribute__((aligned(16))) float s_out[AR_ROWS][D];
   __shared__ float s_lg[AR_WAVES][AR_ECH][AR_HMAX];
@@ -1455,8 +1460,8 @@ __global__ __launch_bounds__(RO_BLOCK) void k_readout(ReadoutK a) {
 }
 
 // Large-batch readout (b_cap >= ro_wave_min_b(), D <= 128): wave per session, grid-strided;
-// 16 lanes per row so one wave instruction moves 4 rows (node rows and scoring rows);
-// the scoring rows are streamed in rounds of 4*KQ and the listwise softmax is
+// RwGeom::RL lanes per row so one wave instruction moves NRG rows (node and scoring rows);
+// the scoring rows are streamed in rounds of NRG*KQ and the listwise softmax is
 // accumulated online (running max / sum / sum of exp-weighted rows per row group), so
 // every table row is read once.  Semantics and outputs identical to k_readout.
 #define RW_BLOCK 512
@@ -1488,42 +1493,64 @@ __device__ __forceinline__ void st_row(float* p, const float (&x)[EPL]) {
   }
 }
 
-// sum over the 4 row groups (lanes l, l^16, l^32, l^48)
+// Row-group geometry of the wave readout: NRG row groups of RL = 64 / NRG lanes per wave;
+// a lane holds EPL = D / RL features of a row, one load instruction moves NRG rows.
+// D = 128 runs 2 groups of 32 lanes (EPL 4): half the row registers of 4 x 16 lanes
+// (221 -> ~120 VGPRs, so 4 waves per SIMD instead of 2 hide the gather latency).
+#ifndef GTR_RW_NRG128
+#define GTR_RW_NRG128 2
+#endif
+template <int D>
+struct RwGeom {
+  static constexpr int NRG = D >= 128 ? GTR_RW_NRG128 : 4;
+  static constexpr int RL = 64 / NRG;
+  static constexpr int EPL = D / RL;
+};
+
+// sum over the NRG row groups (lanes l, l^RL, ...)
+template <int NRG>
 __device__ __forceinline__ float sum_groups(float x) {
-  x = bfly_add<16>(x);
+  if constexpr (NRG == 4) x = bfly_add<16>(x);
   x = bfly_add<32>(x);
   return x;
 }
 
+template <int NRG>
+__device__ __forceinline__ float max_groups(float x) {
+  if constexpr (NRG == 4) x = bfly_max<16>(x);
+  return bfly_max<32>(x);
+}
+
 // Round r of a session's scoring rows: slot q of row group rg loads negative
-// k = r*4*KQ + q*4 + rg (ids fetched by the first 4*KQ lanes, then shuffled).
+// k = r*NRG*KQ + q*NRG + rg (ids fetched by the first NRG*KQ lanes, then shuffled).
 template <int D, int KQ>
-__device__ __forceinline__ void issue_round(float (&rv)[KQ][D / 16], const float* table, const int* negs, int n,
-                                            int r, int lane, int rg, int c0) {
-  constexpr int RND = 4 * KQ;
+__device__ __forceinline__ void issue_round(float (&rv)[KQ][RwGeom<D>::EPL], const float* table, const int* negs,
+                                            int n, int r, int lane, int rg, int c0) {
+  constexpr int NRG = RwGeom<D>::NRG, RND = NRG * KQ;
   const int kl = r * RND + lane;
   const int nid = (lane < RND && kl < n) ? negs[kl] : 0;
 #pragma unroll
   for (int q = 0; q < KQ; ++q) {
-    const int id = __shfl(nid, q * 4 + rg);
-    ld_row<D / 16>(rv[q], table + (size_t)id * D + c0, r * RND + q * 4 + rg < n);
+    const int id = __shfl(nid, q * NRG + rg);
+    ld_row<RwGeom<D>::EPL>(rv[q], table + (size_t)id * D + c0, r * RND + q * NRG + rg < n);
   }
 }
 
 // The same round from the session's negative ids preloaded into registers (nid[i] holds id
-// i * 64 + lane; n <= 256): a round is 16 consecutive ids, all in one register, so the
-// round's row loads need no id load of their own (round 4: every round used to wait for its
-// ids before its rows -- one memory latency per 16 rows on the wave's serial path).
+// i * 64 + lane; n <= 256): a round is RND consecutive ids, all in one register (RND divides
+// 64), so the round's row loads need no id load of their own (round 4: every round used to
+// wait for its ids before its rows -- one memory latency per round on the wave's serial path).
 template <int D, int KQ>
-__device__ __forceinline__ void issue_round_pre(float (&rv)[KQ][D / 16], const float* table, const int (&nid)[4],
-                                                int n, int r, int rg, int c0) {
-  static_assert(4 * KQ == 16, "16 ids per round: a round never straddles two id registers");
-  const int blk = r >> 2;  // wave-uniform
+__device__ __forceinline__ void issue_round_pre(float (&rv)[KQ][RwGeom<D>::EPL], const float* table,
+                                                const int (&nid)[4], int n, int r, int rg, int c0) {
+  constexpr int NRG = RwGeom<D>::NRG, RND = NRG * KQ;
+  static_assert(64 % RND == 0, "a round never straddles two id registers");
+  const int blk = (r * RND) >> 6;  // wave-uniform
   const int src = blk == 0 ? nid[0] : blk == 1 ? nid[1] : blk == 2 ? nid[2] : nid[3];
 #pragma unroll
   for (int q = 0; q < KQ; ++q) {
-    const int id = __shfl(src, (r & 3) * 16 + q * 4 + rg);
-    ld_row<D / 16>(rv[q], table + (size_t)id * D + c0, r * 16 + q * 4 + rg < n);
+    const int id = __shfl(src, ((r * RND) & 63) + q * NRG + rg);
+    ld_row<RwGeom<D>::EPL>(rv[q], table + (size_t)id * D + c0, r * RND + q * NRG + rg < n);
   }
 }
 
@@ -1538,18 +1565,18 @@ struct ScoreAcc {
 // Scores of one round's rows (slot q of row group rg = negative k) -> BPR terms and the
 // online listwise softmax; raw listwise scores go to sc (LDS, or coef_neg when sc null).
 template <int D, int KQ>
-__device__ __forceinline__ void consume_round(ScoreAcc<D / 16>& A, const float (&rv)[KQ][D / 16],
-                                              const float (&se)[D / 16], float pos, int r, int n, int rg, bool lead,
-                                              bool use_bpr, bool use_lw, float inv_bn, float w_bpr, float inv_t,
-                                              float* sc, float* coef_row) {
-  constexpr int EPL = D / 16, RND = 4 * KQ;
+__device__ __forceinline__ void consume_round(ScoreAcc<RwGeom<D>::EPL>& A, const float (&rv)[KQ][RwGeom<D>::EPL],
+                                              const float (&se)[RwGeom<D>::EPL], float pos, int r, int n, int rg,
+                                              bool lead, bool use_bpr, bool use_lw, float inv_bn, float w_bpr,
+                                              float inv_t, float* sc, float* coef_row) {
+  constexpr int EPL = RwGeom<D>::EPL, NRG = RwGeom<D>::NRG, RND = NRG * KQ;
 #pragma unroll
   for (int q = 0; q < KQ; ++q) {
-    const int k = r * RND + q * 4 + rg;
+    const int k = r * RND + q * NRG + rg;
     float d = 0.0f;
 #pragma unroll
     for (int e = 0; e < EPL; ++e) d += se[e] * rv[q][e];
-    d = group_sum(d, 16);
+    d = group_sum(d, RwGeom<D>::RL);
     if (k < n) {
       if (use_bpr) {
         const float sg = 1.0f / (1.0f + expf(-(pos - d)));
@@ -1577,10 +1604,15 @@ __device__ __forceinline__ void consume_round(ScoreAcc<D / 16>& A, const float (
 }
 
 template <int D>
-__global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
-  constexpr int EPL = D / 16;              // features per lane (16 lanes per row)
+#ifndef GTR_RW_WAVES_EU
+#define GTR_RW_WAVES_EU 1
+#endif
+__global__ __launch_bounds__(RW_BLOCK) __attribute__((amdgpu_waves_per_eu(GTR_RW_WAVES_EU))) void k_readout_wave(ReadoutK a) {
+  using RG = RwGeom<D>;
+  constexpr int EPL = RG::EPL;             // features per lane (RL lanes per row)
+  constexpr int NRG = RG::NRG;             // row groups per wave
   constexpr int KQ = 4;                    // row slots per lane per round
-  constexpr int RND = 4 * KQ;              // scoring rows per wave round
+  constexpr int RND = NRG * KQ;            // scoring rows per wave round
   __shared__ float s_bn[3 * D];            // mean | rstd | unbiased var (prologue)
   __shared__ float s_gb[2 * D];            // gamma | beta
   __shared__ float s_scr[2 * RW_BLOCK + D];
@@ -1594,8 +1626,8 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int rg = lane >> 4, c0 = (lane & 15) * EPL;
-  const bool lead = (lane & 15) == 0;
+  const int rg = lane / RG::RL, c0 = (lane & (RG::RL - 1)) * EPL;
+  const bool lead = (lane & (RG::RL - 1)) == 0;
   const int B = a.bt.hdr[1];
   const int n = a.bt.n_neg;
   const uint32_t ctr = a.rng_ctr ? load_step_ctr(a.rng_ctr) + a.ctr_add : 0u;
@@ -1654,7 +1686,7 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
 #pragma unroll
       for (int e = 0; e < EPL; ++e) acc[e] = 0.0f;
 #pragma unroll 1
-      for (int i = n0 + rg; i < n1; i += 4) {
+      for (int i = n0 + rg; i < n1; i += NRG) {
         float ov[EPL], xv[EPL];
         ld_row<EPL>(ov, a.out + (size_t)i * D + c0, true);
         ld_row<EPL>(xv, a.xin + (size_t)i * D + c0, true);
@@ -1667,7 +1699,7 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
         }
       }
 #pragma unroll
-      for (int e = 0; e < EPL; ++e) se[e] = sum_groups(acc[e]) / cnt;
+      for (int e = 0; e < EPL; ++e) se[e] = sum_groups<NRG>(acc[e]) / cnt;
       if (rg == 0) st_row<EPL>(a.se + (size_t)b * D + c0, se);
       if (b == rb) GTR_PH(26, 6);
     } else {
@@ -1681,7 +1713,7 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
       float pos = 0.0f;
 #pragma unroll
       for (int e = 0; e < EPL; ++e) pos += se[e] * tv[e];
-      pos = group_sum(pos, 16);
+      pos = group_sum(pos, RG::RL);
       ScoreAcc<EPL> A;
 #pragma unroll
       for (int e = 0; e < EPL; ++e) { A.dse[e] = 0.0f; A.accl[e] = 0.0f; }
@@ -1711,19 +1743,19 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
       }
       if (b == rb) GTR_PH(26, 7);
       bpr_sum += A.bpr_sum;
-      float dpos = sum_groups(A.dpos);
+      float dpos = sum_groups<NRG>(A.dpos);
 #pragma unroll
-      for (int e = 0; e < EPL; ++e) dse[e] = sum_groups(A.dse[e]);
+      for (int e = 0; e < EPL; ++e) dse[e] = sum_groups<NRG>(A.dse[e]);
       if (use_lw) {
-        const float M = bfly_max<32>(bfly_max<16>(A.mg));
+        const float M = max_groups<NRG>(A.mg);
         const float f = A.zg > 0.0f ? expf(A.mg - M) : 0.0f;
-        const float Z = sum_groups(A.zg * f);
+        const float Z = sum_groups<NRG>(A.zg * f);
         const float lse = M + logf(Z);
         if (lane == 0) lw_sum += lse - pos * inv_t;
         dpos += (expf(pos * inv_t - lse) - 1.0f) * inv_b * inv_t * w_lw;
         const float cf = inv_b * inv_t * w_lw / Z;
 #pragma unroll
-        for (int e = 0; e < EPL; ++e) dse[e] += sum_groups(A.accl[e] * f) * cf;
+        for (int e = 0; e < EPL; ++e) dse[e] += sum_groups<NRG>(A.accl[e] * f) * cf;
         if (sc) {
           __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
           __builtin_amdgcn_wave_barrier();
@@ -1742,7 +1774,7 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
         } else if (lead) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this lane's raw-score stores
 #pragma unroll 1
-          for (int k = rg; k < n; k += 4) {
+          for (int k = rg; k < n; k += NRG) {
             const float d = coef_row[k];
             float cb = expf(d * inv_t - lse) * inv_b * inv_t * w_lw;
             if (use_bpr) {
@@ -1769,7 +1801,7 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
 #pragma unroll
       for (int e = 0; e < EPL; ++e) { gs[e] = 0.0f; gx[e] = 0.0f; }
 #pragma unroll 1
-      for (int i = n0 + rg; i < n1; i += 4) {
+      for (int i = n0 + rg; i < n1; i += NRG) {
         float ov[EPL], dyv[EPL];
         ld_row<EPL>(ov, a.out + (size_t)i * D + c0, true);
 #pragma unroll
@@ -1785,7 +1817,7 @@ __global__ __launch_bounds__(RW_BLOCK) void k_readout_wave(ReadoutK a) {
       // fold into the wave's running sums (sessions in order, row groups by xor tree)
 #pragma unroll
       for (int e = 0; e < EPL; ++e) {
-        const float g1 = sum_groups(gs[e]), g2 = sum_groups(gx[e]);
+        const float g1 = sum_groups<NRG>(gs[e]), g2 = sum_groups<NRG>(gx[e]);
         if (rg == 0) { s_red[wave][c0 + e] += g1; s_red[wave][D + c0 + e] += g2; }
       }
       if (b == rb) GTR_PH(26, 9);

@@ -90,10 +90,12 @@ __device__ __forceinline__ void rows_body(int gid, const gtr_batch& bt, int T, c
   if (key <= 0 || key >= T || prev == key) return;
   const size_t base = (size_t)key * C4 + c;
   float4 pv = make_float4(0.f, 0.f, 0.f, 0.f), mv = pv, vv = pv;
+  int32_t sw = 0;
   if (!grad_dense) {
     pv = reinterpret_cast<const float4*>(table)[base];
     mv = reinterpret_cast<const float4*>(m)[base];
     vv = reinterpret_cast<const float4*>(v)[base];
+    if (lazy_stamp) sw = lazy_stamp[key];
   }
   float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
   int k = i;
@@ -122,6 +124,7 @@ __device__ __forceinline__ void rows_body(int gid, const gtr_batch& bt, int T, c
     return;
   }
   wait();
+  if (lazy_stamp) lazy_mv_forward(mv, vv, sw, lazy_t, st);
   st.apply(pv.x, mv.x, vv.x, g.x);
   st.apply(pv.y, mv.y, vv.y, g.y);
   st.apply(pv.z, mv.z, vv.z, g.z);
@@ -226,17 +229,24 @@ __device__ __forceinline__ void lazy_catch_up_lanes(float4* P, float4* M, float4
       }
     }
   }
+  const bool p_only = lazy_p_only(o.decoupled);  // the tail re-derives m / v (gtr_rows.cuh)
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
     const int c = gl + 16 * k;
-    if (c < C4) { P[c] = p[k]; M[c] = m[k]; V[c] = v[k]; }
+    if (c < C4) {
+      P[c] = p[k];
+      if (!p_only) { M[c] = m[k]; V[c] = v[k]; }
+    }
   }
 }
 
 __device__ __forceinline__ void lazy_claim_row(int key, int T, int D, int32_t t, int gl, int gbase,
                                                int32_t* stamp, const gtr_lazy& lz) {
   int old = 0;
-  if (gl == 0 && key > 0 && key < T) old = atomicExch(stamp + key, t - 1);
+  if (gl == 0 && key > 0 && key < T) {
+    old = atomicOr(stamp + key, GTR_LAZY_CLAIM);  // a later claimer of the row sees the bit
+    if (old & GTR_LAZY_CLAIM) old = t - 1;
+  }
   old = __shfl(old, gbase);
   if (!(key > 0 && key < T) || old >= t - 1) return;
   const int C4 = D / 4;
@@ -393,8 +403,12 @@ __device__ __forceinline__ void row_catch_up_store(RowRegs<EPL>& r, const gtr_la
   const int c = lane * EPL;
   if (c < D) {
     const size_t o = (size_t)key * D + c;
+    const bool p_only = lazy_p_only(st.decoupled);  // the tail re-derives m / v (gtr_rows.cuh)
 #pragma unroll
-    for (int k = 0; k < EPL; ++k) { lz.table[o + k] = r.p[k]; lz.m[o + k] = r.m[k]; lz.v[o + k] = r.v[k]; }
+    for (int k = 0; k < EPL; ++k) {
+      lz.table[o + k] = r.p[k];
+      if (!p_only) { lz.m[o + k] = r.m[k]; lz.v[o + k] = r.v[k]; }
+    }
   }
 }
 
@@ -423,7 +437,10 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_lazy_catchup(gtr_batch bt, int T,
     const int slot = base + lane;
     const int key = (lane < spw && slot < m_cap) ? contrib_key(bt, T, slot, N, B) : T;
     int old = t - 1;
-    if (key > 0 && key < T) old = atomicExch(stamp + key, t - 1);
+    if (key > 0 && key < T) {
+      old = atomicOr(stamp + key, GTR_LAZY_CLAIM);  // claimed: the low bits keep the row's step
+      if (old & GTR_LAZY_CLAIM) old = t - 1;         // another slot of the row claimed it first
+    }
     uint64_t todo = __ballot(old < t - 1);
     if (!todo) continue;
     int i = __builtin_ctzll(todo);
@@ -526,8 +543,10 @@ __device__ __forceinline__ void window_rows(int w, const gtr_batch& bt, int T, c
     float4 pv = sw_ld(reinterpret_cast<const float4*>(tl.table) + base);
     float4 mv = sw_ld(reinterpret_cast<const float4*>(tl.table_m) + base);
     float4 vv = sw_ld(reinterpret_cast<const float4*>(tl.table_v) + base);
+    const int32_t sw = lazy_stamp ? lazy_stamp[key] : 0;
     const float4 g = window_segment_sum<D>(bt, tl.skeys, tl.svals, tl.dx0, tl.se, tl.coef_tgt, tl.coef_neg, tl.carry,
                                            w, s0, e, w1, m_cap, key, gl, gb);
+    if (lazy_stamp) lazy_mv_forward(mv, vv, sw, lazy_t, st);
     st.apply(pv.x, mv.x, vv.x, g.x);
     st.apply(pv.y, mv.y, vv.y, g.y);
     st.apply(pv.z, mv.z, vv.z, g.z);
@@ -1020,9 +1039,10 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_dp_tail(DpTailK a) {
     float4 pv = reinterpret_cast<const float4*>(a.tl.table)[base];
     float4 mv = reinterpret_cast<const float4*>(a.tl.table_m)[base];
     float4 vv = reinterpret_cast<const float4*>(a.tl.table_v)[base];
-    if (a.tl.lazy_consts) {  // rows only other ranks touched are still behind
-      const int old = a.tl.stamp[k];
-      catch_up4(pv, mv, vv, old, t - 1, a.opt, a.tl.lazy_consts);
+    if (a.tl.lazy_consts) {
+      const int sw = a.tl.stamp[k];
+      if (sw & GTR_LAZY_CLAIM) lazy_mv_forward(mv, vv, sw, t, st);  // this rank's begin brought p forward
+      else catch_up4(pv, mv, vv, sw, t - 1, a.opt, a.tl.lazy_consts);  // rows only other ranks touched
     }
     st.apply(pv.x, mv.x, vv.x, g.x);
     st.apply(pv.y, mv.y, vv.y, g.y);
@@ -1088,18 +1108,48 @@ int rs_rounds(int n) {
   return r < 1 ? 1 : (r > RS_MAX_ROUNDS ? RS_MAX_ROUNDS : r);
 }
 
+// Contribution-list build folded into the first histogram pass (gtr_step_begin): each slot's
+// key is derived from the batch (contrib_key, as k_contrib_prep) and written with its slot
+// id and the touched-row stamp -- one launch less per large-batch step.
+struct RsPrep {
+  gtr_batch bt;
+  int T;
+  int32_t* keys;
+  int32_t* vals;
+  int32_t* stamp;
+  const int64_t* step_dev;
+};
+
+template <bool PREP>
 __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const int32_t* keys, int n, int shift, int32_t* hist,
-                                                       int32_t* tot, int rounds) {
+                                                       int32_t* tot, int rounds, RsPrep pp) {
   __shared__ int h[RS_RADIX];
   for (int d = threadIdx.x; d < RS_RADIX; d += RS_THREADS) h[d] = 0;
   __syncthreads();
   const int base = blockIdx.x * RS_THREADS * rounds;
   // every round's key requested before the first count (the loads are independent)
   int kk[RS_MAX_ROUNDS];
+  if (PREP) {
+    const int N = pp.bt.hdr[0], B = pp.bt.hdr[1];
+    const int32_t tnew = pp.stamp ? (int32_t)(*pp.step_dev + 1) : 0;
 #pragma unroll
-  for (int r = 0; r < RS_MAX_ROUNDS; ++r) {
-    const int i = base + r * RS_THREADS + threadIdx.x;
-    kk[r] = (r < rounds && i < n) ? keys[i] : -1;
+    for (int r = 0; r < RS_MAX_ROUNDS; ++r) {
+      const int i = base + r * RS_THREADS + threadIdx.x;
+      kk[r] = -1;
+      if (r < rounds && i < n) {
+        const int key = contrib_key(pp.bt, pp.T, i, N, B);
+        pp.keys[i] = key;
+        pp.vals[i] = i;
+        if (pp.stamp && key > 0 && key < pp.T) pp.stamp[key] = tnew;
+        kk[r] = key;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < RS_MAX_ROUNDS; ++r) {
+      const int i = base + r * RS_THREADS + threadIdx.x;
+      kk[r] = (r < rounds && i < n) ? keys[i] : -1;
+    }
   }
 #pragma unroll
   for (int r = 0; r < RS_MAX_ROUNDS; ++r)
@@ -1158,12 +1208,20 @@ __global__ __launch_bounds__(1024) void k_rs_offs(const int32_t* __restrict__ hi
 
 // tot: the pass's digit totals, read by k_rs_offs; zeroed here for the next call's same
 // pass (the workspace starts zeroed), so no memset node sits in the captured step.
+// step_dev / rng_ctr (the last pass of gtr_step_begin's sort, else null): workgroup 0
+// advances the step and dropout counters -- nothing of this launch reads them, and the
+// kernels after it see the new values (one launch less than a separate k_counters).
 __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const int32_t* kin, const int32_t* vin, int32_t* kout,
                                                           int32_t* vout, int n, int shift, const int32_t* offs,
-                                                          int ntile, int32_t* tot, int rounds) {
+                                                          int ntile, int32_t* tot, int rounds, int64_t* step_dev,
+                                                          uint32_t* rng_ctr) {
   __shared__ int run[RS_RADIX];
   __shared__ int wcnt[RS_THREADS / 64][RS_RADIX];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (blockIdx.x == 0 && tid == 0) {
+    if (step_dev) *step_dev += 1;
+    if (rng_ctr) *rng_ctr += 1;
+  }
   if (blockIdx.x == 0)
     for (int d = tid; d < RS_RADIX; d += RS_THREADS) tot[d] = 0;
   for (int d = tid; d < RS_RADIX; d += RS_THREADS) {
@@ -1228,7 +1286,8 @@ size_t rs_bytes(int n) {
 }
 
 hipError_t rs_sort(void* tmp, const int32_t* keys, int32_t* skeys, const int32_t* vals, int32_t* svals, int n,
-                   int bits, hipStream_t s) {
+                   int bits, hipStream_t s, int64_t* step_dev = nullptr, uint32_t* rng_ctr = nullptr,
+                   const RsPrep* prep = nullptr) {
   const int rounds = rs_rounds(n), tile = RS_THREADS * rounds;
   const int ntile = (n + tile - 1) / tile;
   int32_t* k1 = static_cast<int32_t*>(tmp);
@@ -1247,10 +1306,14 @@ hipError_t rs_sort(void* tmp, const int32_t* keys, int32_t* skeys, const int32_t
     int32_t* ko = last ? skeys : (p % 2 == 0 ? k1 : k2);
     int32_t* vo = last ? svals : (p % 2 == 0 ? v1 : v2);
     int32_t* tp = tot + p * RS_RADIX;
-    hipLaunchKernelGGL(k_rs_hist, dim3(ntile), dim3(RS_THREADS), 0, s, ki, n, p * RS_BITS, hist, tp, rounds);
+    if (p == 0 && prep)  // the first pass builds the contribution list as it counts
+      hipLaunchKernelGGL(k_rs_hist<true>, dim3(ntile), dim3(RS_THREADS), 0, s, ki, n, 0, hist, tp, rounds, *prep);
+    else
+      hipLaunchKernelGGL(k_rs_hist<false>, dim3(ntile), dim3(RS_THREADS), 0, s, ki, n, p * RS_BITS, hist, tp, rounds,
+                         RsPrep{});
     hipLaunchKernelGGL(k_rs_offs, dim3(RS_RADIX / 64), dim3(1024), 0, s, hist, tp, offs, ntile);
     hipLaunchKernelGGL(k_rs_scatter, dim3(ntile), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, n, p * RS_BITS, offs,
-                       ntile, tp, rounds);
+                       ntile, tp, rounds, last ? step_dev : nullptr, last ? rng_ctr : nullptr);
     ki = ko;
     vi = vo;
   }
@@ -1457,6 +1520,15 @@ int gtr_step_begin(const gtr_batch* bt, int num_items, int32_t* keys, int32_t* v
     return GTR_OK;
   }
   if (!keys || !vals || !tmp) { set_error("gtr_step_begin: large batch needs keys/vals/tmp scratch"); return GTR_E_ARG; }
+  if (sort_mode() == 0) {  // the own radix: its first pass builds the list, its last advances the counters
+    size_t need = rs_bytes(m_cap);
+    if (tmp_bytes < need) { set_error("gtr_step_begin: sort workspace of %zu bytes < %zu", tmp_bytes, need); return GTR_E_ARG; }
+    RsPrep pp{};
+    pp.bt = *bt; pp.T = num_items; pp.keys = keys; pp.vals = vals; pp.stamp = stamp; pp.step_dev = step_dev;
+    hipError_t e = rs_sort(tmp, keys, skeys, vals, svals, m_cap, key_bits(num_items), s, step_dev, rng_ctr, &pp);
+    if (e != hipSuccess) { set_error("gtr_step_begin: sort: %s", hipGetErrorString(e)); return (int)e; }
+    return GTR_OK;
+  }
   int rc = gtr_contrib_prep(bt, num_items, keys, vals, stamp, step_dev, stream);
   if (rc) return rc;
   rc = gtr_contrib_sort(keys, vals, skeys, svals, m_cap, num_items, tmp, tmp_bytes, stream);

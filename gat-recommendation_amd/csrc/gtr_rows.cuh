@@ -91,6 +91,33 @@ __device__ __forceinline__ void catch_up4(float4& p, float4& m, float4& v, int f
   }
 }
 
+// Lazy table, one read-modify-write of m / v per touched row (decoupled AdamW): the
+// begin's catch-up claims a lagging row by setting GTR_LAZY_CLAIM in its stamp (the low
+// bits keep the step the row was current through), brings p forward to t-1 and writes p
+// ONLY; the tail reads the claimed stamp, re-derives m / v over the same missed steps
+// (apply_zero_mv: their zero-gradient chain does not involve p, so the floats are the
+// catch-up's own), applies step t and stamps t.  Plain Adam (L2 in the gradient) couples
+// m to p: there the catch-up writes all three and the tail re-derives nothing.
+// GTR_LAZY_PONLY=0 restores the full catch-up write (A/B).
+#define GTR_LAZY_CLAIM 0x40000000
+#ifndef GTR_LAZY_PONLY
+#define GTR_LAZY_PONLY 1
+#endif
+__device__ __forceinline__ bool lazy_p_only(int decoupled) { return GTR_LAZY_PONLY && decoupled; }
+
+// Tail side: a claimed row's m / v brought from its stamp to t-1 (no-op when the catch-up
+// wrote them, or the row was current).
+__device__ __forceinline__ void lazy_mv_forward(float4& m, float4& v, int32_t stamp_word, int32_t t,
+                                                const AdamStep& st) {
+  if (!(stamp_word & GTR_LAZY_CLAIM) || !lazy_p_only(st.decoupled)) return;
+  for (int s = (stamp_word & ~GTR_LAZY_CLAIM) + 1; s <= t - 1; ++s) {
+    st.apply_zero_mv(m.x, v.x);
+    st.apply_zero_mv(m.y, v.y);
+    st.apply_zero_mv(m.z, v.z);
+    st.apply_zero_mv(m.w, v.w);
+  }
+}
+
 // consts[t] exactly as AdamStep::init computes the step's scalars.
 __device__ __forceinline__ void lazy_consts_for(const gtr_adam& o, int64_t t, float* consts) {
   AdamStep st;

@@ -50,6 +50,7 @@ struct RouteK {
   float* node_pe;
   int32_t* bcnt;    // [nblk][P] first-occurrence counts per owner, then exclusive offsets
   int32_t* status;
+  uint32_t* ticket; // arrival counter of k_route_count (scratch tail; zero between launches)
   int T, P, cap, pe_k, m_cap, nblk;
 };
 
@@ -61,9 +62,14 @@ __device__ __forceinline__ bool slot_info(const RouteK& a, int i, int& key, int&
   return valid;
 }
 
-// Pass 1: first occurrences (segment starts of the sorted list) per owner and block.
+__device__ void route_scan_body(const RouteK& a);
+
+// Pass 1: first occurrences (segment starts of the sorted list) per owner and block; the
+// last arriving block then runs pass 2 (the scan) -- one launch for both (the counts are
+// written through and the arrival is a relaxed ticket: no release fence per block).
 __global__ __launch_bounds__(RB_THREADS) void k_route_count(RouteK a) {
   __shared__ int s_cnt[SH_MAXP];
+  __shared__ int s_flag;
   if (threadIdx.x < SH_MAXP) s_cnt[threadIdx.x] = 0;
   __syncthreads();
   for (int r = 0; r < RB_ROUNDS; ++r) {
@@ -74,12 +80,17 @@ __global__ __launch_bounds__(RB_THREADS) void k_route_count(RouteK a) {
     if (first) atomicAdd(&s_cnt[q], 1);  // integer counts: order-independent
   }
   __syncthreads();
-  if (threadIdx.x < a.P) a.bcnt[(size_t)blockIdx.x * a.P + threadIdx.x] = s_cnt[threadIdx.x];
+  if (threadIdx.x < a.P)
+    __hip_atomic_store(a.bcnt + (size_t)blockIdx.x * a.P + threadIdx.x, s_cnt[threadIdx.x], __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  if (!arrive_last_wt(a.ticket, (uint32_t)a.nblk, &s_flag)) return;
+  route_scan_body(a);
+  if (threadIdx.x == 0) reset_counter(a.ticket);
 }
 
 // Pass 2 (one workgroup): exclusive offsets of every block per owner, the owners' totals
 // into the count slots, overflow status.
-__global__ __launch_bounds__(RB_THREADS) void k_route_scan(RouteK a) {
+__device__ void route_scan_body(const RouteK& a) {
   __shared__ int s_part[RB_THREADS][SH_MAXP];
   const int tid = threadIdx.x;
   if (tid == 0) a.status[0] = 0;  // this step's flag (a kernel write: no memset node in the captured step)
@@ -436,7 +447,8 @@ int gtr_shard_route_scratch(int m_cap, int world, size_t* bytes) {
     set_error("gtr_shard_route_scratch: bad arguments");
     return GTR_E_ARG;
   }
-  *bytes = (size_t)((m_cap + RB_SLOTS - 1) / RB_SLOTS) * world * sizeof(int32_t);
+  // [nblk][P] block counts + the arrival ticket (64-byte aligned slot after them)
+  *bytes = (((size_t)((m_cap + RB_SLOTS - 1) / RB_SLOTS) * world * sizeof(int32_t) + 63) & ~(size_t)63) + 64;
   return GTR_OK;
 }
 
@@ -458,15 +470,15 @@ int gtr_shard_route(const gtr_batch* bt, const int32_t* skeys, const int32_t* sv
   k.T = sh->num_items; k.P = sh->world; k.cap = sh->cap;
   k.m_cap = bt->n_cap + bt->b_cap * (1 + bt->n_neg);
   k.nblk = (k.m_cap + RB_SLOTS - 1) / RB_SLOTS;
-  if (scratch_bytes < (size_t)k.nblk * k.P * sizeof(int32_t)) {
-    set_error("gtr_shard_route: scratch of %zu bytes < %zu", scratch_bytes, (size_t)k.nblk * k.P * sizeof(int32_t));
+  const size_t cnt_bytes = ((size_t)k.nblk * k.P * sizeof(int32_t) + 63) & ~(size_t)63;
+  if (scratch_bytes < cnt_bytes + 64) {
+    set_error("gtr_shard_route: scratch of %zu bytes < %zu", scratch_bytes, cnt_bytes + 64);
     return GTR_E_ARG;
   }
   k.bcnt = static_cast<int32_t*>(scratch);
+  k.ticket = reinterpret_cast<uint32_t*>(static_cast<char*>(scratch) + cnt_bytes);
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_route_count, dim3(k.nblk), dim3(RB_THREADS), 0, s, k);
-  GTR_HIP_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_route_scan, dim3(1), dim3(RB_THREADS), 0, s, k);
+  hipLaunchKernelGGL(k_route_count, dim3(k.nblk), dim3(RB_THREADS), 0, s, k);  // + the scan (last arriver)
   GTR_HIP_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_route_write, dim3(k.nblk), dim3(RB_THREADS), 0, s, k);
   GTR_HIP_CHECK_LAUNCH();

@@ -318,6 +318,35 @@ class FusedTrainStep:
         self.resident = None  # bind_resident: batch images bound to this workspace
         self.resident_graphs = None
 
+    def workspace_ranges(self) -> list[tuple[str, int, int]]:
+        """(name, first byte, end byte) of every device buffer the step's kernels write:
+        the contribution keys / values and their sorted copies, the sort scratch, the batch
+        image, the carry scratch and the workspace's activations (the round-3
+        Onesweep fault: check that no carved buffer overlaps another)."""
+        out = []
+
+        def add(name, t):
+            if isinstance(t, torch.Tensor) and t.is_cuda and t.numel() > 0:
+                out.append((name, t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()))
+
+        for name in ("keys", "vals", "skeys", "svals", "sort_tmp", "blob", "carry", "m_tab", "v_tab", "stamp",
+                     "m_flat", "v_flat"):
+            add(name, getattr(self, name, None))
+        for name, t in vars(self.ws).items():
+            add(f"ws.{name}", t)
+        for l, lay in enumerate(getattr(self.ws, "layers", [])):
+            for name, t in lay.items():
+                add(f"ws.layers[{l}].{name}", t)
+        return out
+
+    def check_workspace_overlap(self) -> None:
+        """Raise if two of the step's device buffers overlap (views of one allocation that
+        share bytes are reported by name)."""
+        rs = sorted(self.workspace_ranges(), key=lambda r: r[1])
+        for (n0, a0, b0), (n1, a1, b1) in zip(rs, rs[1:]):
+            if a1 < b0 and not (a0 == a1 and b0 == b1):
+                raise RuntimeError(f"workspace overlap: {n0} [{a0:#x}, {b0:#x}) and {n1} [{a1:#x}, {b1:#x})")
+
     def ensure_caps(self, batch: SessionBatch):
         N, B, E, n = batch.sizes()
         if self.data_parallel and self.world > 1:  # collective: the ranks grow together

@@ -438,8 +438,12 @@ typedef struct gtr_lazy {
   gtr_adam opt;    /* by value */
 } gtr_lazy;
 
-/* gtr_step_begin + the lazy catch-up of every touched row (stamp[row] -> t-1) and
- * consts[t]; the step counter advances after every workgroup has read it.          */
+/* gtr_step_begin + the lazy catch-up of every touched row and consts[t]; the step
+ * counter advances after every workgroup has read it.  A touched row is claimed by
+ * setting bit 30 of its stamp (the low bits keep the step it was current through) and p
+ * is brought to t-1; under AdamW (decoupled) only p is written and the tail re-derives
+ * m / v over the same missed steps, so the row's moments take one read-modify-write per
+ * step.  The tail stamps the row with t.                                             */
 int gtr_step_begin_lazy(const gtr_batch* bt, int num_items, int dim, int32_t* keys, int32_t* vals, int32_t* skeys,
                         int32_t* svals, int32_t* stamp, int64_t* step_dev, uint32_t* rng_ctr, void* tmp,
                         size_t tmp_bytes, const gtr_lazy* lazy, gtr_stream_t stream);

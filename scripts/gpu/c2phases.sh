@@ -1,0 +1,7 @@
+#!/bin/bash
+# Phase stamps of the C2 step's fused layer kernels (timing build; scripts/phase_timing.py).
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+GTR_LIB=$PWD/gat-recommendation_amd/build/timing/libgtr_hip.so timeout -k 10 200 python3 -u scripts/phase_timing.py \
+  --config ${1:-c2} --batch-size ${2:-32} 2>&1 | grep -v amdgpu.ids

@@ -71,3 +71,24 @@ def test_contrib_sort_rejects_a_short_workspace():
     with pytest.raises(RuntimeError, match="workspace"):
         L.check(L.lib().gtr_contrib_sort(keys.data_ptr(), keys.data_ptr(), out.data_ptr(), out.data_ptr(), n, T,
                                          out.data_ptr(), 16, torch.cuda.current_stream().cuda_stream), "contrib_sort")
+
+
+@pytest.mark.parametrize("D,H,K,loss,B", [(128, 4, 16, "listwise", 2400), (64, 1, 0, "bpr", 32)])
+def test_step_workspaces_do_not_overlap(D, H, K, loss, B):
+    """Round-3 Onesweep question: every device buffer a fused step's kernels write (the
+    contribution keys / values, their sorted copies, the sort scratch, the batch image, the
+    carry scratch, the activations) occupies its own bytes -- checked on a large batch (the
+    radix-sort begin path of C3 at B = 8192) and on C2's small one, after a step has run."""
+    from gpu_helpers import batches, make_pair, small_data
+
+    from etpgt.train.fused import FusedTrainStep
+
+    data = small_data()
+    m, _ = make_pair(data.table_rows, D, H, K=K, seed=3)
+    m.train()
+    f = FusedTrainStep(m, loss=loss)
+    n = 100 if loss == "listwise" else 5
+    f(batches(data, B, n, 1, seed=5)[0].to("cuda"))
+    torch.cuda.synchronize()
+    assert len(f.workspace_ranges()) > 20
+    f.check_workspace_overlap()
