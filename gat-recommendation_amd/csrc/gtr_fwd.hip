@@ -1495,10 +1495,12 @@ __device__ __forceinline__ void st_row(float* p, const float (&x)[EPL]) {
 
 // Row-group geometry of the wave readout: NRG row groups of RL = 64 / NRG lanes per wave;
 // a lane holds EPL = D / RL features of a row, one load instruction moves NRG rows.
-// D = 128 runs 2 groups of 32 lanes (EPL 4): half the row registers of 4 x 16 lanes
-// (221 -> ~120 VGPRs, so 4 waves per SIMD instead of 2 hide the gather latency).
+// D = 128 keeps 4 groups of 16 lanes (EPL 8) by measurement: 2 groups of 32 lanes halve
+// the row registers (more waves per SIMD) but each round then moves half the rows per
+// instruction -- head 87.6 -> 102.4 us at C3 B = 8192, 97.9 -> 118.7 us at C5 B = 8192
+// (round-4 A/B, `GTR_RW_NRG128=2`); more waves per EU by launch bounds lost too.
 #ifndef GTR_RW_NRG128
-#define GTR_RW_NRG128 2
+#define GTR_RW_NRG128 4
 #endif
 template <int D>
 struct RwGeom {

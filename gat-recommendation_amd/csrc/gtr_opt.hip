@@ -356,9 +356,14 @@ __global__ __launch_bounds__(GTR_BEGIN_BLOCK) void k_step_begin_lazy(gtr_batch b
     const int key = slot < m_cap ? (int)(ck[slot] >> 13) : T;
     lazy_claim_row(key, T, D, t, tid & 15, lane & ~15, stamp, lz);
   }
-  if (!arrive_last(lz.cnt, gridDim.x, &s_flag)) return;
+  // consts[t] (two f64 pows) depends on t alone: written by the first workgroup's last
+  // wave after its catch-up, not on the last arriver's serial path (nothing in this launch
+  // reads consts[t]; the catch-up reads steps < t)
+  if (blockIdx.x == 0 && tid == GTR_BEGIN_BLOCK - 64) lazy_consts_for(lz.opt, t64, lz.consts);
+  // the last arriver only advances the counters: every workgroup has read *step_dev before
+  // its ticket (t is consumed above) and nothing it wrote is read here -- a relaxed ticket
+  if (!arrive_last_wt(lz.cnt, gridDim.x, &s_flag)) return;
   if (tid == 0) {
-    lazy_consts_for(lz.opt, t64, lz.consts);
     *step_dev = t64;
     if (rng_ctr) *rng_ctr += 1;
     reset_counter(lz.cnt);
