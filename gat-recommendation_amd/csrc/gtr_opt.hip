@@ -425,11 +425,11 @@ __device__ __forceinline__ void row_catch_up_store(RowRegs<EPL>& r, const gtr_la
 // resident wave).
 template <int EPL>
 __global__ __launch_bounds__(GTR_BLOCK) void k_lazy_catchup(gtr_batch bt, int T, int D, int32_t* stamp,
-                                                            const int64_t* step_dev, gtr_lazy lz, int spw) {
+                                                            const int64_t* step_dev, gtr_lazy lz, int spw, int adv) {
   const int lane = threadIdx.x & 63;
   const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
   const int N = bt.hdr[0], B = bt.hdr[1];
-  const int32_t t = (int32_t)(*step_dev + 1);
+  const int32_t t = (int32_t)(*step_dev + (adv ? 0 : 1));  // adv: the sort already advanced the step
   const gtr_adam& o = lz.opt;
   AdamStep st;
   st.lr = o.lr; st.b1 = o.beta1; st.b2 = o.beta2; st.eps = o.eps; st.wd = o.weight_decay;
@@ -1170,62 +1170,93 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const int32_t* keys, int
 // tiles): workgroup w owns digits [64 w, 64 w + 64), its 16 waves a slice of the tiles
 // each (loads in flight together); slices and digits are combined in fixed order.
 #define RS_OFFS_SL 16
+// The digits' base offsets come from a block-wide exclusive scan of the 1024 digit totals
+// (wave scans by DPP-free shuffles + 16 wave sums), not a serial walk; a slice of <= 16
+// tiles keeps its histogram column in registers between the two passes (integer sums:
+// the offsets are exact whatever the order).
+__device__ __forceinline__ int wave_incl_scan_i(int x, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o);
+    if (lane >= o) x += y;
+  }
+  return x;
+}
+
 __global__ __launch_bounds__(1024) void k_rs_offs(const int32_t* __restrict__ hist, int32_t* __restrict__ tot,
                                                  int32_t* __restrict__ offs, int ntile) {
   __shared__ int s_sl[RS_OFFS_SL][64];
-  __shared__ int s_tot[RS_RADIX];
-  __shared__ int s_base;
+  __shared__ int s_dp[RS_RADIX];  // exclusive prefix of the digit totals
+  __shared__ int s_ws[RS_RADIX / 64];
   const int tid = threadIdx.x, dl = tid & 63, sl = tid >> 6;
   const int d = blockIdx.x * 64 + dl;
-  s_tot[tid] = tot[tid];  // 1024 threads == RS_RADIX digits
-  __syncthreads();
-  if (tid == 0) {
-    int b = 0;
-    for (int q = 0; q < blockIdx.x * 64; ++q) b += s_tot[q];
-    s_base = b;
-  }
   const int per = (ntile + RS_OFFS_SL - 1) / RS_OFFS_SL;
   const int b0 = min(ntile, sl * per), b1 = min(ntile, b0 + per);
+  int v[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) v[q] = b0 + q < b1 ? hist[(size_t)(b0 + q) * RS_RADIX + d] : 0;
+  const int tv = tot[tid];  // 1024 threads == RS_RADIX digits
+  const int incl = wave_incl_scan_i(tv, dl);
+  if (dl == 63) s_ws[sl] = incl;
   int sum = 0;
-  for (int c = b0; c < b1; c += 16) {
-    int v[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = c + q < b1 ? hist[(size_t)(c + q) * RS_RADIX + d] : 0;
+  for (int q = 0; q < 16; ++q) sum += v[q];
+  for (int c = b0 + 16; c < b1; c += 16) {  // slices of more than 16 tiles (> 256 tiles)
+    int w[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) sum += v[q];
+    for (int q = 0; q < 16; ++q) w[q] = c + q < b1 ? hist[(size_t)(c + q) * RS_RADIX + d] : 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) sum += w[q];
   }
   s_sl[sl][dl] = sum;
   __syncthreads();
-  int run = s_base;
-  for (int q = 0; q < dl; ++q) run += s_tot[blockIdx.x * 64 + q];
+  int wb = 0;
+  for (int w = 0; w < sl; ++w) wb += s_ws[w];
+  s_dp[tid] = wb + incl - tv;
+  __syncthreads();
+  int run = s_dp[d];
   for (int q = 0; q < sl; ++q) run += s_sl[q][dl];
-  for (int c = b0; c < b1; c += 16) {
-    int v[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) v[q] = c + q < b1 ? hist[(size_t)(c + q) * RS_RADIX + d] : 0;
+  for (int q = 0; q < 16; ++q) {
+    if (b0 + q < b1) offs[(size_t)(b0 + q) * RS_RADIX + d] = run;
+    run += v[q];
+  }
+  for (int c = b0 + 16; c < b1; c += 16) {
+    int w[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) w[q] = c + q < b1 ? hist[(size_t)(c + q) * RS_RADIX + d] : 0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       if (c + q < b1) offs[(size_t)(c + q) * RS_RADIX + d] = run;
-      run += v[q];
+      run += w[q];
     }
   }
 }
 
 // tot: the pass's digit totals, read by k_rs_offs; zeroed here for the next call's same
 // pass (the workspace starts zeroed), so no memset node sits in the captured step.
-// step_dev / rng_ctr (the last pass of gtr_step_begin's sort, else null): workgroup 0
-// advances the step and dropout counters -- nothing of this launch reads them, and the
-// kernels after it see the new values (one launch less than a separate k_counters).
+// Step counters advanced by the last pass of gtr_step_begin's (and the lazy begin's) sort:
+// workgroup 0 advances the step and dropout counters and, for the lazy table, writes
+// consts[t] -- nothing of this launch reads them, and the kernels after it see the new
+// values (one launch less than a separate k_counters / k_counters_lazy).
+struct RsCtr {
+  int64_t* step_dev;  // null: no counters in this pass
+  uint32_t* rng_ctr;
+  float* consts;      // lazy table: consts[t] for the new step t
+  gtr_adam opt;
+};
+
 __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const int32_t* kin, const int32_t* vin, int32_t* kout,
                                                           int32_t* vout, int n, int shift, const int32_t* offs,
-                                                          int ntile, int32_t* tot, int rounds, int64_t* step_dev,
-                                                          uint32_t* rng_ctr) {
+                                                          int ntile, int32_t* tot, int rounds, RsCtr ctr) {
   __shared__ int run[RS_RADIX];
   __shared__ int wcnt[RS_THREADS / 64][RS_RADIX];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (blockIdx.x == 0 && tid == 0) {
-    if (step_dev) *step_dev += 1;
-    if (rng_ctr) *rng_ctr += 1;
+  if (blockIdx.x == 0 && tid == 0 && ctr.step_dev) {
+    const int64_t t = *ctr.step_dev + 1;
+    *ctr.step_dev = t;
+    if (ctr.rng_ctr) *ctr.rng_ctr += 1;
+    if (ctr.consts) lazy_consts_for(ctr.opt, t, ctr.consts);
   }
   if (blockIdx.x == 0)
     for (int d = tid; d < RS_RADIX; d += RS_THREADS) tot[d] = 0;
@@ -1291,8 +1322,7 @@ size_t rs_bytes(int n) {
 }
 
 hipError_t rs_sort(void* tmp, const int32_t* keys, int32_t* skeys, const int32_t* vals, int32_t* svals, int n,
-                   int bits, hipStream_t s, int64_t* step_dev = nullptr, uint32_t* rng_ctr = nullptr,
-                   const RsPrep* prep = nullptr) {
+                   int bits, hipStream_t s, const RsCtr* ctr = nullptr, const RsPrep* prep = nullptr) {
   const int rounds = rs_rounds(n), tile = RS_THREADS * rounds;
   const int ntile = (n + tile - 1) / tile;
   int32_t* k1 = static_cast<int32_t*>(tmp);
@@ -1318,7 +1348,7 @@ hipError_t rs_sort(void* tmp, const int32_t* keys, int32_t* skeys, const int32_t
                          RsPrep{});
     hipLaunchKernelGGL(k_rs_offs, dim3(RS_RADIX / 64), dim3(1024), 0, s, hist, tp, offs, ntile);
     hipLaunchKernelGGL(k_rs_scatter, dim3(ntile), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, n, p * RS_BITS, offs,
-                       ntile, tp, rounds, last ? step_dev : nullptr, last ? rng_ctr : nullptr);
+                       ntile, tp, rounds, (last && ctr) ? *ctr : RsCtr{});
     ki = ko;
     vi = vo;
   }
@@ -1530,7 +1560,9 @@ int gtr_step_begin(const gtr_batch* bt, int num_items, int32_t* keys, int32_t* v
     if (tmp_bytes < need) { set_error("gtr_step_begin: sort workspace of %zu bytes < %zu", tmp_bytes, need); return GTR_E_ARG; }
     RsPrep pp{};
     pp.bt = *bt; pp.T = num_items; pp.keys = keys; pp.vals = vals; pp.stamp = stamp; pp.step_dev = step_dev;
-    hipError_t e = rs_sort(tmp, keys, skeys, vals, svals, m_cap, key_bits(num_items), s, step_dev, rng_ctr, &pp);
+    RsCtr cc{};
+    cc.step_dev = step_dev; cc.rng_ctr = rng_ctr;
+    hipError_t e = rs_sort(tmp, keys, skeys, vals, svals, m_cap, key_bits(num_items), s, &cc, &pp);
     if (e != hipSuccess) { set_error("gtr_step_begin: sort: %s", hipGetErrorString(e)); return (int)e; }
     return GTR_OK;
   }
@@ -1586,10 +1618,28 @@ int gtr_step_begin_lazy(const gtr_batch* bt, int num_items, int dim, int32_t* ke
     return GTR_OK;
   }
   if (!keys || !vals || !tmp) { set_error("gtr_step_begin_lazy: large batch needs keys/vals/tmp scratch"); return GTR_E_ARG; }
-  int rc = gtr_contrib_prep(bt, num_items, keys, vals, nullptr, step_dev, stream);
-  if (rc) return rc;
-  rc = gtr_contrib_sort(keys, vals, skeys, svals, m_cap, num_items, tmp, tmp_bytes, stream);
-  if (rc) return rc;
+  // own radix (default): the list is built in its first pass, the counters and consts[t]
+  // advance in its last, and the catch-up reads the advanced step (adv = 1)
+  const bool own = sort_mode() == 0;
+  if (own) {
+    size_t need = rs_bytes(m_cap);
+    if (tmp_bytes < need) {
+      set_error("gtr_step_begin_lazy: sort workspace of %zu bytes < %zu", tmp_bytes, need);
+      return GTR_E_ARG;
+    }
+    RsPrep pp{};
+    pp.bt = *bt; pp.T = num_items; pp.keys = keys; pp.vals = vals; pp.stamp = nullptr; pp.step_dev = step_dev;
+    RsCtr cc{};
+    cc.step_dev = step_dev; cc.rng_ctr = rng_ctr; cc.consts = lazy->consts; cc.opt = lazy->opt;
+    hipError_t e = rs_sort(tmp, keys, skeys, vals, svals, m_cap, key_bits(num_items), s, &cc, &pp);
+    if (e != hipSuccess) { set_error("gtr_step_begin_lazy: sort: %s", hipGetErrorString(e)); return (int)e; }
+  } else {
+    int rc = gtr_contrib_prep(bt, num_items, keys, vals, nullptr, step_dev, stream);
+    if (rc) return rc;
+    rc = gtr_contrib_sort(keys, vals, skeys, svals, m_cap, num_items, tmp, tmp_bytes, stream);
+    if (rc) return rc;
+  }
+  const int adv = own ? 1 : 0;
   {
     const int blocks = lazy_catchup_blocks();
     const int64_t tasks_per_wave = 2, waves = (int64_t)blocks * (GTR_BLOCK / 64);
@@ -1598,13 +1648,15 @@ int gtr_step_begin_lazy(const gtr_batch* bt, int num_items, int dim, int32_t* ke
     if (const char* e = getenv("GTR_CATCHUP_SPW")) spw = std::max(1, std::min(64, atoi(e)));
     const int spb = spw * (GTR_BLOCK / 64);
     const int grid = std::max(1, std::min((m_cap + spb - 1) / spb, blocks));
-    if (dim <= 64) hipLaunchKernelGGL(k_lazy_catchup<1>, dim3(grid), dim3(GTR_BLOCK), 0, s, *bt, num_items, dim, stamp, step_dev, *lazy, spw);
-    else if (dim == 128) hipLaunchKernelGGL(k_lazy_catchup<2>, dim3(grid), dim3(GTR_BLOCK), 0, s, *bt, num_items, dim, stamp, step_dev, *lazy, spw);
-    else hipLaunchKernelGGL(k_lazy_catchup<4>, dim3(grid), dim3(GTR_BLOCK), 0, s, *bt, num_items, dim, stamp, step_dev, *lazy, spw);
+    if (dim <= 64) hipLaunchKernelGGL(k_lazy_catchup<1>, dim3(grid), dim3(GTR_BLOCK), 0, s, *bt, num_items, dim, stamp, step_dev, *lazy, spw, adv);
+    else if (dim == 128) hipLaunchKernelGGL(k_lazy_catchup<2>, dim3(grid), dim3(GTR_BLOCK), 0, s, *bt, num_items, dim, stamp, step_dev, *lazy, spw, adv);
+    else hipLaunchKernelGGL(k_lazy_catchup<4>, dim3(grid), dim3(GTR_BLOCK), 0, s, *bt, num_items, dim, stamp, step_dev, *lazy, spw, adv);
     GTR_HIP_CHECK_LAUNCH();
   }
-  hipLaunchKernelGGL(k_counters_lazy, dim3(1), dim3(1), 0, s, step_dev, rng_ctr, *lazy);
-  GTR_HIP_CHECK_LAUNCH();
+  if (!own) {
+    hipLaunchKernelGGL(k_counters_lazy, dim3(1), dim3(1), 0, s, step_dev, rng_ctr, *lazy);
+    GTR_HIP_CHECK_LAUNCH();
+  }
   return GTR_OK;
 }
 
