@@ -392,11 +392,15 @@ __device__ __forceinline__ void row_load(RowRegs<EPL>& r, const gtr_lazy& lz, in
   }
 }
 
+// cw: consts[wb + lane] for the last 64 steps (wb = t - 64), loaded once per wave: a row
+// whose gap lies inside that window (nearly every row) runs its chain without a load on
+// its serial path; older steps are fetched 64 at a time as before.
 template <int EPL>
 __device__ __forceinline__ void row_catch_up_store(RowRegs<EPL>& r, const gtr_lazy& lz, int key, int D, int old,
-                                                   int32_t t, int lane, AdamStep st) {
-  for (int t0 = old + 1; t0 <= t - 1; t0 += 64) {
-    const int cnt = min(64, t - t0);
+                                                   int32_t t, int lane, AdamStep st, float2 cw, int wb) {
+  const int wlo = max(old + 1, wb);
+  for (int t0 = old + 1; t0 < wlo; t0 += 64) {
+    const int cnt = min(64, wlo - t0);
     const float2 cc = lane < cnt ? reinterpret_cast<const float2*>(lz.consts)[t0 + lane] : make_float2(0.f, 0.f);
     for (int q = 0; q < cnt; ++q) {
       st.step_size = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cc.x), q));
@@ -404,6 +408,12 @@ __device__ __forceinline__ void row_catch_up_store(RowRegs<EPL>& r, const gtr_la
 #pragma unroll
       for (int k = 0; k < EPL; ++k) st.apply_zero(r.p[k], r.m[k], r.v[k]);
     }
+  }
+  for (int q = wlo - wb; q < t - wb; ++q) {  // steps wlo .. t-1 from the window
+    st.step_size = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cw.x), q));
+    st.inv_bc2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cw.y), q));
+#pragma unroll
+    for (int k = 0; k < EPL; ++k) st.apply_zero(r.p[k], r.m[k], r.v[k]);
   }
   const int c = lane * EPL;
   if (c < D) {
@@ -417,18 +427,19 @@ __device__ __forceinline__ void row_catch_up_store(RowRegs<EPL>& r, const gtr_la
   }
 }
 
-// Lazy catch-up for the large-batch (radix) path.  A wave takes `spw` (<= 64) contribution
-// slots at a time (grid-strided): each lane claims its slot's row (stamp exchange, all in
-// flight together), then the wave brings the claimed rows forward one after the other,
-// loading the next claimed row while the current one runs its chain of missed steps.
-// spw trades claim parallelism against the rows a wave walks serially (host: ~2 tasks per
-// resident wave).
+// Lazy catch-up for the large-batch (radix) path, over the SORTED contribution list.  A
+// wave takes `spw` (<= 64) slots at a time (grid-strided); the lane of a row's first slot
+// (a segment start) is the row's only claimer: it reads the stamp and writes it back with
+// GTR_LAZY_CLAIM -- plain accesses, no atomics, so a popular row's thousands of slots no
+// longer serialize on one stamp word.  The wave then brings its claimed rows forward one
+// after the other, loading the next claimed row while the current one runs its chain of
+// missed steps.  spw trades claim parallelism against the rows a wave walks serially
+// (host: ~2 tasks per resident wave).
 template <int EPL>
-__global__ __launch_bounds__(GTR_BLOCK) void k_lazy_catchup(gtr_batch bt, int T, int D, int32_t* stamp,
-                                                            const int64_t* step_dev, gtr_lazy lz, int spw, int adv) {
+__global__ __launch_bounds__(GTR_BLOCK) void k_lazy_catchup(const int32_t* skeys, int m_cap, int T, int D,
+                                                            int32_t* stamp, const int64_t* step_dev, gtr_lazy lz,
+                                                            int spw, int adv) {
   const int lane = threadIdx.x & 63;
-  const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
-  const int N = bt.hdr[0], B = bt.hdr[1];
   const int32_t t = (int32_t)(*step_dev + (adv ? 0 : 1));  // adv: the sort already advanced the step
   const gtr_adam& o = lz.opt;
   AdamStep st;
@@ -438,13 +449,19 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_lazy_catchup(gtr_batch bt, int T,
   st.step_size = 0.0f;
   st.inv_bc2 = 0.0f;
   const int nw = gridDim.x * (GTR_BLOCK / 64);
+  const int wb = t - 64;  // the last 64 steps' scalars, one per lane (steps >= 1 only are read)
+  const float2 cw = wb + lane >= 1 ? reinterpret_cast<const float2*>(lz.consts)[wb + lane] : make_float2(0.f, 0.f);
   for (int base = (blockIdx.x * (GTR_BLOCK / 64) + (threadIdx.x >> 6)) * spw; base < m_cap; base += nw * spw) {
     const int slot = base + lane;
-    const int key = (lane < spw && slot < m_cap) ? contrib_key(bt, T, slot, N, B) : T;
+    int key = T;
+    if (lane < spw && slot < m_cap) {
+      key = skeys[slot];
+      if (slot > 0 && skeys[slot - 1] == key) key = T;  // not the row's first slot
+    }
     int old = t - 1;
     if (key > 0 && key < T) {
-      old = atomicOr(stamp + key, GTR_LAZY_CLAIM);  // claimed: the low bits keep the row's step
-      if (old & GTR_LAZY_CLAIM) old = t - 1;         // another slot of the row claimed it first
+      old = stamp[key];
+      stamp[key] = old | GTR_LAZY_CLAIM;  // claimed: the low bits keep the row's step
     }
     uint64_t todo = __ballot(old < t - 1);
     if (!todo) continue;
@@ -461,7 +478,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_lazy_catchup(gtr_batch bt, int T,
         k_n = __builtin_amdgcn_readlane(key, i_n);
         row_load<EPL>(nxt, lz, k_n, D, lane);
       }
-      row_catch_up_store<EPL>(cur, lz, k_cur, D, o_cur, t, lane, st);
+      row_catch_up_store<EPL>(cur, lz, k_cur, D, o_cur, t, lane, st, cw, wb);
       if (!todo) break;
       cur = nxt;
       i = i_n;
@@ -525,6 +542,10 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_tail_carry(gtr_batch bt, int T, g
                                 tl.carry);
 }
 
+#ifndef GTR_TAIL_QF
+#define GTR_TAIL_QF 4  // contribution rows in flight per lane in the tail's segment sums (A/B: 8 -> 4 frees
+                       // 20 VGPRs, tail 119 -> 112 us at C3 B = 8192, 391 -> 380 us at C5 B = 8192)
+#endif
 // Rows part of the tail for window w = blk: every segment starting in the window is
 // summed (in-window piece + carries of the following windows) and AdamW-updated.
 template <int D>
@@ -549,8 +570,8 @@ __device__ __forceinline__ void window_rows(int w, const gtr_batch& bt, int T, c
     float4 mv = sw_ld(reinterpret_cast<const float4*>(tl.table_m) + base);
     float4 vv = sw_ld(reinterpret_cast<const float4*>(tl.table_v) + base);
     const int32_t sw = lazy_stamp ? lazy_stamp[key] : 0;
-    const float4 g = window_segment_sum<D>(bt, tl.skeys, tl.svals, tl.dx0, tl.se, tl.coef_tgt, tl.coef_neg, tl.carry,
-                                           w, s0, e, w1, m_cap, key, gl, gb);
+    const float4 g = window_segment_sum<D, GTR_TAIL_QF>(bt, tl.skeys, tl.svals, tl.dx0, tl.se, tl.coef_tgt,
+                                                        tl.coef_neg, tl.carry, w, s0, e, w1, m_cap, key, gl, gb);
     if (lazy_stamp) lazy_mv_forward(mv, vv, sw, lazy_t, st);
     st.apply(pv.x, mv.x, vv.x, g.x);
     st.apply(pv.y, mv.y, vv.y, g.y);
@@ -571,7 +592,10 @@ __device__ __forceinline__ void window_rows(int w, const gtr_batch& bt, int T, c
 #define GTR_TAIL_BLOCK (GTR_BLOCK + 64)
 
 template <int D, bool DEFER>
-__global__ __launch_bounds__(DEFER ? GTR_TAIL_BLOCK : GTR_BLOCK) void k_step_tail(TailK a) {
+#ifndef GTR_TAIL_WAVES_EU
+#define GTR_TAIL_WAVES_EU 1
+#endif
+__global__ __launch_bounds__(DEFER ? GTR_TAIL_BLOCK : GTR_BLOCK) __attribute__((amdgpu_waves_per_eu(DEFER ? 1 : GTR_TAIL_WAVES_EU))) void k_step_tail(TailK a) {
   __shared__ AdamStep s_st;
   __shared__ int32_t s_t;
   __shared__ int s_ready;
@@ -1648,9 +1672,9 @@ int gtr_step_begin_lazy(const gtr_batch* bt, int num_items, int dim, int32_t* ke
     if (const char* e = getenv("GTR_CATCHUP_SPW")) spw = std::max(1, std::min(64, atoi(e)));
     const int spb = spw * (GTR_BLOCK / 64);
     const int grid = std::max(1, std::min((m_cap + spb - 1) / spb, blocks));
-    if (dim <= 64) hipLaunchKernelGGL(k_lazy_catchup<1>, dim3(grid), dim3(GTR_BLOCK), 0, s, *bt, num_items, dim, stamp, step_dev, *lazy, spw, adv);
-    else if (dim == 128) hipLaunchKernelGGL(k_lazy_catchup<2>, dim3(grid), dim3(GTR_BLOCK), 0, s, *bt, num_items, dim, stamp, step_dev, *lazy, spw, adv);
-    else hipLaunchKernelGGL(k_lazy_catchup<4>, dim3(grid), dim3(GTR_BLOCK), 0, s, *bt, num_items, dim, stamp, step_dev, *lazy, spw, adv);
+    if (dim <= 64) hipLaunchKernelGGL(k_lazy_catchup<1>, dim3(grid), dim3(GTR_BLOCK), 0, s, skeys, m_cap, num_items, dim, stamp, step_dev, *lazy, spw, adv);
+    else if (dim == 128) hipLaunchKernelGGL(k_lazy_catchup<2>, dim3(grid), dim3(GTR_BLOCK), 0, s, skeys, m_cap, num_items, dim, stamp, step_dev, *lazy, spw, adv);
+    else hipLaunchKernelGGL(k_lazy_catchup<4>, dim3(grid), dim3(GTR_BLOCK), 0, s, skeys, m_cap, num_items, dim, stamp, step_dev, *lazy, spw, adv);
     GTR_HIP_CHECK_LAUNCH();
   }
   if (!own) {

@@ -80,14 +80,22 @@ __device__ __forceinline__ void catch_up4(float4& p, float4& m, float4& v, int f
   st.lr = o.lr; st.b1 = o.beta1; st.b2 = o.beta2; st.eps = o.eps; st.wd = o.weight_decay;
   st.decoupled = o.decoupled;
   st.decay_mul = (float)(1.0 - (double)o.lr * (double)o.weight_decay);
-  for (int t = from + 1; t <= upto; ++t) {
-    const float2 c = reinterpret_cast<const float2*>(consts)[t];
-    st.step_size = c.x;
-    st.inv_bc2 = c.y;
-    st.apply(p.x, m.x, v.x, 0.0f);
-    st.apply(p.y, m.y, v.y, 0.0f);
-    st.apply(p.z, m.z, v.z, 0.0f);
-    st.apply(p.w, m.w, v.w, 0.0f);
+  // the steps' scalars 8 at a time: one load latency per 8 steps on the chain, not per step
+  for (int t0 = from + 1; t0 <= upto; t0 += 8) {
+    float2 c[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      c[u] = t0 + u <= upto ? reinterpret_cast<const float2*>(consts)[t0 + u] : make_float2(0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (t0 + u > upto) break;
+      st.step_size = c[u].x;
+      st.inv_bc2 = c[u].y;
+      st.apply(p.x, m.x, v.x, 0.0f);
+      st.apply(p.y, m.y, v.y, 0.0f);
+      st.apply(p.z, m.z, v.z, 0.0f);
+      st.apply(p.w, m.w, v.w, 0.0f);
+    }
   }
 }
 
@@ -125,13 +133,17 @@ __device__ __forceinline__ void lazy_consts_for(const gtr_adam& o, int64_t t, fl
   reinterpret_cast<float2*>(consts)[t] = make_float2(st.step_size, st.inv_bc2);
 }
 
-#define TW 128  // slots per window of the large-batch segmented sums (below)
+#ifndef GTR_TAIL_TW
+#define GTR_TAIL_TW 128
+#endif
+#define TW GTR_TAIL_TW  // slots per window of the large-batch segmented sums (below)
 
 // Sum of contributions in slots [s, e) for column float4 `gl` by the C4 = D/4 lanes of
 // one group (group base lane gb): slot ids are fetched one per lane, decoded to a source
 // row (dx0 node row, or se session row for target / negative slots) + coefficient,
-// then broadcast 8 at a time so 8 row loads are in flight per lane.
-template <int D>
+// then broadcast QF at a time so QF row loads are in flight per lane (the sum runs in slot
+// order whatever QF is: bitwise the same).
+template <int D, int QF = 8>
 __device__ __forceinline__ float4 piece_sum(const gtr_batch& bt, const int32_t* svals, int s, int e, const float* dx0,
                                             const float* se, const float* coef_tgt, const float* coef_neg, int gl,
                                             int gb) {
@@ -156,18 +168,18 @@ __device__ __forceinline__ float4 piece_sum(const gtr_batch& bt, const int32_t* 
         cf = coef_neg[q];
       }
     }
-    for (int q0 = 0; q0 < cnt; q0 += 8) {
-      float4 v[8];
-      float f[8];
+    for (int q0 = 0; q0 < cnt; q0 += QF) {
+      float4 v[QF];
+      float f[QF];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < QF; ++u) {
         const int cq = __shfl(code, gb + ((q0 + u) & (C4 - 1)));
         f[u] = __shfl(cf, gb + ((q0 + u) & (C4 - 1)));
         const float* src = cq < 0 ? se + (size_t)(cq & 0x7FFFFFFF) * D : dx0 + (size_t)cq * D;
         v[u] = q0 + u < cnt ? reinterpret_cast<const float4*>(src)[gl] : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < QF; ++u) {
         if (q0 + u < cnt) {
           g.x += f[u] * v[u].x; g.y += f[u] * v[u].y; g.z += f[u] * v[u].z; g.w += f[u] * v[u].w;
         }
@@ -249,13 +261,13 @@ __device__ __forceinline__ int window_bounds(const int32_t* skeys, int w0, int w
 // Sum of the segment of `key` that starts at s0 inside window w (in-window end e): the
 // in-window piece, then -- if the segment reaches the window's end -- the carries of the
 // following windows in window order.
-template <int D>
+template <int D, int QF = 8>
 __device__ __forceinline__ float4 window_segment_sum(const gtr_batch& bt, const int32_t* skeys, const int32_t* svals,
                                                      const float* dx0, const float* se, const float* coef_tgt,
                                                      const float* coef_neg, const float* carry, int w, int s0, int e,
                                                      int w1, int m_cap, int key, int gl, int gb) {
   constexpr int C4 = D / 4;
-  float4 g = piece_sum<D>(bt, svals, s0, e, dx0, se, coef_tgt, coef_neg, gl, gb);
+  float4 g = piece_sum<D, QF>(bt, svals, s0, e, dx0, se, coef_tgt, coef_neg, gl, gb);
   if (e == w1) {  // the segment may continue: add the carries in window order
     for (int w2 = w + 1; w2 * TW < m_cap && skeys[w2 * TW] == key; ++w2) {
       const float4 c = reinterpret_cast<const float4*>(carry)[(size_t)w2 * C4 + gl];
