@@ -125,6 +125,10 @@ def main():
                     help="1: launch on the pre-staged batch images (one graph per image); 0: copy each image "
                          "into the step's blob per step (default: 1 on one GPU without the sharded table, "
                          "else 0)")
+    ap.add_argument("--step-graph", type=int, default=1,
+                    help="one GPU on resident images: the K timed steps launched as hipGraphs of up to 256 "
+                         "consecutive steps (FusedTrainStep.capture_steps; every step the full step) instead of "
+                         "one graph launch per step (0)")
     ap.add_argument("--dp", action="store_true", help="force the data-parallel step (exchange) even at N=1")
     ap.add_argument("--global-batch", type=int, default=None,
                     help="strong scaling: fixed global batch split over the ranks, SyncBN (1 GPU semantics)")
@@ -248,6 +252,17 @@ def main():
         if args.warmup == 0:
             one(0)  # the images' graphs are captured after one eager step (FusedTrainStep)
         step.prepare_resident()  # no capture inside the timed region
+    # K timed steps as multi-step graphs (captured here, outside the timed region): the
+    # steps follow each other inside one graph instead of one graph launch per step.
+    # Chunks of S <= 256 steps; above 256, S is a multiple of the image count, so every
+    # chunk starts on the same image and one graph serves them all.
+    seq = None
+    if resident and not args.no_graph and args.step_graph and args.steps > 0 and pg_world is None:
+        nimg = len(staged)
+        S = args.steps if args.steps <= 256 else max(nimg, (256 // nimg) * nimg)
+        full, rem = divmod(args.steps, S)
+        seq = (step.capture_steps(args.warmup, S) if full else None, full,
+               step.capture_steps(args.warmup, rem) if rem else None, S)
     torch.cuda.synchronize(dev)
     if world > 1:
         torch.distributed.barrier()
@@ -255,8 +270,14 @@ def main():
     t_start = time.perf_counter()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record()
-    for i in range(args.steps):
-        loss = one(args.warmup + i)
+    if seq is not None:
+        for _ in range(seq[1]):
+            loss = step.run_steps(seq[0])
+        if seq[2] is not None:
+            loss = step.run_steps(seq[2])
+    else:
+        for i in range(args.steps):
+            loss = one(args.warmup + i)
     ev1.record()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -351,6 +372,9 @@ def main():
                                 f"({step.shard.volume()})") if shard else step.dp is not None,
                 "hip_graph": not args.no_graph,
                 "batch_images": "resident, one graph per image" if resident else "copied per step (D2D)",
+                "step_graph": (f"{seq[3]} consecutive steps per hipGraph launch ({seq[1]} x {seq[3]}"
+                               + (f" + {args.steps % seq[3]}" if seq[2] is not None else "") + ")"
+                               if seq is not None else "one graph launch per step"),
                 "lazy_table": lazy,
                 "lagged_sweep": lagged,
                 "gemm": gemm_mode(D),

@@ -929,6 +929,7 @@ __global__ __launch_bounds__(AR_BLOCK) __attribute__((amdgpu_waves_per_eu(GTR_AR
     const int e2 = two ? a.bt.in_ptr[t0 + 2] : em;
     const int ne0 = em - e0, ne = e2 - e0;
     static_assert(AR_RPW == 2, "the paired body covers two rows per wave");
+    GTR_PH(20 + a.layer, 8);
     if (ne > AR_ECH || H > AR_HMAX) {
       one_row(0);
       one_row(1);
@@ -968,6 +969,7 @@ __global__ __launch_bounds__(AR_BLOCK) __attribute__((amdgpu_waves_per_eu(GTR_AR
           for (int u = 0; u < 4; ++u) logit(jj + u, kv[u]);
         }
       }
+      GTR_PH(20 + a.layer, 9);
       for (int j = AR_VR; j < ne; j += 4) {
         float kv[4][VPL];
 #pragma unroll
@@ -981,10 +983,12 @@ __global__ __launch_bounds__(AR_BLOCK) __attribute__((amdgpu_waves_per_eu(GTR_AR
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      GTR_PH(20 + a.layer, 10);
       float z0 = 0.0f, z1 = 0.0f;
       for (int e = 0; e < ne0; ++e) z0 += expf(s_lg[wave][e][head] - m0);
       for (int e = ne0; e < ne; ++e) z1 += expf(s_lg[wave][e][head] - m1);
       const float zd0 = z0 + 1e-16f, zd1 = z1 + 1e-16f;
+      GTR_PH(20 + a.layer, 11);
 #pragma unroll
       for (int v = 0; v < VPL; ++v) { ag0[v] = 0.0f; ag1[v] = 0.0f; }
       auto accum = [&](int e, const float (&vr)[VPL]) {
@@ -1029,8 +1033,10 @@ __global__ __launch_bounds__(AR_BLOCK) __attribute__((amdgpu_waves_per_eu(GTR_AR
         store_vec<VPL>(s_out[rl] + d0, o, act);
         if (lane == 0) a.gate[t] = beta;
       };
+      GTR_PH(20 + a.layer, 12);
       finish(t0, wave * AR_RPW, ag0, s0);
       if (two) finish(t0 + 1, wave * AR_RPW + 1, ag1, s1);
+      GTR_PH(20 + a.layer, 13);
     }
   }
   if (!a.train) return;

@@ -774,6 +774,46 @@ class FusedTrainStep:
                 coll()
         return self.ws.loss_out[0]
 
+    def capture_steps(self, start: int, n: int) -> dict:
+        """``n`` consecutive training steps over the resident images start, start + 1, ...
+        (mod their count) captured as ONE hipGraph: the steps' launches follow each other
+        inside the graph, so the queue runs step after step without a graph launch -- and
+        its host round trip -- between them.  Single GPU only (the data-parallel and
+        sharded steps keep their collectives between graph pieces).  Every step is the
+        full step (``run_resident`` of the same images n times, launch for launch); the
+        handle is for ``run_steps``."""
+        if self.resident is None:
+            raise RuntimeError("bind_resident first")
+        if not self.use_graph:
+            raise RuntimeError("capture_steps needs use_graph=True")
+        if self.dp is not None or self.shard_state is not None or self.world > 1:
+            raise NotImplementedError("multi-step graphs are single-GPU: collectives stay between graph pieces")
+        if n <= 0:
+            raise ValueError("capture_steps needs n >= 1")
+        nimg = len(self.resident)
+
+        def fn():
+            for k in range(n):
+                bs = self.resident[(start + k) % nimg][1]
+                self._with_bs(bs, lambda: self._launch(False))
+
+        return {"graph": self._capture(fn), "n": int(n), "lz_cap": self.lz.cap if self.lazy else None}
+
+    def run_steps(self, h: dict):
+        """Replay a ``capture_steps`` graph: ``h["n"]`` training steps in one launch."""
+        self.eng.check_intact()
+        if not self.model.training:
+            raise RuntimeError("FusedTrainStep requires model.train()")
+        n = h["n"]
+        if self.lazy:
+            if h["lz_cap"] != self.lz.cap or self._host_steps + n + 2 >= self.lz.cap:
+                raise RuntimeError("the lazy table's step constants were (or would have to be) reallocated: "
+                                   "capture the steps again")
+            self._host_steps += n
+            self._dirty = True
+        h["graph"].replay()
+        return self.ws.loss_out[0]
+
     def _capture_pieces(self, with_pe: bool):
         if not self._graph_collectives():
             return [(self._capture(launch), coll) for launch, coll in self._graph_pieces(with_pe)]

@@ -23,7 +23,9 @@ import torch  # noqa: E402
 K, G, S = 32, 1024, 16
 KERNELS = {20: ("attn_rows L0", 4), 21: ("attn_rows L1", 4), 26: ("readout_wave", 6)}
 # detail stamps: (name, from slot, to slot); only workgroups that reached both
-DETAIL = {20: [("bucket arrive", 2, 4), ("bucket merge", 4, 5), ("top arrive", 5, 6), ("top merge", 6, 7)],
+DETAIL = {20: [("csr offsets", 0, 8), ("ids+K/V rows", 8, 9), ("K rest", 9, 10), ("softmax z", 10, 11),
+               ("aggregate", 11, 12), ("gate+stores", 12, 13), ("other waves", 13, 1),
+               ("bucket arrive", 2, 4), ("bucket merge", 4, 5), ("top arrive", 5, 6), ("top merge", 6, 7)],
           26: [("se (node rows)", 1, 6), ("scoring rounds", 6, 7), ("lse + coefs", 7, 8), ("bwd node rows", 8, 9)]}
 DETAIL[21] = DETAIL[20]
 

@@ -436,6 +436,47 @@ def test_resident_images_equal_copied_blob(lazy):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("lazy", [False, True])
+def test_multi_step_graph_equals_per_step_graphs(lazy):
+    """capture_steps / run_steps (bench.py's timed loop: K steps as ONE hipGraph over the
+    resident images) trains bit for bit like K run_resident calls (one graph launch per
+    step): losses of every replay, parameters, AdamW moments, with the eager sweep and
+    the lazy table; a replay after a reallocation of the lazy constants is refused."""
+    from etpgt.data.batch import Caps
+
+    T = data().table_rows
+    m1, _ = make_pair(T, 64, 2, K=0, dropout=0.1, seed=9)
+    m2 = copy.deepcopy(m1)
+    m1.train(); m2.train()
+    bl = batches(data(), 32, 5, 3, seed=15)
+    caps = Caps(max(b.num_nodes for b in bl), 32, max(b.num_edges for b in bl), 5)
+    f1 = FusedTrainStep(m1, loss="bpr", caps=caps, lazy=lazy)
+    f2 = FusedTrainStep(m2, loss="bpr", caps=caps, lazy=lazy)
+    st1 = [torch.from_numpy(b.packed(f1.caps)[1]).cuda() for b in bl]
+    st2 = [torch.from_numpy(b.packed(f2.caps)[1]).cuda() for b in bl]
+    f1.bind_resident(st1)
+    f2.bind_resident(st2)
+    for i in range(2):
+        assert float(f1.run_resident(i)) == float(f2.run_resident(i))
+    f1.prepare_resident()
+    f2.prepare_resident()
+    h = f2.capture_steps(2, 4)  # images 2, 0, 1, 2
+    for rep in range(3):
+        for k in range(4):
+            l1 = float(f1.run_resident((2 + k) % 3))
+        assert l1 == float(f2.run_steps(h)), rep
+    assert f1.steps == f2.steps == 14
+    f1.flush()
+    f2.flush()
+    for a, b in zip(m1.parameters(), m2.parameters()):
+        assert torch.equal(a, b)
+    assert torch.equal(f1.m_tab, f2.m_tab) and torch.equal(f1.v_tab, f2.v_tab)
+    if lazy:
+        f2._lazy_alloc(2 * f2.lz.cap)
+        with pytest.raises(RuntimeError, match="capture the steps again"):
+            f2.run_steps(h)
+
+
 @pytest.mark.parametrize("gemm,D,H,K,loss", [("split", 64, 1, 0, "model_bpr"), ("split", 128, 4, 16, "listwise"),
                                              ("split", 32, 2, 0, "dual"), ("f32", 128, 4, 16, "listwise")])
 def test_train_grads_gemm_modes(gemm, D, H, K, loss, monkeypatch):
