@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 4: the one-GPU scaling pieces (scale_pieces.sh) and the kernel stats of the C2
+# The one-GPU scaling pieces (scale_pieces.sh) and the kernel stats of the C2
 # data-parallel step over a one-rank RCCL group.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
