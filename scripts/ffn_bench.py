@@ -75,7 +75,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     args = ap.parse_args()
     data = make_sessions_and_graph(seed=42)
-    for D, H, L, B in ((64, 2, 3, 32), (128, 4, 3, 32), (128, 4, 3, 1024)):
+    for D, H, L, B in ((64, 2, 3, 32), (128, 4, 3, 32), (128, 4, 3, 1024), (256, 4, 3, 32)):
         print(json.dumps(run(data, D, H, L, B, 5, args.steps, args.warmup)), flush=True)
 
 
