@@ -863,6 +863,9 @@ def build_provenance() -> dict:
             "lib_mtime_utc": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(os.path.getmtime(_lib.LIB_PATH)))}
 
 
+C1_PUBLISHED_T = 188  # 45,952 parameters of the optimized model, d=64, H=2, L=2, no PE
+
+
 def c1_quick(dev, reps: int) -> dict:
     """Config C1 (BASELINE.json configs[0]): run_full_pipeline.py's quick
     validation -- the reference's own 100-session synthetic data (scripts/data 00 -> 02 ->
@@ -882,7 +885,11 @@ def c1_quick(dev, reps: int) -> dict:
     sd = P.sessionize_events(ev)
     g = P.build_co_event_graph(sd)
     sub, gs = P.create_test_subset(sd, g, num_sessions=100)
-    batch, T = P.create_batch_from_sessions(sub, gs, batch_size=16, num_negatives=5)
+    batch, T_data = P.create_batch_from_sessions(sub, gs, batch_size=16, num_negatives=5)
+    # the published run's catalog: T = 188 items (45,952 parameters, docs/EXPERIMENTS.md:88),
+    # from the reference's processed data, which the synthetic generator does not reproduce
+    # (its first 100 sessions hold T_data distinct items); the batch's ids all lie below it
+    T = max(T_data, C1_PUBLISHED_T)
     cfg = dict(num_items=T, embedding_dim=64, hidden_dim=64, num_layers=2, num_heads=2, use_laplacian_pe=False,
                dropout=0.1)
     hip, hip_loss, params = [], None, None
@@ -915,8 +922,9 @@ def c1_quick(dev, reps: int) -> dict:
         if i > 0:
             cpu.append(time.time() - t)
     return {
-        "workload": f"run_full_pipeline.py quick validation: 100 synthetic sessions (reference generator, seed 42), "
-                    f"16-session batch, T={T}, d=64, 2 heads, 2 layers, no LapPE, listwise, Adam(1e-3), 3 steps",
+        "workload": f"run_full_pipeline.py quick validation: 100 synthetic sessions (reference generator, seed 42; "
+                    f"{T_data} distinct items), 16-session batch, catalog T={T} as in the published run, d=64, "
+                    f"2 heads, 2 layers, no LapPE, listwise, Adam(1e-3), 3 steps",
         "hip_ms_per_3_steps": round(1e3 * float(np.median(hip)), 3),
         "cpu_oracle_ms_per_3_steps": round(1e3 * float(np.median(cpu)), 3),
         "cpu_threads": torch.get_num_threads(),
