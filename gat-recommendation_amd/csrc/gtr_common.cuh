@@ -495,7 +495,7 @@ inline int gemm_split(int dim) {
 // Diagnostic build only (make timing): per-workgroup phase stamps of the layer
 // kernels, s_memrealtime (100 MHz) taken by thread 0; read back by gtr_dbg_*_phases.
 #define GTR_PH_KERNELS 32
-#define GTR_PH_GROUPS 1024
+#define GTR_PH_GROUPS 4096
 #define GTR_PH_SLOTS 16
 #ifdef GTR_PHASE_TIMING
 #define GTR_PH_DECL static __device__ unsigned long long g_ph[GTR_PH_KERNELS][GTR_PH_GROUPS][GTR_PH_SLOTS];

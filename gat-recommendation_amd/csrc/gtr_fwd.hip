@@ -127,21 +127,42 @@ __device__ __forceinline__ void bn_fwd_finalize(const ConvFwdK& a, int g, int Gn
   // (st_wt) -- no agent-scope release fence anywhere (round 4: the bucket level's fence was
   // part of the ~10 us tail a last arriver added to k_attn_rows)
   if (nbk > 1) {
-    const int bk = g / GTR_PART_BUCKET, b0 = bk * GTR_PART_BUCKET;
-    if (!arrive_last_wt(a.cnt + 4 + 2 * bk, (uint32_t)min(GTR_PART_BUCKET, Gn - b0), s_flag)) return;
+    constexpr int PB = GTR_PART_BUCKET;
+    const int bk = g / PB, b0 = bk * PB;
+    if (!arrive_last_wt(a.cnt + 4 + 2 * bk, (uint32_t)min(PB, Gn - b0), s_flag)) return;
     GTR_PH(20 + a.layer, 4);
     float* row0 = a.bn_part + (size_t)b0 * PW;
-    bn_merge_parts<D, BLK>(row0, min(GTR_PART_BUCKET, Gn - b0), red, PW, row0, true);
+    bn_merge_parts<D, BLK>(row0, min(PB, Gn - b0), red, PW, row0, true);
     if (tid == 0) reset_counter(a.cnt + 4 + 2 * bk);
     GTR_PH(20 + a.layer, 5);
-    if (!arrive_last_wt(a.cnt, (uint32_t)nbk, s_flag)) return;
+    // past PB buckets (> 1024 workgroups: C3 / C5 at B = 8192 run ~3.5k) a third level:
+    // super-buckets of PB bucket rows, merged by their last arriving bucket merger into the
+    // super-bucket's first row, so that no merger walks more than PB rows (a 111-row top
+    // merge measured 21 us of the launch's serial tail; one PB-row merge ~5 us).  The
+    // super-bucket counters use the odd slots cnt[5 + 2 sb] next to the buckets' even ones;
+    // the backward's bucket counters for this layer's sums use the same odd slots in later
+    // launches (p_cnt = cnt + 1), and every counter is reset to zero by its last arriver.
+    // C3 B = 8192: attention forward 62-68 -> 52 us per layer.
+    const int nsb = (nbk + PB - 1) / PB;
+    int ntop = nbk;
+    size_t top_stride = (size_t)PB * PW;
+    if (nsb > 1) {
+      const int sb = bk / PB, k0 = sb * PB;
+      if (!arrive_last_wt(a.cnt + 5 + 2 * sb, (uint32_t)min(PB, nbk - k0), s_flag)) return;
+      float* srow = a.bn_part + (size_t)k0 * PB * PW;  // bucket k0's merged row
+      bn_merge_parts<D, BLK>(srow, min(PB, nbk - k0), red, (size_t)PB * PW, srow, true);
+      if (tid == 0) reset_counter(a.cnt + 5 + 2 * sb);
+      ntop = nsb;
+      top_stride = (size_t)PB * PB * PW;
+    }
+    if (!arrive_last_wt(a.cnt, (uint32_t)ntop, s_flag)) return;
     GTR_PH(20 + a.layer, 6);
-    if (a.merge_only) {  // the buckets' rows -> ONE row (row 0, bucket 0's own row: may alias)
-      bn_merge_parts<D, BLK>(a.bn_part, nbk, red, (size_t)GTR_PART_BUCKET * PW, a.bn_part);
+    if (a.merge_only) {  // the top rows -> ONE row (row 0, bucket 0's own row: may alias)
+      bn_merge_parts<D, BLK>(a.bn_part, ntop, red, top_stride, a.bn_part);
       if (tid == 0) reset_counter(a.cnt);
       return;
     }
-    bn_stats_from_parts<D, BLK>(a.bn_part, nbk, a.bn_eps, s_bn, s_bn + D, s_uvar, red, (size_t)GTR_PART_BUCKET * PW);
+    bn_stats_from_parts<D, BLK>(a.bn_part, ntop, a.bn_eps, s_bn, s_bn + D, s_uvar, red, top_stride);
     GTR_PH(20 + a.layer, 7);
   } else {
     if (!arrive_last_wt(a.cnt, (uint32_t)Gn, s_flag)) return;

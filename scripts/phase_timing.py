@@ -21,7 +21,7 @@ sys.path.insert(0, os.path.join(ROOT, "gat-recommendation_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-K, G, S = 32, 1024, 16
+K, G, S = 32, 4096, 16
 FWD_NAMES = {0: "conv_fwd L0", 1: "conv_fwd L1", 16: "readout"}
 BWD_NAMES = {0: "conv_bwd L0", 1: "conv_bwd L1"}
 FWD_PHASES = ["stage", "proj", "attn", "bnpart"]

@@ -20,7 +20,7 @@ sys.path.insert(0, os.path.join(ROOT, "gat-recommendation_amd"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-K, G, S = 32, 1024, 16
+K, G, S = 32, 4096, 16
 KERNELS = {20: ("attn_rows L0", 4), 21: ("attn_rows L1", 4), 26: ("readout_wave", 6)}
 # detail stamps: (name, from slot, to slot); only workgroups that reached both
 DETAIL = {20: [("csr offsets", 0, 8), ("ids+K/V rows", 8, 9), ("K rest", 9, 10), ("softmax z", 10, 11),
@@ -74,6 +74,11 @@ def main():
             tails = [(st[st[:, k] > 0, k] - st[st[:, k] > 0, k - 1]).max() * 10e-3 if (st[:, k] > 0).any() else 0.0
                      for k in range(1, nst)]
             r["tail"].append(tails)
+            # when workgroups start and finish their main phase (relative to the first start)
+            t0 = start.min()
+            fin = np.where(st[:, 1] > 0, st[:, 1], last)
+            r.setdefault("gen", []).append([np.percentile(start - t0, q) * 10e-3 for q in (50, 90, 100)]
+                                           + [np.percentile(fin - t0, q) * 10e-3 for q in (50, 90, 100)])
             for dn, a0, a1 in DETAIL.get(kid, []):
                 ok = (st[:, a0] > 0) & (st[:, a1] >= st[:, a0])
                 if ok.any():
@@ -84,6 +89,10 @@ def main():
         print(f"{name:14s} wgs {int(np.median(r['n'])):5d} span {np.median(r['span']):7.2f} us  skew "
               f"{np.median(r['skew']):6.2f}  phase means " + " ".join(f"{v:6.2f}" for v in np.median(r['ph'], axis=0))
               + "  phase max " + " ".join(f"{v:6.2f}" for v in np.median(r['tail'], axis=0)))
+        if "gen" in r:
+            g = np.median(np.array(r["gen"]), axis=0)
+            print(f"    starts p50/p90/max {g[0]:6.2f} {g[1]:6.2f} {g[2]:6.2f}   main done p50/p90/max "
+                  f"{g[3]:6.2f} {g[4]:6.2f} {g[5]:6.2f} us")
         for dn, v in r.get("det", {}).items():
             v = np.array(v)
             print(f"    {dn:16s} mean {np.median(v[:, 0]):7.2f}  max {np.median(v[:, 1]):7.2f}  (wgs {int(np.median(v[:, 2]))})")
