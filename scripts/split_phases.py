@@ -59,6 +59,10 @@ def main():
             live = st[:, 0] > 0
             if not live.any():
                 continue
+            # stamps are not cleared between steps: keep this step's workgroups (a batch with
+            # fewer row groups than an earlier one leaves the extra slots' old stamps behind)
+            med = np.median(st[live, 0])
+            live &= np.abs(st[:, 0] - med) < 50000  # 500 us at the 100 MHz stamp clock
             st = st[live]
             start = st[:, 0]
             last = np.where(st[:, 1:nst] > 0, st[:, 1:nst], 0).max(1)
