@@ -443,6 +443,16 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
 #pragma unroll
     for (int u = 0; u < PER; ++u) cur[u] = nxt[u];
     fetch(t + 2 * gridDim.x, nxt);  // in flight during the MFMAs
+    // the epilogue's residual / previous-output values requested before the MFMA chain, so
+    // that the tile's stores do not wait one memory round after it
+    float ydv[4], pov[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = t * BM + rs * 16 + lg * 4 + i;
+      const size_t o = (size_t)row * D + col;
+      ydv[i] = row < N ? a.dy[o] : 0.0f;
+      pov[i] = (!DOWN && a.has_prev && row < N) ? a.p_out[o] : 0.0f;
+    }
     f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
     const float* arow = A + (rs * 16 + lr) * AS + lg * 4;
 #pragma unroll
@@ -453,15 +463,15 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
       if (row < N) {
         const size_t o = (size_t)row * D + col;
         if (DOWN) {  // z = y + dropout(h W2^T + b2)
-          a.dx0[o] = a.dy[o] + (acc[i] + b2c) * dr.mul(st_o, (uint32_t)o);
+          a.dx0[o] = ydv[i] + (acc[i] + b2c) * dr.mul(st_o, (uint32_t)o);
           continue;
         }
-        const float dx = a.dy[o] + acc[i];
+        const float dx = ydv[i] + acc[i];
         if (a.has_prev) {
           const float d = dx * dr.mul(st_prev, (uint32_t)o);
           a.p_dy[o] = d;
           s1 += d;
-          s2 += d * ((a.p_out[o] - pm) * pr);
+          s2 += d * ((pov[i] - pm) * pr);
         } else {
           a.dx0[o] = dx;
         }
