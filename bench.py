@@ -258,9 +258,7 @@ def main():
     # chunk starts on the same image and one graph serves them all.
     seq = None
     if resident and not args.no_graph and args.step_graph and args.steps > 0 and pg_world is None:
-        nimg = len(staged)
-        S = args.steps if args.steps <= 256 else max(nimg, (256 // nimg) * nimg)
-        full, rem = divmod(args.steps, S)
+        S, full, rem = step_graph_plan(args.steps, len(staged))
         seq = (step.capture_steps(args.warmup, S) if full else None, full,
                step.capture_steps(args.warmup, rem) if rem else None, S)
     torch.cuda.synchronize(dev)
@@ -580,6 +578,18 @@ def measure_tail(step, iters) -> float:
         durs.append((e0, e1))
     torch.cuda.synchronize()
     return float(np.median([a.elapsed_time(b) for a, b in durs]))
+
+
+def step_graph_plan(steps: int, nimg: int, cap: int = 256) -> tuple[int, int, int]:
+    """Chunking of K timed steps into multi-step graphs: (S, full, rem) with K = full * S +
+    rem.  K <= cap: one graph of K steps.  Above, S is a multiple of the image count (so
+    every chunk, and the remainder, starts on the same resident image and one graph serves
+    all full chunks)."""
+    if steps <= cap:
+        return steps, 1, 0
+    S = max(nimg, (cap // nimg) * nimg)
+    full, rem = divmod(steps, S)
+    return S, full, rem
 
 
 def gemm_mode(D: int) -> str:

@@ -453,3 +453,22 @@ def test_plan_caps_covers_a_ranks_partial_batch_off_the_stride_grid():
     assert grid_only.n_cap < 100  # the grid windows miss the long sessions
     caps = bld.plan_caps(2, position=1 * B, extra=[(pos1, b_last)])
     assert caps.n_cap >= 100 and caps.e_cap >= 800 and caps.b_cap >= B
+
+
+def test_bench_step_graph_plan_covers_exactly_k_steps():
+    """bench.py's multi-step graph chunking (FusedTrainStep.capture_steps): the K timed
+    steps are exactly full * S + rem; above 256 steps every chunk is a multiple of the
+    resident image count, so each chunk and the remainder start on the same image."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    for steps in (1, 5, 20, 200, 256, 257, 1000, 4097):
+        for nimg in (4, 7, 64):
+            S, full, rem = bench.step_graph_plan(steps, nimg)
+            assert full * S + rem == steps and 0 <= rem < S or (full == 1 and rem == 0 and S == steps)
+            if steps > 256:
+                assert S % nimg == 0 and S <= max(256, nimg)
+            else:
+                assert (S, full, rem) == (steps, 1, 0)
