@@ -73,8 +73,8 @@ class ShardState:
         self.v = torch.zeros_like(self.table)
         self.stamp = torch.zeros(self.local_rows, dtype=torch.int32, device=dev)
         self.status = torch.zeros(4, dtype=torch.int32, device=dev)
-        self.status_host = torch.zeros(4, dtype=torch.int32).pin_memory()
-        self._status_event = None
+        self._checks = 0
+        self._check_every = max(1, int(os.environ.get("GTR_SHARD_CHECK_EVERY", "64")))
         self.consts = None
         self.stale = False  # the model's item_embedding.weight lags the shards
         self.s = L.GtrShard()
@@ -105,27 +105,20 @@ class ShardState:
         return True
 
     def check_status(self, block: bool = False):
-        """Raise if any step since the last check overflowed an exchange block.  The
-        per-step check copies the status word asynchronously and reads it one step later;
-        ``block=True`` (sync_table / export) waits for every queued step and reads the
-        word as it stands after the LAST one."""
-        if block:
-            torch.cuda.current_stream(self.step.dev).synchronize()
-            self._status_event = None
-            if int(self.status[1].item()) != 0:
-                raise RuntimeError("row-sharded table: a batch requested more rows from one owner than the "
-                                   "exchange capacity holds (raise GTR_SHARD_SLACK)")
+        """Raise if any step since the last check overflowed an exchange block.  Every rank
+        checks at the same host steps -- every GTR_SHARD_CHECK_EVERY-th call (64) and at
+        ``block=True`` (sync_table / export) -- after its queue has drained.  The overflow
+        flag reaches every rank inside the flagged step (k_shard_update folds the ranks'
+        flags into the sticky status[1]), so all ranks raise together, at the same step,
+        instead of one rank leaving the others blocked in the next collective.
+        A flagged step trains as a zero-gradient step on the rows it could not fetch."""
+        self._checks += 1
+        if not block and self._checks % self._check_every:
             return
-        if self._status_event is not None and self._status_event.query():
-            self._status_event.synchronize()
-            if int(self.status_host[1]) != 0:
-                raise RuntimeError("row-sharded table: a batch requested more rows from one owner than the "
-                                   "exchange capacity holds (raise GTR_SHARD_SLACK)")
-            self._status_event = None
-        if self._status_event is None:
-            self.status_host.copy_(self.status, non_blocking=True)
-            self._status_event = torch.cuda.Event()
-            self._status_event.record()
+        torch.cuda.current_stream(self.step.dev).synchronize()
+        if int(self.status[1].item()) != 0:
+            raise RuntimeError("row-sharded table: a batch requested more rows from one owner than the "
+                               "exchange capacity holds (raise GTR_SHARD_SLACK)")
 
     # ---------------------------------------------------------------- the full table
     def flush(self):
