@@ -799,6 +799,40 @@ class FusedTrainStep:
 
         return {"graph": self._capture(fn), "n": int(n), "lz_cap": self.lz.cap if self.lazy else None}
 
+    def capture_steps_copied(self, images, start: int, n: int) -> dict | None:
+        """``n`` consecutive data-parallel steps, each copying pre-staged image
+        (start + k) mod len(images) into the step's blob (the D2D copy ``load_blob`` makes)
+        and running the step with its RCCL collectives, captured as ONE hipGraph.  Only
+        where the collectives are captured in the step's graph anyway (RCCL, N > 1 or
+        GTR_GRAPH_COLL=1); the row-sharded table keeps per-step launches.  Every rank
+        captures, then the ranks agree (all-reduce outside any capture): if any rank's
+        capture was refused, every rank returns None and keeps the per-step path."""
+        if not self.use_graph or self.shard_state is not None or not self._graph_collectives():
+            return None
+        if n <= 0:
+            raise ValueError("capture_steps_copied needs n >= 1")
+        nimg = len(images)
+        for img in images:
+            if img.numel() != self.blob.numel() or img.dtype != self.blob.dtype or img.device != self.blob.device:
+                raise ValueError("images must match the step's blob (size, dtype, device)")
+
+        def fn():
+            for k in range(n):
+                self.blob.copy_(images[(start + k) % nimg], non_blocking=True)
+                self._launch(False)
+
+        g, err = None, None
+        try:
+            g = self._capture(fn)
+        except RuntimeError as e:
+            if "captur" not in str(e).lower():
+                raise
+            err = e
+            torch.cuda.synchronize(self.dev)
+        if self._ranks_agree_refused(err is not None):
+            return None
+        return {"graph": g, "n": int(n), "lz_cap": self.lz.cap if self.lazy else None}
+
     def run_steps(self, h: dict):
         """Replay a ``capture_steps`` graph: ``h["n"]`` training steps in one launch."""
         self.eng.check_intact()
