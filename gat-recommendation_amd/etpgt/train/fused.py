@@ -799,15 +799,16 @@ class FusedTrainStep:
 
         return {"graph": self._capture(fn), "n": int(n), "lz_cap": self.lz.cap if self.lazy else None}
 
-    def capture_steps_copied(self, images, start: int, n: int) -> dict | None:
+    def capture_steps_copied(self, images, start: int, n: int, reserve: int = 0) -> dict | None:
         """``n`` consecutive data-parallel steps, each copying pre-staged image
         (start + k) mod len(images) into the step's blob (the D2D copy ``load_blob`` makes)
         and running the step with its RCCL collectives, captured as ONE hipGraph.  Only
         where the collectives are captured in the step's graph anyway (RCCL, N > 1 or
-        GTR_GRAPH_COLL=1); the row-sharded table keeps per-step launches.  Every rank
-        captures, then the ranks agree (all-reduce outside any capture): if any rank's
-        capture was refused, every rank returns None and keeps the per-step path."""
-        if not self.use_graph or self.shard_state is not None or not self._graph_collectives():
+        GTR_GRAPH_COLL=1).  Every rank captures, then the ranks agree (all-reduce outside
+        any capture): if any rank's capture was refused, every rank returns None and keeps
+        the per-step path.  The row-sharded table's per-step constants are grown first for
+        ``reserve`` more steps (their pointers are captured)."""
+        if not self.use_graph or not self._graph_collectives():
             return None
         if n <= 0:
             raise ValueError("capture_steps_copied needs n >= 1")
@@ -815,6 +816,10 @@ class FusedTrainStep:
         for img in images:
             if img.numel() != self.blob.numel() or img.dtype != self.blob.dtype or img.device != self.blob.device:
                 raise ValueError("images must match the step's blob (size, dtype, device)")
+
+        if self.shard_state is not None and self.shard_state.ensure_steps(self._host_steps + max(reserve, n) + 2):
+            self.graph = self.graph_pe = self.graph_b = None  # consts moved: the per-step graphs recapture
+            self.resident_graphs = None
 
         def fn():
             for k in range(n):
@@ -831,7 +836,8 @@ class FusedTrainStep:
             torch.cuda.synchronize(self.dev)
         if self._ranks_agree_refused(err is not None):
             return None
-        return {"graph": g, "n": int(n), "lz_cap": self.lz.cap if self.lazy else None}
+        return {"graph": g, "n": int(n), "lz_cap": self.lz.cap if self.lazy else None,
+                "consts": self.shard_state.consts.data_ptr() if self.shard_state is not None else None}
 
     def run_steps(self, h: dict):
         """Replay a ``capture_steps`` graph: ``h["n"]`` training steps in one launch."""
@@ -839,6 +845,12 @@ class FusedTrainStep:
         if not self.model.training:
             raise RuntimeError("FusedTrainStep requires model.train()")
         n = h["n"]
+        if self.shard_state is not None:
+            self._host_steps += n
+            if self.shard_state.ensure_steps(self._host_steps) or h.get("consts") != self.shard_state.consts.data_ptr():
+                raise RuntimeError("the row-sharded table's step constants were (or would have to be) reallocated: "
+                                   "capture the steps again")
+            self.shard_state.check_status()
         if self.lazy:
             if h["lz_cap"] != self.lz.cap or self._host_steps + n + 2 >= self.lz.cap:
                 raise RuntimeError("the lazy table's step constants were (or would have to be) reallocated: "

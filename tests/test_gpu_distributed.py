@@ -464,3 +464,61 @@ def test_dp_multi_step_graph_equals_per_step_launches():
     for l1, l2 in out:
         assert l1 == l2
     assert same
+
+
+def _shard_multi_worker(port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GTR_GRAPH_COLL="1")
+    import torch.distributed as dist
+
+    from etpgt.data.batch import Caps
+
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        data = small_data()
+        T = data.table_rows
+        m1, _ = make_pair(T, D, H, K=0, seed=35)
+        m2 = copy.deepcopy(m1)
+        m1.train(); m2.train()
+        bl = batches(data, B, NNEG, 3, seed=36)
+        caps = Caps(max(b.num_nodes for b in bl), B, max(b.num_edges for b in bl), NNEG)
+        kw = dict(lr=1e-2, weight_decay=1e-2, loss="bpr", shard_table=True, sync_bn=True, caps=caps)
+        f1 = FusedTrainStep(m1, **kw)
+        f2 = FusedTrainStep(m2, **kw)
+        st1 = [torch.from_numpy(b.packed(f1.caps)[1]).cuda() for b in bl]
+        st2 = [torch.from_numpy(b.packed(f2.caps)[1]).cuda() for b in bl]
+        for i in range(2):
+            f1.load_blob(st1[i]); l1 = float(f1.run())
+            f2.load_blob(st2[i]); l2 = float(f2.run())
+            assert l1 == l2
+        h = f2.capture_steps_copied(st2, 2, 4, reserve=12)
+        out = []
+        for rep in range(3):
+            for k in range(4):
+                f1.load_blob(st1[(2 + k) % 3])
+                l1 = float(f1.run())
+            out.append((l1, float(f2.run_steps(h))))
+        f1.sync_table(); f2.sync_table()
+        same = all(torch.equal(a, b) for a, b in zip(m1.parameters(), m2.parameters()))
+        q.put((out, same, h is not None, f1.steps, f2.steps))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_multi_step_graph_equals_per_step_launches():
+    """The strong-scaling legs' row-sharded step (all-to-alls and SyncBN gathers inside the
+    step graph) as ONE multi-step hipGraph equals per-step launches bit for bit, over RCCL
+    with one rank."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_shard_multi_worker, args=(_free_port(), q))
+    p.start()
+    try:
+        out, same, captured, s1, s2 = collect(q, [p], 1, 300)[0]
+    finally:
+        p.join(timeout=60)
+    assert p.exitcode == 0
+    assert captured and s1 == s2 == 14
+    for l1, l2 in out:
+        assert l1 == l2
+    assert same
