@@ -146,6 +146,8 @@ def main():
     ap.add_argument("--recall-sessions", type=int, default=2048, help="held-out sessions of the Recall@10 leg")
     ap.add_argument("--e2e-steps", type=int, default=200,
                     help="end-to-end leg: steps with the batch built on the device inside the step (0 = skip)")
+    ap.add_argument("--trainer-epochs", type=int, default=1,
+                    help="drop-in leg: timed Trainer.train_epoch epochs over a DeviceSessionLoader (0 = skip)")
     ap.add_argument("--tail-probe", type=int, default=1,
                     help="re-launch the step tail alone to time it (0 = skip; PMC passes skip it so that the "
                          "per-step kernel counts stay exact)")
@@ -328,6 +330,11 @@ def main():
     if rank == 0 and world == 1 and args.e2e_steps > 0:
         e2e = e2e_probe(cfg, data, dev, B, args.e2e_steps)
         log(f"end to end: {e2e['device_batch_build_sessions_per_s']} sessions/s")
+    trainer_leg = None
+    if rank == 0 and world == 1 and args.trainer_epochs > 0 and not shard:
+        trainer_leg = trainer_epoch_probe(cfg, data, dev, B, args.trainer_epochs)
+        trainer_leg["vs_headline_ms_per_step"] = round(trainer_leg["ms_per_step"] / ms_per_step, 4)
+        log(f"trainer epoch: {trainer_leg['sessions_per_s']} sessions/s, {trainer_leg['ms_per_step']} ms/step")
     gather = gather_c = None
     if rank == 0 and world == 1 and args.gather_batch > 0:
         gather = gather_probe(dev, args.gather_batch, "c5")
@@ -372,6 +379,7 @@ def main():
                 "parallelism": f"dp{world}" + ("+rowshard" if shard else ""),
                 "transport": "rccl" if backend == "nccl" else "gloo (shared-device rehearsal)",
                 "process_group_world": pg_world,
+                "visible_gpus": torch.cuda.device_count(),
                 "launcher": ("bench.py --gpus (torch.distributed.run child)" if os.environ.get("GTR_BENCH_SPAWNED")
                              else "external (torchrun / torch.distributed.run)" if "WORLD_SIZE" in os.environ
                              else "none (one process)"),
@@ -416,6 +424,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "end_to_end": e2e,
+            "trainer_epoch": trainer_leg,
             "gather_roofline": gather,
             "gather_roofline_infinity_cache": gather_c,
             "recall_parity": recall,
@@ -462,9 +471,12 @@ def strong_scaling_legs(world: int, global_batches: list, steps: int = 0) -> dic
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
                         "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID", "GTR_BENCH_SPAWNED")
-           and not k.startswith("TORCHELASTIC")}
+           and not k.startswith("TORCHELASTIC")
+           # a launcher may pin each rank to one device: the N-rank child must see all N
+           and k not in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES")}
     env["GTR_STRONG_CHILD"] = "1"
     lean = ["--cpu-seconds", "0", "--gather-batch", "0", "--recall-steps", "0", "--e2e-steps", "0", "--c1-reps", "0",
+            "--trainer-epochs", "0",
             "--tail-probe", "0", "--strong-batches", "0"]
     res = {"config": "c4", "workload": CONFIGS["c4"]["name"], "n_gpus": world, "legs": []}
     for G in global_batches:
@@ -493,6 +505,11 @@ def strong_scaling_legs(world: int, global_batches: list, steps: int = 0) -> dic
             leg["error"] = line["error"]
         else:
             c = line["config"]
+            seen = c.get("visible_gpus")
+            if c.get("process_group_world", 1) not in (None, world) or (
+                    seen is not None and seen < world and not str(c.get("transport", "")).startswith("gloo")):
+                leg["error"] = (f"the child ran {c.get('process_group_world')} ranks on {seen} visible GPU(s), "
+                                f"not {world}")
             leg.update({"value": line["value"], "unit": line["unit"], "ms_per_step": line["ms_per_step"],
                         "gpu_ms_per_step_events": c["gpu_ms_per_step_events"], "steps": line["steps"],
                         "parallelism": c["parallelism"], "process_group_world": c["process_group_world"],
@@ -688,6 +705,63 @@ def e2e_probe(cfg, data, dev, B, steps):
         "note": "device: k_bb_scan + k_bb_write in the captured step, epoch order walked by a device cursor; "
                 "host: per-session example + collate + pack + H2D per step",
     }
+
+
+def trainer_epoch_probe(cfg, data, dev, B, epochs: int = 1, steps_per_graph: int | None = None):
+    """The drop-in path at the headline shape: ``Trainer.train_epoch`` (trainer.py:80-133)
+    over a ``DeviceSessionLoader`` on the synthetic sessions, i.e. what
+    ``scripts/train/train_baseline.py`` runs -- every batch built on the device inside the
+    step, the epoch's full batches as multi-step hipGraphs (``steps_per_graph``), the
+    partial last batch eager, the epoch loss read once.  One untimed epoch (captures),
+    then ``epochs`` timed epochs, wall clock around ``train_epoch`` (host work included:
+    the epoch order draw, its upload, capacity planning)."""
+    from etpgt.data.gpu_batch import GpuSessionStore
+    from etpgt.data.synthetic import random_pe_table
+    from etpgt.model import create_graph_transformer_optimized
+    from etpgt.train.dataloader import DeviceSessionLoader
+    from etpgt.train.losses import create_loss_function
+    from etpgt.train.trainer import Trainer
+
+    T = data.table_rows
+    torch.manual_seed(42)
+    model = create_graph_transformer_optimized(T, embedding_dim=cfg["D"], hidden_dim=cfg["D"], num_layers=2,
+                                               num_heads=cfg["H"], dropout=0.1, use_laplacian_pe=cfg["K"] > 0,
+                                               laplacian_k=max(cfg["K"], 1))
+    if cfg["K"] > 0:
+        model.laplacian_pe._cached_pe = random_pe_table(T, cfg["K"])
+    store = GpuSessionStore.from_synthetic(data, dev)
+    loader = DeviceSessionLoader.from_store(store, B, cfg["n_neg"], shuffle=True, seed=42)
+    opt = torch.optim.AdamW(model.parameters(), lr=1e-3, weight_decay=1e-5)
+    lf = None if cfg["loss"] == "bpr" else create_loss_function(cfg["loss"])
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as tmp:
+        tr = Trainer(model, loader, None, opt, device=str(dev), output_dir=tmp, loss_fn=lf)
+        if steps_per_graph is not None:
+            tr.steps_per_graph = steps_per_graph
+        tr.train_epoch()  # untimed: captures the step and chunk graphs
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        losses = [tr.train_epoch() for _ in range(epochs)]
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t
+    n_steps = len(loader.batch_sizes()) * epochs
+    sessions = loader.num_sessions * epochs
+    out = {
+        "sessions_per_s": round(sessions / el, 1),
+        "ms_per_step": round(el * 1e3 / n_steps, 4),
+        "steps": n_steps,
+        "epochs": epochs,
+        "batch": B,
+        "steps_per_graph": tr.steps_per_graph,
+        "chunk_graphs": tr._chunk_graph is not None,
+        "epoch_loss": round(losses[-1], 6),
+        "note": "Trainer.train_epoch over DeviceSessionLoader (train_baseline.py's path): batch build inside the "
+                "step, full batches as multi-step hipGraphs, partial last batch eager; wall clock per epoch",
+    }
+    del tr, model
+    torch.cuda.empty_cache()
+    return out
 
 
 def gather_probe(dev, B, config="c5", nbatch=4, steps=20):

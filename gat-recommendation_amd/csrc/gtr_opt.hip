@@ -654,7 +654,10 @@ __global__ __launch_bounds__(DEFER ? GTR_TAIL_BLOCK : GTR_BLOCK) __attribute__((
         float t = 0.0f;
         for (int q = 0; q < GTR_BLOCK; ++q) t += s_acc[q];
         a.tl.loss_out[0] = t;
+        if (a.tl.loss_acc) a.tl.loss_acc[0] += (double)t;
       }
+    } else if (sb == 0 && a.tl.loss_acc && tid == 0) {  // the readout wrote the loss itself
+      a.tl.loss_acc[0] += (double)a.tl.loss_out[0];
     }
     return;
   }
@@ -790,7 +793,10 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_step_tail_wgrad(TailWK a) {
         float t = 0.0f;
         for (int q = 0; q < GTR_BLOCK; ++q) t += s_acc[q];
         a.tl.loss_out[0] = t;
+        if (a.tl.loss_acc) a.tl.loss_acc[0] += (double)t;
       }
+    } else if (blk == 0 && a.tl.loss_acc && tid == 0) {
+      a.tl.loss_acc[0] += (double)a.tl.loss_out[0];
     }
   }
 }
@@ -1101,6 +1107,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_dp_tail(DpTailK a) {
       float l = 0.0f;
       for (int q = 0; q < W; ++q) l += a.recv[(size_t)q * a.lay.words + a.lay.loss_off];
       a.tl.loss_out[0] = l * inv_w;
+      if (a.tl.loss_acc) a.tl.loss_acc[0] += (double)(l * inv_w);
     }
     return;
   }
@@ -1739,7 +1746,7 @@ int gtr_step_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* t
     k.nb_rows = (int)(((int64_t)m_cap * (dim / 4) + GTR_BLOCK - 1) / GTR_BLOCK);
   }
   k.nb_small = nseg > 0 ? (int)((t.flat_total + GTR_BLOCK - 1) / GTR_BLOCK) : 0;
-  if (k.nb_small == 0 && t.loss_part) k.nb_small = 1;
+  if (k.nb_small == 0 && (t.loss_part || t.loss_acc)) k.nb_small = 1;
   k.nvec = (int64_t)num_items * dim / 4;
   k.vpr_log2 = 0;
   while ((1 << k.vpr_log2) < dim / 4) ++k.vpr_log2;
@@ -1835,7 +1842,7 @@ int gtr_step_tail_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_la
   k.nseg = nseg;
   k.small_total = (int)tot;
   k.nb_small = (int)((tot + GTR_BLOCK - 1) / GTR_BLOCK);
-  if (k.nb_small == 0 && t.loss_part) k.nb_small = 1;
+  if (k.nb_small == 0 && (t.loss_part || t.loss_acc)) k.nb_small = 1;
   const int grid = k.nb_wg + k.nb_rows + k.nb_small;
   hipStream_t s = (hipStream_t)stream;
   switch (D) {

@@ -428,6 +428,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_shard_update(UpdateK a) {
     float l = 0.0f;
     for (int q = 0; q < W; ++q) l += a.small_all[(size_t)q * a.small_words + F];
     a.tl.loss_out[0] = l * inv_w;
+    if (a.tl.loss_acc) a.tl.loss_acc[0] += (double)(l * inv_w);
   }
 }
 

@@ -96,12 +96,12 @@ class GtrTail(C.Structure):
         ("table", P), ("table_m", P), ("table_v", P), ("stamp", P),
         ("flat", P), ("flat_m", P), ("flat_v", P), ("flat_total", i64),
         ("loss_part", P), ("loss_out", P), ("loss_nparts", i32), ("pad0", i32), ("carry", P),
-        ("sweep_from", i64), ("lazy_consts", P), ("rng_inc", P),
+        ("sweep_from", i64), ("lazy_consts", P), ("rng_inc", P), ("loss_acc", P),
     ]
 
 
 SWEEP_SLOTS = 8
-ABI_VERSION = 6  # GTR_ABI_VERSION of include/gtr.h
+ABI_VERSION = 7  # GTR_ABI_VERSION of include/gtr.h
 
 
 class GtrLazy(C.Structure):

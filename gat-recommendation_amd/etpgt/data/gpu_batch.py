@@ -119,7 +119,14 @@ class GpuBatchBuilder:
         if o.ndim != 1 or o.size == 0 or o.min() < 0 or o.max() >= self.store.S:
             raise ValueError("order must list session ids in [0, S)")
         self.order_h = o
-        self.order_d = torch.from_numpy(o.astype(np.int32)).to(self.store.device)
+        new = torch.from_numpy(o.astype(np.int32))
+        prev = getattr(self, "order_d", None)
+        if prev is not None and prev.numel() == new.numel():
+            # in place: a step graph captured with this builder holds the buffer's address
+            # (a fresh tensor would leave the graph reading the previous epoch's freed order)
+            prev.copy_(new)
+        else:
+            self.order_d = new.to(self.store.device)
         self.seek(position)
 
     def seek(self, position: int) -> None:

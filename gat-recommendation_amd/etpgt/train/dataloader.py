@@ -171,15 +171,32 @@ class DeviceSessionLoader:
 
     def __init__(self, dataset: SessionDataset, batch_size: int, num_negatives: int, shuffle: bool = True,
                  device: str = "cuda", seed: int = 0, rank: int = 0, world: int = 1):
-        from etpgt.data.gpu_batch import GpuBatchBuilder, GpuSessionStore
+        from etpgt.data.gpu_batch import GpuSessionStore
+
+        self.dataset = dataset
+        self._setup(GpuSessionStore.from_dataset(dataset, device), len(dataset), batch_size, num_negatives, shuffle,
+                    seed, rank, world)
+
+    @classmethod
+    def from_store(cls, store, batch_size: int, num_negatives: int, shuffle: bool = True, seed: int = 0,
+                   rank: int = 0, world: int = 1) -> "DeviceSessionLoader":
+        """The same loader over a session store already resident on the device
+        (``GpuSessionStore.from_synthetic``: the bench's RetailRocket-shaped sessions)."""
+        self = cls.__new__(cls)
+        self.dataset = None
+        self._setup(store, int(store.S), batch_size, num_negatives, shuffle, seed, rank, world)
+        return self
+
+    def _setup(self, store, num_sessions, batch_size, num_negatives, shuffle, seed, rank, world):
+        from etpgt.data.gpu_batch import GpuBatchBuilder
 
         if not 0 <= rank < world:
             raise ValueError("rank must lie in [0, world)")
-        self.dataset = dataset
+        self.num_sessions = int(num_sessions)
         self.batch_size = int(batch_size)
         self.shuffle = bool(shuffle)
         self.rank, self.world = int(rank), int(world)
-        self.store = GpuSessionStore.from_dataset(dataset, device)
+        self.store = store
         self.builder = GpuBatchBuilder(self.store, self.batch_size, num_negatives, seed=seed,
                                        stride=self.batch_size * self.world)
         self.epoch = -1
@@ -190,19 +207,19 @@ class DeviceSessionLoader:
 
     def batch_sizes(self) -> list[int]:
         """Sessions of this rank's batches in an epoch."""
-        S, B, P = len(self.dataset), self.batch_size, self.world
+        S, B, P = self.num_sessions, self.batch_size, self.world
         full, rem = divmod(S, B * P)
         last = rem // P
         return [B] * full + ([last] if last > 0 else [])
 
     def batch_start(self, i: int) -> int:
         """Cursor position (epoch order, plus epoch * S) of this rank's batch i."""
-        S, B, P = len(self.dataset), self.batch_size, self.world
+        S, B, P = self.num_sessions, self.batch_size, self.world
         b = self.batch_sizes()[i]
         return self.epoch * S + i * B * P + self.rank * b
 
     def _epoch_order(self) -> np.ndarray:
-        n = len(self.dataset)
+        n = self.num_sessions
         torch.empty((), dtype=torch.int64).random_()  # _BaseDataLoaderIter.__init__: _base_seed
         if not self.shuffle:
             return np.arange(n, dtype=np.int64)
@@ -215,7 +232,7 @@ class DeviceSessionLoader:
         """Draw the next epoch's order and put the builder at its start."""
         self.epoch += 1
         self.order = self._epoch_order()
-        self.builder.set_epoch_order(self.order, position=self.epoch * len(self.dataset) + self.rank * self.batch_size)
+        self.builder.set_epoch_order(self.order, position=self.epoch * self.num_sessions + self.rank * self.batch_size)
 
     def __iter__(self):
         self.start_epoch()

@@ -80,6 +80,9 @@ class FusedTrainStep:
         self.adam.lr, self.adam.beta1, self.adam.beta2 = float(lr), float(betas[0]), float(betas[1])
         self.adam.eps, self.adam.weight_decay, self.adam.decoupled = float(eps), float(weight_decay), int(decoupled)
         self.step_dev = torch.zeros(1, dtype=torch.int64, device=self.dev)
+        # device-side running sum of the steps' losses (gtr_tail.loss_acc): the Trainer reads
+        # it once per epoch instead of one loss per step (steps chained in one graph)
+        self.loss_acc = torch.zeros(1, dtype=torch.float64, device=self.dev)
         self.adam.step_dev = self.step_dev.data_ptr()
         self.adam.step_offset = 0  # kernels after gtr_step_begin see the current step
         tab_rows = 1 if self.shard_table else T  # sharded: the moments live in the shards
@@ -98,6 +101,7 @@ class FusedTrainStep:
         self.lazy = bool(lazy) or self.lagged
         self._host_steps = 0
         self._dirty = False
+        self._gen = 0  # bumped whenever a buffer a captured graph points at may have moved
         self.lz = None
         if self.lazy:
             self._lazy_alloc(1 << 16)
@@ -140,6 +144,7 @@ class FusedTrainStep:
             self.sweep.consts = consts.data_ptr()
         self.graph = self.graph_pe = self.graph_b = None  # captured pointers changed
         self.resident_graphs = None
+        self._gen += 1
 
     def flush(self):
         """Bring every table row up to the current step (lazy mode; no-op otherwise)."""
@@ -167,6 +172,7 @@ class FusedTrainStep:
         eng = self.eng
         caps = self._agree(caps)
         self.caps = caps
+        self._gen += 1  # every buffer below is reallocated: multi-step handles go stale
         self.ws = eng.workspace(caps, split=self._force_split, sync=self.sync_bn and self.world > 1)
         from etpgt.data.batch import blob_layout
 
@@ -216,6 +222,7 @@ class FusedTrainStep:
         # with consumer-side reduction the readout leaves its loss partials to the tail
         t.loss_part = ws.loss_part.data_ptr() if self.cfg.consumer_reduce else None
         t.loss_out = ws.loss_out.data_ptr()
+        t.loss_acc = self.loss_acc.data_ptr()
         t.loss_nparts = readout_grid(caps.b_cap)
         # untouched-row AdamW spread over the layer kernels' idle CUs (single GPU, small
         # grids): the chain's 2L launches each sweep a slice of the table (gtr_sweep)
@@ -393,6 +400,7 @@ class FusedTrainStep:
         self.builder = builder
         self.graph = self.graph_pe = self.graph_b = None
         self.resident_graphs = None
+        self._gen += 1
 
     def _planned_caps(self, builder, num_batches: int | None, extra=()) -> Caps:
         """Capacities of the builder's next batches; data parallel: agreed over the ranks
@@ -416,6 +424,7 @@ class FusedTrainStep:
         self.builder = None
         self.graph = self.graph_pe = self.graph_b = None
         self.resident_graphs = None
+        self._gen += 1
 
     # ------------------------------------------------------------------ launches
     def _sync_alloc(self):
@@ -724,6 +733,7 @@ class FusedTrainStep:
                 raise ValueError("resident images must match the step's blob (size, dtype, device)")
         self.resident = [(b, self.eng.batch_struct(self.caps, b, None)) for b in blobs]
         self.resident_graphs = None
+        self._gen += 1
 
     def _with_bs(self, bs, fn):
         saved = self.bs
@@ -797,7 +807,8 @@ class FusedTrainStep:
                 bs = self.resident[(start + k) % nimg][1]
                 self._with_bs(bs, lambda: self._launch(False))
 
-        return {"graph": self._capture(fn), "n": int(n), "lz_cap": self.lz.cap if self.lazy else None}
+        return {"graph": self._capture(fn), "n": int(n), "lz_cap": self.lz.cap if self.lazy else None,
+                "gen": self._gen}
 
     def capture_steps_copied(self, images, start: int, n: int, reserve: int = 0) -> dict | None:
         """``n`` consecutive data-parallel steps, each copying pre-staged image
@@ -806,8 +817,8 @@ class FusedTrainStep:
         where the collectives are captured in the step's graph anyway (RCCL, N > 1 or
         GTR_GRAPH_COLL=1).  Every rank captures, then the ranks agree (all-reduce outside
         any capture): if any rank's capture was refused, every rank returns None and keeps
-        the per-step path.  The row-sharded table's per-step constants are grown first for
-        ``reserve`` more steps (their pointers are captured)."""
+        the per-step path.  The per-step constants (row-sharded table, lazy table) are
+        grown first for ``reserve`` more steps (their pointers are captured)."""
         if not self.use_graph or not self._graph_collectives():
             return None
         if n <= 0:
@@ -817,46 +828,91 @@ class FusedTrainStep:
             if img.numel() != self.blob.numel() or img.dtype != self.blob.dtype or img.device != self.blob.device:
                 raise ValueError("images must match the step's blob (size, dtype, device)")
 
-        if self.shard_state is not None and self.shard_state.ensure_steps(self._host_steps + max(reserve, n) + 2):
-            self.graph = self.graph_pe = self.graph_b = None  # consts moved: the per-step graphs recapture
-            self.resident_graphs = None
-
         def fn():
             for k in range(n):
                 self.blob.copy_(images[(start + k) % nimg], non_blocking=True)
                 self._launch(False)
 
-        g, err = None, None
-        try:
-            g = self._capture(fn)
-        except RuntimeError as e:
-            if "captur" not in str(e).lower():
-                raise
-            err = e
-            torch.cuda.synchronize(self.dev)
-        if self._ranks_agree_refused(err is not None):
+        return self._capture_multi(fn, n, reserve, collective=True)
+
+    def capture_steps_built(self, n: int, reserve: int = 0) -> dict | None:
+        """``n`` consecutive steps over the attached device batch builder's next batches
+        (``attach_builder``: each step's captured build writes the next batch into the
+        blob and advances the device cursor by the global batch) as ONE hipGraph -- the
+        drop-in ``Trainer``'s epoch loop (trainer.py:80-133) runs its full batches in such
+        chunks.  Single GPU, or data parallel with RCCL collectives captured in the step;
+        None where the step cannot be captured whole (gloo: collectives between graph
+        pieces), and then on every rank.  Replay with ``run_steps``; every step is the full
+        step of ``run()``."""
+        if self.builder is None:
+            raise RuntimeError("capture_steps_built needs a device batch builder (attach_builder)")
+        if n <= 0:
+            raise ValueError("capture_steps_built needs n >= 1")
+        multi = self.dp is not None or self.shard is not None
+        if not self.use_graph or (multi and not self._graph_collectives()):
             return None
+
+        def fn():
+            for _ in range(n):
+                self._launch(False)
+
+        return self._capture_multi(fn, n, reserve, collective=multi)
+
+    def _capture_multi(self, fn, n: int, reserve: int, collective: bool) -> dict | None:
+        """Capture ``fn`` (n steps) as one graph after growing the per-step constants for
+        ``reserve`` more steps; with collectives, every rank agrees on refusal."""
+        need = self._host_steps + max(reserve, n) + 2
+        if self.lazy and need >= self.lz.cap:
+            cap = self.lz.cap
+            while need >= cap:
+                cap *= 2
+            self._lazy_alloc(cap)
+        if self.shard_state is not None and self.shard_state.ensure_steps(need):
+            self.graph = self.graph_pe = self.graph_b = None  # consts moved: the per-step graphs recapture
+            self.resident_graphs = None
+            self._gen += 1
+        g, err = None, None
+        if not collective:
+            g = self._capture(fn)
+        else:
+            try:
+                g = self._capture(fn)
+            except RuntimeError as e:
+                if "captur" not in str(e).lower():
+                    raise
+                err = e
+                torch.cuda.synchronize(self.dev)
+            if self._ranks_agree_refused(err is not None):
+                return None
         return {"graph": g, "n": int(n), "lz_cap": self.lz.cap if self.lazy else None,
-                "consts": self.shard_state.consts.data_ptr() if self.shard_state is not None else None}
+                "consts": self.shard_state.consts.data_ptr() if self.shard_state is not None else None,
+                "gen": self._gen}
 
     def run_steps(self, h: dict):
-        """Replay a ``capture_steps`` graph: ``h["n"]`` training steps in one launch."""
+        """Replay a ``capture_steps`` / ``capture_steps_copied`` graph: ``h["n"]`` training
+        steps in one launch.  Every check runs before any state changes: a handle whose
+        captured buffers were rebound since (``_gen``), or whose per-step constants would
+        have to grow, raises and leaves the step untouched."""
         self.eng.check_intact()
         if not self.model.training:
             raise RuntimeError("FusedTrainStep requires model.train()")
         n = h["n"]
+        if h.get("gen") != self._gen:
+            raise RuntimeError("the step's buffers were rebound since this multi-step graph was captured: "
+                               "capture the steps again")
         if self.shard_state is not None:
-            self._host_steps += n
-            if self.shard_state.ensure_steps(self._host_steps) or h.get("consts") != self.shard_state.consts.data_ptr():
+            ss = self.shard_state
+            if h.get("consts") != ss.consts.data_ptr() or self._host_steps + n + 2 >= ss.consts.shape[0]:
                 raise RuntimeError("the row-sharded table's step constants were (or would have to be) reallocated: "
                                    "capture the steps again")
-            self.shard_state.check_status()
+        if self.lazy and (h["lz_cap"] != self.lz.cap or self._host_steps + n + 2 >= self.lz.cap):
+            raise RuntimeError("the lazy table's step constants were (or would have to be) reallocated: "
+                               "capture the steps again")
+        self._host_steps += n
         if self.lazy:
-            if h["lz_cap"] != self.lz.cap or self._host_steps + n + 2 >= self.lz.cap:
-                raise RuntimeError("the lazy table's step constants were (or would have to be) reallocated: "
-                                   "capture the steps again")
-            self._host_steps += n
             self._dirty = True
+        if self.shard_state is not None:
+            self.shard_state.check_status(steps=n)
         h["graph"].replay()
         return self.ws.loss_out[0]
 
@@ -928,7 +984,8 @@ class FusedTrainStep:
             if self.shard_state.ensure_steps(self._host_steps):
                 self.graph = self.graph_pe = self.graph_b = None  # consts moved: recapture
                 self.resident_graphs = None
-            self.shard_state.check_status()
+                self._gen += 1
+            self.shard_state.check_status(steps=1)
         if self.lazy:
             if self._host_steps + 2 >= self.lz.cap:
                 self._lazy_alloc(2 * self.lz.cap)

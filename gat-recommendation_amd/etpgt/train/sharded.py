@@ -101,20 +101,29 @@ class ShardState:
         """Grow the per-step scalar table before step ``steps``; True if pointers moved."""
         if steps + 2 < self.consts.shape[0]:
             return False
-        self._alloc_consts(2 * self.consts.shape[0])
+        cap = 2 * self.consts.shape[0]
+        while steps + 2 >= cap:
+            cap *= 2
+        self._alloc_consts(cap)
         return True
 
-    def check_status(self, block: bool = False):
-        """Raise if any step since the last check overflowed an exchange block.  Every rank
-        checks at the same host steps -- every GTR_SHARD_CHECK_EVERY-th call (64) and at
-        ``block=True`` (sync_table / export) -- after its queue has drained.  The overflow
-        flag reaches every rank inside the flagged step (k_shard_update folds the ranks'
-        flags into the sticky status[1]), so all ranks raise together, at the same step,
-        instead of one rank leaving the others blocked in the next collective.
-        A flagged step trains as a zero-gradient step on the rows it could not fetch."""
-        self._checks += 1
-        if not block and self._checks % self._check_every:
+    def check_status(self, block: bool = False, steps: int = 1):
+        """Raise if any step since the last check overflowed an exchange block.  Called
+        before every launch with the number of steps that launch runs (1, or n for a
+        multi-step graph); every rank counts the same steps, so every rank checks at the
+        same host step -- once GTR_SHARD_CHECK_EVERY (64) steps have been launched since the
+        last check, and at ``block=True`` (sync_table / export) -- after its queue has
+        drained.  A check drains the queue up to the steps launched BEFORE it, so an
+        overflow is raised at most check_every + n steps after the flagged step (n: the
+        steps per launch).  The overflow flag reaches every rank inside the flagged step
+        (k_shard_update folds the ranks' flags into the sticky status[1]), so all ranks
+        raise together instead of one rank leaving the others blocked in the next
+        collective.  A flagged step trains as a zero-gradient step on the rows it could
+        not fetch."""
+        self._checks += int(steps)
+        if not block and self._checks < self._check_every:
             return
+        self._checks = 0
         torch.cuda.current_stream(self.step.dev).synchronize()
         if int(self.status[1].item()) != 0:
             raise RuntimeError("row-sharded table: a batch requested more rows from one owner than the "

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import json
 import logging
+import os
 from pathlib import Path
 
 import torch
@@ -70,6 +71,9 @@ class Trainer:
         self.history = {"train_loss": [], "val_metrics": []}
         self._fused_flag = fused
         self._fused = None
+        # device-built epochs: full batches per multi-step hipGraph (1: one graph per batch)
+        self.steps_per_graph = max(1, int(os.environ.get("GTR_TRAINER_STEPS_PER_GRAPH", "32")))
+        self._chunk_graph = None
 
     # ------------------------------------------------------------------ fused path
     def _fused_step(self):
@@ -110,8 +114,14 @@ class Trainer:
     # ------------------------------------------------------------------ loops
     def _train_epoch_device_batches(self, fused) -> float:
         """One epoch of a ``DeviceSessionLoader`` through the fused step: the batch build
-        runs inside the captured step (no host work per batch); the partial last batch is
-        launched eagerly."""
+        runs inside the captured step (no host work per batch).  The full batches run in
+        chunks of ``steps_per_graph`` consecutive steps captured as ONE hipGraph
+        (``FusedTrainStep.capture_steps_built``: each step's build advances the device
+        cursor), so the queue runs batch after batch without a host round trip between
+        them; the batches that do not fill a chunk launch one step graph each, and the
+        partial last batch is launched eagerly.  The epoch's loss is the tail's device-side
+        running sum (``gtr_tail.loss_acc``), read once: the mean over batches of the
+        per-batch losses, as trainer.py:130-133 computes it."""
         loader = self.train_loader
         loader.start_epoch()
         sizes = loader.batch_sizes()
@@ -124,16 +134,31 @@ class Trainer:
             fused.attach_builder(bld, num_batches=max(full, 1), extra=extra)
         else:  # capacities for this epoch's order (rebinds only if they grew; agreed over ranks)
             fused.refresh_builder_caps(max(full, 1), extra=extra)
-        total = torch.zeros((), dtype=torch.float64, device=self.device)
-        for i, b in enumerate(sizes):
-            if b == loader.batch_size:
-                loss = fused.run()  # the captured build advances the cursor by the global batch
-            else:
-                bld.seek(loader.batch_start(i))  # last, partial batch: this rank's even share
-                loss = fused.run_partial(b)
-            total += loss
+        fused.loss_acc.zero_()
+        K = self.steps_per_graph
+        i = 0
+        if full > 0:
+            fused.run()  # first full batch: eager warm-up + per-step capture on a fresh binding
+            i = 1
+        while K > 1 and full - i >= K:
+            h = self._chunk_graph
+            if h is None or h["n"] != K or h.get("gen") != fused._gen or h.get("step") is not fused:
+                # captured once per binding; every rank reaches this point together
+                h = fused.capture_steps_built(K, reserve=full)
+                if h is None:
+                    break  # not capturable whole (gloo): one step graph per batch
+                h["step"] = fused
+                self._chunk_graph = h
+            fused.run_steps(h)
+            i += K
+        for _ in range(i, full):
+            fused.run()  # the captured build advances the cursor by the global batch
+        for j, b in enumerate(sizes):
+            if b != loader.batch_size:  # last, partial batch: this rank's even share
+                bld.seek(loader.batch_start(j))
+                fused.run_partial(b)
         bld.check_status(fused.group)  # collective under a process group: every rank raises together
-        return float(total.item()) / max(len(sizes), 1)
+        return float(fused.loss_acc.item()) / max(len(sizes), 1)
 
     def train_epoch(self) -> float:
         self.model.train()

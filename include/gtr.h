@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GTR_ABI_VERSION 6 /* 6: gtr_layer.ffn + gtr_ffn_fwd / gtr_ffn_bwd / gtr_ffn_wgrad (the FFN variant); 5: gtr_config.loss_batch / wfold_stride, gtr_layer.wfold, gtr_segment.live_groups, hdr[6] halo source rows; 4: gtr_step_tail_wgrad on split-K slabs; 3: gtr_config.begin / ctr_add, gtr_tail.rng_inc */
+#define GTR_ABI_VERSION 7 /* 7: gtr_tail.loss_acc; 6: gtr_layer.ffn + gtr_ffn_fwd / gtr_ffn_bwd / gtr_ffn_wgrad (the FFN variant); 5: gtr_config.loss_batch / wfold_stride, gtr_layer.wfold, gtr_segment.live_groups, hdr[6] halo source rows; 4: gtr_step_tail_wgrad on split-K slabs; 3: gtr_config.begin / ctr_add, gtr_tail.rng_inc */
 
 #define GTR_OK 0
 #define GTR_E_ARG 1001      /* bad argument / unsupported shape */
@@ -477,6 +477,9 @@ typedef struct gtr_tail {
   const float* lazy_consts; /* lazy mode (gtr_lazy.consts): no untouched-row sweep; touched rows
                                are stamped with the step; the dp tail catches rows up first */
   uint32_t* rng_inc;        /* optional: += 1 at the end of the tail (fused begin, gtr_begin) */
+  double* loss_acc;         /* optional: += the step's loss (one thread, after loss_out is final):
+                               a device-side running sum over the steps of an epoch, so steps
+                               chained in one hipGraph need no per-step loss read (trainer.py:130) */
 } gtr_tail;
 
 /* Floats of gtr_tail.carry needed at contribution capacity m_cap (0: not used).      */

@@ -3,7 +3,7 @@
 # usage: envab.sh "VAR=value[,VAR=value] ..." [bench args...]   (first variant = baseline)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
-LEAN="--cpu-seconds 0 --gather-batch 0 --recall-steps 0 --e2e-steps 0 --tail-probe 0 --strong-batches 0 --c1-reps 0"
+LEAN="--cpu-seconds 0 --gather-batch 0 --recall-steps 0 --e2e-steps 0 --trainer-epochs 0 --tail-probe 0 --strong-batches 0 --c1-reps 0"
 VARS=$1; shift
 EXTRA=${*:---config c2}
 for r in 1 2 3; do

@@ -10,7 +10,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 CFG=$1; TAG=$2; shift 2
 EXTRA="$*"
-LEAN="--config $CFG --cpu-seconds 0 --gather-batch 0 --recall-steps 0 --e2e-steps 0 --tail-probe 0 --strong-batches 0 $EXTRA"
+LEAN="--config $CFG --cpu-seconds 0 --gather-batch 0 --recall-steps 0 --e2e-steps 0 --trainer-epochs 0 --tail-probe 0 --strong-batches 0 $EXTRA"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- \
   python3 bench.py $LEAN --steps 200 --warmup 20 > gpurun_out/${TAG}_prof_bench.json 2> gpurun_out/${TAG}_prof.err \
   || { tail -20 gpurun_out/${TAG}_prof.err; exit 1; }

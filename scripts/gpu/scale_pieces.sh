@@ -6,7 +6,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-LEAN="--cpu-seconds 0 --gather-batch 0 --recall-steps 0 --e2e-steps 0 --c1-reps 0 --tail-probe 0 --strong-batches 0"
+LEAN="--cpu-seconds 0 --gather-batch 0 --recall-steps 0 --e2e-steps 0 --trainer-epochs 0 --c1-reps 0 --tail-probe 0 --strong-batches 0"
 run() { local tag=$1; shift; timeout -k 10 400 "$@" > gpurun_out/sp_$tag.json 2> gpurun_out/sp_$tag.err || { tail -20 gpurun_out/sp_$tag.err; exit 1; }
   python3 -c "import json;d=json.load(open('gpurun_out/sp_$tag.json'));print('$tag', d['value'], d['ms_per_step'], d['config']['parallelism'], d['config'].get('dp_exchange'))"; }
 run c5s_8192 python3 bench.py --config c5s --steps 30 --warmup 5 $LEAN

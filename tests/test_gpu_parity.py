@@ -475,6 +475,14 @@ def test_multi_step_graph_equals_per_step_graphs(lazy):
         f2._lazy_alloc(2 * f2.lz.cap)
         with pytest.raises(RuntimeError, match="capture the steps again"):
             f2.run_steps(h)
+    # any rebind (here: the resident images) makes the handle stale; the refused
+    # replay changes no host state
+    h = f2.capture_steps(0, 2)
+    steps_before = f2._host_steps
+    f2.bind_resident(st2)
+    with pytest.raises(RuntimeError, match="capture the steps again"):
+        f2.run_steps(h)
+    assert f2._host_steps == steps_before
 
 
 @pytest.mark.parametrize("gemm,D,H,K,loss", [("split", 64, 1, 0, "model_bpr"), ("split", 128, 4, 16, "listwise"),

@@ -410,7 +410,7 @@ def test_device_loader_epoch_order_matches_torch_dataloader():
 
     def dev_loader(shuffle):
         dl = DeviceSessionLoader.__new__(DeviceSessionLoader)  # order logic only (no GPU store)
-        dl.dataset, dl.shuffle = ds, shuffle
+        dl.dataset, dl.shuffle, dl.num_sessions = ds, shuffle, len(ds)
         return dl
 
     torch.manual_seed(42)
