@@ -826,6 +826,45 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_attn_fwd(ConvFwdK a) {
 #define GTR_AR_WAVES_EU 6
 #endif
 
+// The BatchNorm partial (count, mean, M2) of a workgroup's nrow output rows (s_out:
+// [AR_ROWS][D] in LDS), written through into bn_part row g for the last arrivers.
+template <int D>
+__device__ __forceinline__ void bn_rows_partial(const ConvFwdK& a, int g, int nrow, const float* s_out, float* s_red) {
+  const int tid = threadIdx.x;
+  constexpr int NS = AR_BLOCK / D >= 1 ? AR_BLOCK / D : 1;
+  float* part = a.bn_part + (size_t)g * (1 + 2 * D);
+  {
+    const int j = tid % D, sl = tid / D;
+    float sum = 0.0f;
+    if (sl < NS)
+      for (int i = sl; i < nrow; i += NS) sum += s_out[i * D + j];
+    s_red[sl * D + j] = sum;
+    __syncthreads();
+    if (tid < D) {
+      float tot = 0.0f;
+      for (int q2 = 0; q2 < NS; ++q2) tot += s_red[q2 * D + tid];
+      const float mean = tot / (float)nrow;
+      s_red[NS * D + tid] = mean;
+      st_wt(part + 1 + tid, mean);  // write-through: read by another workgroup in this launch
+    }
+    __syncthreads();
+    float m2 = 0.0f;
+    if (sl < NS) {
+      const float mean = s_red[NS * D + j];
+      for (int i = sl; i < nrow; i += NS) { const float d = s_out[i * D + j] - mean; m2 += d * d; }
+    }
+    __syncthreads();
+    s_red[sl * D + j] = m2;
+    __syncthreads();
+    if (tid < D) {
+      float tot = 0.0f;
+      for (int q2 = 0; q2 < NS; ++q2) tot += s_red[q2 * D + tid];
+      st_wt(part + 1 + D + tid, tot);
+    }
+    if (tid == 0) st_wt(part, (float)nrow);
+  }
+}
+
 template <int D>
 __global__ __launch_bounds__(AR_BLOCK) __attribute__((amdgpu_waves_per_eu(GTR_AR_WAVES_EU, 8))) void k_attn_rows(ConvFwdK a) {
   constexpr int VPL = D >= 64 ? D / 64 : 1;
@@ -1064,38 +1103,219 @@ __global__ __launch_bounds__(AR_BLOCK) __attribute__((amdgpu_waves_per_eu(GTR_AR
   // ---- this workgroup's BatchNorm partial (count, mean, M2) over its rows
   __syncthreads();
   GTR_PH(20 + a.layer, 1);
-  constexpr int NS = AR_BLOCK / D >= 1 ? AR_BLOCK / D : 1;
-  float* part = a.bn_part + (size_t)g * (1 + 2 * D);
-  {
-    const int j = tid % D, sl = tid / D;
-    float sum = 0.0f;
-    if (sl < NS)
-      for (int i = sl; i < nrow; i += NS) sum += s_out[i][j];
-    s_red[sl * D + j] = sum;
-    __syncthreads();
-    if (tid < D) {
-      float tot = 0.0f;
-      for (int q2 = 0; q2 < NS; ++q2) tot += s_red[q2 * D + tid];
-      const float mean = tot / (float)nrow;
-      s_red[NS * D + tid] = mean;
-      st_wt(part + 1 + tid, mean);  // write-through: read by another workgroup in this launch
-    }
-    __syncthreads();
-    float m2 = 0.0f;
-    if (sl < NS) {
-      const float mean = s_red[NS * D + j];
-      for (int i = sl; i < nrow; i += NS) { const float d = s_out[i][j] - mean; m2 += d * d; }
-    }
-    __syncthreads();
-    s_red[sl * D + j] = m2;
-    __syncthreads();
-    if (tid < D) {
-      float tot = 0.0f;
-      for (int q2 = 0; q2 < NS; ++q2) tot += s_red[q2 * D + tid];
-      st_wt(part + 1 + D + tid, tot);
-    }
-    if (tid == 0) st_wt(part, (float)nrow);
+  bn_rows_partial<D>(a, g, nrow, &s_out[0][0], s_red);
+  GTR_PH(20 + a.layer, 2);
+  bn_fwd_finalize<D, AR_BLOCK>(a, g, Gn, &s_flag, s_red, s_bn, s_uv);
+  GTR_PH(20 + a.layer, 3);
+}
+
+// Split path, row-parallel attention with float4 lanes and an online softmax (round 5;
+// gtr_attn_fwd for D <= 128, H <= AR_HMAX).  A destination row of D floats is LPR = D/4
+// lanes holding one float4 each, so one wave instruction gathers RPI = 64/LPR source
+// rows (D = 128: two) -- twice the bytes per instruction of k_attn_rows' VPL = D/64.
+// A wave owns two consecutive rows (their in-edges are contiguous: one id load), and its
+// RPI sub-groups of LPR lanes walk the pair's edges in rounds of U edges per sub-group:
+// every edge's K AND V rows are requested in the same round, the next round's rows are
+// requested before this round's arithmetic (the rounds of a hub row overlap), and each
+// lane folds its edges into a running (max, sum, weighted-V) per row and head (online
+// softmax, no second gather pass).  The sub-groups' states are then combined with xor
+// butterflies; alpha = exp(l - m) / (sum + 1e-16) is written in a lane-parallel pass
+// over the (edge, head) pairs from the logits kept in LDS (a pair of more than AR_ECH
+// edges: in the alpha buffer itself, rewritten in place).  PyG TransformerConv
+// (SURVEY.md Appendix A): softmax over in-edges, dropout on alpha, sum alpha*V,
+// beta gate.  The weighted sum is (sum_e exp(l_e - m) mask_e V_e) / (sum + 1e-16) with
+// the running rescale: the reference's value up to fp32 reordering (oracle tests, 1e-3).
+#ifndef AR4_U
+#define AR4_U 4
+#endif
+#ifndef GTR_AR4_WAVES_EU
+#define GTR_AR4_WAVES_EU 6
+#endif
+
+template <int O>
+__device__ __forceinline__ float xor_add(float x) {
+  if constexpr (O >= 16) return bfly_add<O>(x);
+  else return x + __shfl_xor(x, O);
+}
+template <int O>
+__device__ __forceinline__ float xor_max(float x) {
+  if constexpr (O >= 16) return bfly_max<O>(x);
+  else return fmaxf(x, __shfl_xor(x, O));
+}
+
+struct OnlineSm {
+  float m, z;
+  float4 acc;
+};
+
+// fold one edge (logit l, dropout multiplier mk, V row v) into a running state
+__device__ __forceinline__ void sm_push(OnlineSm& s, float l, float mk, const float4& v) {
+  const float mn = fmaxf(s.m, l);
+  const float sc = s.m == -INFINITY ? 0.0f : expf(s.m - mn);
+  const float p = expf(l - mn);
+  s.z = s.z * sc + p;
+  const float w = p * mk;
+  s.acc.x = s.acc.x * sc + w * v.x;
+  s.acc.y = s.acc.y * sc + w * v.y;
+  s.acc.z = s.acc.z * sc + w * v.z;
+  s.acc.w = s.acc.w * sc + w * v.w;
+  s.m = mn;
+}
+
+// combine the states of lanes l and l ^ O (both lanes end with the same state)
+template <int O>
+__device__ __forceinline__ void sm_combine(OnlineSm& s) {
+  const float mn = xor_max<O>(s.m);
+  const float f = s.m == -INFINITY ? 0.0f : expf(s.m - mn);
+  s.z = xor_add<O>(s.z * f);
+  s.acc.x = xor_add<O>(s.acc.x * f);
+  s.acc.y = xor_add<O>(s.acc.y * f);
+  s.acc.z = xor_add<O>(s.acc.z * f);
+  s.acc.w = xor_add<O>(s.acc.w * f);
+  s.m = mn;
+}
+
+// combine over the xor offsets O, 2 O, ... below END (the lanes of one row's sub-groups)
+template <int O, int END>
+__device__ __forceinline__ void sm_combine_upto(OnlineSm& s) {
+  if constexpr (O < END) {
+    sm_combine<O>(s);
+    sm_combine_upto<O * 2, END>(s);
   }
+}
+
+template <int D>
+__global__ __launch_bounds__(AR_BLOCK) __attribute__((amdgpu_waves_per_eu(GTR_AR4_WAVES_EU, 8))) void k_attn_rows4(ConvFwdK a) {
+  constexpr int LPR = D / 4, RPI = 64 / LPR, U = AR4_U;
+  constexpr int SPR = RPI / 2;   // sub-groups per row of the pair
+  constexpr int EPR = U * SPR;   // edges of a row per round
+  static_assert(RPI >= 2, "a sub-group per row of the pair");
+  __shared__ __attribute__((aligned(16))) float s_out[AR_ROWS][D];
+  __shared__ float s_lg[AR_WAVES][AR_ECH][AR_HMAX];
+  __shared__ float s_mz[AR_WAVES][2][AR_HMAX][2];
+  __shared__ float s_red[2 * AR_BLOCK + D];
+  __shared__ float s_bn[2 * D];
+  __shared__ float s_uv[D];
+  __shared__ int s_flag;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int N = a.bt.hdr[0];
+  const int Gn = (N + AR_ROWS - 1) / AR_ROWS;
+  const int g = blockIdx.x;
+  if (g >= Gn) return;  // block-uniform: only live workgroups write partials and arrive
+  const int r0 = g * AR_ROWS, nrow = min(AR_ROWS, N - r0);
+  GTR_PH(20 + a.layer, 0);
+  const uint32_t ctr = a.rng_ctr ? load_step_ctr(a.rng_ctr) + a.ctr_add : 0u;
+  const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
+  const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
+  const int sub = lane / LPR, c4 = lane - sub * LPR, col = 4 * c4;
+  const int rr = sub / SPR, si = sub - rr * SPR;  // this lane's row of the pair, its slot in the row
+  const int C = a.C, H = a.H;
+  const int HL = C >= 4 ? C / 4 : 1;  // lanes of one head inside a sub-group
+  const int head = col / C;
+  const bool leader = (c4 & (HL - 1)) == 0;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int t0 = r0 + wave * AR_RPW;
+  if (t0 < N) {  // wave-uniform
+    const bool two = t0 + 1 < N;
+    const int e0 = a.bt.in_ptr[t0], em = a.bt.in_ptr[t0 + 1];
+    const int e2 = two ? a.bt.in_ptr[t0 + 2] : em;
+    const int ne0 = em - e0, ne = e2 - e0;
+    const bool mine = rr == 0 || two;          // this lane's row exists
+    const int eb = rr == 0 ? 0 : ne0;          // the row's first edge (pair-local)
+    const int nr = rr == 0 ? ne0 : ne - ne0;   // the row's in-edges
+    const int nmax = max(ne0, ne - ne0);
+    GTR_PH(20 + a.layer, 8);
+    const float* qrow = a.qkvs + (size_t)(t0 + rr) * (4 * D) + col;
+    const float4 q = mine ? *reinterpret_cast<const float4*>(qrow) : z4;
+    const float4 sv = mine ? *reinterpret_cast<const float4*>(qrow + 3 * D) : z4;
+    const bool lds_lg = ne <= AR_ECH;
+    const float* K = a.qkvs + D + col;
+    const float* V = a.qkvs + 2 * D + col;
+    OnlineSm st{-INFINITY, 0.0f, z4};
+    // the pair's source ids, one per lane (pairs of more than 64 in-edges: per round)
+    const bool one_chunk = ne <= 64;
+    const int my_src = lane < ne ? a.bt.in_src[e0 + lane] : 0;
+    for (int j = 0; j < nmax; j += EPR) {
+      int ids = my_src, ib = eb;
+      if (!one_chunk) {  // hub pair: this round's ids -- row 0's edges j.. in lanes 0-31, row 1's in 32-63
+        const int k = j + (lane & 31);
+        const bool okid = lane < 32 ? k < ne0 : ne0 + k < ne;
+        ids = okid ? a.bt.in_src[e0 + (lane < 32 ? k : ne0 + k)] : 0;
+        ib = rr * 32 - j;
+      }
+      float4 kc[U], vc[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = j + u * SPR + si;  // edge k of this lane's row
+        const int src = __shfl(ids, (ib + k) & 63);
+        const size_t off = (mine && k < nr) ? (size_t)src * (4 * D) : 0;  // row 0 of the buffer: in bounds
+        kc[u] = *reinterpret_cast<const float4*>(K + off);
+        vc[u] = *reinterpret_cast<const float4*>(V + off);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = j + u * SPR + si;
+        float dt = q.x * kc[u].x + q.y * kc[u].y + q.z * kc[u].z + q.w * kc[u].w;
+        const float l = group_sum(dt, HL) / a.sqrt_c;
+        if (mine && k < nr) {
+          const int e = eb + k;
+          const int eg = e0 + e;
+          if (leader) {
+            if (lds_lg) s_lg[wave][e][head] = l;
+            else a.alpha[(size_t)eg * H + head] = l;
+          }
+          sm_push(st, l, dr.mul(st_attn, (uint32_t)(eg * H + head)), vc[u]);
+        }
+      }
+    }
+    GTR_PH(20 + a.layer, 9);
+    sm_combine_upto<LPR, LPR * SPR>(st);  // the row's SPR sub-groups
+    const float zd = st.z + 1e-16f;
+    if (si == 0 && leader) {
+      s_mz[wave][rr][head][0] = st.m;
+      s_mz[wave][rr][head][1] = zd;
+    }
+    if (!lds_lg) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // raw logits in alpha
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    GTR_PH(20 + a.layer, 10);
+    const float4 w1 = *reinterpret_cast<const float4*>(a.w_beta + col);  // the gate's weights, late: registers
+    const float4 w2 = *reinterpret_cast<const float4*>(a.w_beta + D + col);
+    const float4 w3 = *reinterpret_cast<const float4*>(a.w_beta + 2 * D + col);
+    // alpha of every (edge, head) pair of the row pair, lane-parallel (contiguous stores)
+    for (int idx = lane; idx < ne * H; idx += 64) {
+      const int e = idx / H, h = idx - e * H;
+      const int r = e >= ne0 ? 1 : 0;
+      const size_t at = (size_t)(e0 + e) * H + h;
+      const float l = lds_lg ? s_lg[wave][e][h] : a.alpha[at];
+      a.alpha[at] = expf(l - s_mz[wave][r][h][0]) / s_mz[wave][r][h][1];
+    }
+    GTR_PH(20 + a.layer, 11);
+    // aggregate, beta gate, outputs (slot 0 of each row's sub-groups stores the row)
+    const float4 ag = make_float4(st.acc.x / zd, st.acc.y / zd, st.acc.z / zd, st.acc.w / zd);
+    float uu = w1.x * ag.x + w2.x * sv.x + w3.x * (ag.x - sv.x);
+    uu += w1.y * ag.y + w2.y * sv.y + w3.y * (ag.y - sv.y);
+    uu += w1.z * ag.z + w2.z * sv.z + w3.z * (ag.z - sv.z);
+    uu += w1.w * ag.w + w2.w * sv.w + w3.w * (ag.w - sv.w);
+    uu = group_sum_c<LPR>(uu);
+    const float beta = 1.0f / (1.0f + expf(-uu));
+    const float4 o = make_float4(beta * sv.x + (1.0f - beta) * ag.x, beta * sv.y + (1.0f - beta) * ag.y,
+                                 beta * sv.z + (1.0f - beta) * ag.z, beta * sv.w + (1.0f - beta) * ag.w);
+    if (si == 0 && mine) {
+      const int t = t0 + rr;
+      *reinterpret_cast<float4*>(a.agg + (size_t)t * D + col) = ag;
+      *reinterpret_cast<float4*>(a.out + (size_t)t * D + col) = o;
+      *reinterpret_cast<float4*>(&s_out[wave * AR_RPW + rr][col]) = o;
+      if (c4 == 0) a.gate[t] = beta;
+    }
+    GTR_PH(20 + a.layer, 12);
+    GTR_PH(20 + a.layer, 13);
+  }
+  if (!a.train) return;
+  __syncthreads();
+  GTR_PH(20 + a.layer, 1);
+  bn_rows_partial<D>(a, g, nrow, &s_out[0][0], s_red);
   GTR_PH(20 + a.layer, 2);
   bn_fwd_finalize<D, AR_BLOCK>(a, g, Gn, &s_flag, s_red, s_bn, s_uv);
   GTR_PH(20 + a.layer, 3);
@@ -2100,10 +2320,16 @@ extern "C" int gtr_attn_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     // max(n_cap / row_group, n_cap / 8) rows, gtr.h)
     static_assert(AR_ROWS == 8, "gtr.h sizes bn_part for 8-row partials");
     const int grid = (bt->n_cap + AR_ROWS - 1) / AR_ROWS;
-    switch (cfg->dim) {
-      case 32: hipLaunchKernelGGL(k_attn_rows<32>, dim3(grid), dim3(AR_BLOCK), 0, s, k); break;
-      case 64: hipLaunchKernelGGL(k_attn_rows<64>, dim3(grid), dim3(AR_BLOCK), 0, s, k); break;
-      default: hipLaunchKernelGGL(k_attn_rows<128>, dim3(grid), dim3(AR_BLOCK), 0, s, k); break;
+    // float4 lanes + online softmax (k_attn_rows4) unless GTR_ATTN=rows (the round-4 body,
+    // also the path for more than AR_HMAX heads)
+    const bool v4 = cfg->heads <= AR_HMAX && !(am && am[0] == 'r');
+    switch (cfg->dim * 2 + (v4 ? 1 : 0)) {
+      case 64: hipLaunchKernelGGL(k_attn_rows<32>, dim3(grid), dim3(AR_BLOCK), 0, s, k); break;
+      case 65: hipLaunchKernelGGL(k_attn_rows4<32>, dim3(grid), dim3(AR_BLOCK), 0, s, k); break;
+      case 128: hipLaunchKernelGGL(k_attn_rows<64>, dim3(grid), dim3(AR_BLOCK), 0, s, k); break;
+      case 129: hipLaunchKernelGGL(k_attn_rows4<64>, dim3(grid), dim3(AR_BLOCK), 0, s, k); break;
+      case 256: hipLaunchKernelGGL(k_attn_rows<128>, dim3(grid), dim3(AR_BLOCK), 0, s, k); break;
+      default: hipLaunchKernelGGL(k_attn_rows4<128>, dim3(grid), dim3(AR_BLOCK), 0, s, k); break;
     }
     GTR_HIP_CHECK_LAUNCH();
     return GTR_OK;

@@ -105,7 +105,11 @@ def test_train_grads(D, H, K, loss):
             assert_close(dict(m.named_buffers())[name], b, name=name)
 
 
-def test_edge_cases_train():
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_edge_cases_train(split, monkeypatch):
+    """split "1": the same edge cases on the split layer path (row-parallel attention
+    kernels: rows without in-edges, single-node sessions, dense sessions)."""
+    monkeypatch.setenv("GTR_SPLIT", split)
     T = data().table_rows
     m, ref = make_pair(T, 64, 2, K=0, seed=3)
     m.train(); ref.train()
@@ -125,10 +129,14 @@ def test_edge_cases_train():
         assert_close(hp[name].grad, p.grad, rtol=2e-3, name=f"grad {name}", floor=1e-6 * gscale)
 
 
+@pytest.mark.parametrize("split", ["0", "1"])
 @pytest.mark.parametrize("D,H", [(64, 2), (128, 4)])
-def test_long_sessions_general_path_train(D, H):
+def test_long_sessions_general_path_train(D, H, split, monkeypatch):
     """Row groups beyond the LDS carve (70-row session, 1600-edge session) run the
-    general global-memory path next to fast-path groups of the same batch."""
+    general global-memory path next to fast-path groups of the same batch; split "1":
+    the row-parallel attention kernels' hub pairs (more than 64 in-edges per row pair,
+    ids per round, logits parked in the alpha buffer)."""
+    monkeypatch.setenv("GTR_SPLIT", split)
     T = data().table_rows
     m, ref = make_pair(T, D, H, K=0, seed=4)
     m.train(); ref.train()
