@@ -338,6 +338,236 @@ __global__ __launch_bounds__(BR_BLOCK) void k_attn_rows_bwd_dst(ConvBwdK a) {
   if (two) store_vec<VPL>(a.dqkvs + (size_t)(t0 + 1) * (4 * D) + d0, dq1, act);
 }
 
+// Destination-row backward with float4 lanes (round 5; the layout of k_attn_rows4): a
+// wave owns two consecutive rows, each row's SPR sub-groups of LPR = D/4 lanes walk its
+// in-edges U at a time with the edge's V row, K row and alpha requested in the same round.
+// Per row: BatchNorm backward and the beta-gate backward (-> dS, dA, du); per edge
+// da = <dA, V> * mask and the row's sdot = sum alpha * da; dlogit = alpha (da - sdot)
+// (written for the source-row launch) and dQ = sum dlogit / sqrt(C) * K.  A row of at most
+// U * SPR in-edges keeps its K rows in registers (one gather round); longer rows take a
+// second round of K loads.  Same arithmetic as k_attn_rows_bwd_dst up to fp32 reordering.
+#ifndef BR4_U
+#define BR4_U 4
+#endif
+
+template <int O>
+__device__ __forceinline__ float xor_add_b(float x) {
+  if constexpr (O >= 16) return bfly_add<O>(x);
+  else return x + __shfl_xor(x, O);
+}
+template <int O, int END>
+__device__ __forceinline__ float xor_sum_upto(float x) {
+  if constexpr (O < END) return xor_sum_upto<O * 2, END>(xor_add_b<O>(x));
+  else return x;
+}
+
+template <int D>
+__global__ __launch_bounds__(BR_BLOCK) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_attn_rows_bwd_dst4(ConvBwdK a) {
+  constexpr int LPR = D / 4, RPI = 64 / LPR, U = BR4_U;
+  constexpr int SPR = RPI / 2, EPR = U * SPR;
+  static_assert(RPI >= 2, "a sub-group per row of the pair");
+  __shared__ float s_gs[2 * D];
+  __shared__ float s_da[BR_WAVES][BR_ECH][BR_HMAX];
+  __shared__ float s_sd[BR_WAVES][2][BR_HMAX];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // BatchNorm constants of this lane's four columns (bwd_row_consts at float4 width)
+  int Nstat = a.bt.hdr[0];
+  const float* gs = a.gsum;
+  if (a.sync) {
+    float n = 0.0f;
+    for (int q = 0; q < a.nparts_fwd; ++q) n += a.part_all[(size_t)q * (1 + 2 * D)];
+    Nstat = (int)(n + 0.5f);
+    for (int j = tid; j < 2 * D; j += BR_BLOCK) {
+      float acc = 0.0f;
+      for (int q = 0; q < a.nparts_bwd; ++q) acc += a.gpart_all[(size_t)q * 2 * D + j];
+      s_gs[j] = acc;
+    }
+    __syncthreads();
+    gs = s_gs;
+  }
+  const int Nl = a.bt.hdr[0];
+  const int t0 = (blockIdx.x * BR_WAVES + wave) * BR_RPW;
+  if (t0 >= Nl) return;  // wave-uniform
+  const int sub = lane / LPR, c4 = lane - sub * LPR, col = 4 * c4;
+  const int rr = sub / SPR, si = sub - rr * SPR;
+  const int C = a.C, H = a.H;
+  const int HL = C >= 4 ? C / 4 : 1;
+  const int head = col / C;
+  const bool leader = (c4 & (HL - 1)) == 0;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const bool two = t0 + 1 < Nl;
+  const int e0 = a.bt.in_ptr[t0], em = a.bt.in_ptr[t0 + 1];
+  const int e2 = two ? a.bt.in_ptr[t0 + 2] : em;
+  const int ne0 = em - e0, ne = e2 - e0;
+  const bool mine = rr == 0 || two;
+  const int eb = rr == 0 ? 0 : ne0;
+  const int nr = rr == 0 ? ne0 : ne - ne0;
+  const int nmax = max(ne0, ne - ne0);
+  const int t = t0 + rr;
+  const bool lds_da = ne <= BR_ECH;
+  const int my_src = lane < ne ? a.bt.in_src[e0 + lane] : 0;
+  const uint32_t ctr = a.rng_ctr ? load_step_ctr(a.rng_ctr) + a.ctr_add : 0u;
+  const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
+  const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
+  const size_t ro = (size_t)(mine ? t : t0) * D + col;
+  const float4 dyv = *reinterpret_cast<const float4*>(a.dy + ro);
+  const float4 ov = *reinterpret_cast<const float4*>(a.out + ro);
+  const float4 agv = *reinterpret_cast<const float4*>(a.agg + ro);
+  const float4 sv = *reinterpret_cast<const float4*>(a.qkvs + (size_t)(mine ? t : t0) * (4 * D) + 3 * D + col);
+  const float beta = a.gate[mine ? t : t0];
+  // ---- BatchNorm backward, then the beta gate (as bwd_dst_row, per float4)
+  float4 dag, ds;
+  {
+    const float invN = 1.0f / (float)Nstat;
+    const float4 g4 = *reinterpret_cast<const float4*>(a.gamma + col);
+    const float4 mu = *reinterpret_cast<const float4*>(a.stats + col);
+    const float4 rs = *reinterpret_cast<const float4*>(a.stats + D + col);
+    const float4 s1 = *reinterpret_cast<const float4*>(gs + col);
+    const float4 s2 = *reinterpret_cast<const float4*>(gs + D + col);
+    const float4 w1 = *reinterpret_cast<const float4*>(a.w_beta + col);
+    const float4 w2 = *reinterpret_cast<const float4*>(a.w_beta + D + col);
+    const float4 w3 = *reinterpret_cast<const float4*>(a.w_beta + 2 * D + col);
+    float gv[4], dbeta = 0.0f;
+    const float dyc[4] = {dyv.x, dyv.y, dyv.z, dyv.w}, oc[4] = {ov.x, ov.y, ov.z, ov.w};
+    const float agc[4] = {agv.x, agv.y, agv.z, agv.w}, sc[4] = {sv.x, sv.y, sv.z, sv.w};
+    const float gc[4] = {g4.x, g4.y, g4.z, g4.w}, muc[4] = {mu.x, mu.y, mu.z, mu.w};
+    const float rsc[4] = {rs.x, rs.y, rs.z, rs.w}, s1c[4] = {s1.x, s1.y, s1.z, s1.w};
+    const float s2c[4] = {s2.x, s2.y, s2.z, s2.w};
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const float xh = (oc[v] - muc[v]) * rsc[v];
+      gv[v] = (dyc[v] - s1c[v] * invN - xh * (s2c[v] * invN)) * rsc[v] * gc[v];
+      dbeta += gv[v] * (sc[v] - agc[v]);
+    }
+    dbeta = group_sum_c<LPR>(dbeta);
+    const float du = dbeta * beta * (1.0f - beta);
+    if (mine && si == 0 && c4 == 0) a.du[t] = du;
+    const float w1c[4] = {w1.x, w1.y, w1.z, w1.w}, w2c[4] = {w2.x, w2.y, w2.z, w2.w}, w3c[4] = {w3.x, w3.y, w3.z, w3.w};
+    float dgc[4], dsc[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      dgc[v] = gv[v] * (1.0f - beta) + du * (w1c[v] + w3c[v]);
+      dsc[v] = gv[v] * beta + du * (w2c[v] - w3c[v]);
+    }
+    dag = make_float4(dgc[0], dgc[1], dgc[2], dgc[3]);
+    ds = make_float4(dsc[0], dsc[1], dsc[2], dsc[3]);
+    if (mine && si == 0) {
+      *reinterpret_cast<float4*>(a.dqkvs + (size_t)t * (4 * D) + 3 * D + col) = ds;
+      *reinterpret_cast<float4*>(a.dagg + (size_t)t * D + col) = dag;
+    }
+  }
+  const float* K = a.qkvs + D + col;
+  const float* V = a.qkvs + 2 * D + col;
+  const float isc = 1.0f / a.sqrt_c;
+  // ---- pass 1: da per edge (LDS, or the dlogit buffer for a hub pair) and sdot
+  float4 kh[U];      // single-round rows: the K rows, kept for dQ
+  float dah[U], alh[U];
+  float sdot = 0.0f;
+  auto ids_of = [&](int j, int& ids, int& ib) {
+    ids = my_src;
+    ib = eb;
+    if (ne > 64) {  // hub pair: this round's ids -- row 0's edges j.. in lanes 0-31, row 1's in 32-63
+      const int k = j + (lane & 31);
+      const bool okid = lane < 32 ? k < ne0 : ne0 + k < ne;
+      ids = okid ? a.bt.in_src[e0 + (lane < 32 ? k : ne0 + k)] : 0;
+      ib = rr * 32 - j;
+    }
+  };
+  for (int j = 0; j < nmax; j += EPR) {
+    int ids, ib;
+    ids_of(j, ids, ib);
+    float4 vc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = j + u * SPR + si;
+      const bool ok = mine && k < nr;
+      const int src = __shfl(ids, (ib + k) & 63);
+      const size_t off = ok ? (size_t)src * (4 * D) : 0;
+      vc[u] = *reinterpret_cast<const float4*>(V + off);
+      kh[u] = *reinterpret_cast<const float4*>(K + off);
+      alh[u] = ok ? a.alpha[(size_t)(e0 + eb + k) * H + head] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = j + u * SPR + si;
+      float d = dag.x * vc[u].x + dag.y * vc[u].y + dag.z * vc[u].z + dag.w * vc[u].w;
+      d = group_sum(d, HL);
+      dah[u] = 0.0f;
+      if (mine && k < nr) {
+        const int e = eb + k, eg = e0 + e;
+        const float da = d * dr.mul(st_attn, (uint32_t)(eg * H + head));
+        dah[u] = da;
+        sdot = __builtin_fmaf(alh[u], da, sdot);
+        if (leader) {
+          if (lds_da) s_da[wave][e][head] = da;
+          else a.dlogit[(size_t)eg * H + head] = da;  // parked; rewritten as dlogit below
+        }
+      }
+    }
+  }
+  sdot = xor_sum_upto<LPR, LPR * SPR>(sdot);  // the row's sub-groups
+  // ---- pass 2: dlogit = alpha (da - sdot), dQ
+  float4 dq = z4;
+  if (nmax <= EPR) {  // every row of the pair in one round: K rows, alpha and da in registers
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = u * SPR + si;
+      if (mine && k < nr) {
+        const int eg = e0 + eb + k;
+        const float dl = alh[u] * (dah[u] - sdot);
+        if (leader) a.dlogit[(size_t)eg * H + head] = dl;
+        const float c = dl * isc;
+        dq.x = __builtin_fmaf(c, kh[u].x, dq.x);
+        dq.y = __builtin_fmaf(c, kh[u].y, dq.y);
+        dq.z = __builtin_fmaf(c, kh[u].z, dq.z);
+        dq.w = __builtin_fmaf(c, kh[u].w, dq.w);
+      }
+    }
+  } else {
+    if (!lds_da) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // parked da in dlogit
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int j = 0; j < nmax; j += EPR) {
+      int ids, ib;
+      ids_of(j, ids, ib);
+      float4 kc[U];
+      float al[U], dv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = j + u * SPR + si;
+        const bool ok = mine && k < nr;
+        const int src = __shfl(ids, (ib + k) & 63);
+        kc[u] = *reinterpret_cast<const float4*>(K + (ok ? (size_t)src * (4 * D) : 0));
+        const size_t at = (size_t)(e0 + eb + k) * H + head;
+        al[u] = ok ? a.alpha[at] : 0.0f;
+        dv[u] = ok ? (lds_da ? s_da[wave][eb + k][head] : a.dlogit[at]) : 0.0f;
+      }
+      // every lane of a head group has its parked da before its leader overwrites it
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int k = j + u * SPR + si;
+        if (mine && k < nr) {
+          const float dl = al[u] * (dv[u] - sdot);
+          if (leader) a.dlogit[(size_t)(e0 + eb + k) * H + head] = dl;
+          const float c = dl * isc;
+          dq.x = __builtin_fmaf(c, kc[u].x, dq.x);
+          dq.y = __builtin_fmaf(c, kc[u].y, dq.y);
+          dq.z = __builtin_fmaf(c, kc[u].z, dq.z);
+          dq.w = __builtin_fmaf(c, kc[u].w, dq.w);
+        }
+      }
+    }
+  }
+  dq.x = xor_sum_upto<LPR, LPR * SPR>(dq.x);
+  dq.y = xor_sum_upto<LPR, LPR * SPR>(dq.y);
+  dq.z = xor_sum_upto<LPR, LPR * SPR>(dq.z);
+  dq.w = xor_sum_upto<LPR, LPR * SPR>(dq.w);
+  if (mine && si == 0) *reinterpret_cast<float4*>(a.dqkvs + (size_t)t * (4 * D) + col) = dq;
+  (void)s_sd;
+}
+
 template <int D>
 __global__ __launch_bounds__(BR_BLOCK) void k_attn_rows_bwd_src(ConvBwdK a) {
   constexpr int VPL = LayerGeom<D>::VPL;
@@ -448,6 +678,93 @@ __global__ __launch_bounds__(BR_BLOCK) void k_attn_rows_bwd_src(ConvBwdK a) {
   }
 }
 
+// Source-row backward with float4 lanes (round 5; the layout of k_attn_rows_bwd_dst4): a
+// wave owns two consecutive SOURCE rows (their out-edges are contiguous in the CSR by
+// source), each row's SPR sub-groups walk its out-edges U at a time, gathering the
+// destination's Q row and dA row per edge: dK = sum dlogit / sqrt(C) * Q[dst],
+// dV = sum alpha * mask * dA[dst].  The sub-groups' partial sums are combined by xor
+// butterflies (same sums as k_attn_rows_bwd_src up to fp32 reordering).
+template <int D>
+__global__ __launch_bounds__(BR_BLOCK) __attribute__((amdgpu_waves_per_eu(6, 8))) void k_attn_rows_bwd_src4(ConvBwdK a) {
+  constexpr int LPR = D / 4, RPI = 64 / LPR, U = BR4_U;
+  constexpr int SPR = RPI / 2, EPR = U * SPR;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // source rows: the batch rows, plus the ghost rows of a halo batch (hdr[6], gtr.h)
+  const int Nl = max(a.bt.hdr[0], a.bt.hdr[6]);
+  const int s0 = (blockIdx.x * BR_WAVES + wave) * BR_RPW;
+  if (s0 >= Nl) return;  // wave-uniform
+  const int sub = lane / LPR, c4 = lane - sub * LPR, col = 4 * c4;
+  const int rr = sub / SPR, si = sub - rr * SPR;
+  const int C = a.C, H = a.H;
+  const int head = col / C;
+  const bool two = s0 + 1 < Nl;
+  const int i0 = a.bt.out_ptr[s0], im = a.bt.out_ptr[s0 + 1];
+  const int i2 = two ? a.bt.out_ptr[s0 + 2] : im;
+  const int n0 = im - i0, n = i2 - i0;
+  const bool mine = rr == 0 || two;
+  const int eb = rr == 0 ? 0 : n0;
+  const int nr = rr == 0 ? n0 : n - n0;
+  const int nmax = max(n0, n - n0);
+  const uint32_t ctr = a.rng_ctr ? load_step_ctr(a.rng_ctr) + a.ctr_add : 0u;
+  const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
+  const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
+  const float isc = 1.0f / a.sqrt_c;
+  const int my_p = lane < n ? a.bt.out_edge[i0 + lane] : 0;
+  const int my_t = lane < n ? a.bt.out_dst[i0 + lane] : 0;
+  float4 dk = make_float4(0.f, 0.f, 0.f, 0.f), dv = dk;
+  for (int j = 0; j < nmax; j += EPR) {
+    int ps = my_p, ts = my_t, ib = eb;
+    if (n > 64) {  // hub pair: this round's out-edges -- row 0's in lanes 0-31, row 1's in 32-63
+      const int k = j + (lane & 31);
+      const bool ok = lane < 32 ? k < n0 : n0 + k < n;
+      const int at = i0 + (lane < 32 ? k : n0 + k);
+      ps = ok ? a.bt.out_edge[at] : 0;
+      ts = ok ? a.bt.out_dst[at] : 0;
+      ib = rr * 32 - j;
+    }
+    float4 qv[U], gv[U];
+    float dl[U], ad[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = j + u * SPR + si;
+      const bool ok = mine && k < nr;
+      // every lane joins both shuffles (a lane a shuffle skips reads as 0 to the others)
+      const int p = __shfl(ps, (ib + k) & 63);
+      const int tt = __shfl(ts, (ib + k) & 63);
+      const int t = ok ? tt : 0;
+      qv[u] = *reinterpret_cast<const float4*>(a.qkvs + (size_t)t * (4 * D) + col);
+      gv[u] = *reinterpret_cast<const float4*>(a.dagg + (size_t)t * D + col);
+      const size_t at = (size_t)p * H + head;
+      dl[u] = ok ? a.dlogit[at] * isc : 0.0f;
+      ad[u] = ok ? a.alpha[at] * dr.mul(st_attn, (uint32_t)(p * H + head)) : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      dk.x = __builtin_fmaf(dl[u], qv[u].x, dk.x);
+      dk.y = __builtin_fmaf(dl[u], qv[u].y, dk.y);
+      dk.z = __builtin_fmaf(dl[u], qv[u].z, dk.z);
+      dk.w = __builtin_fmaf(dl[u], qv[u].w, dk.w);
+      dv.x = __builtin_fmaf(ad[u], gv[u].x, dv.x);
+      dv.y = __builtin_fmaf(ad[u], gv[u].y, dv.y);
+      dv.z = __builtin_fmaf(ad[u], gv[u].z, dv.z);
+      dv.w = __builtin_fmaf(ad[u], gv[u].w, dv.w);
+    }
+  }
+  dk.x = xor_sum_upto<LPR, LPR * SPR>(dk.x);
+  dk.y = xor_sum_upto<LPR, LPR * SPR>(dk.y);
+  dk.z = xor_sum_upto<LPR, LPR * SPR>(dk.z);
+  dk.w = xor_sum_upto<LPR, LPR * SPR>(dk.w);
+  dv.x = xor_sum_upto<LPR, LPR * SPR>(dv.x);
+  dv.y = xor_sum_upto<LPR, LPR * SPR>(dv.y);
+  dv.z = xor_sum_upto<LPR, LPR * SPR>(dv.z);
+  dv.w = xor_sum_upto<LPR, LPR * SPR>(dv.w);
+  if (mine && si == 0) {
+    float* row = a.dqkvs + (size_t)(s0 + rr) * (4 * D);
+    *reinterpret_cast<float4*>(row + D + col) = dk;
+    *reinterpret_cast<float4*>(row + 2 * D + col) = dv;
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // weight gradients
 // ------------------------------------------------------------------------------------
@@ -539,6 +856,22 @@ extern "C" int gtr_attn_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   const char* am = getenv("GTR_ATTN");  // "group": the fused kernels' row-group body (A/B)
   if (cfg->dim <= 128 && !(am && am[0] == 'g')) {
     const int grid = (bt->n_cap + BR_WAVES * BR_RPW - 1) / (BR_WAVES * BR_RPW);
+    // float4 lanes (k_attn_rows_bwd_dst4) unless GTR_ATTN=rows or more than BR_HMAX heads
+    const bool v4 = cfg->heads <= BR_HMAX && !(am && am[0] == 'r');
+    if (v4) {
+      switch (cfg->dim) {
+        case 32: hipLaunchKernelGGL(k_attn_rows_bwd_dst4<32>, dim3(grid), dim3(BR_BLOCK), 0, s, k); break;
+        case 64: hipLaunchKernelGGL(k_attn_rows_bwd_dst4<64>, dim3(grid), dim3(BR_BLOCK), 0, s, k); break;
+        default: hipLaunchKernelGGL(k_attn_rows_bwd_dst4<128>, dim3(grid), dim3(BR_BLOCK), 0, s, k); break;
+      }
+      switch (cfg->dim) {
+        case 32: hipLaunchKernelGGL(k_attn_rows_bwd_src4<32>, dim3(grid), dim3(BR_BLOCK), 0, s, k); break;
+        case 64: hipLaunchKernelGGL(k_attn_rows_bwd_src4<64>, dim3(grid), dim3(BR_BLOCK), 0, s, k); break;
+        default: hipLaunchKernelGGL(k_attn_rows_bwd_src4<128>, dim3(grid), dim3(BR_BLOCK), 0, s, k); break;
+      }
+      GTR_HIP_CHECK_LAUNCH();
+      return GTR_OK;
+    }
     switch (cfg->dim) {
       case 32:
         hipLaunchKernelGGL(k_attn_rows_bwd_dst<32>, dim3(grid), dim3(BR_BLOCK), 0, s, k);

@@ -194,6 +194,7 @@ def test_c4_sharded_full_table_bitwise_dp_and_matches_oracle(world):
     trio, rlosses, touched = _oracle()
     for s in range(STEPS):  # the global loss is the mean of the equal-sized rank losses
         g = sum(res[r][0][s] for r in range(world)) / world
+        print(f"step {s}: loss {g:.7f} oracle {rlosses[s]:.7f} rel {abs(g - rlosses[s]) / abs(rlosses[s]):.2e}")
         assert abs(g - rlosses[s]) <= 1e-3 * abs(rlosses[s]), (s, g, rlosses[s])
     hip = {n: torch.from_numpy(v) for n, v in res[0][4].items()}
     tab = "item_embedding.weight"
