@@ -1,0 +1,7 @@
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp ROUND=r05 PMC=${PMC:-0}
+GTR_SPLIT=1 bash scripts/gpu/profile.sh c4 c4_b1024 --global-batch 1024 > gpurun_out/p_c4.log 2>&1 || { tail -20 gpurun_out/p_c4.log; exit 1; }
+bash scripts/gpu/profile.sh c3 c3_b8192 --batch-size 8192 > gpurun_out/p_c3.log 2>&1 || { tail -20 gpurun_out/p_c3.log; exit 1; }
+python3 scripts/kstat_summary.py gpurun_out/c4_b1024_kernel_stats.csv 28
+python3 scripts/kstat_summary.py gpurun_out/c3_b8192_kernel_stats.csv 20

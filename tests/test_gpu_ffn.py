@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 import etpgt_ref as R  # noqa: E402
 from etpgt.model import create_graph_transformer  # noqa: E402
-from gpu_helpers import (OracleTrio, assert_close, assert_close_norm, batches, edge_case_batch, ref_batch,  # noqa: E402
+from gpu_helpers import (OracleTrio, assert_close, batches, edge_case_batch, ref_batch,  # noqa: E402
                          small_data)
 
 pytestmark = pytest.mark.gpu
