@@ -34,6 +34,8 @@
 
 #include "gtr_layer.cuh"
 
+#include <type_traits>
+
 namespace gtr {  // gtr_gemm_gen.hip: the LDS-staged GEMMs for D = 256 and FFN expansions != 4
 int gen_qkvs_fwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_embed* emb, const gtr_layer* layers, int l,
                  hipStream_t s);
@@ -48,6 +50,8 @@ int gen_ffn_wgrad(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* l
 namespace {
 
 using namespace gtr;
+
+GTR_PH_DECL
 
 #define GM_BLOCK 512
 #define GM_WAVES (GM_BLOCK / 64)
@@ -110,9 +114,11 @@ struct ProjK {
 
 // Inputs of one thread's float4 of X for one tile: layer 0 the item row (+ its LapPE row),
 // layers >= 1 the previous layer's out and in rows.
+template <int NPE>
 struct ProjIn {
   float4 u, v;
-  float4 pe[4];
+  float4 pe[NPE > 0 ? NPE : 1];  // D = 64 (4 waves per SIMD, 128 VGPRs): no PE prefetch
+  int item;  // layer 0: the tile row's item id (the LapPE fallback path reads by it)
 };
 
 template <int D, int MODE>
@@ -120,6 +126,8 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
   constexpr bool FIRST = MODE == PJ_FIRST, FOLD = MODE == PJ_FOLD, DH = MODE == PJ_FFN_DH;
   using G = ProjGeom<D>;
   constexpr int CT = G::CT, RT = G::RT, BM = G::BM, XS = G::XS, C4 = G::C4, KPE = G::KPE;
+  constexpr int NPE = FIRST && D >= 128 ? 4 : 0;  // LapPE float4s prefetched per thread
+  using ProjIn = ::ProjIn<NPE>;
   __shared__ __attribute__((aligned(16))) float Xs[2][BM * XS];
   __shared__ __attribute__((aligned(16))) float s_pw[KPE * D];  // W_pe^T [KPE][D] (layer 0)
   __shared__ __attribute__((aligned(16))) float s_c[4 * D];     // bpe | mean | rstd | gamma | beta
@@ -127,13 +135,19 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
   const int N = a.bt.hdr[0];
   const int ntile = (N + BM - 1) / BM;
   if ((int)blockIdx.x >= ntile) return;  // block-uniform
+  GTR_PH(10 + a.layer, 0);
+  // Round 5: the waves' column tiles rotate with the workgroup's position on its XCD
+  // (blocks b and b + 8 share an XCD), so that the 32 CUs of an XCD, loading W_all at
+  // the same moment, do not all request the same W rows (the same L2 channels) at once;
+  // only which wave computes which columns changes, not the arithmetic.
+  const int wsw = (wave + ((int)blockIdx.x >> 3)) & (GM_WAVES - 1);
   // ---- W fragments of this wave's column tiles (ct = wave + c * GM_WAVES, the fused
   //      kernel's assignment) and biases, held in registers for every tile of the block
   float4 wf[CT][D / 16];
   float bias[CT];
 #pragma unroll
   for (int c = 0; c < CT; ++c) {
-    const int ct = wave + c * GM_WAVES;
+    const int ct = wsw + c * GM_WAVES;
     if (DH) {  // B[k][col] = W2[k][col], W2 = [D, 4D] row-major
       const float* wcol = a.w_all + (size_t)(lg * 4) * (4 * D) + ct * 16 + lr;
 #pragma unroll
@@ -210,18 +224,19 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
     const int r = t * BM + xi;
     const bool live = r < N;
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    in.item = item;
     in.u = z;
     in.v = z;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) in.pe[q] = z;
+    for (int q = 0; q < NPE; ++q) in.pe[q] = z;
     if (!live) return;
     if (FIRST) {
       in.u = *reinterpret_cast<const float4*>(a.table + (size_t)item * D + xj);
-      if (pe_lds && (a.pe_k & 3) == 0) {
+      if (NPE > 0 && pe_lds && (a.pe_k & 3) == 0) {
         const float* pr = a.bt.node_pe ? a.bt.node_pe + (size_t)r * a.pe_k : a.pe_tab + (size_t)item * a.pe_k;
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          if (4 * q < a.pe_k) in.pe[q] = *reinterpret_cast<const float4*>(pr + 4 * q);
+          if (q < NPE && 4 * q < a.pe_k) in.pe[q] = *reinterpret_cast<const float4*>(pr + 4 * q);
       }
     } else {
       const size_t o = (size_t)r * D + xj;
@@ -240,12 +255,12 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
         val = in.u;
         if (a.pe_k > 0) {
           float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-          if (pe_lds && (a.pe_k & 3) == 0) {
+          if (NPE > 0 && pe_lds && (a.pe_k & 3) == 0) {
 #pragma unroll
-            for (int kq = 0; kq < 4; ++kq) {  // k = 0, 4, .. < pe_k: the fused loop's order
+            for (int kq = 0; kq < (NPE > 0 ? NPE : 1); ++kq) {  // k = 0, 4, .. < pe_k: the fused loop's order
               if (4 * kq >= a.pe_k) break;
               const int k = 4 * kq;
-              pe_fma4(acc, in.pe[kq], s_pw + k * D + xj, D);
+              pe_fma4(acc, in.pe[kq < NPE ? kq : 0], s_pw + k * D + xj, D);
             }
           } else {
             const float* pr = a.bt.node_pe ? a.bt.node_pe + (size_t)r * a.pe_k : a.pe_tab + (size_t)item * a.pe_k;
@@ -279,24 +294,34 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
     *reinterpret_cast<float4*>(X + xi * XS + xj) = val;
   };
 
-  // two tiles in flight behind the one being multiplied (its rows were requested two
-  // tiles earlier, its item ids three): one workgroup per CU needs the depth to cover the
-  // gather latency
+  // Pipeline (round 5).  Phase k multiplies tile T_k = t0 + k GS out of LDS buffer k % 2;
+  // in the middle of its MFMA chain the waves build tile T_{k+1} into the other buffer
+  // from register set S[(k+1) % 2] (its rows requested two phases earlier), then request
+  // the rows of T_{k+3} into that same set, and the item ids of T_{k+5}; one barrier per
+  // phase.  Two explicit register sets (the loop is unrolled by two, so no set is ever
+  // COPIED: a copy of an in-flight load is a use, whose wait -- vector loads retire in
+  // order -- drained every load behind it at each tile boundary).
   const int GS = gridDim.x;
-  int t = blockIdx.x;
-  int it = item_of(t), it_next = item_of(t + GS);
-  ProjIn cur, nxt;
-  fetch(t, it, cur);
-  fetch(t + GS, it_next, nxt);
-  int it_nn = item_of(t + 2 * GS);
-  int buf = 0;
-  for (; t < ntile; t += GS) {
-    float* X = Xs[buf];
-    produce(t, it, cur, X);
-    __syncthreads();
-    ProjIn nn;
-    fetch(t + 2 * GS, it_nn, nn);  // past the last tile: zeros, nothing loaded
-    const int it3 = item_of(t + 3 * GS);
+  const int t0 = blockIdx.x;
+  ProjIn S0, S1;
+  {
+    const int i0 = item_of(t0), i1 = item_of(t0 + GS);
+    fetch(t0, i0, S0);
+    fetch(t0 + GS, i1, S1);
+  }
+  int I0 = item_of(t0 + 2 * GS), I1 = item_of(t0 + 3 * GS);
+  produce(t0, S0.item, S0, Xs[0]);
+  fetch(t0 + 2 * GS, I0, S0);
+  I0 = item_of(t0 + 4 * GS);
+  __syncthreads();
+  GTR_PH(10 + a.layer, 2);
+  constexpr int KB_STAGE = D / 32;  // the k block after which the next tile is built
+  auto phase = [&](auto P, int t) {
+    constexpr int p = decltype(P)::value;
+    ProjIn& Sn = p ? S0 : S1;  // the set of tile t + GS (then refilled with t + 3 GS)
+    int& In = p ? I0 : I1;     // the item ids of tile t + 3 GS (then of t + 5 GS)
+    const float* X = Xs[p];
+    const bool more = t + GS < ntile;  // block-uniform
     // ---- QKVS = X . W_all^T (f32 MFMA, k order of the fused kernel)
     f32x4 acc[RT][CT];
 #pragma unroll
@@ -312,12 +337,18 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
       for (int r = 0; r < RT; ++r)
 #pragma unroll
         for (int c = 0; c < CT; ++c) acc[r][c] = GM_MFMA4(av[r], wf[c][kb], acc[r][c]);
+      if (kb == KB_STAGE) {
+        if (more) produce(t + GS, Sn.item, Sn, Xs[p ^ 1]);
+        fetch(t + 3 * GS, In, Sn);  // past the last tile: zeros, nothing loaded
+        In = item_of(t + 5 * GS);
+      }
     }
+    if (t == t0) GTR_PH(10 + a.layer, 3);
 #pragma unroll
     for (int r = 0; r < RT; ++r)
 #pragma unroll
       for (int c = 0; c < CT; ++c) {
-        const int col = (wave + c * GM_WAVES) * 16 + lr;
+        const int col = (wsw + c * GM_WAVES) * 16 + lr;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int row = t * BM + r * 16 + lg * 4 + i;
@@ -328,13 +359,16 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
           }
         }
       }
-    cur = nxt;
-    nxt = nn;
-    it = it_next;
-    it_next = it_nn;
-    it_nn = it3;
-    buf ^= 1;
+    if (t == t0) GTR_PH(10 + a.layer, 4);
+    __syncthreads();  // the next tile's X is built; this tile's buffer is free
+    if (t == t0) GTR_PH(10 + a.layer, 5);
+  };
+  for (int t = t0; t < ntile; t += 2 * GS) {
+    phase(std::integral_constant<int, 0>{}, t);
+    if (t + GS >= ntile) break;  // block-uniform
+    phase(std::integral_constant<int, 1>{}, t + GS);
   }
+  GTR_PH(10 + a.layer, 1);
 }
 
 template <int D>
@@ -381,7 +415,9 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
   const int N = a.bt.hdr[0];
   const int ntile = (N + BM - 1) / BM;
-  const int ct = wave % NCT, rs = wave / NCT;  // this wave's column tile and 16-row slice
+  // this wave's column tile and 16-row slice; the column tiles rotate with the workgroup's
+  // position on its XCD (see k_proj: the XCD's CUs fetch different W columns at once)
+  const int ct = (wave + ((int)blockIdx.x >> 3)) % NCT, rs = wave / NCT;
   const int col = ct * 16 + lr;
   // ---- W_all column fragments (B[k][col] = W_all[k][col], k = kb*16 + lg*4 + j): the
   //      fused kernel's bv, held in registers for every tile
@@ -418,20 +454,15 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
                                   : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   };
-  int t = blockIdx.x;
-  float4 cur[PER], nxt[PER];
-  fetch(t, cur);
-  fetch(t + gridDim.x, nxt);  // two tiles in flight behind the one being multiplied
-  int buf = 0;
-  for (; t < ntile; t += gridDim.x) {
-    float* A = As[buf];
+  // a tile's dQKVS rows (h = dropout(GELU(a)) for DX_FFN_DOWN) -> LDS
+  auto stage = [&](int tt, const float4 (&src)[PER], float* A) {
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int idx = tid + u * GM_BLOCK;
       const int i = idx / (K / 4), c = (idx - i * (K / 4)) * 4;
-      float4 v = cur[u];
+      float4 v = src[u];
       if (DOWN) {  // h = dropout(GELU(a)) (rows past N are zero: GELU(0) = 0)
-        const uint32_t e = (uint32_t)((size_t)(t * BM + i) * K + c);
+        const uint32_t e = (uint32_t)((size_t)(tt * BM + i) * K + c);
         v.x = gelu_erf(v.x) * dr.mul(st_h, e);
         v.y = gelu_erf(v.y) * dr.mul(st_h, e + 1);
         v.z = gelu_erf(v.z) * dr.mul(st_h, e + 2);
@@ -439,10 +470,24 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
       }
       *reinterpret_cast<float4*>(A + i * AS + c) = v;
     }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < PER; ++u) cur[u] = nxt[u];
-    fetch(t + 2 * gridDim.x, nxt);  // in flight during the MFMAs
+  };
+  // Pipeline (round 5, as k_proj): phase k multiplies tile T_k out of LDS buffer k % 2,
+  // stages T_{k+1} from register set S[(k+1) % 2] into the other buffer in the middle of
+  // its MFMA chain and refills that set with T_{k+3}; two explicit sets, never copied.
+  const int GD = gridDim.x;
+  const int t0 = blockIdx.x;
+  float4 S0[PER], S1[PER];
+  fetch(t0, S0);
+  fetch(t0 + GD, S1);
+  stage(t0, S0, As[0]);
+  fetch(t0 + 2 * GD, S0);
+  __syncthreads();
+  constexpr int KB_STAGE = K / 32;
+  auto phase = [&](auto P, int t) {
+    constexpr int p = decltype(P)::value;
+    float4 (&Sn)[PER] = p ? S0 : S1;
+    const float* A = As[p];
+    const bool more = t + GD < ntile;  // block-uniform
     // the epilogue's residual / previous-output values requested before the MFMA chain, so
     // that the tile's stores do not wait one memory round after it
     float ydv[4], pov[4];
@@ -456,7 +501,13 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
     f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
     const float* arow = A + (rs * 16 + lr) * AS + lg * 4;
 #pragma unroll
-    for (int kb = 0; kb < K / 16; ++kb) acc = GM_MFMA4(*reinterpret_cast<const float4*>(arow + kb * 16), wb[kb], acc);
+    for (int kb = 0; kb < K / 16; ++kb) {
+      acc = GM_MFMA4(*reinterpret_cast<const float4*>(arow + kb * 16), wb[kb], acc);
+      if (kb == KB_STAGE) {
+        if (more) stage(t + GD, Sn, As[p ^ 1]);
+        fetch(t + 3 * GD, Sn);  // past the last tile: zeros, nothing loaded
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = t * BM + rs * 16 + lg * 4 + i;
@@ -477,7 +528,12 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
         }
       }
     }
-    buf ^= 1;
+    __syncthreads();  // the next tile is staged; this tile's buffer is free
+  };
+  for (int t = t0; t < ntile; t += 2 * GD) {
+    phase(std::integral_constant<int, 0>{}, t);
+    if (t + GD >= ntile) break;  // block-uniform
+    phase(std::integral_constant<int, 1>{}, t + GD);
   }
   if (DOWN || !a.has_prev) return;
   // ---- the previous layer's BatchNorm backward sums: one partial row per workgroup (its
@@ -626,6 +682,8 @@ int gemm_grid(int tiles, int per_cu) {
 
 }  // namespace
 
+GTR_PH_READER(gtr_dbg_gemm_phases)
+
 extern "C" int gtr_qkvs_fwd(const gtr_config* cfg, const gtr_batch* bt, const gtr_embed* emb,
                             const gtr_layer* layers, int l, gtr_stream_t stream) {
   if (!cfg || !bt || !layers || l < 0 || l >= cfg->num_layers) {
@@ -649,7 +707,8 @@ extern "C" int gtr_qkvs_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
               "or, under sync_bn, the ranks' merged rows (split_sync)");
     return GTR_E_ARG;
   }
-  if (D == 256) {  // LDS-staged GEMM (gtr_gemm_gen.hip): no SyncBN merged-row mode there
+  const char* gg = getenv("GTR_GEMM_GEN");  // A/B: the LDS-staged GEMMs at D = 64 / 128 too
+  if (D == 256 || (gg && gg[0] == '1' && !(cfg->sync_bn && cfg->training))) {  // LDS-staged GEMM (gtr_gemm_gen.hip): no SyncBN merged-row mode there
     if (cfg->sync_bn && cfg->training) { set_error("gtr_qkvs_fwd: dim 256 on the split path has no SyncBN"); return GTR_E_ARG; }
     if (l == 0 && cfg->pe_k > 0 && (!emb->wpe || !emb->bpe)) { set_error("gtr_qkvs_fwd: Laplacian PE not precomputed"); return GTR_E_ARG; }
     return gen_qkvs_fwd(cfg, bt, emb, layers, l, (hipStream_t)stream);
@@ -721,7 +780,8 @@ extern "C" int gtr_qkvs_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   }
   if (!cfg->training) { set_error("gtr_qkvs_bwd: backward requires training mode"); return GTR_E_ARG; }
   if (cfg->sync_bn && !cfg->split_sync) { set_error("gtr_qkvs_bwd: sync_bn needs split_sync"); return GTR_E_ARG; }
-  if (D == 256) {
+  const char* gg = getenv("GTR_GEMM_GEN");
+  if (D == 256 || (gg && gg[0] == '1' && !cfg->sync_bn)) {
     if (cfg->sync_bn) { set_error("gtr_qkvs_bwd: dim 256 on the split path has no SyncBN"); return GTR_E_ARG; }
     if (l > 0 && layers[l - 1].ffn && !layers[l - 1].ffn->dz) { set_error("gtr_qkvs_bwd: layer %d's FFN has no dz rows", l - 1); return GTR_E_ARG; }
     return gen_qkvs_bwd(cfg, bt, layers, l, dx0, (hipStream_t)stream);

@@ -10,6 +10,8 @@
 
 #include "gtr_common.cuh"
 
+#include <type_traits>
+
 namespace gtr {
 
 enum { WJ_MM = 0, WJ_GATE = 1, WJ_COLSUM = 2 };
@@ -232,24 +234,32 @@ __device__ __forceinline__ void wgrad_tile_mfma(const WJob& J, int tile, int t0,
   const bool colsum = !NARROW && n0 == 0;
   float4 cs = make_float4(0.f, 0.f, 0.f, 0.f);
   // rows 16 ahead in flight (4 row quads): at 2 waves per SIMD one 8-row round of MFMAs
-  // (~1k cycles) is shorter than a load's latency from MALL under a full-chip stream
-  float4 a0, b0, a1, b1, a2, b2, a3, b3;
-  ld(r0 + kq, a0, b0);
-  ld(r0 + 4 + kq, a1, b1);
-  ld(r0 + 8 + kq, a2, b2);
-  ld(r0 + 12 + kq, a3, b3);
-  for (int t = r0; t < r1; t += 8) {
-    float4 a4, b4, a5, b5;
-    ld(t + 16 + kq, a4, b4);
-    ld(t + 20 + kq, a5, b5);
-    mma(a0, b0);
-    mma(a1, b1);
+  // (~1k cycles) is shorter than a load's latency from MALL under a full-chip stream.
+  // Round 5: a ring of three register sets of 8 rows, the loop unrolled by three so that
+  // no set is ever COPIED (a copy of an in-flight load is a use whose wait -- vector
+  // loads retire in order -- drained the 16 rows in flight at every step).
+  float4 ra[3][2], rb[3][2];
+  ld(r0 + kq, ra[0][0], rb[0][0]);
+  ld(r0 + 4 + kq, ra[0][1], rb[0][1]);
+  ld(r0 + 8 + kq, ra[1][0], rb[1][0]);
+  ld(r0 + 12 + kq, ra[1][1], rb[1][1]);
+  auto stepk = [&](auto S, int t) {
+    constexpr int c = decltype(S)::value, n = (c + 2) % 3;
+    ld(t + 16 + kq, ra[n][0], rb[n][0]);
+    ld(t + 20 + kq, ra[n][1], rb[n][1]);
+    mma(ra[c][0], rb[c][0]);
+    mma(ra[c][1], rb[c][1]);
     if (colsum) {
-      cs.x += a0.x; cs.y += a0.y; cs.z += a0.z; cs.w += a0.w;
-      cs.x += a1.x; cs.y += a1.y; cs.z += a1.z; cs.w += a1.w;
+      cs.x += ra[c][0].x; cs.y += ra[c][0].y; cs.z += ra[c][0].z; cs.w += ra[c][0].w;
+      cs.x += ra[c][1].x; cs.y += ra[c][1].y; cs.z += ra[c][1].z; cs.w += ra[c][1].w;
     }
-    a0 = a2; b0 = b2; a1 = a3; b1 = b3;
-    a2 = a4; b2 = b4; a3 = a5; b3 = b5;
+  };
+  for (int t = r0; t < r1; t += 24) {
+    stepk(std::integral_constant<int, 0>{}, t);
+    if (t + 8 >= r1) break;
+    stepk(std::integral_constant<int, 1>{}, t + 8);
+    if (t + 16 >= r1) break;
+    stepk(std::integral_constant<int, 2>{}, t + 16);
   }
   if (colsum) {  // the four row lanes of a column, then the row splits in order
     cs.x = bfly_add<32>(bfly_add<16>(cs.x)); cs.y = bfly_add<32>(bfly_add<16>(cs.y));

@@ -1,0 +1,11 @@
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+for v in base NOSTORE NOMMA; do
+  L=$PWD/gat-recommendation_amd/build/libgtr_hip.so
+  [ $v != base ] && L=$PWD/gat-recommendation_amd/build/var_$v/libgtr_hip.so
+  for cb in "c3 8192" "c4 1024"; do
+    echo "== $v $cb"
+    GTR_SPLIT=1 GTR_LIB=$L timeout -k 10 200 python3 -u scripts/dbg/kbench.py $cb 2>&1 | grep "^{" || exit 1
+  done
+done
