@@ -48,11 +48,17 @@ struct RouteK {
   int32_t* negatives_c;
   const float* pe_tab;
   float* node_pe;
-  int32_t* bcnt;    // [nblk][P] first-occurrence counts per owner, then exclusive offsets
+  int32_t* bcnt;    // [nblk][2P] first-occurrence counts per (class, owner), then exclusive offsets
   int32_t* status;
   uint32_t* ticket; // arrival counter of k_route_count (scratch tail; zero between launches)
+  int32_t* node_mark;  // [T] (cap_s > 0): rows a node reads, stamped with the step
   int T, P, cap, pe_k, m_cap, nblk;
+  int cap_s, blk, ncls, n_cap;  // class-1 slots per peer, id-block stride, classes (1 / 2)
+  const int64_t* step_dev;      // this step (node_mark stamps): *step_dev + step_offset
+  int step_offset, pad_t;
 };
+
+__device__ __forceinline__ int32_t route_step(const RouteK& a) { return (int32_t)(*a.step_dev + a.step_offset); }
 
 __device__ __forceinline__ bool slot_info(const RouteK& a, int i, int& key, int& owner, bool& first) {
   key = i < a.m_cap ? a.skeys[i] : a.T;
@@ -62,26 +68,41 @@ __device__ __forceinline__ bool slot_info(const RouteK& a, int i, int& key, int&
   return valid;
 }
 
+// Class of slot i's row: 0 if a node of the batch reads the row, 1 if only the scoring
+// readout does (targets / negatives).  Within a row's segment of the sorted list the node
+// slots come first (slots ascending), so a segment's first slot decides; k_route_count
+// stamps node_mark[row] for class-0 segments, which later slots of the segment read.
+__device__ __forceinline__ int slot_class(const RouteK& a, int i, int key, bool first) {
+  if (a.ncls == 1) return 0;
+  if (a.svals[i] < a.n_cap) return 0;
+  if (first) return 1;
+  return a.node_mark[key] == route_step(a) ? 0 : 1;
+}
+
 __device__ void route_scan_body(const RouteK& a);
 
 // Pass 1: first occurrences (segment starts of the sorted list) per owner and block; the
 // last arriving block then runs pass 2 (the scan) -- one launch for both (the counts are
 // written through and the arrival is a relaxed ticket: no release fence per block).
 __global__ __launch_bounds__(RB_THREADS) void k_route_count(RouteK a) {
-  __shared__ int s_cnt[SH_MAXP];
+  __shared__ int s_cnt[2 * SH_MAXP];
   __shared__ int s_flag;
-  if (threadIdx.x < SH_MAXP) s_cnt[threadIdx.x] = 0;
+  if (threadIdx.x < 2 * SH_MAXP) s_cnt[threadIdx.x] = 0;
   __syncthreads();
   for (int r = 0; r < RB_ROUNDS; ++r) {
     const int i = blockIdx.x * RB_SLOTS + r * RB_THREADS + threadIdx.x;
     int key, q;
     bool first;
     slot_info(a, i, key, q, first);
-    if (first) atomicAdd(&s_cnt[q], 1);  // integer counts: order-independent
+    if (first) {
+      const int c = slot_class(a, i, key, true);
+      if (a.ncls == 2 && c == 0) a.node_mark[key] = route_step(a);  // read by k_route_write (next launch)
+      atomicAdd(&s_cnt[c * a.P + q], 1);  // integer counts: order-independent
+    }
   }
   __syncthreads();
-  if (threadIdx.x < a.P)
-    __hip_atomic_store(a.bcnt + (size_t)blockIdx.x * a.P + threadIdx.x, s_cnt[threadIdx.x], __ATOMIC_RELAXED,
+  if (threadIdx.x < a.ncls * a.P)
+    __hip_atomic_store(a.bcnt + (size_t)blockIdx.x * a.ncls * a.P + threadIdx.x, s_cnt[threadIdx.x], __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   if (!arrive_last_wt(a.ticket, (uint32_t)a.nblk, &s_flag)) return;
   route_scan_body(a);
@@ -91,37 +112,39 @@ __global__ __launch_bounds__(RB_THREADS) void k_route_count(RouteK a) {
 // Pass 2 (one workgroup): exclusive offsets of every block per owner, the owners' totals
 // into the count slots, overflow status.
 __device__ void route_scan_body(const RouteK& a) {
-  __shared__ int s_part[RB_THREADS][SH_MAXP];
+  __shared__ int s_part[RB_THREADS][2 * SH_MAXP];
   const int tid = threadIdx.x;
+  const int NQ = a.ncls * a.P;  // (class, owner) counters, class-major
   if (tid == 0) a.status[0] = 0;  // this step's flag (a kernel write: no memset node in the captured step)
   const int per = (a.nblk + RB_THREADS - 1) / RB_THREADS;
   const int b0 = min(a.nblk, tid * per), b1 = min(a.nblk, b0 + per);
-  for (int q = 0; q < a.P; ++q) {
+  for (int q = 0; q < NQ; ++q) {
     int s = 0;
-    for (int b = b0; b < b1; ++b) s += a.bcnt[(size_t)b * a.P + q];
+    for (int b = b0; b < b1; ++b) s += a.bcnt[(size_t)b * NQ + q];
     s_part[tid][q] = s;
   }
   __syncthreads();
-  if (tid < a.P) {  // scan over the threads' chunks for owner q
+  if (tid < NQ) {  // scan over the threads' chunks for (class, owner) tid
     int run = 0;
     for (int t = 0; t < RB_THREADS; ++t) {
       const int v = s_part[t][tid];
       s_part[t][tid] = run;
       run += v;
     }
-    const int lim = a.cap - 1;
-    a.send_ids[(size_t)tid * a.cap] = min(run, lim);
+    const int c = tid / a.P, q = tid - c * a.P;
+    const int lim = (c ? a.cap_s : a.cap) - 1;
+    a.send_ids[(size_t)q * a.blk + (c ? a.cap : 0)] = min(run, lim);
     if (run > lim) {
       a.status[0] = 1;
       atomicOr(a.status + 1, 1);
     }
   }
   __syncthreads();
-  for (int q = 0; q < a.P; ++q) {
+  for (int q = 0; q < NQ; ++q) {
     int run = s_part[tid][q];
     for (int b = b0; b < b1; ++b) {
-      const int v = a.bcnt[(size_t)b * a.P + q];
-      a.bcnt[(size_t)b * a.P + q] = run;
+      const int v = a.bcnt[(size_t)b * NQ + q];
+      a.bcnt[(size_t)b * NQ + q] = run;
       run += v;
     }
   }
@@ -130,10 +153,11 @@ __device__ void route_scan_body(const RouteK& a) {
 // Pass 3: inclusive first-occurrence rank of each slot among its owner's rows (slot
 // order), compact row q*cap + rank, owner lists, remapped batch ids (+ PE rows).
 __global__ __launch_bounds__(RB_THREADS) void k_route_write(RouteK a) {
-  __shared__ int s_run[SH_MAXP];
-  __shared__ int s_wt[RB_THREADS / 64][SH_MAXP];
+  __shared__ int s_run[2 * SH_MAXP];
+  __shared__ int s_wt[RB_THREADS / 64][2 * SH_MAXP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid < a.P) s_run[tid] = a.bcnt[(size_t)blockIdx.x * a.P + tid];
+  const int NQ = a.ncls * a.P;
+  if (tid < NQ) s_run[tid] = a.bcnt[(size_t)blockIdx.x * NQ + tid];
   __syncthreads();
   const unsigned long long le = lane == 63 ? ~0ull : ((1ull << (lane + 1)) - 1ull);
   for (int r = 0; r < RB_ROUNDS; ++r) {
@@ -141,26 +165,32 @@ __global__ __launch_bounds__(RB_THREADS) void k_route_write(RouteK a) {
     int key, q;
     bool first;
     const bool valid = slot_info(a, i, key, q, first);
+    const int c = valid ? slot_class(a, i, key, first) : 0;
+    const int cq = c * a.P + q;  // this slot's (class, owner) counter
     int mine = 0;
-    for (int o = 0; o < a.P; ++o) {
-      const unsigned long long bal = __ballot(first && q == o);
+    for (int o = 0; o < NQ; ++o) {
+      const unsigned long long bal = __ballot(first && cq == o);
       if (lane == 0) s_wt[wave][o] = __popcll(bal);
-      if (q == o) mine = __popcll(bal & le);
+      if (cq == o) mine = __popcll(bal & le);
     }
     __syncthreads();
-    int base = s_run[q];
-    for (int w = 0; w < wave; ++w) base += s_wt[w][q];
+    int base = s_run[cq];
+    for (int w = 0; w < wave; ++w) base += s_wt[w][cq];
     if (valid) {
-      const int incl = base + mine;  // first occurrences of owner q in [0, i]
-      int compact = q * a.cap + incl;
-      if (incl > a.cap - 1) {
+      const int incl = base + mine;  // first occurrences of (class c, owner q) in [0, i]
+      const int lim = (c ? a.cap_s : a.cap) - 1;
+      // the fetched-row ("compact table") row and the id / gradient block slot
+      int compact = c ? a.P * a.cap + q * a.cap_s + incl : q * a.cap + incl;
+      int gslot = q * a.blk + (c ? a.cap : 0) + incl;
+      if (incl > lim) {
         compact = q * a.cap;  // in bounds; the step is flagged invalid
+        gslot = q * a.blk;
         a.status[0] = 1;
         atomicOr(a.status + 1, 1);
       } else if (first) {
-        a.send_ids[compact] = key;
+        a.send_ids[gslot] = key;
       }
-      a.ckeys[i] = compact;
+      a.ckeys[i] = gslot;
       const int s = a.svals[i];
       const gtr_batch& bt = a.bt;
       if (s < bt.n_cap) {
@@ -176,7 +206,7 @@ __global__ __launch_bounds__(RB_THREADS) void k_route_write(RouteK a) {
       a.ckeys[i] = -1;
     }
     __syncthreads();
-    if (tid < a.P) {
+    if (tid < NQ) {
       int t = 0;
       for (int w = 0; w < RB_THREADS / 64; ++w) t += s_wt[w][tid];
       s_run[tid] += t;
@@ -185,9 +215,22 @@ __global__ __launch_bounds__(RB_THREADS) void k_route_write(RouteK a) {
   }
 }
 
-__device__ __forceinline__ int peer_count(const int32_t* ids, int r, int cap) {
-  const int c = ids[(size_t)r * cap];
+// Count of a class block starting at ids[off] with `cap` slots (count included).
+__device__ __forceinline__ int block_count(const int32_t* ids, size_t off, int cap) {
+  const int c = ids[off];
   return c < 0 ? 0 : (c > cap - 1 ? cap - 1 : c);
+}
+
+// Entry e of the [P][blk] id / gradient blocks: peer r, class c, slot j of the class
+// block (1.. its count), and its count; false for count slots and unused slots.
+__device__ __forceinline__ bool entry_of(const gtr_shard& sh, const int32_t* ids, int64_t e, int& r, int& c, int& j) {
+  const int blk = sh.cap + sh.cap_s;
+  r = (int)(e / blk);
+  const int jj = (int)(e - (int64_t)r * blk);
+  c = jj >= sh.cap ? 1 : 0;
+  j = c ? jj - sh.cap : jj;
+  if (r >= sh.world || j < 1) return false;
+  return j <= block_count(ids, (size_t)r * blk + (c ? sh.cap : 0), c ? sh.cap_s : sh.cap);
 }
 
 // Owner side, step t: every requested row as it stands after step t-1, into its slot of
@@ -204,9 +247,11 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_shard_serve(gtr_shard sh, const i
   const int64_t gid = (int64_t)blockIdx.x * GTR_BLOCK + threadIdx.x;
   const int64_t e = gid / C4;
   const int c = (int)(gid - e * C4);
-  const int r = (int)(e / sh.cap), j = (int)(e - (int64_t)r * sh.cap);
-  if (r >= sh.world || j < 1 || j > peer_count(recv_ids, r, sh.cap)) return;
+  int r, cls, j;
+  if (!entry_of(sh, recv_ids, e, r, cls, j)) return;
   const int local = recv_ids[e] / sh.world;
+  // class 0 rows -> send_rows [P][cap][D], class 1 -> send_rows + P cap D, [P][cap_s][D]
+  const int64_t orow = cls ? (int64_t)sh.world * sh.cap + (int64_t)r * sh.cap_s + j : (int64_t)r * sh.cap + j;
   const int32_t t = (int32_t)(*sh.opt.step_dev + sh.opt.step_offset);
   const int old = sh.stamp[local];
   const size_t at = (size_t)local * C4 + c;
@@ -216,7 +261,13 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_shard_serve(gtr_shard sh, const i
     float4 v = reinterpret_cast<const float4*>(sh.v)[at];
     catch_up4(p, m, v, old, t - 1, sh.opt, sh.consts);
   }
-  reinterpret_cast<float4*>(send_rows)[e * C4 + c] = p;
+  reinterpret_cast<float4*>(send_rows)[orow * C4 + c] = p;
+}
+
+// The gradient row of id-block slot g ([P][blk] slots) in a [P][grad_stride] buffer.
+__device__ __forceinline__ int64_t grad_row_off(int64_t g, int blk, int64_t grad_stride, int D) {
+  const int64_t q = g / blk;
+  return q * grad_stride + (g - q * blk) * D;
 }
 
 struct PackK {
@@ -225,6 +276,8 @@ struct PackK {
   const int32_t* ckeys;
   float* send_grads;
   float* small_pack;
+  int64_t grad_stride, small_stride;
+  int blk, world, rows_part, small_part;
   const int32_t* status;  // this rank's overflow flag of the step (status[0]) -> small_pack[F + 1]
   int T, nb_rows, nseg, m_cap;
   int windowed, pad0;  // 1 (m_cap > GTR_BEGIN_MCAP): rows part = one block per TW-slot window
@@ -261,7 +314,7 @@ __device__ __forceinline__ void shard_pack_window(int w, const PackK& a) {
     if (key > 0)  // padding_idx = 0: no gradient (the owner still applies g = 0)
       g = window_segment_sum<D>(a.bt, sk, a.tl.svals, a.tl.dx0, a.tl.se, a.tl.coef_tgt, a.tl.coef_neg, a.tl.carry, w,
                                 s0, e, w1, a.m_cap, key, gl, gb);
-    reinterpret_cast<float4*>(a.send_grads)[(size_t)ck * C4 + gl] = g;
+    reinterpret_cast<float4*>(a.send_grads + grad_row_off(ck, a.blk, a.grad_stride, D))[gl] = g;
   }
 }
 
@@ -301,7 +354,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_shard_pack(PackK a) {
       g = piece_sum<D>(a.bt, a.tl.svals, i, e, a.tl.dx0, a.tl.se, a.tl.coef_tgt, a.tl.coef_neg, gl, gb);
     if (start) {
       const int ck = a.ckeys[i];
-      if (ck >= 0) reinterpret_cast<float4*>(a.send_grads)[(size_t)ck * C4 + gl] = g;
+      if (ck >= 0) reinterpret_cast<float4*>(a.send_grads + grad_row_off(ck, a.blk, a.grad_stride, D))[gl] = g;
     }
     (void)lane;
     return;
@@ -310,6 +363,14 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_shard_pack(PackK a) {
   const AdamStep unused{};
   small_body((int64_t)sb * GTR_BLOCK + tid, a.segs, a.nseg, a.bt.hdr, nullptr, nullptr, nullptr, a.small_pack,
              unused);
+  if (a.small_stride > 0) {  // the small pack rides in every peer's gradient block
+    __syncthreads();
+    const int64_t e = (int64_t)sb * GTR_BLOCK + tid;
+    if (e < a.tl.flat_total) {
+      const float v = a.small_pack[e];  // this thread's own write above (same thread)
+      for (int q = 1; q < a.world; ++q) a.small_pack[q * a.small_stride + e] = v;
+    }
+  }
   if (sb == 0) {  // local loss after the flat gradient
     float acc = 0.0f;
     if (a.tl.loss_part)
@@ -324,22 +385,34 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_shard_pack(PackK a) {
       } else {
         t = a.tl.loss_out[0];
       }
-      a.small_pack[a.tl.flat_total] = t;
-      a.small_pack[a.tl.flat_total + 1] = a.status[0] != 0 ? 1.0f : 0.0f;
+      const float flag = a.status[0] != 0 ? 1.0f : 0.0f;
+      for (int q = 0; q < (a.small_stride > 0 ? a.world : 1); ++q) {
+        a.small_pack[q * a.small_stride + a.tl.flat_total] = t;
+        a.small_pack[q * a.small_stride + a.tl.flat_total + 1] = flag;
+      }
     }
   }
 }
 
-// Position of `key` among peer r's requested ids (ascending, slots 1..count), or -1.
-__device__ __forceinline__ int peer_find(const int32_t* ids, int r, int cap, int key) {
-  const int32_t* p = ids + (size_t)r * cap + 1;
-  int lo = 0, hi = peer_count(ids, r, cap);
+// Position of `key` in a class block of ascending ids (slots 1..count) at ids[off], or -1.
+__device__ __forceinline__ int block_find(const int32_t* ids, size_t off, int cap, int key) {
+  const int32_t* p = ids + off + 1;
+  int lo = 0, hi = block_count(ids, off, cap);
   const int n = hi;
   while (lo < hi) {
     const int mid = (lo + hi) >> 1;
     if (p[mid] < key) lo = mid + 1; else hi = mid;
   }
   return (lo < n && p[lo] == key) ? lo + 1 : -1;
+}
+
+// Slot of `key` in peer r's id block (either class), or -1.
+__device__ __forceinline__ int peer_find(const gtr_shard& sh, const int32_t* ids, int r, int key) {
+  const int blk = sh.cap + sh.cap_s;
+  const int p0 = block_find(ids, (size_t)r * blk, sh.cap, key);
+  if (p0 >= 0 || sh.cap_s == 0) return p0;
+  const int p1 = block_find(ids, (size_t)r * blk + sh.cap, sh.cap_s, key);
+  return p1 >= 0 ? sh.cap + p1 : -1;
 }
 
 struct UpdateK {
@@ -382,16 +455,18 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_shard_update(UpdateK a) {
     const int64_t gid = (int64_t)blockIdx.x * GTR_BLOCK + tid;
     const int64_t e = gid / C4;
     const int c = (int)(gid - e * C4);
-    const int r = (int)(e / sh.cap), j = (int)(e - (int64_t)r * sh.cap);
-    if (r >= W || j < 1 || j > peer_count(a.recv_ids, r, sh.cap)) return;
+    int r, cls, j;
+    if (!entry_of(sh, a.recv_ids, e, r, cls, j)) return;
+    const int blk = sh.cap + sh.cap_s;
     const int key = a.recv_ids[e];
     for (int q = 0; q < r; ++q)
-      if (peer_find(a.recv_ids, q, sh.cap, key) >= 0) return;  // a lower rank leads this row
+      if (peer_find(sh, a.recv_ids, q, key) >= 0) return;  // a lower rank leads this row
+    const int64_t gs = sh.grad_stride > 0 ? sh.grad_stride : (int64_t)blk * D;
     float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int q = r; q < W; ++q) {
-      const int at = q == r ? j : peer_find(a.recv_ids, q, sh.cap, key);
+      const int at = q == r ? (int)(e - (int64_t)r * blk) : peer_find(sh, a.recv_ids, q, key);
       if (at < 0) continue;
-      const float4 v = reinterpret_cast<const float4*>(a.recv_grads)[((size_t)q * sh.cap + at) * C4 + c];
+      const float4 v = reinterpret_cast<const float4*>(a.recv_grads + q * gs + (int64_t)at * D)[c];
       g.x += v.x; g.y += v.y; g.z += v.z; g.w += v.w;
     }
     g.x *= inv_w; g.y *= inv_w; g.z *= inv_w; g.w *= inv_w;
@@ -434,6 +509,7 @@ __global__ __launch_bounds__(GTR_BLOCK) void k_shard_update(UpdateK a) {
 
 bool shard_ok(const gtr_shard* s) {
   return s && s->world >= 1 && s->world <= SH_MAXP && s->rank >= 0 && s->rank < s->world && s->cap >= 2 &&
+         (s->cap_s == 0 || (s->cap_s >= 2 && s->node_mark)) && s->grad_stride >= 0 && s->small_stride >= 0 &&
          s->num_items > 0 && s->local_rows == (s->num_items - s->rank + s->world - 1) / s->world &&
          (s->dim == 32 || s->dim == 64 || s->dim == 128 || s->dim == 256) && s->table && s->m && s->v && s->stamp &&
          s->consts && s->consts_cap > 0 && s->status && s->opt.step_dev;
@@ -449,7 +525,7 @@ int gtr_shard_route_scratch(int m_cap, int world, size_t* bytes) {
     return GTR_E_ARG;
   }
   // [nblk][P] block counts + the arrival ticket (64-byte aligned slot after them)
-  *bytes = (((size_t)((m_cap + RB_SLOTS - 1) / RB_SLOTS) * world * sizeof(int32_t) + 63) & ~(size_t)63) + 64;
+  *bytes = (((size_t)((m_cap + RB_SLOTS - 1) / RB_SLOTS) * 2 * world * sizeof(int32_t) + 63) & ~(size_t)63) + 64;
   return GTR_OK;
 }
 
@@ -469,9 +545,13 @@ int gtr_shard_route(const gtr_batch* bt, const int32_t* skeys, const int32_t* sv
   k.pe_tab = pe_tab; k.node_pe = node_pe; k.pe_k = node_pe ? pe_k : 0;
   k.status = sh->status;
   k.T = sh->num_items; k.P = sh->world; k.cap = sh->cap;
+  k.cap_s = sh->cap_s; k.blk = sh->cap + sh->cap_s; k.ncls = sh->cap_s > 0 ? 2 : 1; k.n_cap = bt->n_cap;
+  k.node_mark = sh->node_mark;
+  k.step_dev = sh->opt.step_dev;
+  k.step_offset = (int)sh->opt.step_offset;
   k.m_cap = bt->n_cap + bt->b_cap * (1 + bt->n_neg);
   k.nblk = (k.m_cap + RB_SLOTS - 1) / RB_SLOTS;
-  const size_t cnt_bytes = ((size_t)k.nblk * k.P * sizeof(int32_t) + 63) & ~(size_t)63;
+  const size_t cnt_bytes = ((size_t)k.nblk * k.ncls * k.P * sizeof(int32_t) + 63) & ~(size_t)63;
   if (scratch_bytes < cnt_bytes + 64) {
     set_error("gtr_shard_route: scratch of %zu bytes < %zu", scratch_bytes, cnt_bytes + 64);
     return GTR_E_ARG;
@@ -492,7 +572,7 @@ int gtr_shard_serve(const gtr_shard* sh, const int32_t* recv_ids, float* send_ro
     return GTR_E_ARG;
   }
   hipStream_t s = (hipStream_t)stream;
-  const int64_t entries = (int64_t)sh->world * sh->cap;
+  const int64_t entries = (int64_t)sh->world * (sh->cap + sh->cap_s);
   const int64_t threads = entries * (sh->dim / 4);
   const dim3 grid((unsigned)((threads + GTR_BLOCK - 1) / GTR_BLOCK));
   switch (sh->dim) {
@@ -519,6 +599,12 @@ int gtr_shard_pack(const gtr_batch* bt, const gtr_shard* sh, const gtr_tail* tai
   k.ckeys = ckeys;
   k.send_grads = send_grads;
   k.small_pack = small_pack;
+  k.blk = sh->cap + sh->cap_s;
+  k.world = sh->world;
+  k.grad_stride = sh->grad_stride > 0 ? sh->grad_stride : (int64_t)k.blk * sh->dim;
+  k.small_stride = sh->small_stride;
+  k.rows_part = sh->pack_parts == 0 || (sh->pack_parts & 1);
+  k.small_part = sh->pack_parts == 0 || (sh->pack_parts & 2);
   k.status = sh->status;
   k.T = sh->num_items;
   k.m_cap = bt->n_cap + bt->b_cap * (1 + bt->n_neg);
@@ -526,7 +612,9 @@ int gtr_shard_pack(const gtr_batch* bt, const gtr_shard* sh, const gtr_tail* tai
   // large batches: windowed segment sums (one block per window + carries), bitwise the
   // single-GPU tail's and the data-parallel pack's order
   k.windowed = k.m_cap > GTR_BEGIN_MCAP ? 1 : 0;
-  if (k.windowed) {
+  if (!k.rows_part) {
+    k.nb_rows = 0;  // the small part only (launched after the weight gradients)
+  } else if (k.windowed) {
     if (!tail->carry) {
       set_error("gtr_shard_pack: large batch (m_cap > %d) needs the carry scratch", GTR_BEGIN_MCAP);
       return GTR_E_ARG;
@@ -551,6 +639,8 @@ int gtr_shard_pack(const gtr_batch* bt, const gtr_shard* sh, const gtr_tail* tai
   for (int i = 0; i < nseg; ++i) k.segs[i] = segs[i];
   int nb_small = (int)((tail->flat_total + GTR_BLOCK - 1) / GTR_BLOCK);
   if (nb_small == 0) nb_small = 1;
+  if (!k.small_part) nb_small = 0;
+  if (k.nb_rows + nb_small == 0) return GTR_OK;
   const dim3 grid(k.nb_rows + nb_small);
   switch (sh->dim) {
     case 32: hipLaunchKernelGGL(k_shard_pack<32>, grid, dim3(GTR_BLOCK), 0, s, k); break;
@@ -576,7 +666,7 @@ int gtr_shard_update(const gtr_shard* sh, const gtr_tail* tail, const int32_t* r
   k.recv_grads = recv_grads;
   k.small_all = small_all;
   k.small_words = small_words;
-  const int64_t entries = (int64_t)sh->world * sh->cap;
+  const int64_t entries = (int64_t)sh->world * (sh->cap + sh->cap_s);
   k.nb_rows = (int)((entries * (sh->dim / 4) + GTR_BLOCK - 1) / GTR_BLOCK);
   const int nb_small = (int)((tail->flat_total + 1 + GTR_BLOCK - 1) / GTR_BLOCK);
   const dim3 grid(k.nb_rows + nb_small);

@@ -101,7 +101,7 @@ class GtrTail(C.Structure):
 
 
 SWEEP_SLOTS = 8
-ABI_VERSION = 7  # GTR_ABI_VERSION of include/gtr.h
+ABI_VERSION = 8  # GTR_ABI_VERSION of include/gtr.h
 
 
 class GtrLazy(C.Structure):
@@ -134,8 +134,9 @@ class GtrDpLayout(C.Structure):
 class GtrShard(C.Structure):
     _fields_ = [
         ("num_items", i32), ("world", i32), ("rank", i32), ("cap", i32), ("local_rows", i32), ("dim", i32),
-        ("table", P), ("m", P), ("v", P), ("stamp", P), ("consts", P), ("consts_cap", i32), ("pad", i32),
-        ("status", P), ("opt", GtrAdam),
+        ("table", P), ("m", P), ("v", P), ("stamp", P), ("consts", P), ("consts_cap", i32), ("cap_s", i32),
+        ("status", P), ("opt", GtrAdam), ("node_mark", P), ("grad_stride", i64), ("small_stride", i64),
+        ("pack_parts", i32), ("pad1", i32),
     ]
 
 

@@ -589,19 +589,34 @@ class FusedTrainStep:
             sh.route(bs, st())
 
         def fwd(l):
-            eng.layer_fwd(ws, cfg, bc, l, eng.fill_embed(tab), st(), self.split)
+            with sh.side():  # beside the class-1 (scoring) rows' exchange when forked
+                eng.layer_fwd(ws, cfg, bc, l, eng.fill_embed(tab), st(), self.split)
 
         def head():
+            sh.join()
             eng.run_head(ws, cfg, bc, L.RO_FWD | L.RO_LOSS | L.RO_BWD, self.loss_kind, self.temperature, self.alpha,
                          table=tab)
+
+        # the scoring rows beside the forward and the gradient rows beside the weight
+        # gradients: RCCL, the step captured whole (or eager) -- never across the
+        # boundaries of separately captured pieces
+        overlap = sh.can_overlap and (not self.use_graph or self._graph_collectives())
 
         def bwd(l):
             eng.layer_bwd(ws, cfg, bc, l, st(), self.split)
             if l == 0:
-                eng._wgrad(ws, cfg, bc, 0, Lc, st())
-                sh.pack(bs, st())
+                if overlap:  # gradient rows packed first; they travel beside the weight gradients
+                    sh.pack(bs, st(), parts=1)
+                    sh.fork()
+                    with sh.side():
+                        eng._wgrad(ws, cfg, bc, 0, Lc, st())
+                        sh.pack(bs, st(), parts=2)
+                else:
+                    eng._wgrad(ws, cfg, bc, 0, Lc, st())
+                    sh.pack(bs, st())
 
-        pieces = [(begin_route, sh.exchange_ids), (lambda: sh.serve(st()), sh.exchange_rows)]
+        last = sh.exchange_grads
+        pieces = [(begin_route, sh.exchange_ids), (lambda: sh.serve(st()), lambda: sh.exchange_rows(overlap))]
         if not self.sync_bn:
             def middle():
                 for l in range(Lc):
@@ -609,14 +624,14 @@ class FusedTrainStep:
                 head()
                 for l in range(Lc - 1, -1, -1):
                     bwd(l)
-            pieces.append((middle, sh.exchange_grads))
+            pieces.append((middle, last))
         else:
             for l in range(Lc):
-                pieces.append(((lambda l=l: fwd(l)), (lambda l=l: self._gather_fwd(l))))
+                pieces.append(((lambda l=l: fwd(l)), (lambda l=l: (sh.join(), self._gather_fwd(l)))))
             pieces.append((head, lambda: self._gather_bwd(Lc - 1)))
             for l in range(Lc - 1, 0, -1):
                 pieces.append(((lambda l=l: bwd(l)), (lambda l=l: self._gather_bwd(l - 1))))
-            pieces.append(((lambda: bwd(0)), sh.exchange_grads))
+            pieces.append(((lambda: bwd(0)), last))
         pieces.append((lambda: sh.update(st()), None))
         return pieces
 

@@ -29,6 +29,7 @@ with the lazy table (same per-rank sums, same rank-ordered averaging, same catch
 
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import math
 import os
@@ -79,6 +80,14 @@ class ShardState:
         self.stale = False  # the model's item_embedding.weight lags the shards
         self.s = L.GtrShard()
         self._alloc_consts(1 << 12)
+        # rows a node of the batch reads, stamped with the step (two-class exchange)
+        self.node_mark = torch.zeros(T, dtype=torch.int32, device=dev)
+        self.s.node_mark = self.node_mark.data_ptr()
+        # collectives that overlap compute need a device transport (RCCL): gloo stages
+        # through the host in line with the step
+        import torch.distributed as dist
+
+        self.device_collectives = dist.is_available() and dist.is_initialized() and dist.get_backend(group) == "nccl"
 
     def _alloc_consts(self, cap: int):
         c = torch.zeros(cap, 2, dtype=torch.float32, device=self.step.dev)
@@ -168,21 +177,41 @@ class ShardExchange:
         eng, caps, dev = step.eng, step.caps, step.dev
         P, D = state.world, eng.D
         self.m_cap = caps.n_cap + caps.b_cap * (1 + caps.n_neg)
-        self.cap = shard_capacity(self.m_cap, eng.T, P)
-        state.s.cap = self.cap
-        slots = P * self.cap
+        # two row classes (include/gtr.h gtr_shard): class 0 = rows a node reads (layer 0
+        # needs them), class 1 = rows only the scoring readout reads, which travel during
+        # the forward; default at P > 1 (GTR_SHARD_SPLIT=0 / 1 overrides)
+        e = os.environ.get("GTR_SHARD_SPLIT")
+        self.split = (e == "1") if e is not None else P > 1
+        if self.split:
+            self.cap = shard_capacity(caps.n_cap, eng.T, P)
+            self.cap_s = shard_capacity(self.m_cap, eng.T, P)
+        else:
+            self.cap = shard_capacity(self.m_cap, eng.T, P)
+            self.cap_s = 0
+        self.blk = self.cap + self.cap_s
+        state.s.cap, state.s.cap_s = self.cap, self.cap_s
+        state.s.grad_stride, state.s.small_stride, state.s.pack_parts = 0, 0, 0
+        slots = P * self.blk
+        rows = P * self.cap + P * self.cap_s
         i32 = dict(dtype=torch.int32, device=dev)
         f32 = dict(dtype=torch.float32, device=dev)
         # one rank: nothing crosses a link, so every receive buffer IS its send buffer and
         # the exchanges are no-ops (no 2 x slots x D copies per step; the kernels never read
-        # and write the same buffer of a pair in one launch)
-        self.alias = P == 1
+        # and write the same buffer of a pair in one launch); GTR_SHARD_NOALIAS=1 keeps the
+        # copies (a one-rank rehearsal of the collectives and their overlap)
+        self.alias = P == 1 and os.environ.get("GTR_SHARD_NOALIAS") != "1"
         self.send_ids = torch.zeros(slots, **i32)
         self.recv_ids = self.send_ids if self.alias else torch.zeros(slots, **i32)
-        self.send_rows = torch.zeros(slots, D, **f32)
-        self.recv_rows = self.send_rows if self.alias else torch.zeros(slots, D, **f32)  # the compact "table"
+        self.send_rows = torch.zeros(rows, D, **f32)
+        self.recv_rows = self.send_rows if self.alias else torch.zeros(rows, D, **f32)  # the compact "table"
         self.send_grads = torch.zeros(slots, D, **f32)
         self.recv_grads = self.send_grads if self.alias else torch.zeros(slots, D, **f32)
+        # overlap: a compute stream forked from the step's stream beside a collective; the
+        # collective itself stays on the step's stream (RCCL captured on a forked stream
+        # does not survive hipGraph capture on this stack -- scripts/dbg/capture_probe.py)
+        self.can_overlap = not self.alias and state.device_collectives
+        self.cs = torch.cuda.Stream(dev) if self.can_overlap else None
+        self.forked = False
         self.ckeys = torch.zeros(self.m_cap, **i32)
         self.node_item_c = torch.zeros(caps.n_cap, **i32)
         self.target_c = torch.zeros(caps.b_cap, **i32)
@@ -197,6 +226,21 @@ class ShardExchange:
         self.small_pack = self.small_all[0] if self.alias else torch.zeros(self.small_words, **f32)
         self.bs_c = self._compact(step.bs)
         self.bs_c_pe = self._compact(step.bs_pe) if step.bs_pe is not None else None
+
+    def fork(self):
+        """Compute launched under ``side()`` from here on runs on the compute stream, after
+        the work queued so far; collectives queued next on the step's stream run beside it."""
+        self.cs.wait_stream(torch.cuda.current_stream(self.step.dev))
+        self.forked = True
+
+    def side(self):
+        return torch.cuda.stream(self.cs) if self.forked else contextlib.nullcontext()
+
+    def join(self):
+        """The step's stream waits for the compute forked since ``fork``."""
+        if self.forked:
+            torch.cuda.current_stream(self.step.dev).wait_stream(self.cs)
+            self.forked = False
 
     def _compact(self, bs):
         """The batch struct the layer kernels read: ids -> compact rows; PE per node."""
@@ -236,19 +280,38 @@ class ShardExchange:
         L.check(L.lib().gtr_shard_serve(C.byref(self.state.s), self.recv_ids.data_ptr(), self.send_rows.data_ptr(),
                                         stream), "shard_serve")
 
-    def exchange_rows(self):
-        if not self.alias:
-            all_to_all(self.recv_rows, self.send_rows, self.state.group)
+    def exchange_rows(self, overlap: bool = False):
+        """The rows layer 0 needs (class 0), then the class-1 rows -- beside the forward
+        when ``overlap`` (the forward forked onto the compute stream, joined before the
+        readout).  One class: all rows at once."""
+        if self.alias:
+            return
+        n = self.state.world * self.cap
+        all_to_all(self.recv_rows[:n], self.send_rows[:n], self.state.group)
+        if self.cap_s:
+            if overlap and self.can_overlap:
+                self.fork()
+            all_to_all(self.recv_rows[n:], self.send_rows[n:], self.state.group)
 
-    def pack(self, bs, stream):
+    def pack(self, bs, stream, parts: int = 0):
+        """parts: 1 the gradient rows, 2 the small-parameter pack (after the weight
+        gradients), 0 both."""
         st = self.step
-        L.check(L.lib().gtr_shard_pack(C.byref(bs), C.byref(self.state.s), C.byref(st.tail), self.ckeys.data_ptr(),
-                                       st.segs, st.nseg, self.send_grads.data_ptr(), self.small_pack.data_ptr(),
-                                       stream), "shard_pack")
+        self.state.s.pack_parts = parts
+        try:
+            L.check(L.lib().gtr_shard_pack(C.byref(bs), C.byref(self.state.s), C.byref(st.tail), self.ckeys.data_ptr(),
+                                           st.segs, st.nseg, self.send_grads.data_ptr(), self.small_pack.data_ptr(),
+                                           stream), "shard_pack")
+        finally:
+            self.state.s.pack_parts = 0
 
     def exchange_grads(self):
+        """The gradient rows' all-to-all (beside the forked weight gradients + small pack
+        when overlapping), the join, then the all-gather of the small packs."""
         if not self.alias:
             all_to_all(self.recv_grads, self.send_grads, self.state.group)
+        self.join()
+        if not self.alias:
             all_gather_packs(self.small_all, self.small_pack, self.state.group)
 
     def update(self, stream):
@@ -261,5 +324,6 @@ class ShardExchange:
     def volume(self) -> dict:
         """Bytes each rank sends per step over the collectives (fixed-size blocks)."""
         P, D = self.state.world, self.step.eng.D
-        return {"ids": 4 * P * self.cap, "rows": 4 * P * self.cap * D, "grads": 4 * P * self.cap * D,
-                "small": 4 * self.small_words * P, "cap": self.cap}
+        return {"ids": 4 * P * self.blk, "rows_layer0": 4 * P * self.cap * D, "rows_scoring": 4 * P * self.cap_s * D,
+                "grads": 4 * P * self.blk * D, "small": 4 * self.small_words * P, "cap": self.cap,
+                "cap_scoring": self.cap_s, "overlap_capable": self.can_overlap}

@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define GTR_ABI_VERSION 7 /* 7: gtr_tail.loss_acc; 6: gtr_layer.ffn + gtr_ffn_fwd / gtr_ffn_bwd / gtr_ffn_wgrad (the FFN variant); 5: gtr_config.loss_batch / wfold_stride, gtr_layer.wfold, gtr_segment.live_groups, hdr[6] halo source rows; 4: gtr_step_tail_wgrad on split-K slabs; 3: gtr_config.begin / ctr_add, gtr_tail.rng_inc */
+#define GTR_ABI_VERSION 8 /* 8: gtr_shard.cap_s / grad_stride / small_stride / pack_parts / node_mark (two-class exchange); 7: gtr_tail.loss_acc; 6: gtr_layer.ffn + gtr_ffn_fwd / gtr_ffn_bwd / gtr_ffn_wgrad (the FFN variant); 5: gtr_config.loss_batch / wfold_stride, gtr_layer.wfold, gtr_segment.live_groups, hdr[6] halo source rows; 4: gtr_step_tail_wgrad on split-K slabs; 3: gtr_config.begin / ctr_add, gtr_tail.rng_inc */
 
 #define GTR_OK 0
 #define GTR_E_ARG 1001      /* bad argument / unsupported shape */
@@ -543,13 +543,19 @@ int gtr_dp_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tai
  * Replaces, across P ranks, the one dense nn.Embedding(T, d) of base.py:36 and its dense
  * AdamW state (train_baseline.py:252-256): global row r lives on rank r % P as local row
  * r / P, with its exp_avg / exp_avg_sq and a lazy-table stamp (gtr_lazy semantics: the
- * step through which the row is current).  Exchange buffers are [P][cap] blocks whose
- * slot 0 holds the block's count; "compact" row q*cap + 1 + j of a requester's fetched
- * rows is the j-th (ascending) row it requested from owner q.  A step:
+ * step through which the row is current).  A step:
  *   gtr_step_begin (global keys, stamp NULL) -> gtr_shard_route -> all-to-all send_ids
  *   -> gtr_shard_serve -> all-to-all send_rows -> forward/backward on the compact batch
  *   (table = fetched rows) -> gtr_shard_pack -> all-to-all send_grads + all-gather of
- *   small_pack -> gtr_shard_update.                                                   */
+ *   small_pack -> gtr_shard_update.
+ * Rows come in two classes when cap_s > 0: class 0 = rows some node of the batch reads
+ * (needed by layer 0), class 1 = rows only the scoring readout reads (targets /
+ * negatives: needed after the layers), so the class-1 rows can travel during the forward.
+ * Per peer q, the id and gradient blocks hold blk = cap + cap_s slots: class 0 at
+ * [0, cap) (slot 0 its count), class 1 at [cap, blk) (slot cap its count); ids ascending
+ * per class.  The fetched-row buffer ("compact table") is [P*cap + P*cap_s][D]: class-0
+ * row j of owner q at q*cap + j, class-1 row j at P*cap + q*cap_s + j, so each class is
+ * one [P][cap_c][D] all-to-all.  cap_s = 0: one class, blk = cap (all rows class 0).   */
 typedef struct gtr_shard {
   int32_t num_items;   /* T (global rows)                                       */
   int32_t world;       /* P (<= 16)                                             */
@@ -563,10 +569,16 @@ typedef struct gtr_shard {
   int32_t* stamp;      /* [local_rows] step through which the row is current   */
   float* consts;       /* [consts_cap][2] per-step AdamW scalars (gtr_lazy)     */
   int32_t consts_cap;
-  int32_t pad;
+  int32_t cap_s;       /* class-1 slots per peer block (count included); 0: one class */
   int32_t* status;     /* [2]: [0] this step overflowed a block, [1] sticky:
                         * bit 0 this rank overflowed, bit 1 some rank did      */
   gtr_adam opt;        /* by value; step_offset 0 (runs after gtr_step_begin)   */
+  int32_t* node_mark;  /* [T] scratch (cap_s > 0): step stamp of the rows a node reads */
+  int64_t grad_stride; /* floats per peer block of send_grads / recv_grads (0: blk*D) */
+  int64_t small_stride;/* > 0: gtr_shard_pack writes small_pack P times, q*small_stride
+                          apart (the small pack riding in each peer's gradient block) */
+  int32_t pack_parts;  /* gtr_shard_pack: 1 the rows part, 2 the small part, 0 / 3 both */
+  int32_t pad1;
 } gtr_shard;
 
 /* Bytes of route scratch at contribution capacity m_cap.                            */

@@ -46,7 +46,7 @@ def test_python_binding_matches_header(libpath):
 
     assert set(_lib.EXPORTS) == set(header_functions())
     lib = _lib.lib()
-    assert lib.gtr_abi_version() == _lib.ABI_VERSION == 7
+    assert lib.gtr_abi_version() == _lib.ABI_VERSION == 8
     assert lib.gtr_version() >= 100
 
 
