@@ -136,6 +136,10 @@ def main():
     ap.add_argument("--shard-table", action="store_true",
                     help="row-sharded item table + AdamW state (rank p owns rows r %% P == p), rows and row "
                          "gradients by all-to-all (etpgt.train.sharded)")
+    ap.add_argument("--fit-blocks", type=int, default=1,
+                    help="row-sharded table: exchange blocks sized to the staged batches' distinct rows per "
+                         "owner (FusedTrainStep.fit_shard_blocks; the ranks agree on the maximum) instead of the "
+                         "static bound (1/0)")
     ap.add_argument("--lazy", type=int, default=None,
                     help="deferred zero-gradient AdamW of untouched table rows (1/0; default: per config)")
     ap.add_argument("--lagged", type=int, default=None,
@@ -226,7 +230,8 @@ def main():
     lagged = (bool(args.lagged) if args.lagged is not None else dp_on) and not lazy and not shard
     w = build_workload(args.config, args.batch_size, args.num_batches, dev, rank, use_graph=not args.no_graph,
                        data_parallel=True if (args.dp or args.sync_bn) else None, lazy=lazy,
-                       sync_bn=args.sync_bn and world > 1, lagged=lagged, shard_table=shard)
+                       sync_bn=args.sync_bn and world > 1, lagged=lagged, shard_table=shard,
+                       fit_blocks=bool(args.fit_blocks))
     step, staged, batches, data, T, B, touched, st = (w[k] for k in ("step", "staged", "batches", "data", "T", "B",
                                                                    "touched", "stats"))
     log(f"data: T={T} sessions={data.num_sessions} edges={data.edge_keys.size} setup {time.time()-t0:.1f}s {st}")
@@ -384,7 +389,9 @@ def main():
                              else "external (torchrun / torch.distributed.run)" if "WORLD_SIZE" in os.environ
                              else "none (one process)"),
                 "dp_exchange": ("row-sharded table: all-to-all of row ids, rows and row gradients "
-                                f"({step.shard.volume()})") if shard else step.dp is not None,
+                                f"({step.shard.volume()}; blocks "
+                                + ("fitted to the staged batches" if args.fit_blocks else "static bound") + ")")
+                               if shard else step.dp is not None,
                 "hip_graph": not args.no_graph,
                 "batch_images": "resident, one graph per image" if resident else "copied per step (D2D)",
                 "step_graph": (f"{seq[3]} consecutive steps per hipGraph launch ({seq[1]} x {seq[3]}"
@@ -529,7 +536,7 @@ def strong_scaling_legs(world: int, global_batches: list, steps: int = 0) -> dic
 
 def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, use_graph: bool = True,
                    data_parallel: bool | None = None, lazy: bool = False, sync_bn: bool = False,
-                   lagged: bool = False, shard_table: bool = False) -> dict:
+                   lagged: bool = False, shard_table: bool = False, fit_blocks: bool = False) -> dict:
     """Synthetic RetailRocket-shaped data, the model of `config`, a bound fused step
     and `num_batches` packed batches pre-staged in HBM."""
     from etpgt.data.batch import Caps
@@ -560,6 +567,8 @@ def build_workload(config: str, B: int, num_batches: int, dev, rank: int = 0, us
     caps = Caps(max(b.num_nodes for b in batches), B, max(b.num_edges for b in batches), cfg["n_neg"])
     step._bind(caps)  # data parallel: the ranks agree on the largest capacities
     caps = step.caps
+    if shard_table and fit_blocks:  # exchange blocks sized to these batches (collective)
+        step.fit_shard_blocks(batches)
     staged = [torch.from_numpy(b.packed(caps)[1]).to(dev) for b in batches]
     touched = float(np.mean([len(set(b.x.tolist()) | set(b.target_item.tolist()) | set(b.negative_items.tolist()))
                              for b in batches]))

@@ -33,7 +33,7 @@ namespace {
 using namespace gtr;
 
 #define RB_THREADS 256
-#define RB_ROUNDS 4
+#define RB_ROUNDS 1
 #define RB_SLOTS (RB_THREADS * RB_ROUNDS)
 #define SH_MAXP 16
 

@@ -28,6 +28,7 @@ with the oracle's autograd gradients.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 
 import torch
@@ -184,8 +185,11 @@ class DpExchange:
         self.lay = DpLayout(eng.flat.layout.total, m_cap, eng.D, self.world)
         self.lay_s = self.lay.struct()
         dev = step.dev
-        self.pack = torch.zeros(self.lay.words, dtype=torch.float32, device=dev)
+        # one rank: the gathered packs ARE the rank's pack (no copy, no collective, and the
+        # step is one graph); GTR_DP_NOALIAS=1 keeps the RCCL all-gather (a one-rank rehearsal)
+        self.alias = self.world == 1 and os.environ.get("GTR_DP_NOALIAS") != "1"
         self.recv = torch.zeros(self.world, self.lay.words, dtype=torch.float32, device=dev)
+        self.pack = self.recv[0] if self.alias else torch.zeros(self.lay.words, dtype=torch.float32, device=dev)
         self.slot = torch.full((eng.T, self.world, 2), -1, dtype=torch.int32, device=dev)
 
     def launch_pack(self, bs, stream_handle):
@@ -194,7 +198,8 @@ class DpExchange:
                                     C.byref(self.lay_s), self.pack.data_ptr(), stream_handle), "dp_pack")
 
     def exchange(self):
-        all_gather_packs(self.recv, self.pack, self.group)
+        if not self.alias:
+            all_gather_packs(self.recv, self.pack, self.group)
 
     def launch_tail(self, bs, stream_handle):
         st = self.step

@@ -168,6 +168,32 @@ class FusedTrainStep:
         n, b, e = (int(v) for v in t.tolist())
         return Caps(n, b, e, caps.n_neg)
 
+    def fit_shard_blocks(self, batches):
+        """Row-sharded table: size the exchange blocks to the most distinct rows any rank
+        asks one owner for over ``batches`` (each rank passes its own; the ranks agree on
+        the maximum -- a collective) instead of the static bound of ``shard_capacity``
+        (the all-to-alls move whole blocks, so smaller blocks are less xGMI
+        traffic per step).  A later batch that needs more rows overflows its block: the
+        step is flagged and applied as a zero-gradient step, and the host raises at the
+        next check.  Rebuilds the exchange buffers: captured graphs go stale."""
+        if self.shard is None:
+            raise RuntimeError("fit_shard_blocks needs the row-sharded table (shard_table=True)")
+        from etpgt.train.sharded import ShardExchange, block_rows
+
+        r = block_rows(batches, self.world, self.shard.split)
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dev = self.dev if dist.get_backend(self.group) != "gloo" else "cpu"
+            t = torch.tensor(list(r), dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            r = tuple(int(v) for v in t.tolist())
+        self.shard = ShardExchange(self, self.shard_state, rows=r)
+        self.graph = self.graph_pe = self.graph_b = None
+        self.resident_graphs = None
+        self._gen += 1
+        return self.shard.cap, self.shard.cap_s
+
     def _bind(self, caps: Caps):
         eng = self.eng
         caps = self._agree(caps)
@@ -706,9 +732,26 @@ class FusedTrainStep:
 
         return dist.is_available() and dist.is_initialized() and dist.get_backend(self.group) == "nccl"
 
+    def _collective_free(self) -> bool:
+        """True when no piece of the step runs a real collective: one rank with aliased
+        exchange buffers (DpExchange.alias / ShardExchange.alias), no SyncBN gathers, no
+        early union -- the pieces then run as ONE graph, with no host launch between them."""
+        if self.sync_bn or self.early_union:
+            return False
+        if self.shard is not None:
+            return self.shard.alias
+        if self.dp is not None:
+            return self.dp.alias
+        return True
+
+    def _one_graph(self) -> bool:
+        """The whole step captured as one graph (collective-free, or RCCL collectives
+        captured inside it)."""
+        return self._collective_free() or self._graph_collectives()
+
     def _graph_pieces(self, with_pe: bool):
         pieces = self._pieces(with_pe)
-        if len(pieces) == 1 or not self._graph_collectives():
+        if len(pieces) == 1 or not self._one_graph():
             return pieces
 
         def whole():
@@ -830,11 +873,11 @@ class FusedTrainStep:
         (start + k) mod len(images) into the step's blob (the D2D copy ``load_blob`` makes)
         and running the step with its RCCL collectives, captured as ONE hipGraph.  Only
         where the collectives are captured in the step's graph anyway (RCCL, N > 1 or
-        GTR_GRAPH_COLL=1).  Every rank captures, then the ranks agree (all-reduce outside
+        GTR_GRAPH_COLL=1), or where the step has none (one rank, aliased exchange buffers).  Every rank captures, then the ranks agree (all-reduce outside
         any capture): if any rank's capture was refused, every rank returns None and keeps
         the per-step path.  The per-step constants (row-sharded table, lazy table) are
         grown first for ``reserve`` more steps (their pointers are captured)."""
-        if not self.use_graph or not self._graph_collectives():
+        if not self.use_graph or not self._one_graph():
             return None
         if n <= 0:
             raise ValueError("capture_steps_copied needs n >= 1")
@@ -848,7 +891,7 @@ class FusedTrainStep:
                 self.blob.copy_(images[(start + k) % nimg], non_blocking=True)
                 self._launch(False)
 
-        return self._capture_multi(fn, n, reserve, collective=True)
+        return self._capture_multi(fn, n, reserve, collective=not self._collective_free())
 
     def capture_steps_built(self, n: int, reserve: int = 0) -> dict | None:
         """``n`` consecutive steps over the attached device batch builder's next batches
@@ -864,14 +907,14 @@ class FusedTrainStep:
         if n <= 0:
             raise ValueError("capture_steps_built needs n >= 1")
         multi = self.dp is not None or self.shard is not None
-        if not self.use_graph or (multi and not self._graph_collectives()):
+        if not self.use_graph or (multi and not self._one_graph()):
             return None
 
         def fn():
             for _ in range(n):
                 self._launch(False)
 
-        return self._capture_multi(fn, n, reserve, collective=multi)
+        return self._capture_multi(fn, n, reserve, collective=multi and not self._collective_free())
 
     def _capture_multi(self, fn, n: int, reserve: int, collective: bool) -> dict | None:
         """Capture ``fn`` (n steps) as one graph after growing the per-step constants for

@@ -53,6 +53,31 @@ def shard_capacity(m_cap: int, num_items: int, world: int, slack: float | None =
     return 1 + min(exact, even)
 
 
+def block_rows(batches, world: int, split: bool) -> tuple[int, int]:
+    """The most distinct rows one rank asks one owner for in one step, over ``batches``
+    (host SessionBatch objects): (class 0, class 1) with two row classes -- class 0 the
+    rows a node of the batch reads, class 1 the rows only the scoring readout reads
+    (targets / negatives) -- or (all rows, 0) with one.  Owner of row r: r % world."""
+    import numpy as np
+
+    def arr(t):
+        return np.asarray(t.detach().cpu() if hasattr(t, "detach") else t, dtype=np.int64).reshape(-1)
+
+    def most(rows):
+        return int(np.bincount(rows % world, minlength=world).max()) if rows.size else 0
+
+    m0 = m1 = 0
+    for b in batches:
+        nodes = np.unique(arr(b.x))
+        score = np.unique(np.concatenate([arr(b.target_item), arr(b.negative_items)]))
+        if split:
+            m0 = max(m0, most(nodes))
+            m1 = max(m1, most(np.setdiff1d(score, nodes, assume_unique=True)))
+        else:
+            m0 = max(m0, most(np.union1d(nodes, score)))
+    return m0, m1
+
+
 class ShardState:
     """This rank's rows of the item table and their AdamW / lazy-table state."""
 
@@ -172,7 +197,10 @@ class ShardState:
 class ShardExchange:
     """Per-capacity exchange buffers and launches of the sharded step."""
 
-    def __init__(self, step, state: ShardState):
+    def __init__(self, step, state: ShardState, rows: tuple[int, int] | None = None):
+        """``rows``: (class 0, class 1) distinct rows per owner and step to size the blocks
+        for (``block_rows`` over the batches to run, agreed across the ranks --
+        ``FusedTrainStep.fit_shard_blocks``); None: the static bound ``shard_capacity``."""
         self.step, self.state = step, state
         eng, caps, dev = step.eng, step.caps, step.dev
         P, D = state.world, eng.D
@@ -188,6 +216,10 @@ class ShardExchange:
         else:
             self.cap = shard_capacity(self.m_cap, eng.T, P)
             self.cap_s = 0
+        if rows is not None:  # blocks sized to the batches (never above the static bound)
+            self.cap = max(2, min(self.cap, 1 + int(rows[0])))
+            if self.split:
+                self.cap_s = max(2, min(self.cap_s, 1 + int(rows[1])))
         self.blk = self.cap + self.cap_s
         state.s.cap, state.s.cap_s = self.cap, self.cap_s
         state.s.grad_stride, state.s.small_stride, state.s.pack_parts = 0, 0, 0

@@ -250,6 +250,33 @@ def test_shard_capacity_bounds():
     assert shard_capacity(107_000, 10**6, 8, slack=1.5) == 1 + 20_063 + 64  # 1.5 x the even share
 
 
+def test_block_rows_counts_distinct_rows_per_owner_and_class():
+    """block_rows (the fitted exchange blocks): per batch, the distinct rows of each owner
+    (r % P) in class 0 (rows a node reads) and class 1 (rows only targets / negatives
+    read), maximised over batches and owners -- checked against a brute-force count."""
+    import numpy as np
+
+    from etpgt.train.sharded import block_rows
+
+    class B:
+        def __init__(self, x, t, n):
+            self.x, self.target_item, self.negative_items = torch.tensor(x), torch.tensor(t), torch.tensor(n)
+
+    rng = np.random.default_rng(3)
+    bl = [B(rng.integers(1, 200, 30), rng.integers(1, 200, 8), rng.integers(1, 200, (8, 12))) for _ in range(4)]
+    for P in (1, 3, 8):
+        w0 = w1 = wa = 0
+        for b in bl:
+            nodes = set(b.x.tolist())
+            score = set(b.target_item.tolist()) | set(b.negative_items.reshape(-1).tolist())
+            for q in range(P):
+                w0 = max(w0, sum(1 for r in nodes if r % P == q))
+                w1 = max(w1, sum(1 for r in score - nodes if r % P == q))
+                wa = max(wa, sum(1 for r in nodes | score if r % P == q))
+        assert block_rows(bl, P, True) == (w0, w1)
+        assert block_rows(bl, P, False) == (wa, 0)
+
+
 def _trainer_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     import tempfile

@@ -151,10 +151,14 @@ def _worker(rank, world, port, q, ncases):
             f2 = FusedTrainStep(m2, lr=1e-2, weight_decay=1e-2, loss=loss, shard_table=True, sync_bn=sync)
             bl = batches(data, B, 5, steps * world, seed=46)
             same_loss = True
+            static = None
             for s in range(steps):
                 l1 = float(f1(bl[s * world + rank].to("cuda")))
                 l2 = float(f2(bl[s * world + rank].to("cuda")))
                 same_loss = same_loss and l1 == l2
+                if s == 0 and sync:  # blocks sized to this run's batches from step 1 on
+                    static = (f2.shard.cap, f2.shard.cap_s)
+                    f2.fit_shard_blocks([bl[k * world + rank] for k in range(steps)])
             f1.flush()
             f2.sync_table()
             p1, mt1, vt1 = _state(m1, f1)
@@ -162,6 +166,7 @@ def _worker(rank, world, port, q, ncases):
             same = all(torch.equal(p1[n], p2[n]) for n in p1) and torch.equal(mt1, mt2) and torch.equal(vt1, vt2)
             bad = [n for n in p1 if not torch.equal(p1[n], p2[n])]
             vol = f2.shard.volume()
+            vol["static"] = static
             out.append((same_loss, same, bad, {n: v.cpu().numpy() for n, v in p2.items()}, vol))
         q.put((rank, out))
     finally:
@@ -172,7 +177,9 @@ def _worker(rank, world, port, q, ncases):
 def test_shard_ranks_bitwise_equal_replicated_dp(world, ncases):
     """2 (4) ranks sharing the GPU over gloo: the sharded step equals the replicated
     data-parallel step (lazy table) bit for bit -- BPR at D=64, and (2 ranks) listwise at
-    D=128 / 4 heads / LapPE with SyncBN -- and the gathered tables agree across ranks."""
+    D=128 / 4 heads / LapPE with SyncBN, its exchange blocks refitted to the run's batches
+    after the first step (FusedTrainStep.fit_shard_blocks) -- and the gathered tables agree
+    across ranks."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -193,6 +200,9 @@ def test_shard_ranks_bitwise_equal_replicated_dp(world, ncases):
             same_loss, same, bad, _, vol = res[r][case]
             assert same_loss, (case, r)
             assert same, (case, r, bad)
+            if vol["static"] is not None:  # fitted blocks: smaller, and every rank agrees on them
+                assert vol["cap"] <= vol["static"][0] and vol["cap_scoring"] < vol["static"][1], vol
+                assert (vol["cap"], vol["cap_scoring"]) == (res[0][case][4]["cap"], res[0][case][4]["cap_scoring"])
         for r in range(1, world):
             for k, v in res[0][case][3].items():
                 assert np.array_equal(v, res[r][case][3][k]), f"replicas diverged: {k}"
