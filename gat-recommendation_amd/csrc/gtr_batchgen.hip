@@ -159,6 +159,10 @@ __global__ __launch_bounds__(BB_BLOCK) void k_bb_count(const int32_t* sess_ptr, 
   if (lane == 0) { nodes[s] = u; edges[s] = e; }
 }
 
+template <int BLK>
+__device__ void write_header_tails(const BBK& a, const int* np, const int* ep, int es, int N, int E, bool over,
+                                   int64_t cur);
+
 // Single workgroup: node / edge offsets of the batch, header, session offsets (PyG
 // ptr), row-group ranges, CSR tails and zeroed unused regions (as pack_batch writes);
 // records the batch start and advances the cursor.
@@ -209,76 +213,34 @@ __global__ __launch_bounds__(BB_SCAN_BLOCK) void k_bb_scan(BBK a) {
   __syncthreads();  // every thread has read *cursor
   const gtr_batch& bt = a.bt;
   const bool over = N > bt.n_cap || E > bt.e_cap || B > bt.b_cap;
-  const int R = a.R;
-  const int G = (N + R - 1) / R;
-  const int g_cap = (bt.n_cap + R - 1) / R;
-  int32_t* hdr = const_cast<int32_t*>(bt.hdr);
-  if (tid == 0) {
-    hdr[0] = over ? 0 : N; hdr[1] = over ? 0 : B; hdr[2] = over ? 0 : E; hdr[3] = bt.n_neg;
-    hdr[4] = over ? 0 : G; hdr[5] = R; hdr[6] = 0; hdr[7] = 0;
-    a.status[0] = over ? 1 : 0;
-    if (over) a.status[1] |= 1;  // sticky over the batches built since the host cleared it
-    *a.start = cur;
-    *a.cursor = cur + a.stride;
-  }
-  if (over) return;
-  int32_t* node_ptr = const_cast<int32_t*>(bt.node_ptr);
-  for (int b = tid; b <= bt.b_cap; b += BB_SCAN_BLOCK) node_ptr[b] = b <= B ? s_np[b] : N;
-  int32_t* grp_row = const_cast<int32_t*>(bt.grp_row);
-  int32_t* grp_edge = const_cast<int32_t*>(bt.grp_edge);
-  for (int g = tid; g <= g_cap; g += BB_SCAN_BLOCK) {
-    int r = N, e = E;
-    if (g < G) {  // first session whose first node is >= g*R
-      const int v = g * R;
-      int lo = 0, hi = B;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (s_np[mid] < v) lo = mid + 1; else hi = mid;
-      }
-      r = lo < B ? s_np[lo] : N;
-      e = lo < B ? a.scratch[2 * lo] : E;
-    }
-    grp_row[g] = r;
-    grp_edge[g] = e;
-  }
-  int32_t* node_item = const_cast<int32_t*>(bt.node_item);
-  int32_t* in_ptr = const_cast<int32_t*>(bt.in_ptr);
-  int32_t* out_ptr = const_cast<int32_t*>(bt.out_ptr);
-  for (int i = N + tid; i <= bt.n_cap; i += BB_SCAN_BLOCK) {
-    if (i < bt.n_cap) node_item[i] = 0;
-    in_ptr[i] = E;
-    out_ptr[i] = E;
-  }
-  int32_t* in_src = const_cast<int32_t*>(bt.in_src);
-  int32_t* out_edge = const_cast<int32_t*>(bt.out_edge);
-  int32_t* out_dst = const_cast<int32_t*>(bt.out_dst);
-  for (int i = E + tid; i < bt.e_cap; i += BB_SCAN_BLOCK) { in_src[i] = 0; out_edge[i] = 0; out_dst[i] = 0; }
-  int32_t* target = const_cast<int32_t*>(bt.target);
-  int32_t* negs = const_cast<int32_t*>(bt.negatives);
-  for (int b = B + tid; b < bt.b_cap; b += BB_SCAN_BLOCK) target[b] = 0;
-  for (int i = B * bt.n_neg + tid; i < bt.b_cap * bt.n_neg; i += BB_SCAN_BLOCK) negs[i] = 0;
+  if (tid == 0) *a.cursor = cur + a.stride;
+  write_header_tails<BB_SCAN_BLOCK>(a, s_np, a.scratch, 2, N, E, over, cur);
 }
 
-// Wave per session: nodes, induced edges, CSR by destination and by source, target,
-// negatives.
-__global__ __launch_bounds__(BB_BLOCK) void k_bb_write(BBK a) {
-  __shared__ int s_uq[BB_WAVES][64];
-  __shared__ int s_clk[BB_WAVES][64];
-  __shared__ unsigned long long s_row[BB_WAVES][64];
-  __shared__ unsigned long long s_col[BB_WAVES][64];
-  __shared__ int s_inoff[BB_WAVES][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int b = blockIdx.x * BB_WAVES + w;
-  if (a.status[0] != 0 || b >= a.B) return;
-  const int64_t pos = *a.start + b;
+// LDS of one wave's session (k_bb_write / k_bb_one)
+struct BBWave {
+  int uq[64];
+  int clk[64];
+  unsigned long long row[64];
+  unsigned long long col[64];
+  int inoff[64];
+};
+
+// One wave writes session b (epoch position pos, first edge e0, first node n0): nodes,
+// induced edges, CSR by destination and by source, target, negatives.
+__device__ void write_session(const BBK& a, int b, int64_t pos, int e0, int n0, BBWave& L) {
+  const int lane = threadIdx.x & 63;
   const int s = a.order[pos % a.S];
   int uq, len, tgt, click;
-  const int u = session_nodes(a.sess_ptr, a.sess_items, a.max_len, s, lane, s_uq[w], uq, len, tgt, click);
-  session_adjacency(a.slots, a.mask, a.T, u, lane, s_uq[w], s_row[w], s_col[w]);
-  const int e0 = a.scratch[2 * b], n0 = a.scratch[2 * b + 1];
+  const int u = session_nodes(a.sess_ptr, a.sess_items, a.max_len, s, lane, L.uq, uq, len, tgt, click);
+  session_adjacency(a.slots, a.mask, a.T, u, lane, L.uq, L.row, L.col);
+  unsigned long long* s_row_w = L.row;
+  unsigned long long* s_col_w = L.col;
+  int* s_inoff_w = L.inoff;
+  int* s_clk_w = L.clk;
   const gtr_batch& bt = a.bt;
-  const unsigned long long row = lane < u ? s_row[w][lane] : 0ull;
-  const unsigned long long col = lane < u ? s_col[w][lane] : 0ull;
+  const unsigned long long row = lane < u ? s_row_w[lane] : 0ull;
+  const unsigned long long col = lane < u ? s_col_w[lane] : 0ull;
   const int indeg = __popcll(col), outdeg = __popcll(row);
   int iin = indeg, iout = outdeg;
 #pragma unroll
@@ -287,8 +249,8 @@ __global__ __launch_bounds__(BB_BLOCK) void k_bb_write(BBK a) {
     if (lane >= o) { iin += ti; iout += to; }
   }
   const int in_off = iin - indeg, out_off = iout - outdeg;
-  s_inoff[w][lane] = in_off;
-  s_clk[w][lane] = click;
+  s_inoff_w[lane] = in_off;
+  s_clk_w[lane] = click;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -309,7 +271,7 @@ __global__ __launch_bounds__(BB_BLOCK) void k_bb_write(BBK a) {
     for (int k = 0; r; ++k) {  // out-edges of source `lane`, destinations ascending
       const int y = __ffsll((unsigned long long)r) - 1;
       r &= r - 1ull;
-      oe[k] = e0 + s_inoff[w][y] + __popcll(s_col[w][y] & ((1ull << lane) - 1ull));
+      oe[k] = e0 + s_inoff_w[y] + __popcll(s_col_w[y] & ((1ull << lane) - 1ull));
       od[k] = n0 + y;
     }
   }
@@ -333,12 +295,136 @@ __global__ __launch_bounds__(BB_BLOCK) void k_bb_write(BBK a) {
     const uint32_t h = mix3((uint32_t)a.seed, (uint32_t)pos, round * 64u + (uint32_t)lane);
     const int cand = 1 + (int)(h % (uint32_t)(a.T - 1));
     bool seen = false;
-    for (int i = 0; i < len; ++i) seen |= s_clk[w][i] == cand;
+    for (int i = 0; i < len; ++i) seen |= s_clk_w[i] == cand;
     const unsigned long long ok = __ballot(!seen);
     const int rk = __popcll(ok & ((1ull << lane) - 1ull));
     if (!seen && filled + rk < n) negs[filled + rk] = cand;
     filled += __popcll(ok);
   }
+}
+
+// Wave per session, offsets from k_bb_scan.
+__global__ __launch_bounds__(BB_BLOCK) void k_bb_write(BBK a) {
+  __shared__ BBWave s_w[BB_WAVES];
+  const int w = threadIdx.x >> 6;
+  const int b = blockIdx.x * BB_WAVES + w;
+  if (a.status[0] != 0 || b >= a.B) return;
+  write_session(a, b, *a.start + b, a.scratch[2 * b], a.scratch[2 * b + 1], s_w[w]);
+}
+
+// The header / tails part of the build (k_bb_scan's, or k_bb_one's last workgroup):
+// node_ptr, row-group ranges, CSR tails and zeroed unused regions.  np[b] / ep[b]: node /
+// edge offset of session b (np[B] = N).
+template <int BLK>
+__device__ void write_header_tails(const BBK& a, const int* np, const int* ep, int es, int N, int E, bool over,
+                                   int64_t cur) {
+  const int tid = threadIdx.x;
+  const int B = a.B;
+  const gtr_batch& bt = a.bt;
+  const int R = a.R;
+  const int G = (N + R - 1) / R;
+  const int g_cap = (bt.n_cap + R - 1) / R;
+  int32_t* hdr = const_cast<int32_t*>(bt.hdr);
+  if (tid == 0) {
+    hdr[0] = over ? 0 : N; hdr[1] = over ? 0 : B; hdr[2] = over ? 0 : E; hdr[3] = bt.n_neg;
+    hdr[4] = over ? 0 : G; hdr[5] = R; hdr[6] = 0; hdr[7] = 0;
+    a.status[0] = over ? 1 : 0;
+    if (over) a.status[1] |= 1;  // sticky over the batches built since the host cleared it
+    *a.start = cur;
+  }
+  if (over) return;
+  int32_t* node_ptr = const_cast<int32_t*>(bt.node_ptr);
+  for (int b = tid; b <= bt.b_cap; b += BLK) node_ptr[b] = b <= B ? np[b] : N;
+  int32_t* grp_row = const_cast<int32_t*>(bt.grp_row);
+  int32_t* grp_edge = const_cast<int32_t*>(bt.grp_edge);
+  for (int g = tid; g <= g_cap; g += BLK) {
+    int r = N, e = E;
+    if (g < G) {  // first session whose first node is >= g*R
+      const int v = g * R;
+      int lo = 0, hi = B;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (np[mid] < v) lo = mid + 1; else hi = mid;
+      }
+      r = lo < B ? np[lo] : N;
+      e = lo < B ? ep[(size_t)lo * es] : E;
+    }
+    grp_row[g] = r;
+    grp_edge[g] = e;
+  }
+  int32_t* node_item = const_cast<int32_t*>(bt.node_item);
+  int32_t* in_ptr = const_cast<int32_t*>(bt.in_ptr);
+  int32_t* out_ptr = const_cast<int32_t*>(bt.out_ptr);
+  for (int i = N + tid; i <= bt.n_cap; i += BLK) {
+    if (i < bt.n_cap) node_item[i] = 0;
+    in_ptr[i] = E;
+    out_ptr[i] = E;
+  }
+  int32_t* in_src = const_cast<int32_t*>(bt.in_src);
+  int32_t* out_edge = const_cast<int32_t*>(bt.out_edge);
+  int32_t* out_dst = const_cast<int32_t*>(bt.out_dst);
+  for (int i = E + tid; i < bt.e_cap; i += BLK) { in_src[i] = 0; out_edge[i] = 0; out_dst[i] = 0; }
+  int32_t* target = const_cast<int32_t*>(bt.target);
+  int32_t* negs = const_cast<int32_t*>(bt.negatives);
+  for (int b = B + tid; b < bt.b_cap; b += BLK) target[b] = 0;
+  for (int i = B * bt.n_neg + tid; i < bt.b_cap * bt.n_neg; i += BLK) negs[i] = 0;
+}
+
+// Batches of up to BB_BLOCK sessions in ONE launch (round 5; the Trainer's C2 steps build
+// B = 32): every workgroup reads the cursor and scans the B sessions' node / edge counts
+// itself (B <= BB_BLOCK: one value per thread), its waves then write their sessions; the
+// last workgroup writes the header, node_ptr, row-group ranges and the zeroed tails.  The
+// last workgroup to ARRIVE (after every workgroup has read the cursor) advances it; the
+// arrival ticket is scratch[2 * b_cap] (zero-initialised, reset by that workgroup).  One
+// launch instead of k_bb_scan + k_bb_write: the single-workgroup scan and its dependent
+// launch boundary go.
+__global__ __launch_bounds__(BB_BLOCK) void k_bb_one(BBK a) {
+  __shared__ BBWave s_w[BB_WAVES];
+  __shared__ int s_np[BB_BLOCK + 1], s_ep[BB_BLOCK + 1];
+  __shared__ int s_ws[2][BB_WAVES];
+  __shared__ int s_flag;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int B = a.B;
+  const int64_t cur = *a.cursor;
+  int cn = 0, ce = 0;
+  if (tid < B) {
+    const int s = a.order[(cur + tid) % a.S];
+    cn = a.sess_nodes[s];
+    ce = a.sess_edges[s];
+  }
+  int in = cn, ie = ce;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int tn = __shfl_up(in, o), te = __shfl_up(ie, o);
+    if (lane >= o) { in += tn; ie += te; }
+  }
+  if (lane == 63) { s_ws[0][w] = in; s_ws[1][w] = ie; }
+  __syncthreads();
+  int bn = 0, be = 0, N = 0, E = 0;
+#pragma unroll
+  for (int q = 0; q < BB_WAVES; ++q) {
+    if (q < w) { bn += s_ws[0][q]; be += s_ws[1][q]; }
+    N += s_ws[0][q];
+    E += s_ws[1][q];
+  }
+  s_np[tid] = bn + in - cn;  // past B: N (the counts there are 0)
+  s_ep[tid] = be + ie - ce;
+  if (tid == 0) { s_np[BB_BLOCK] = N; s_ep[BB_BLOCK] = E; }
+  // every workgroup has read *cursor once its scan is in LDS: the last to arrive advances it
+  uint32_t* ticket = reinterpret_cast<uint32_t*>(a.scratch + 2 * a.bt.b_cap);
+  if (arrive_last_wt(ticket, gridDim.x, &s_flag) && tid == 0) {
+    *a.cursor = cur + a.stride;
+    reset_counter(ticket);
+  }
+  const gtr_batch& bt = a.bt;
+  const bool over = N > bt.n_cap || E > bt.e_cap || B > bt.b_cap;
+  if ((int)blockIdx.x == (int)gridDim.x - 1) {
+    write_header_tails<BB_BLOCK>(a, s_np, s_ep, 1, N, E, over, cur);
+    return;
+  }
+  const int b = blockIdx.x * BB_WAVES + w;
+  if (over || b >= B) return;
+  write_session(a, b, cur + b, s_ep[b], s_np[b], s_w[w]);
 }
 
 }  // namespace
@@ -406,6 +492,12 @@ extern "C" int gtr_build_batch_strided(const gtr_sessions* ss, const uint64_t* s
   k.seed = (int32_t)seed;
   k.stride = stride;
   hipStream_t s = (hipStream_t)stream;
+  const char* one = getenv("GTR_BB_ONE");  // 0: always the scan + write pair
+  if (B <= BB_BLOCK && !(one && one[0] == '0')) {  // one launch (k_bb_one)
+    hipLaunchKernelGGL(k_bb_one, dim3((B + BB_WAVES - 1) / BB_WAVES + 1), dim3(BB_BLOCK), 0, s, k);
+    GTR_HIP_CHECK_LAUNCH();
+    return GTR_OK;
+  }
   hipLaunchKernelGGL(k_bb_scan, dim3(1), dim3(BB_SCAN_BLOCK), 0, s, k);
   GTR_HIP_CHECK_LAUNCH();
   hipLaunchKernelGGL(k_bb_write, dim3((B + BB_WAVES - 1) / BB_WAVES), dim3(BB_BLOCK), 0, s, k);

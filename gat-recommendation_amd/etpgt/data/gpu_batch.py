@@ -161,8 +161,9 @@ class GpuBatchBuilder:
         B = self.B if B is None else int(B)
         if not 0 < B <= caps.b_cap:
             raise ValueError(f"batch of {B} sessions does not fit b_cap {caps.b_cap}")
-        if self.scratch is None or self.scratch.numel() < 2 * caps.b_cap:
-            self.scratch = torch.zeros(2 * caps.b_cap, dtype=torch.int32, device=self.store.device)
+        if self.scratch is None or self.scratch.numel() < 2 * caps.b_cap + 2:
+            # + 2: the one-launch build's arrival ticket (gtr_build_batch, zero between builds)
+            self.scratch = torch.zeros(2 * caps.b_cap + 2, dtype=torch.int32, device=self.store.device)
         st = self.store
         stride = max(self.stride, B)
         L.check(L.lib().gtr_build_batch_strided(C.byref(st.ss), st.slots.data_ptr(), st.num_slots, st.max_len,

@@ -653,7 +653,9 @@ int gtr_edge_hash_build(const int64_t* keys, int64_t num_edges, uint64_t* slots,
 int gtr_session_counts(const gtr_sessions* ss, const uint64_t* slots, int64_t num_slots, int max_len,
                        int32_t* nodes, int32_t* edges, gtr_stream_t stream);
 /* One batch of the B sessions order[(*cursor + b) % S] into *out (device blob arrays;
- * hdr sizes live), then *cursor += B.  scratch: [2 * b_cap] int32; start: [1] int64;
+ * hdr sizes live), then *cursor += B.  scratch: [2 * b_cap + 2] int32, zero-initialised
+ * (word 2 * b_cap: the arrival ticket of the one-launch build for B <= 256, reset by the
+ * build itself); start: [1] int64;
  * status [2]: status[0] = this batch's code -- 1 (and an empty header) if the batch exceeds
  * out's capacities, 2 if a session leaves no item to sample negatives from (it holds
  * nearly the whole catalog: the reference would reject forever); status[1] |= each code

@@ -316,7 +316,9 @@ def test_dp_rccl_world1_graph_captured_collectives():
 
 
 def _refuse_worker(port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GTR_GRAPH_COLL="1")
+    # GTR_DP_NOALIAS: the one-rank all-gather stays a real RCCL collective (by default one
+    # rank aliases the exchange and the step has no collective to refuse)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GTR_GRAPH_COLL="1", GTR_DP_NOALIAS="1")
     import torch.distributed as dist
 
     torch.cuda.set_device(0)
@@ -422,7 +424,8 @@ def test_dp_resident_images_equal_copied_blob():
 
 
 def _multi_worker(port, q):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GTR_GRAPH_COLL="1")
+    # a real one-rank RCCL all-gather captured in the step graph (GTR_DP_NOALIAS)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GTR_GRAPH_COLL="1", GTR_DP_NOALIAS="1")
     import torch.distributed as dist
 
     from etpgt.data.batch import Caps
