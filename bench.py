@@ -268,10 +268,12 @@ def main():
         S, full, rem = step_graph_plan(args.steps, len(staged))
         seq = (step.capture_steps(args.warmup, S) if full else None, full,
                step.capture_steps(args.warmup, rem) if rem else None, S)
-    elif not resident and not args.no_graph and args.step_graph and args.steps > 0 and pg_world is not None:
-        # data parallel with the RCCL collectives inside the step's graph: the timed steps
-        # (image copy + step) as multi-step graphs too; None on every rank if any rank's
-        # capture was refused (then one graph launch per step, as before)
+    elif not resident and not args.no_graph and args.step_graph and args.steps > 0 and (pg_world is not None
+                                                                                      or shard):
+        # data parallel with the RCCL collectives inside the step's graph, or the one-rank
+        # sharded step (aliased exchange, no collective): the timed steps (image copy +
+        # step) as multi-step graphs too; None on every rank if any rank's capture was
+        # refused (then one graph launch per step, as before)
         S, full, rem = step_graph_plan(args.steps, len(staged))
         g_full = step.capture_steps_copied(staged, args.warmup, S, reserve=args.steps) if full else None
         g_rem = step.capture_steps_copied(staged, args.warmup, rem, reserve=args.steps) if rem else None
