@@ -58,6 +58,19 @@ GTR_PH_DECL
 
 #define GM_MFMA4(a, b, c) mfma4(a, b, c)
 
+// k_proj computes QKVS^T tiles (W fragment as the MFMA's A operand, the X rows as B): a
+// lane's four accumulators are then four CONSECUTIVE output columns of one row, stored as
+// one float4, instead of one column of four rows (four scalar stores).  The products and
+// the k order per instruction are the same.  GTR_PROJ_T=0 at build time: the X . W^T form.
+#ifndef GTR_PROJ_T
+#define GTR_PROJ_T 1
+#endif
+// k_dx likewise (dX^T = W^T-fragment x dQKVS rows): float4 residual loads, stores and
+// BatchNorm-sum columns per lane.  GTR_DX_T=0 at build time: the dQKVS . W form.
+#ifndef GTR_DX_T
+#define GTR_DX_T 1
+#endif
+
 // k_proj modes: layer 0 (item row + LapPE), layer >= 1 (BatchNorm fold of the previous
 // layer), rows taken as they are (after a feed-forward block), FFN hidden-gradient GEMM
 enum { PJ_FIRST = 0, PJ_FOLD = 1, PJ_READY = 2, PJ_FFN_DH = 3 };
@@ -131,6 +144,7 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
   __shared__ __attribute__((aligned(16))) float Xs[2][BM * XS];
   __shared__ __attribute__((aligned(16))) float s_pw[KPE * D];  // W_pe^T [KPE][D] (layer 0)
   __shared__ __attribute__((aligned(16))) float s_c[4 * D];     // bpe | mean | rstd | gamma | beta
+  __shared__ __attribute__((aligned(16))) float s_bias[4 * D];  // b_all (GTR_PROJ_T epilogue)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
   const int N = a.bt.hdr[0];
   const int ntile = (N + BM - 1) / BM;
@@ -163,6 +177,8 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
       bias[c] = a.b_all[ct * 16 + lr];
     }
   }
+  if (GTR_PROJ_T)
+    for (int j = tid; j < 4 * D; j += GM_BLOCK) s_bias[j] = DH ? 0.0f : a.b_all[j];
   const bool pe_lds = FIRST && a.pe_k > 0 && a.pe_k <= KPE;
   if (FIRST) {
     // transposed (k-major): a thread's four output columns of one k are one float4, and a
@@ -336,7 +352,8 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
 #pragma unroll
       for (int r = 0; r < RT; ++r)
 #pragma unroll
-        for (int c = 0; c < CT; ++c) acc[r][c] = GM_MFMA4(av[r], wf[c][kb], acc[r][c]);
+        for (int c = 0; c < CT; ++c)
+          acc[r][c] = GTR_PROJ_T ? GM_MFMA4(wf[c][kb], av[r], acc[r][c]) : GM_MFMA4(av[r], wf[c][kb], acc[r][c]);
       if (kb == KB_STAGE) {
         if (more) produce(t + GS, Sn.item, Sn, Xs[p ^ 1]);
         fetch(t + 3 * GS, In, Sn);  // past the last tile: zeros, nothing loaded
@@ -344,21 +361,46 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
       }
     }
     if (t == t0) GTR_PH(10 + a.layer, 3);
+    if (GTR_PROJ_T) {  // lane (lr, lg): row lr of the 16-row tile, columns 4 lg .. 4 lg + 3
 #pragma unroll
-    for (int r = 0; r < RT; ++r)
+      for (int r = 0; r < RT; ++r) {
+        const int row = t * BM + r * 16 + lr;
+        if (row >= N) continue;
 #pragma unroll
-      for (int c = 0; c < CT; ++c) {
-        const int col = (wsw + c * GM_WAVES) * 16 + lr;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = t * BM + r * 16 + lg * 4 + i;
-          if (row < N) {
-            const size_t o = (size_t)row * (4 * D) + col;
-            if (DH) a.qkvs[o] = acc[r][c][i] * dr.mul(st_h, (uint32_t)o) * gelu_erf_grad(a.fa[o]);
-            else a.qkvs[o] = acc[r][c][i] + bias[c];
+        for (int c = 0; c < CT; ++c) {
+          const int col = (wsw + c * GM_WAVES) * 16 + lg * 4;
+          const size_t o = (size_t)row * (4 * D) + col;
+          float4 v;
+          if (DH) {
+            const float4 f = *reinterpret_cast<const float4*>(a.fa + o);
+            v.x = acc[r][c][0] * dr.mul(st_h, (uint32_t)o) * gelu_erf_grad(f.x);
+            v.y = acc[r][c][1] * dr.mul(st_h, (uint32_t)(o + 1)) * gelu_erf_grad(f.y);
+            v.z = acc[r][c][2] * dr.mul(st_h, (uint32_t)(o + 2)) * gelu_erf_grad(f.z);
+            v.w = acc[r][c][3] * dr.mul(st_h, (uint32_t)(o + 3)) * gelu_erf_grad(f.w);
+          } else {
+            const float4 b = *reinterpret_cast<const float4*>(s_bias + col);
+            v = make_float4(acc[r][c][0] + b.x, acc[r][c][1] + b.y, acc[r][c][2] + b.z, acc[r][c][3] + b.w);
           }
+          *reinterpret_cast<float4*>(a.qkvs + o) = v;
         }
       }
+    } else {
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+#pragma unroll
+        for (int c = 0; c < CT; ++c) {
+          const int col = (wsw + c * GM_WAVES) * 16 + lr;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = t * BM + r * 16 + lg * 4 + i;
+            if (row < N) {
+              const size_t o = (size_t)row * (4 * D) + col;
+              if (DH) a.qkvs[o] = acc[r][c][i] * dr.mul(st_h, (uint32_t)o) * gelu_erf_grad(a.fa[o]);
+              else a.qkvs[o] = acc[r][c][i] + bias[c];
+            }
+          }
+        }
+    }
     if (t == t0) GTR_PH(10 + a.layer, 4);
     __syncthreads();  // the next tile's X is built; this tile's buffer is free
     if (t == t0) GTR_PH(10 + a.layer, 5);
@@ -410,7 +452,7 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
   using G = DxGeom<D>;
   constexpr int NCT = G::NCT, BM = G::BM, K = G::K, AS = G::AS, PER = G::PER;
   __shared__ __attribute__((aligned(16))) float As[2][BM * AS];
-  __shared__ float s_bnp[GM_WAVES / NCT][2 * D];
+  __shared__ __attribute__((aligned(16))) float s_bnp[GM_WAVES / NCT][2 * D];
   __shared__ int s_flag;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
   const int N = a.bt.hdr[0];
@@ -443,6 +485,17 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
   float pm = 0.0f, pr = 0.0f;
   if (a.has_prev) { pm = a.p_stats[col]; pr = a.p_stats[D + col]; }
   float s1 = 0.0f, s2 = 0.0f;
+  // GTR_DX_T: this lane's four columns col4 .. col4 + 3 of row rs*16 + lr
+  const int col4 = ct * 16 + lg * 4;
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 b24 = z4, pm4 = z4, pr4 = z4, s14 = z4, s24 = z4;
+  if (GTR_DX_T) {
+    if (DOWN) b24 = *reinterpret_cast<const float4*>(a.b2 + col4);
+    if (a.has_prev) {
+      pm4 = *reinterpret_cast<const float4*>(a.p_stats + col4);
+      pr4 = *reinterpret_cast<const float4*>(a.p_stats + D + col4);
+    }
+  }
   // this thread's float4s of a tile's dQKVS rows: row i = idx / (K/4), column (idx % (K/4))*4
   auto fetch = [&](int t, float4 (&v)[PER]) {
 #pragma unroll
@@ -491,22 +544,64 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
     // the epilogue's residual / previous-output values requested before the MFMA chain, so
     // that the tile's stores do not wait one memory round after it
     float ydv[4], pov[4];
+    float4 ydv4 = z4, pov4 = z4;
+    const int rowT = t * BM + rs * 16 + lr;
+    if (GTR_DX_T) {
+      if (rowT < N) {
+        const size_t o = (size_t)rowT * D + col4;
+        ydv4 = *reinterpret_cast<const float4*>(a.dy + o);
+        if (!DOWN && a.has_prev) pov4 = *reinterpret_cast<const float4*>(a.p_out + o);
+      }
+    } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = t * BM + rs * 16 + lg * 4 + i;
-      const size_t o = (size_t)row * D + col;
-      ydv[i] = row < N ? a.dy[o] : 0.0f;
-      pov[i] = (!DOWN && a.has_prev && row < N) ? a.p_out[o] : 0.0f;
+      for (int i = 0; i < 4; ++i) {
+        const int row = t * BM + rs * 16 + lg * 4 + i;
+        const size_t o = (size_t)row * D + col;
+        ydv[i] = row < N ? a.dy[o] : 0.0f;
+        pov[i] = (!DOWN && a.has_prev && row < N) ? a.p_out[o] : 0.0f;
+      }
     }
     f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
     const float* arow = A + (rs * 16 + lr) * AS + lg * 4;
 #pragma unroll
     for (int kb = 0; kb < K / 16; ++kb) {
-      acc = GM_MFMA4(*reinterpret_cast<const float4*>(arow + kb * 16), wb[kb], acc);
+      acc = GTR_DX_T ? GM_MFMA4(wb[kb], *reinterpret_cast<const float4*>(arow + kb * 16), acc)
+                     : GM_MFMA4(*reinterpret_cast<const float4*>(arow + kb * 16), wb[kb], acc);
       if (kb == KB_STAGE) {
         if (more) stage(t + GD, Sn, As[p ^ 1]);
         fetch(t + 3 * GD, Sn);  // past the last tile: zeros, nothing loaded
       }
+    }
+    if (GTR_DX_T) {
+      if (rowT < N) {
+        const size_t o = (size_t)rowT * D + col4;
+        float4 v;
+        if (DOWN) {  // z = y + dropout(h W2^T + b2)
+          v.x = ydv4.x + (acc[0] + b24.x) * dr.mul(st_o, (uint32_t)o);
+          v.y = ydv4.y + (acc[1] + b24.y) * dr.mul(st_o, (uint32_t)(o + 1));
+          v.z = ydv4.z + (acc[2] + b24.z) * dr.mul(st_o, (uint32_t)(o + 2));
+          v.w = ydv4.w + (acc[3] + b24.w) * dr.mul(st_o, (uint32_t)(o + 3));
+          *reinterpret_cast<float4*>(a.dx0 + o) = v;
+        } else {
+          v = make_float4(ydv4.x + acc[0], ydv4.y + acc[1], ydv4.z + acc[2], ydv4.w + acc[3]);
+          if (a.has_prev) {
+            v.x *= dr.mul(st_prev, (uint32_t)o);
+            v.y *= dr.mul(st_prev, (uint32_t)(o + 1));
+            v.z *= dr.mul(st_prev, (uint32_t)(o + 2));
+            v.w *= dr.mul(st_prev, (uint32_t)(o + 3));
+            *reinterpret_cast<float4*>(a.p_dy + o) = v;
+            s14.x += v.x; s14.y += v.y; s14.z += v.z; s14.w += v.w;
+            s24.x += v.x * ((pov4.x - pm4.x) * pr4.x);
+            s24.y += v.y * ((pov4.y - pm4.y) * pr4.y);
+            s24.z += v.z * ((pov4.z - pm4.z) * pr4.z);
+            s24.w += v.w * ((pov4.w - pm4.w) * pr4.w);
+          } else {
+            *reinterpret_cast<float4*>(a.dx0 + o) = v;
+          }
+        }
+      }
+      __syncthreads();  // the next tile is staged; this tile's buffer is free
+      return;
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -538,11 +633,25 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
   if (DOWN || !a.has_prev) return;
   // ---- the previous layer's BatchNorm backward sums: one partial row per workgroup (its
   //      tiles in order), reduced by the bucketed last arrivers (fixed order: deterministic)
-  s1 = bfly_add<32>(bfly_add<16>(s1));
-  s2 = bfly_add<32>(bfly_add<16>(s2));
-  if (lg == 0) {
-    s_bnp[rs][col] = s1;
-    s_bnp[rs][D + col] = s2;
+  if (GTR_DX_T) {  // a column's rows sit in the 16 lanes of one lane group: xor 1 .. 8
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      s14.x += __shfl_xor(s14.x, o); s14.y += __shfl_xor(s14.y, o);
+      s14.z += __shfl_xor(s14.z, o); s14.w += __shfl_xor(s14.w, o);
+      s24.x += __shfl_xor(s24.x, o); s24.y += __shfl_xor(s24.y, o);
+      s24.z += __shfl_xor(s24.z, o); s24.w += __shfl_xor(s24.w, o);
+    }
+    if (lr == 0) {
+      *reinterpret_cast<float4*>(&s_bnp[rs][col4]) = s14;
+      *reinterpret_cast<float4*>(&s_bnp[rs][D + col4]) = s24;
+    }
+  } else {
+    s1 = bfly_add<32>(bfly_add<16>(s1));
+    s2 = bfly_add<32>(bfly_add<16>(s2));
+    if (lg == 0) {
+      s_bnp[rs][col] = s1;
+      s_bnp[rs][D + col] = s2;
+    }
   }
   __syncthreads();
   float* part = a.p_gpart + (size_t)blockIdx.x * 2 * D;
