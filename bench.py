@@ -440,7 +440,12 @@ def main():
             "c1_quick_validation": c1,
         }
     if world > 1:
-        torch.distributed.destroy_process_group()
+        # every collective of the run is done (the MAX all-reduce and the replica check
+        # above); the process group is NOT destroyed: a one-rank RCCL communicator that ran
+        # graph-captured all-to-alls did not come back from destroy_process_group on this
+        # stack (tests/test_gpu_distributed.py, scripts/dbg/capture_probe.py), and a rank
+        # stuck there would hold up the line.  The ranks leave through os._exit below.
+        torch.distributed.barrier()
     if rank == 0:
         legs = [int(x) for x in args.strong_batches.split(",") if x.strip() and int(x) > 0]
         if legs and not cfg.get("shard") and os.environ.get("GTR_STRONG_CHILD") != "1":
@@ -449,6 +454,11 @@ def main():
             out["strong_scaling"] = strong_scaling_legs(world, legs, args.strong_steps)
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(out) + "\n").encode())
+    if world > 1:
+        sys.stdout.flush()
+        sys.stderr.flush()
+        torch.cuda.synchronize()
+        os._exit(0)  # no teardown of the RCCL communicator (see above); the line is written
 
 
 def _child_line(cmd: list, env: dict, timeout: float) -> dict:
