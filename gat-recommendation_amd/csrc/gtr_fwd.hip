@@ -17,6 +17,12 @@
 //   the last BatchNorm's backward partial sums.
 
 #include "gtr_layer.cuh"
+
+// The fused forward's projection as QKVS^T tiles (float4 stores; bitwise the same values).
+// GTR_CONV_T=0 at build time: the X . W^T form with scalar stores.
+#ifndef GTR_CONV_T
+#define GTR_CONV_T 1
+#endif
 #include "gtr_rows.cuh"
 
 #ifndef GTR_WPRE_MAXD
@@ -576,6 +582,18 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
 #pragma unroll
         for (int ks = 0; ks < D / 32; ++ks) split8(wf[2 * ks], wf[2 * ks + 1], bh[ks], bl[ks]);
       }
+      // f32 path (round 5): QKVS^T tiles (the W fragment as the MFMA's A operand; the same
+      // products in the same k order, bitwise), so a lane holds four consecutive columns of
+      // one row: one float4 store to qkvs and one to LDS instead of four of each
+      const int col4 = ct * 16 + lg * 4;
+      const int which4 = col4 / D, cc4 = col4 - which4 * D;
+      float4 bias4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      float* ldst4 = nullptr;
+      constexpr bool TT = !SPLIT && GTR_CONV_T;
+      if constexpr (TT) {
+        bias4 = *reinterpret_cast<const float4*>(a.b_all + col4);
+        if (fast) ldst4 = (which4 == 0 ? QSs : which4 == 1 ? KVs : which4 == 2 ? KVs + RMAX * XS : QSs + RMAX * XS) + cc4;
+      }
       for (int rt = 0; rt * 16 < m; ++rt) {
         f32x4 acc = {0.0f, 0.0f, 0.0f, 0.0f};
         if constexpr (SPLIT) {
@@ -589,15 +607,25 @@ __device__ __forceinline__ void conv_fwd_body(const ConvFwdK& a, int rb) {
           const float* xrow = XO + (rt * 16 + lr) * XS + lg * 4;
 #pragma unroll
           for (int kb = 0; kb < D / 16; ++kb)
-            acc = mfma4(*reinterpret_cast<const float4*>(xrow + kb * 16), wf[kb], acc);
+            acc = TT ? mfma4(wf[kb], *reinterpret_cast<const float4*>(xrow + kb * 16), acc)
+                     : mfma4(*reinterpret_cast<const float4*>(xrow + kb * 16), wf[kb], acc);
         }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int row = rt * 16 + lg * 4 + i;
+        if constexpr (TT) {
+          const int row = rt * 16 + lr;
           if (row < m) {
-            const float v = acc[i] + bias;
-            a.qkvs[(size_t)(rc + row) * (4 * D) + col] = v;
-            if (ldst) ldst[row * XS] = v;
+            const float4 v = make_float4(acc[0] + bias4.x, acc[1] + bias4.y, acc[2] + bias4.z, acc[3] + bias4.w);
+            *reinterpret_cast<float4*>(a.qkvs + (size_t)(rc + row) * (4 * D) + col4) = v;
+            if (ldst4) *reinterpret_cast<float4*>(ldst4 + row * XS) = v;
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int row = rt * 16 + lg * 4 + i;
+            if (row < m) {
+              const float v = acc[i] + bias;
+              a.qkvs[(size_t)(rc + row) * (4 * D) + col] = v;
+              if (ldst) ldst[row * XS] = v;
+            }
           }
         }
       }
