@@ -1156,11 +1156,12 @@ struct RsPrep {
   const int64_t* step_dev;
 };
 
-template <bool PREP>
+template <bool PREP, int BITS>
 __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const int32_t* keys, int n, int shift, int32_t* hist,
                                                        int32_t* tot, int rounds, RsPrep pp) {
-  __shared__ int h[RS_RADIX];
-  for (int d = threadIdx.x; d < RS_RADIX; d += RS_THREADS) h[d] = 0;
+  constexpr int RADIX = 1 << BITS;
+  __shared__ int h[RADIX];
+  for (int d = threadIdx.x; d < RADIX; d += RS_THREADS) h[d] = 0;
   __syncthreads();
   const int base = blockIdx.x * RS_THREADS * rounds;
   // every round's key requested before the first count (the loads are independent)
@@ -1189,10 +1190,10 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const int32_t* keys, int
   }
 #pragma unroll
   for (int r = 0; r < RS_MAX_ROUNDS; ++r)
-    if (kk[r] >= 0) atomicAdd(&h[((uint32_t)kk[r] >> shift) & (RS_RADIX - 1)], 1);  // integer counts
+    if (kk[r] >= 0) atomicAdd(&h[((uint32_t)kk[r] >> shift) & (RADIX - 1)], 1);  // integer counts
   __syncthreads();
-  for (int d = threadIdx.x; d < RS_RADIX; d += RS_THREADS) {
-    hist[(size_t)blockIdx.x * RS_RADIX + d] = h[d];  // tile-major, coalesced
+  for (int d = threadIdx.x; d < RADIX; d += RS_THREADS) {
+    hist[(size_t)blockIdx.x * RADIX + d] = h[d];  // tile-major, coalesced
     if (h[d]) atomicAdd(tot + d, h[d]);             // digit totals (integer: order-free)
   }
 }
@@ -1214,19 +1215,23 @@ __device__ __forceinline__ int wave_incl_scan_i(int x, int lane) {
   return x;
 }
 
+template <int BITS>
 __global__ __launch_bounds__(1024) void k_rs_offs(const int32_t* __restrict__ hist, int32_t* __restrict__ tot,
                                                  int32_t* __restrict__ offs, int ntile) {
-  __shared__ int s_sl[RS_OFFS_SL][64];
-  __shared__ int s_dp[RS_RADIX];  // exclusive prefix of the digit totals
-  __shared__ int s_ws[RS_RADIX / 64];
+  // RADIX threads: thread tid scans digit tid; for the offsets, workgroup w owns digits
+  // [64 w, 64 w + 64) and its NSL = RADIX / 64 waves a slice of the tiles each
+  constexpr int RADIX = 1 << BITS, NSL = RADIX / 64;
+  __shared__ int s_sl[NSL][64];
+  __shared__ int s_dp[RADIX];  // exclusive prefix of the digit totals
+  __shared__ int s_ws[RADIX / 64];
   const int tid = threadIdx.x, dl = tid & 63, sl = tid >> 6;
   const int d = blockIdx.x * 64 + dl;
-  const int per = (ntile + RS_OFFS_SL - 1) / RS_OFFS_SL;
+  const int per = (ntile + NSL - 1) / NSL;
   const int b0 = min(ntile, sl * per), b1 = min(ntile, b0 + per);
   int v[16];
 #pragma unroll
-  for (int q = 0; q < 16; ++q) v[q] = b0 + q < b1 ? hist[(size_t)(b0 + q) * RS_RADIX + d] : 0;
-  const int tv = tot[tid];  // 1024 threads == RS_RADIX digits
+  for (int q = 0; q < 16; ++q) v[q] = b0 + q < b1 ? hist[(size_t)(b0 + q) * RADIX + d] : 0;
+  const int tv = tot[tid];  // RADIX threads == RADIX digits
   const int incl = wave_incl_scan_i(tv, dl);
   if (dl == 63) s_ws[sl] = incl;
   int sum = 0;
@@ -1235,7 +1240,7 @@ __global__ __launch_bounds__(1024) void k_rs_offs(const int32_t* __restrict__ hi
   for (int c = b0 + 16; c < b1; c += 16) {  // slices of more than 16 tiles (> 256 tiles)
     int w[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) w[q] = c + q < b1 ? hist[(size_t)(c + q) * RS_RADIX + d] : 0;
+    for (int q = 0; q < 16; ++q) w[q] = c + q < b1 ? hist[(size_t)(c + q) * RADIX + d] : 0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) sum += w[q];
   }
@@ -1249,16 +1254,16 @@ __global__ __launch_bounds__(1024) void k_rs_offs(const int32_t* __restrict__ hi
   for (int q = 0; q < sl; ++q) run += s_sl[q][dl];
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
-    if (b0 + q < b1) offs[(size_t)(b0 + q) * RS_RADIX + d] = run;
+    if (b0 + q < b1) offs[(size_t)(b0 + q) * RADIX + d] = run;
     run += v[q];
   }
   for (int c = b0 + 16; c < b1; c += 16) {
     int w[16];
 #pragma unroll
-    for (int q = 0; q < 16; ++q) w[q] = c + q < b1 ? hist[(size_t)(c + q) * RS_RADIX + d] : 0;
+    for (int q = 0; q < 16; ++q) w[q] = c + q < b1 ? hist[(size_t)(c + q) * RADIX + d] : 0;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-      if (c + q < b1) offs[(size_t)(c + q) * RS_RADIX + d] = run;
+      if (c + q < b1) offs[(size_t)(c + q) * RADIX + d] = run;
       run += w[q];
     }
   }
@@ -1277,11 +1282,13 @@ struct RsCtr {
   gtr_adam opt;
 };
 
+template <int BITS>
 __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const int32_t* kin, const int32_t* vin, int32_t* kout,
                                                           int32_t* vout, int n, int shift, const int32_t* offs,
                                                           int ntile, int32_t* tot, int rounds, RsCtr ctr) {
-  __shared__ int run[RS_RADIX];
-  __shared__ int wcnt[RS_THREADS / 64][RS_RADIX];
+  constexpr int RADIX = 1 << BITS;
+  __shared__ int run[RADIX];
+  __shared__ int wcnt[RS_THREADS / 64][RADIX];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (blockIdx.x == 0 && tid == 0 && ctr.step_dev) {
     const int64_t t = *ctr.step_dev + 1;
@@ -1290,9 +1297,9 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const int32_t* kin, c
     if (ctr.consts) lazy_consts_for(ctr.opt, t, ctr.consts);
   }
   if (blockIdx.x == 0)
-    for (int d = tid; d < RS_RADIX; d += RS_THREADS) tot[d] = 0;
-  for (int d = tid; d < RS_RADIX; d += RS_THREADS) {
-    run[d] = offs[(size_t)blockIdx.x * RS_RADIX + d];
+    for (int d = tid; d < RADIX; d += RS_THREADS) tot[d] = 0;
+  for (int d = tid; d < RADIX; d += RS_THREADS) {
+    run[d] = offs[(size_t)blockIdx.x * RADIX + d];
 #pragma unroll
     for (int w = 0; w < RS_THREADS / 64; ++w) wcnt[w][d] = 0;
   }
@@ -1312,10 +1319,10 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const int32_t* kin, c
       key_n = i2 < n ? kin[i2] : 0;
       val_n = i2 < n ? vin[i2] : 0;
     }
-    const int d = ((uint32_t)key >> shift) & (RS_RADIX - 1);
+    const int d = ((uint32_t)key >> shift) & (RADIX - 1);
     unsigned long long match = __ballot(live);
 #pragma unroll
-    for (int b = 0; b < RS_BITS; ++b) {
+    for (int b = 0; b < BITS; ++b) {
       const unsigned long long bb = __ballot((d >> b) & 1);
       match &= ((d >> b) & 1) ? bb : ~bb;
     }
@@ -1329,7 +1336,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const int32_t* kin, c
       vout[pos] = val;
     }
     __syncthreads();
-    for (int q = tid; q < RS_RADIX; q += RS_THREADS) {
+    for (int q = tid; q < RADIX; q += RS_THREADS) {
       int t = 0;
 #pragma unroll
       for (int w = 0; w < RS_THREADS / 64; ++w) { t += wcnt[w][q]; wcnt[w][q] = 0; }
@@ -1363,7 +1370,14 @@ hipError_t rs_sort(void* tmp, const int32_t* keys, int32_t* skeys, const int32_t
   int32_t* hist = v2 + n;
   int32_t* offs = hist + (size_t)RS_RADIX * ntile;
   int32_t* tot = offs + (size_t)RS_RADIX * ntile;  // [passes][RS_RADIX] digit totals (kept zero between calls)
-  const int passes = (bits + RS_BITS - 1) / RS_BITS;  // <= 3 for int32 keys below 2^30
+  // digit width: keys of <= 18 bits (T < 2^18: C3 / C4's 82k table) at >= 256k items in
+  // two passes of 9-bit digits -- half the histogram / offset work and twice the run length
+  // of a digit's scattered writes per tile (C3 B = 8192: 0.7710 -> 0.7686 ms per step; at
+  // C4 B = 1024, 107k items, 10-bit digits measured 0.3324 against 0.3333); otherwise
+  // 10-bit digits (two passes up to T = 1M).  Any width gives the same stable order.
+  const char* rb = getenv("GTR_RS_BITS");
+  const int RB = rb ? (atoi(rb) == 9 ? 9 : 10) : (bits <= 18 && n >= (1 << 18) ? 9 : 10);
+  const int passes = (bits + RB - 1) / RB;  // <= 4 for int32 keys below 2^30
   if (passes > 4) return hipErrorInvalidValue;
   const int32_t* ki = keys;
   const int32_t* vi = vals;
@@ -1372,14 +1386,27 @@ hipError_t rs_sort(void* tmp, const int32_t* keys, int32_t* skeys, const int32_t
     int32_t* ko = last ? skeys : (p % 2 == 0 ? k1 : k2);
     int32_t* vo = last ? svals : (p % 2 == 0 ? v1 : v2);
     int32_t* tp = tot + p * RS_RADIX;
-    if (p == 0 && prep)  // the first pass builds the contribution list as it counts
-      hipLaunchKernelGGL(k_rs_hist<true>, dim3(ntile), dim3(RS_THREADS), 0, s, ki, n, 0, hist, tp, rounds, *prep);
-    else
-      hipLaunchKernelGGL(k_rs_hist<false>, dim3(ntile), dim3(RS_THREADS), 0, s, ki, n, p * RS_BITS, hist, tp, rounds,
-                         RsPrep{});
-    hipLaunchKernelGGL(k_rs_offs, dim3(RS_RADIX / 64), dim3(1024), 0, s, hist, tp, offs, ntile);
-    hipLaunchKernelGGL(k_rs_scatter, dim3(ntile), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, n, p * RS_BITS, offs,
-                       ntile, tp, rounds, (last && ctr) ? *ctr : RsCtr{});
+    const RsCtr cc = (last && ctr) ? *ctr : RsCtr{};
+    if (RB == 9) {
+      if (p == 0 && prep)  // the first pass builds the contribution list as it counts
+        hipLaunchKernelGGL((k_rs_hist<true, 9>), dim3(ntile), dim3(RS_THREADS), 0, s, ki, n, 0, hist, tp, rounds, *prep);
+      else
+        hipLaunchKernelGGL((k_rs_hist<false, 9>), dim3(ntile), dim3(RS_THREADS), 0, s, ki, n, p * 9, hist, tp, rounds,
+                           RsPrep{});
+      hipLaunchKernelGGL(k_rs_offs<9>, dim3(512 / 64), dim3(512), 0, s, hist, tp, offs, ntile);
+      hipLaunchKernelGGL(k_rs_scatter<9>, dim3(ntile), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, n, p * 9, offs, ntile,
+                         tp, rounds, cc);
+    } else {
+      if (p == 0 && prep)
+        hipLaunchKernelGGL((k_rs_hist<true, 10>), dim3(ntile), dim3(RS_THREADS), 0, s, ki, n, 0, hist, tp, rounds,
+                           *prep);
+      else
+        hipLaunchKernelGGL((k_rs_hist<false, 10>), dim3(ntile), dim3(RS_THREADS), 0, s, ki, n, p * 10, hist, tp,
+                           rounds, RsPrep{});
+      hipLaunchKernelGGL(k_rs_offs<10>, dim3(1024 / 64), dim3(1024), 0, s, hist, tp, offs, ntile);
+      hipLaunchKernelGGL(k_rs_scatter<10>, dim3(ntile), dim3(RS_THREADS), 0, s, ki, vi, ko, vo, n, p * 10, offs, ntile,
+                         tp, rounds, cc);
+    }
     ki = ko;
     vi = vo;
   }
