@@ -841,7 +841,13 @@ __global__ __launch_bounds__(CONV_BLOCK) void k_attn_fwd(ConvFwdK a) {
 // head) and their maximum; the softmax denominator; V rows four in flight -> alpha,
 // dropout, the weighted sum; the beta gate -> agg / out / gate (PyG TransformerConv,
 // SURVEY.md Appendix A).  The workgroup's 8 output rows give one BatchNorm partial.
-#define AR_BLOCK 256
+// 8 waves, 16 rows: one BatchNorm partial per 16 rows (half the partials of 4 waves, so
+// the bucketed last-arriver merges at the launch's end are half as long): C3 B = 8192
+// 0.7676 -> 0.7589 ms per step, C4 B = 1024 (split) 0.3618 -> 0.3586; 16 waves measured
+// 0.776 ms at C3 B = 8192.  -DAR_BLOCK=... at build time for A/B.
+#ifndef AR_BLOCK
+#define AR_BLOCK 512
+#endif
 #define AR_WAVES (AR_BLOCK / 64)
 #define AR_RPW 2                   // rows per wave
 #define AR_ROWS (AR_WAVES * AR_RPW)  // rows per workgroup = one BatchNorm partial
@@ -2346,7 +2352,7 @@ extern "C" int gtr_attn_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   if (cfg->dim <= 128 && !(am && am[0] == 'g')) {
     // row-parallel: one BatchNorm partial per AR_ROWS rows (gtr_layer.bn_part holds
     // max(n_cap / row_group, n_cap / 8) rows, gtr.h)
-    static_assert(AR_ROWS == 8, "gtr.h sizes bn_part for 8-row partials");
+    static_assert(AR_ROWS >= 8 && AR_ROWS % 8 == 0, "gtr.h sizes bn_part for (at most) 8-row partials");
     const int grid = (bt->n_cap + AR_ROWS - 1) / AR_ROWS;
     // float4 lanes + online softmax (k_attn_rows4) unless GTR_ATTN=rows (the round-4 body,
     // also the path for more than AR_HMAX heads)
