@@ -16,6 +16,29 @@ namespace gtr {
 
 void set_error(const char* fmt, ...);
 
+// A global array as a raw buffer (MUBUF, hardware bounds check): loads past `bytes` return
+// zero and stores past it are dropped, with no branch.  Used where a per-lane condition
+// would otherwise put a load or store under an exec-skipping branch: the compiler cannot
+// count a memory op that may not have issued, so the next wait on a load issued before it
+// becomes vmcnt(0) -- which also waits for every later load and store in flight.
+struct Buf {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ Buf(const void* p, uint64_t bytes)
+      : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0,
+                                            (int)(uint32_t)(bytes < 0xFFFFFFFFull ? bytes : 0xFFFFFFFFull),
+                                            0x00020000)) {}
+  __device__ __forceinline__ float4 ld4(uint32_t off) const {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0));
+  }
+  __device__ __forceinline__ int ld_i32(uint32_t off) const {
+    return (int)__builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, 0);
+  }
+  __device__ __forceinline__ void st4(uint32_t off, float4 v) const {
+    typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, (int)off, 0, 0);
+  }
+};
+
 // Cross-lane butterflies without the LDS crossbar.  Step O of an ASCENDING butterfly
 // (offsets 1, 2, 4, ...) combines each lane with its xor-O partner:
 //  - O = 1, 2: DPP quad_perm, an exact xor permutation inside a quad;

@@ -232,27 +232,26 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
     pb = *reinterpret_cast<const float4*>(a.p_beta + xj);
   }
 
+  // Round 5: every load of the tile pipeline issues unconditionally (rows past N and
+  // tiles past the last read row N - 1, whose values produce() then discards) and the
+  // stores go through bounds-checked buffers, so no memory op sits under an exec-skipping
+  // branch and the compiler counts them: the wait for a set's rows no longer drains the
+  // other set's rows and the previous tile's stores (vmcnt(0)).
+  const Buf xin_buf(a.xin, (uint64_t)N * D * 4), qkvs_buf(a.qkvs, (uint64_t)N * 4 * D * 4);
   auto item_of = [&](int t) -> int {
-    const int r = t * BM + xi;
-    return (FIRST && t < ntile && r < N) ? a.bt.node_item[r] : 0;
+    return FIRST ? a.bt.node_item[min(t * BM + xi, N - 1)] : 0;
   };
   auto fetch = [&](int t, int item, ProjIn& in) {
-    const int r = t * BM + xi;
-    const bool live = r < N;
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int r = min(t * BM + xi, N - 1);
     in.item = item;
-    in.u = z;
-    in.v = z;
-#pragma unroll
-    for (int q = 0; q < NPE; ++q) in.pe[q] = z;
-    if (!live) return;
+    in.v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (FIRST) {
       in.u = *reinterpret_cast<const float4*>(a.table + (size_t)item * D + xj);
       if (NPE > 0 && pe_lds && (a.pe_k & 3) == 0) {
         const float* pr = a.bt.node_pe ? a.bt.node_pe + (size_t)r * a.pe_k : a.pe_tab + (size_t)item * a.pe_k;
+        // float4 q past pe_k re-reads float4 0 (unused: produce() stops at pe_k)
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if (q < NPE && 4 * q < a.pe_k) in.pe[q] = *reinterpret_cast<const float4*>(pr + 4 * q);
+        for (int q = 0; q < NPE; ++q) in.pe[q] = *reinterpret_cast<const float4*>(pr + (4 * q < a.pe_k ? 4 * q : 0));
       }
     } else {
       const size_t o = (size_t)r * D + xj;
@@ -265,7 +264,7 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
   auto produce = [&](int t, int item, const ProjIn& in, float* X) {
     const int r = t * BM + xi;
     float4 val = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (r < N) {
+    {
       const size_t o = (size_t)r * D + xj;
       if (FIRST) {
         val = in.u;
@@ -279,7 +278,7 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
               pe_fma4(acc, in.pe[kq < NPE ? kq : 0], s_pw + k * D + xj, D);
             }
           } else {
-            const float* pr = a.bt.node_pe ? a.bt.node_pe + (size_t)r * a.pe_k : a.pe_tab + (size_t)item * a.pe_k;
+            const float* pr = a.bt.node_pe ? a.bt.node_pe + (size_t)min(r, N - 1) * a.pe_k : a.pe_tab + (size_t)item * a.pe_k;
             for (int k = 0; k < a.pe_k; ++k) {
               const float pk = pr[k];
 #pragma unroll
@@ -305,7 +304,8 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
         val.z = (((po.z - mu.z) * rs.z * pg.z + pb.z) + px.z) * dr.mul(st_prev, (uint32_t)(o + 2));
         val.w = (((po.w - mu.w) * rs.w * pg.w + pb.w) + px.w) * dr.mul(st_prev, (uint32_t)(o + 3));
       }
-      *reinterpret_cast<float4*>(a.xin + o) = val;
+      if (r >= N) val = make_float4(0.f, 0.f, 0.f, 0.f);
+      xin_buf.st4((uint32_t)(o * 4), val);  // rows past N: dropped
     }
     *reinterpret_cast<float4*>(X + xi * XS + xj) = val;
   };
@@ -365,14 +365,13 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
 #pragma unroll
       for (int r = 0; r < RT; ++r) {
         const int row = t * BM + r * 16 + lr;
-        if (row >= N) continue;
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
           const int col = (wsw + c * GM_WAVES) * 16 + lg * 4;
           const size_t o = (size_t)row * (4 * D) + col;
           float4 v;
           if (DH) {
-            const float4 f = *reinterpret_cast<const float4*>(a.fa + o);
+            const float4 f = *reinterpret_cast<const float4*>(a.fa + (size_t)min(row, N - 1) * (4 * D) + col);
             v.x = acc[r][c][0] * dr.mul(st_h, (uint32_t)o) * gelu_erf_grad(f.x);
             v.y = acc[r][c][1] * dr.mul(st_h, (uint32_t)(o + 1)) * gelu_erf_grad(f.y);
             v.z = acc[r][c][2] * dr.mul(st_h, (uint32_t)(o + 2)) * gelu_erf_grad(f.z);
@@ -381,7 +380,7 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
             const float4 b = *reinterpret_cast<const float4*>(s_bias + col);
             v = make_float4(acc[r][c][0] + b.x, acc[r][c][1] + b.y, acc[r][c][2] + b.z, acc[r][c][3] + b.w);
           }
-          *reinterpret_cast<float4*>(a.qkvs + o) = v;
+          qkvs_buf.st4((uint32_t)(o * 4), v);  // rows past N: dropped
         }
       }
     } else {
@@ -496,24 +495,29 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
       pr4 = *reinterpret_cast<const float4*>(a.p_stats + D + col4);
     }
   }
-  // this thread's float4s of a tile's dQKVS rows: row i = idx / (K/4), column (idx % (K/4))*4
+  // this thread's float4s of a tile's dQKVS rows: row i = idx / (K/4), column (idx % (K/4))*4.
+  // Round 5 (as k_proj): the loads issue unconditionally -- rows past N and tiles past the
+  // last read row N - 1, zeroed by stage() -- and the epilogue stores go through
+  // bounds-checked buffers, so the compiler counts every memory op of the pipeline and
+  // the wait for a register set does not drain the other set and the tile's stores.
+  const Buf dx0_buf(a.dx0, (uint64_t)N * D * 4), pdy_buf(a.p_dy, (uint64_t)N * D * 4);
   auto fetch = [&](int t, float4 (&v)[PER]) {
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int idx = tid + u * GM_BLOCK;
       const int i = idx / (K / 4), c = (idx - i * (K / 4)) * 4;
-      const int r = t * BM + i;
-      v[u] = (t < ntile && r < N) ? *reinterpret_cast<const float4*>(a.dqkvs + (size_t)r * K + c)
-                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int r = min(t * BM + i, N - 1);
+      v[u] = *reinterpret_cast<const float4*>(a.dqkvs + (size_t)r * K + c);
     }
   };
-  // a tile's dQKVS rows (h = dropout(GELU(a)) for DX_FFN_DOWN) -> LDS
+  // a tile's dQKVS rows (h = dropout(GELU(a)) for DX_FFN_DOWN) -> LDS; rows past N zero
   auto stage = [&](int tt, const float4 (&src)[PER], float* A) {
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int idx = tid + u * GM_BLOCK;
       const int i = idx / (K / 4), c = (idx - i * (K / 4)) * 4;
       float4 v = src[u];
+      if (tt * BM + i >= N) v = make_float4(0.f, 0.f, 0.f, 0.f);
       if (DOWN) {  // h = dropout(GELU(a)) (rows past N are zero: GELU(0) = 0)
         const uint32_t e = (uint32_t)((size_t)(tt * BM + i) * K + c);
         v.x = gelu_erf(v.x) * dr.mul(st_h, e);
@@ -530,10 +534,14 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
   const int GD = gridDim.x;
   const int t0 = blockIdx.x;
   float4 S0[PER], S1[PER];
-  fetch(t0, S0);
-  fetch(t0 + GD, S1);
+#pragma unroll
+  for (int u = 0; u < PER; ++u) S0[u] = S1[u] = z4;
+  if (N > 0) {  // (an empty batch: no row to clamp to; stage() zeroes every row)
+    fetch(t0, S0);
+    fetch(t0 + GD, S1);
+  }
   stage(t0, S0, As[0]);
-  fetch(t0 + 2 * GD, S0);
+  if (N > 0) fetch(t0 + 2 * GD, S0);
   __syncthreads();
   constexpr int KB_STAGE = K / 32;
   auto phase = [&](auto P, int t) {
@@ -547,11 +555,9 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
     float4 ydv4 = z4, pov4 = z4;
     const int rowT = t * BM + rs * 16 + lr;
     if (GTR_DX_T) {
-      if (rowT < N) {
-        const size_t o = (size_t)rowT * D + col4;
-        ydv4 = *reinterpret_cast<const float4*>(a.dy + o);
-        if (!DOWN && a.has_prev) pov4 = *reinterpret_cast<const float4*>(a.p_out + o);
-      }
+      const size_t o = (size_t)min(rowT, N - 1) * D + col4;  // (row N - 1's values: unused)
+      ydv4 = *reinterpret_cast<const float4*>(a.dy + o);
+      if (!DOWN && a.has_prev) pov4 = *reinterpret_cast<const float4*>(a.p_out + o);
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -573,15 +579,17 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
       }
     }
     if (GTR_DX_T) {
-      if (rowT < N) {
+      const bool live = rowT < N;
+      {
         const size_t o = (size_t)rowT * D + col4;
+        const uint32_t ob = (uint32_t)(o * 4);  // rows past N: the buffer drops the store
         float4 v;
         if (DOWN) {  // z = y + dropout(h W2^T + b2)
           v.x = ydv4.x + (acc[0] + b24.x) * dr.mul(st_o, (uint32_t)o);
           v.y = ydv4.y + (acc[1] + b24.y) * dr.mul(st_o, (uint32_t)(o + 1));
           v.z = ydv4.z + (acc[2] + b24.z) * dr.mul(st_o, (uint32_t)(o + 2));
           v.w = ydv4.w + (acc[3] + b24.w) * dr.mul(st_o, (uint32_t)(o + 3));
-          *reinterpret_cast<float4*>(a.dx0 + o) = v;
+          dx0_buf.st4(ob, v);
         } else {
           v = make_float4(ydv4.x + acc[0], ydv4.y + acc[1], ydv4.z + acc[2], ydv4.w + acc[3]);
           if (a.has_prev) {
@@ -589,14 +597,16 @@ __global__ __launch_bounds__(GM_BLOCK) void k_dx(DxK a) {
             v.y *= dr.mul(st_prev, (uint32_t)(o + 1));
             v.z *= dr.mul(st_prev, (uint32_t)(o + 2));
             v.w *= dr.mul(st_prev, (uint32_t)(o + 3));
-            *reinterpret_cast<float4*>(a.p_dy + o) = v;
-            s14.x += v.x; s14.y += v.y; s14.z += v.z; s14.w += v.w;
-            s24.x += v.x * ((pov4.x - pm4.x) * pr4.x);
-            s24.y += v.y * ((pov4.y - pm4.y) * pr4.y);
-            s24.z += v.z * ((pov4.z - pm4.z) * pr4.z);
-            s24.w += v.w * ((pov4.w - pm4.w) * pr4.w);
+            pdy_buf.st4(ob, v);
+            // live rows only (a select, not a branch: the same sums as skipping the rest)
+            const float4 t1 = make_float4(s14.x + v.x, s14.y + v.y, s14.z + v.z, s14.w + v.w);
+            const float4 t2 = make_float4(s24.x + v.x * ((pov4.x - pm4.x) * pr4.x),
+                                          s24.y + v.y * ((pov4.y - pm4.y) * pr4.y),
+                                          s24.z + v.z * ((pov4.z - pm4.z) * pr4.z),
+                                          s24.w + v.w * ((pov4.w - pm4.w) * pr4.w));
+            if (live) { s14 = t1; s24 = t2; }
           } else {
-            *reinterpret_cast<float4*>(a.dx0 + o) = v;
+            dx0_buf.st4(ob, v);
           }
         }
       }
@@ -789,6 +799,16 @@ int gemm_grid(int tiles, int per_cu) {
   return tiles < cap ? (tiles > 0 ? tiles : 1) : (cap > 0 ? cap : 1);
 }
 
+// The epilogues store through raw buffers (Buf) addressed by 32-bit byte offsets: the
+// widest array, n_cap rows of 4D floats, must fit in 4 GB.
+int check_buf_rows(const gtr_batch* bt, int D, const char* who) {
+  if ((uint64_t)bt->n_cap * 4 * D * 4 >= (1ull << 32)) {
+    set_error("%s: n_cap %d rows of 4 x %d floats exceed the 4 GB reach of a buffer offset", who, bt->n_cap, D);
+    return GTR_E_ARG;
+  }
+  return GTR_OK;
+}
+
 }  // namespace
 
 GTR_PH_READER(gtr_dbg_gemm_phases)
@@ -800,6 +820,7 @@ extern "C" int gtr_qkvs_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     return GTR_E_ARG;
   }
   const int D = cfg->dim;
+  if (const int rc = check_buf_rows(bt, D, "gtr_qkvs_fwd")) return rc;
   if (D != 64 && D != 128 && D != 256) {
     set_error("gtr_qkvs_fwd: dim %d (the split layer path covers 64 / 128 / 256)", D);
     return GTR_E_ARG;
@@ -883,6 +904,7 @@ extern "C" int gtr_qkvs_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
     return GTR_E_ARG;
   }
   const int D = cfg->dim;
+  if (const int rc = check_buf_rows(bt, D, "gtr_qkvs_bwd")) return rc;
   if (D != 64 && D != 128 && D != 256) {
     set_error("gtr_qkvs_bwd: dim %d (the split layer path covers 64 / 128 / 256)", D);
     return GTR_E_ARG;
@@ -974,6 +996,7 @@ extern "C" int gtr_ffn_fwd(const gtr_config* cfg, const gtr_batch* bt, const gtr
   if (const int rc = ffn_check(cfg, bt, layers, l, "gtr_ffn_fwd", false, thresh, scale, drop_on)) return rc;
   if (ffn_generic(cfg, *layers[l].ffn)) return gen_ffn_fwd(cfg, bt, layers, l, (hipStream_t)stream);
   const int D = cfg->dim;
+  if (const int rc = check_buf_rows(bt, D, "gtr_ffn_fwd")) return rc;
   const gtr_layer& L = layers[l];
   const gtr_ffn& f = *L.ffn;
   hipStream_t s = (hipStream_t)stream;
@@ -1017,6 +1040,7 @@ extern "C" int gtr_ffn_bwd(const gtr_config* cfg, const gtr_batch* bt, const gtr
   int drop_on;
   if (const int rc = ffn_check(cfg, bt, layers, l, "gtr_ffn_bwd", true, thresh, scale, drop_on)) return rc;
   const int D = cfg->dim;
+  if (const int rc = check_buf_rows(bt, D, "gtr_ffn_bwd")) return rc;
   const gtr_layer& L = layers[l];
   const gtr_ffn& f = *L.ffn;
   if (!f.dz || !f.g2 || !f.da) { set_error("gtr_ffn_bwd: missing FFN gradient buffers"); return GTR_E_ARG; }

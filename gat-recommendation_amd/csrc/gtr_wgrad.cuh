@@ -209,20 +209,36 @@ __device__ __forceinline__ void wgrad_tile_mfma(const WJob& J, int tile, int t0,
 #pragma unroll
     for (int q = 0; q < NT; ++q) acc[i][q] = f32x4{0.f, 0.f, 0.f, 0.f};
   const float* Ap = J.A + m0 + c4;
+  // Loads are unconditional: a row past the range reads the range's last row (row 0 for
+  // an empty range) and is zeroed where it is used.  A load under a lane-dependent branch
+  // is skipped when no lane takes it, so the compiler cannot count it and waits for
+  // vmcnt(0) -- every row in flight -- before the next use.
+  const int rlast = max(0, r1 - 1);
+  const int jb0 = min(j16, J.M2 - 1), jb1 = min(16 + j16, J.M2 - 1);
   auto ld = [&](int t, float4& a, float4& b) {
-    a = make_float4(0.f, 0.f, 0.f, 0.f);
-    b = a;
-    if (t >= r1) return;
-    a = *reinterpret_cast<const float4*>(Ap + (size_t)t * J.lda);
+    const int tc = min(t, rlast);
+    a = *reinterpret_cast<const float4*>(Ap + (size_t)tc * J.lda);
     if (NARROW) {
-      const float* brow = J.B + (size_t)(J.bidx ? J.bidx[t] : t) * J.ldb;
-      b.x = j16 < J.M2 ? brow[j16] : (j16 == J.M2 ? 1.0f : 0.0f);
-      b.y = 16 + j16 < J.M2 ? brow[16 + j16] : (16 + j16 == J.M2 ? 1.0f : 0.0f);
+      const float* brow = J.B + (size_t)(J.bidx ? J.bidx[tc] : tc) * J.ldb;
+      b.x = brow[jb0];
+      b.y = brow[jb1];
     } else {
-      b = *reinterpret_cast<const float4*>(J.B + (size_t)t * J.ldb + n0 + c4);
+      b = *reinterpret_cast<const float4*>(J.B + (size_t)tc * J.ldb + n0 + c4);
     }
   };
-  auto mma = [&](const float4& a4, const float4& b4) {
+  // the operands of row t as the MFMAs take them: zero past the range; NARROW columns
+  // past M2 are the bias's ones column (at M2) or zero
+  auto fix = [&](int t, float4& a, float4& b) {
+    if (t >= r1) {
+      a = make_float4(0.f, 0.f, 0.f, 0.f);
+      b = a;
+    } else if (NARROW) {
+      if (j16 >= J.M2) b.x = j16 == J.M2 ? 1.0f : 0.0f;
+      if (16 + j16 >= J.M2) b.y = 16 + j16 == J.M2 ? 1.0f : 0.0f;
+    }
+  };
+  auto mma = [&](float4 a4, float4 b4, int t) {
+    fix(t, a4, b4);
     const float av[4] = {a4.x, a4.y, a4.z, a4.w};
     const float bv[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
@@ -247,11 +263,13 @@ __device__ __forceinline__ void wgrad_tile_mfma(const WJob& J, int tile, int t0,
     constexpr int c = decltype(S)::value, n = (c + 2) % 3;
     ld(t + 16 + kq, ra[n][0], rb[n][0]);
     ld(t + 20 + kq, ra[n][1], rb[n][1]);
-    mma(ra[c][0], rb[c][0]);
-    mma(ra[c][1], rb[c][1]);
+    mma(ra[c][0], rb[c][0], t + kq);
+    mma(ra[c][1], rb[c][1], t + 4 + kq);
     if (colsum) {
-      cs.x += ra[c][0].x; cs.y += ra[c][0].y; cs.z += ra[c][0].z; cs.w += ra[c][0].w;
-      cs.x += ra[c][1].x; cs.y += ra[c][1].y; cs.z += ra[c][1].z; cs.w += ra[c][1].w;
+      const float4 a0 = t + kq < r1 ? ra[c][0] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 a1 = t + 4 + kq < r1 ? ra[c][1] : make_float4(0.f, 0.f, 0.f, 0.f);
+      cs.x += a0.x; cs.y += a0.y; cs.z += a0.z; cs.w += a0.w;
+      cs.x += a1.x; cs.y += a1.y; cs.z += a1.z; cs.w += a1.w;
     }
   };
   for (int t = r0; t < r1; t += 24) {
