@@ -134,11 +134,17 @@ struct ProjIn {
   int item;  // layer 0: the tile row's item id (the LapPE fallback path reads by it)
 };
 
-template <int D, int MODE>
-__global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 64 ? 4 : 2))) void k_proj(ProjK a) {
+// CS > 1 (round 5, small batches): the output columns are split over CS workgroups per
+// row-tile stream (workgroup b: column slice b % CS of stream b / CS), each holding 1/CS of
+// W_all in registers: at a few thousand rows (one or two tiles per CU) the launch is its
+// W prologue plus one tile's MFMA chain, both CS times shorter per workgroup; the X tile
+// is built by every slice (its xin store by slice 0 only).  Same products, same k order.
+template <int D, int MODE, int CS = 1>
+__global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 64 || CS > 1 ? 4 : 2))) void k_proj(ProjK a) {
   constexpr bool FIRST = MODE == PJ_FIRST, FOLD = MODE == PJ_FOLD, DH = MODE == PJ_FFN_DH;
   using G = ProjGeom<D>;
-  constexpr int CT = G::CT, RT = G::RT, BM = G::BM, XS = G::XS, C4 = G::C4, KPE = G::KPE;
+  static_assert(G::CT % CS == 0, "column slices of whole tiles per wave");
+  constexpr int CT = G::CT / CS, RT = G::RT, BM = G::BM, XS = G::XS, C4 = G::C4, KPE = G::KPE;
   constexpr int NPE = FIRST && D >= 128 ? 4 : 0;  // LapPE float4s prefetched per thread
   using ProjIn = ::ProjIn<NPE>;
   __shared__ __attribute__((aligned(16))) float Xs[2][BM * XS];
@@ -148,7 +154,8 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 15, lg = lane >> 4;
   const int N = a.bt.hdr[0];
   const int ntile = (N + BM - 1) / BM;
-  if ((int)blockIdx.x >= ntile) return;  // block-uniform
+  const int cg = (int)blockIdx.x % CS;  // this workgroup's column slice
+  if ((int)blockIdx.x / CS >= ntile) return;  // block-uniform
   GTR_PH(10 + a.layer, 0);
   // Round 5: the waves' column tiles rotate with the workgroup's position on its XCD
   // (blocks b and b + 8 share an XCD), so that the 32 CUs of an XCD, loading W_all at
@@ -161,7 +168,7 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
   float bias[CT];
 #pragma unroll
   for (int c = 0; c < CT; ++c) {
-    const int ct = wsw + c * GM_WAVES;
+    const int ct = wsw + (cg * CT + c) * GM_WAVES;
     if (DH) {  // B[k][col] = W2[k][col], W2 = [D, 4D] row-major
       const float* wcol = a.w_all + (size_t)(lg * 4) * (4 * D) + ct * 16 + lr;
 #pragma unroll
@@ -237,7 +244,7 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
   // stores go through bounds-checked buffers, so no memory op sits under an exec-skipping
   // branch and the compiler counts them: the wait for a set's rows no longer drains the
   // other set's rows and the previous tile's stores (vmcnt(0)).
-  const Buf xin_buf(a.xin, (uint64_t)N * D * 4), qkvs_buf(a.qkvs, (uint64_t)N * 4 * D * 4);
+  const Buf xin_buf(a.xin, cg == 0 ? (uint64_t)N * D * 4 : 0), qkvs_buf(a.qkvs, (uint64_t)N * 4 * D * 4);
   auto item_of = [&](int t) -> int {
     return FIRST ? a.bt.node_item[min(t * BM + xi, N - 1)] : 0;
   };
@@ -317,8 +324,8 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
   // phase.  Two explicit register sets (the loop is unrolled by two, so no set is ever
   // COPIED: a copy of an in-flight load is a use, whose wait -- vector loads retire in
   // order -- drained every load behind it at each tile boundary).
-  const int GS = gridDim.x;
-  const int t0 = blockIdx.x;
+  const int GS = gridDim.x / CS;
+  const int t0 = blockIdx.x / CS;
   ProjIn S0, S1;
   {
     const int i0 = item_of(t0), i1 = item_of(t0 + GS);
@@ -367,7 +374,7 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
         const int row = t * BM + r * 16 + lr;
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
-          const int col = (wsw + c * GM_WAVES) * 16 + lg * 4;
+          const int col = (wsw + (cg * CT + c) * GM_WAVES) * 16 + lg * 4;
           const size_t o = (size_t)row * (4 * D) + col;
           float4 v;
           if (DH) {
@@ -388,7 +395,7 @@ __global__ __launch_bounds__(GM_BLOCK) __attribute__((amdgpu_waves_per_eu(D == 6
       for (int r = 0; r < RT; ++r)
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
-          const int col = (wsw + c * GM_WAVES) * 16 + lr;
+          const int col = (wsw + (cg * CT + c) * GM_WAVES) * 16 + lr;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
             const int row = t * BM + r * 16 + lg * 4 + i;
@@ -787,13 +794,18 @@ __global__ __launch_bounds__(GM_BLOCK) void k_ffn_wgrad(FfnWK a) {
 
 // Persistent grid: `per_cu` workgroups per CU (the register / LDS budget: 2 at D = 64,
 // 1 at D = 128), never more than the tiles.
-int gemm_grid(int tiles, int per_cu) {
+int gemm_cus() {
   static int cus = 0;
   if (cus <= 0) {
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
   }
+  return cus;
+}
+
+int gemm_grid(int tiles, int per_cu) {
+  const int cus = gemm_cus();
   const char* e = getenv("GTR_GEMM_GRID");  // tuning / tests
   const int cap = e ? atoi(e) : cus * per_cu;
   return tiles < cap ? (tiles > 0 ? tiles : 1) : (cap > 0 ? cap : 1);
@@ -882,8 +894,27 @@ extern "C" int gtr_qkvs_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   }
   k.w_all = L.w_all; k.b_all = L.b_all; k.xin = L.xin; k.qkvs = L.qkvs;
   const int bm = D == 64 ? ProjGeom<64>::BM : ProjGeom<128>::BM;
-  const int grid = gemm_grid((bt->n_cap + bm - 1) / bm, D == 64 ? 2 : 1);
+  const int tiles = (bt->n_cap + bm - 1) / bm;
   hipStream_t s = (hipStream_t)stream;
+  // Column slices at D = 128 when the row tiles number at most one per CU (a few thousand
+  // rows: C4 / C5 at B = 1024, 225 tiles): one workgroup per CU, i.e. CUs / 4 streams of
+  // ~4 pipelined tiles each.  Per-launch (C4 B = 1024, layer 0 / 1): 19.2 / 17.8 us whole
+  // rows, 15.7 / 13.8 us in slices at 4 tiles per stream (24.4 / 19.2 at 1, 18.2 / 15.2 at 2,
+  // 20.5 / 17.3 at 3, 18.6 / 16.1 at 6).  GTR_PROJ_CS=1|4 and GTR_PROJ_CS_TPB override.
+  const char* pcs = getenv("GTR_PROJ_CS");
+  const int cs = D != 128 ? 1 : pcs ? (atoi(pcs) == 4 ? 4 : 1) : (tiles <= gemm_cus() ? 4 : 1);
+  if (cs == 4) {
+    const char* tpb = getenv("GTR_PROJ_CS_TPB");
+    const int nst = gemm_cus() / 4 > 0 ? gemm_cus() / 4 : 1;
+    const int tp = tpb && atoi(tpb) > 0 ? atoi(tpb) : (tiles + nst - 1) / nst;
+    const int grid = 4 * gemm_grid((tiles + tp - 1) / tp, 2);  // streams of row tiles, four column slices each
+    if (l == 0) hipLaunchKernelGGL((k_proj<128, PJ_FIRST, 4>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
+    else if (ready) hipLaunchKernelGGL((k_proj<128, PJ_READY, 4>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
+    else hipLaunchKernelGGL((k_proj<128, PJ_FOLD, 4>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
+    GTR_HIP_CHECK_LAUNCH();
+    return GTR_OK;
+  }
+  const int grid = gemm_grid(tiles, D == 64 ? 2 : 1);
   if (D == 64) {
     if (l == 0) hipLaunchKernelGGL((k_proj<64, PJ_FIRST>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
     else if (ready) hipLaunchKernelGGL((k_proj<64, PJ_READY>), dim3(grid), dim3(GM_BLOCK), 0, s, k);
