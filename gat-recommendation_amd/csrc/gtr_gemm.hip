@@ -901,6 +901,7 @@ extern "C" int gtr_qkvs_fwd(const gtr_config* cfg, const gtr_batch* bt, const gt
   // ~4 pipelined tiles each.  Per-launch (C4 B = 1024, layer 0 / 1): 19.2 / 17.8 us whole
   // rows, 15.7 / 13.8 us in slices at 4 tiles per stream (24.4 / 19.2 at 1, 18.2 / 15.2 at 2,
   // 20.5 / 17.3 at 3, 18.6 / 16.1 at 6).  GTR_PROJ_CS=1|4 and GTR_PROJ_CS_TPB override.
+  // (Half-width slices at C3 B = 8192, four waves per SIMD: 49.5 / 46.5 -> 79 / 53 us.)
   const char* pcs = getenv("GTR_PROJ_CS");
   const int cs = D != 128 ? 1 : pcs ? (atoi(pcs) == 4 ? 4 : 1) : (tiles <= gemm_cus() ? 4 : 1);
   if (cs == 4) {
