@@ -215,11 +215,23 @@ __device__ __forceinline__ void wgrad_tile_mfma(const WJob& J, int tile, int t0,
   // vmcnt(0) -- every row in flight -- before the next use.
   const int rlast = max(0, r1 - 1);
   const int jb0 = min(j16, J.M2 - 1), jb1 = min(16 + j16, J.M2 - 1);
-  auto ld = [&](int t, float4& a, float4& b) {
+  // NARROW rows of B gathered through bidx: the row ids are loaded 24 rows (three
+  // k-steps) before the row itself (ring ri below), so a gathered row's load does not
+  // wait on an id requested just before it -- with in-order returns that wait was a
+  // vmcnt(0) per k-step (the LapPE job: 14 us of the C3 B = 8192 launch).
+  // (the id is loaded unconditionally -- from A's words when there is no bidx, unused --
+  // so the load is counted: a load under the bidx branch made the loop wait vmcnt(0))
+  const int32_t* ib = J.bidx ? J.bidx : reinterpret_cast<const int32_t*>(J.A);
+  auto idx = [&](int t) -> int {
+    const int tc = min(t, rlast);
+    const int v = __builtin_nontemporal_load(ib + tc);
+    return J.bidx ? v : tc;
+  };
+  auto ld = [&](int t, int bi, float4& a, float4& b) {
     const int tc = min(t, rlast);
     a = *reinterpret_cast<const float4*>(Ap + (size_t)tc * J.lda);
     if (NARROW) {
-      const float* brow = J.B + (size_t)(J.bidx ? J.bidx[tc] : tc) * J.ldb;
+      const float* brow = J.B + (size_t)bi * J.ldb;
       b.x = brow[jb0];
       b.y = brow[jb1];
     } else {
@@ -255,14 +267,30 @@ __device__ __forceinline__ void wgrad_tile_mfma(const WJob& J, int tile, int t0,
   // no set is ever COPIED (a copy of an in-flight load is a use whose wait -- vector
   // loads retire in order -- drained the 16 rows in flight at every step).
   float4 ra[3][2], rb[3][2];
-  ld(r0 + kq, ra[0][0], rb[0][0]);
-  ld(r0 + 4 + kq, ra[0][1], rb[0][1]);
-  ld(r0 + 8 + kq, ra[1][0], rb[1][0]);
-  ld(r0 + 12 + kq, ra[1][1], rb[1][1]);
+  int ri[3][2] = {{0, 0}, {0, 0}, {0, 0}};  // NARROW: ids of the rows set n loads next
+  if (NARROW) {
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      ri[q][0] = idx(r0 + 8 * q + kq);
+      ri[q][1] = idx(r0 + 8 * q + 4 + kq);
+    }
+  }
+  ld(r0 + kq, ri[0][0], ra[0][0], rb[0][0]);
+  ld(r0 + 4 + kq, ri[0][1], ra[0][1], rb[0][1]);
+  ld(r0 + 8 + kq, ri[1][0], ra[1][0], rb[1][0]);
+  ld(r0 + 12 + kq, ri[1][1], ra[1][1], rb[1][1]);
+  if (NARROW) {
+    ri[0][0] = idx(r0 + 24 + kq); ri[0][1] = idx(r0 + 28 + kq);
+    ri[1][0] = idx(r0 + 32 + kq); ri[1][1] = idx(r0 + 36 + kq);
+  }
   auto stepk = [&](auto S, int t) {
     constexpr int c = decltype(S)::value, n = (c + 2) % 3;
-    ld(t + 16 + kq, ra[n][0], rb[n][0]);
-    ld(t + 20 + kq, ra[n][1], rb[n][1]);
+    ld(t + 16 + kq, ri[n][0], ra[n][0], rb[n][0]);
+    ld(t + 20 + kq, ri[n][1], ra[n][1], rb[n][1]);
+    if (NARROW) {  // set n's next rows (three k-steps on)
+      ri[n][0] = idx(t + 40 + kq);
+      ri[n][1] = idx(t + 44 + kq);
+    }
     mma(ra[c][0], rb[c][0], t + kq);
     mma(ra[c][1], rb[c][1], t + 4 + kq);
     if (colsum) {
