@@ -84,6 +84,25 @@ def test_status_codes_raise(libpath):
         _lib.check(rc, "conv_fwd")
 
 
+def test_split_gemms_refuse_rows_past_the_buffer_offset_reach(libpath):
+    """The split-path GEMMs store through raw buffers with 32-bit byte offsets: a batch whose
+    n_cap rows of 4D floats exceed 4 GB is refused before any device work (argument check
+    only, no GPU needed)."""
+    from etpgt.backend import _lib
+
+    lib = _lib.lib()
+    cfg = _lib.GtrConfig(num_items=100, dim=128, heads=4, num_layers=2, training=1, row_group=16)
+    bt = _lib.GtrBatch(n_cap=(1 << 32) // (4 * 128 * 4), b_cap=1, e_cap=1, n_neg=1)
+    layers = (_lib.GtrLayer * 2)()
+    emb = _lib.GtrEmbed()
+    rc = lib.gtr_qkvs_fwd(ctypes.byref(cfg), ctypes.byref(bt), ctypes.byref(emb), layers, 1, None)
+    assert rc != 0
+    assert "4 GB" in lib.gtr_last_error().decode()
+    rc = lib.gtr_qkvs_bwd(ctypes.byref(cfg), ctypes.byref(bt), layers, 1, None, None)
+    assert rc != 0
+    assert "4 GB" in lib.gtr_last_error().decode()
+
+
 def test_lap_plan_is_nnz_balanced(libpath):
     """gtr_lap_plan (host-only): every nonzero lands in exactly one item of <= chunk
     nonzeros, in row order; split rows list their consecutive partial slots."""
