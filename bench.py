@@ -441,11 +441,13 @@ def main():
         }
     if world > 1:
         # every collective of the run is done (the MAX all-reduce and the replica check
-        # above); the process group is NOT destroyed: a one-rank RCCL communicator that ran
-        # graph-captured all-to-alls did not come back from destroy_process_group on this
-        # stack (tests/test_gpu_distributed.py, scripts/dbg/capture_probe.py), and a rank
-        # stuck there would hold up the line.  The ranks leave through os._exit below.
+        # above).  The captured graphs hold RCCL collectives, and a communicator whose
+        # collectives are still captured in a live graph does not come back from
+        # destroy_process_group (scripts/dbg/teardown_probe.py): release them first
+        seq = None
+        step.close()
         torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
     if rank == 0:
         legs = [int(x) for x in args.strong_batches.split(",") if x.strip() and int(x) > 0]
         if legs and not cfg.get("shard") and os.environ.get("GTR_STRONG_CHILD") != "1":
@@ -454,11 +456,6 @@ def main():
             out["strong_scaling"] = strong_scaling_legs(world, legs, args.strong_steps)
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(out) + "\n").encode())
-    if world > 1:
-        sys.stdout.flush()
-        sys.stderr.flush()
-        torch.cuda.synchronize()
-        os._exit(0)  # no teardown of the RCCL communicator (see above); the line is written
 
 
 def _child_line(cmd: list, env: dict, timeout: float) -> dict:

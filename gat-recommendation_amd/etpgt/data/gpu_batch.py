@@ -164,6 +164,13 @@ class GpuBatchBuilder:
         if self.scratch is None or self.scratch.numel() < 2 * caps.b_cap + 2:
             # + 2: the one-launch build's arrival ticket (gtr_build_batch, zero between builds)
             self.scratch = torch.zeros(2 * caps.b_cap + 2, dtype=torch.int32, device=self.store.device)
+            self._ticket_at = 2 * caps.b_cap
+        elif getattr(self, "_ticket_at", None) != 2 * caps.b_cap:
+            # rebound to other capacities: the ticket words may hold a node / edge offset the
+            # multi-workgroup scan (B > 256) wrote there -- the last-arriver test would then
+            # never fire and the cursor would stop advancing
+            self.scratch[2 * caps.b_cap: 2 * caps.b_cap + 2].zero_()
+            self._ticket_at = 2 * caps.b_cap
         st = self.store
         stride = max(self.stride, B)
         L.check(L.lib().gtr_build_batch_strided(C.byref(st.ss), st.slots.data_ptr(), st.num_slots, st.max_len,

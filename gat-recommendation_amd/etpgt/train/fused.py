@@ -547,6 +547,9 @@ class FusedTrainStep:
         halves around the gradient all-gather in DP mode; with SyncBN also a cut after
         every producer of BatchNorm partials (all-gather of the partials)."""
         if self.shard is not None:
+            # a launch or capture that raised between fork() and join() (e.g. a refused RCCL
+            # capture retried piece by piece) must not leave later launches on the forked stream
+            self.shard.forked = False
             return self._shard_pieces(with_pe)
         if self.dp is None:
             def whole():
@@ -946,6 +949,22 @@ class FusedTrainStep:
                 "consts": self.shard_state.consts.data_ptr() if self.shard_state is not None else None,
                 "gen": self._gen}
 
+    def stale_reason(self, h: dict) -> str | None:
+        """Why a multi-step handle can no longer be replayed (None: it can): its captured
+        buffers were rebound (``_gen``), or the per-step constants it points at were -- or
+        for its ``h["n"]`` more steps would have to be -- reallocated."""
+        n = h["n"]
+        if h.get("gen") != self._gen:
+            return "the step's buffers were rebound since this multi-step graph was captured: capture the steps again"
+        if self.shard_state is not None:
+            ss = self.shard_state
+            if h.get("consts") != ss.consts.data_ptr() or self._host_steps + n + 2 >= ss.consts.shape[0]:
+                return ("the row-sharded table's step constants were (or would have to be) reallocated: "
+                        "capture the steps again")
+        if self.lazy and (h["lz_cap"] != self.lz.cap or self._host_steps + n + 2 >= self.lz.cap):
+            return "the lazy table's step constants were (or would have to be) reallocated: capture the steps again"
+        return None
+
     def run_steps(self, h: dict):
         """Replay a ``capture_steps`` / ``capture_steps_copied`` graph: ``h["n"]`` training
         steps in one launch.  Every check runs before any state changes: a handle whose
@@ -955,17 +974,9 @@ class FusedTrainStep:
         if not self.model.training:
             raise RuntimeError("FusedTrainStep requires model.train()")
         n = h["n"]
-        if h.get("gen") != self._gen:
-            raise RuntimeError("the step's buffers were rebound since this multi-step graph was captured: "
-                               "capture the steps again")
-        if self.shard_state is not None:
-            ss = self.shard_state
-            if h.get("consts") != ss.consts.data_ptr() or self._host_steps + n + 2 >= ss.consts.shape[0]:
-                raise RuntimeError("the row-sharded table's step constants were (or would have to be) reallocated: "
-                                   "capture the steps again")
-        if self.lazy and (h["lz_cap"] != self.lz.cap or self._host_steps + n + 2 >= self.lz.cap):
-            raise RuntimeError("the lazy table's step constants were (or would have to be) reallocated: "
-                               "capture the steps again")
+        why = self.stale_reason(h)
+        if why is not None:
+            raise RuntimeError(why)
         self._host_steps += n
         if self.lazy:
             self._dirty = True
@@ -1072,6 +1083,21 @@ class FusedTrainStep:
             raise ValueError("Expected more than 1 value per channel when training (BatchNorm1d)")
         with_pe = self.load(batch)
         return self.run(with_pe)
+
+    def close(self):
+        """Drop every captured graph of this step (per-step, per-image and, by bumping the
+        binding generation, the multi-step handles callers hold -- those must be dropped by
+        their holders too) and drain the device.  A graph that captured an RCCL collective
+        pins its communicator: ``dist.destroy_process_group()`` does not return while such
+        a graph is alive (scripts/dbg/teardown_probe.py), so multi-rank drivers call this
+        first.  The step stays usable: the next ``run`` captures again."""
+        import gc
+
+        self.graph = self.graph_pe = self.graph_b = None
+        self.resident_graphs = None
+        self._gen += 1
+        gc.collect()
+        torch.cuda.synchronize(self.dev)
 
     # ------------------------------------------------------------------ state
     @property

@@ -43,16 +43,24 @@ class Trainer:
     def __init__(self, model: nn.Module, train_loader, val_loader, optimizer: torch.optim.Optimizer,
                  device: str = "cuda", output_dir: Path | str = "outputs", max_epochs: int = 100,
                  patience: int = 10, eval_every: int = 1, k_values: list[int] | None = None,
-                 loss_fn: nn.Module | None = None, fused: bool | None = None, sync_bn: bool | None = None):
-        """Reference signature (trainer.py:23-67) plus two optional keywords: ``fused``
-        (force / forbid the fused HIP step) and ``sync_bn`` (data parallel: BatchNorm
+                 loss_fn: nn.Module | None = None, fused: bool | None = None, sync_bn: bool | None = None,
+                 shard_table: bool | None = None):
+        """Reference signature (trainer.py:23-67) plus three optional keywords: ``fused``
+        (force / forbid the fused HIP step), ``sync_bn`` (data parallel: BatchNorm
         statistics over every rank's batch; default on when the default process group spans
-        more than one rank, so P ranks train exactly like one GPU on the global batch).
-        Under a process group only rank 0 writes checkpoints and history.json."""
+        more than one rank, so P ranks train exactly like one GPU on the global batch) and
+        ``shard_table`` (data parallel: the item table and its AdamW moments row-sharded
+        across the ranks -- rank p owns rows r % P == p, rows and row gradients travel by
+        all-to-all, etpgt.train.sharded -- instead of replicated on every rank; default
+        off, ``GTR_SHARD_TABLE=1`` turns it on).  Results equal the replicated step bit for
+        bit.  Under a process group only rank 0 writes checkpoints and history.json."""
         from etpgt.train.distributed import world_info
 
         self.rank, self.world = world_info()
         self.sync_bn = (self.world > 1) if sync_bn is None else bool(sync_bn)
+        if shard_table is None:
+            shard_table = os.environ.get("GTR_SHARD_TABLE") == "1"
+        self.shard_table = bool(shard_table) and self.world > 1
         self.model = model.to(device)
         self.train_loader = train_loader
         self.val_loader = val_loader
@@ -104,8 +112,23 @@ class Trainer:
         self._fused = FusedTrainStep(self.model, lr=g["lr"], betas=g["betas"], eps=g["eps"],
                                      weight_decay=g["weight_decay"], decoupled=type(opt) is torch.optim.AdamW,
                                      loss=spec[0], temperature=spec[1], alpha=spec[2],
-                                     sync_bn=self.sync_bn and self.world > 1)
+                                     sync_bn=self.sync_bn and self.world > 1, shard_table=self.shard_table)
         return self._fused
+
+    def _sync_table(self):
+        """Row-sharded table: bring the ranks' shards into the model's item table before
+        anything reads the model (evaluation, checkpoints).  Collective: every rank calls it
+        at the same point of ``train``."""
+        if self._fused is not None and self._fused.shard_state is not None:
+            self._fused.sync_table()
+
+    def close(self):
+        """Release the captured step graphs (they hold RCCL collectives under a process
+        group): call before ``dist.destroy_process_group()``, whose communicator teardown
+        waits for every graph that captured one of its collectives to be destroyed."""
+        self._chunk_graph = None
+        if self._fused is not None:
+            self._fused.close()
 
     def _sync_optimizer_state(self):
         if self._fused is not None:
@@ -142,8 +165,11 @@ class Trainer:
             i = 1
         while K > 1 and full - i >= K:
             h = self._chunk_graph
-            if h is None or h["n"] != K or h.get("gen") != fused._gen or h.get("step") is not fused:
-                # captured once per binding; every rank reaches this point together
+            if h is None or h["n"] != K or h.get("step") is not fused or fused.stale_reason(h) is not None:
+                # captured once per binding (and again when the lazy / sharded per-step
+                # constants must grow); every rank counts the same steps, so every rank
+                # reaches this point together
+                self._chunk_graph = h = None  # a stale graph is released before the next capture
                 h = fused.capture_steps_built(K, reserve=full)
                 if h is None:
                     break  # not capturable whole (gloo): one step graph per batch
@@ -200,6 +226,7 @@ class Trainer:
 
     @torch.no_grad()
     def evaluate(self) -> dict:
+        self._sync_table()
         self.model.eval()
         preds, targets = [], []
         for batch in self.val_loader:

@@ -24,7 +24,10 @@ Differences, each deliberate:
   ``world * --batch-size`` sessions (``DeviceSessionLoader(rank, world)``) with gradients
   averaged and BatchNorm statistics synchronised across the ranks (SyncBN), i.e. like one
   GPU on the global batch.  Every rank evaluates the full validation set (the replicas
-  are identical); rank 0 writes the outputs.
+  are identical); rank 0 writes the outputs.  ``--shard-table on`` (added) keeps the item
+  table and its AdamW moments row-sharded across the ranks instead of replicated
+  (etpgt.train.sharded; bitwise the replicated step).  At the end the captured step graphs
+  are released and the process group destroyed.
 """
 
 from __future__ import annotations
@@ -87,6 +90,9 @@ def parse_args(argv=None):
     p.add_argument("--device", type=str, default="cuda", help="Device (cuda/cpu)")
     p.add_argument("--device-batches", type=str, default="auto", choices=["auto", "on", "off"],
                    help="build batches on the GPU inside the training step (auto: on for CUDA graph transformers)")
+    p.add_argument("--shard-table", type=str, default="auto", choices=["auto", "on", "off"],
+                   help="data parallel: row-shard the item table and its AdamW moments across the ranks "
+                        "(auto: GTR_SHARD_TABLE=1)")
     return p.parse_args(argv)
 
 
@@ -176,11 +182,23 @@ def main(argv=None):
     logger.info(f"Model parameters: {num_params:,}")
     optimizer = torch.optim.AdamW(model.parameters(), lr=args.lr, weight_decay=args.weight_decay)
     output_dir = Path(args.output_dir) / args.model
+    shard = None if args.shard_table == "auto" else args.shard_table == "on"
     trainer = Trainer(model=model, train_loader=train_loader, val_loader=val_loader, optimizer=optimizer,
                       device=args.device, output_dir=output_dir, max_epochs=args.max_epochs, patience=args.patience,
-                      eval_every=args.eval_every)
+                      eval_every=args.eval_every, shard_table=shard)
+    if world > 1 and trainer.shard_table:
+        logger.info("Item table row-sharded across the ranks")
     logger.info("Starting training...")
-    trainer.train()
+    try:
+        trainer.train()
+    finally:
+        # captured graphs hold RCCL collectives: released before the communicator goes
+        trainer.close()
+        if world > 1:
+            import torch.distributed as dist
+
+            if dist.is_initialized():
+                dist.destroy_process_group()
     logger.info("Training complete!")
     logger.info(f"Best validation recall@10: {trainer.best_val_metric:.4f}")
     return trainer

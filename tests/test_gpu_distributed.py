@@ -523,15 +523,11 @@ def _shard_multi_worker(port, q, two_class=False):
         f1.sync_table(); f2.sync_table()
         same = all(torch.equal(a, b) for a, b in zip(m1.parameters(), m2.parameters()))
         q.put((out, same, h is not None, f1.steps, f2.steps))
-        if two_class:
-            # a one-rank RCCL communicator that ran graph-captured all-to-alls does not
-            # come back from destroy_process_group on this stack (the same hang shows in
-            # scripts/dbg/capture_probe.py without any of this code): hand the result over
-            # and leave without the teardown
-            torch.cuda.synchronize()
-            q.close()
-            q.join_thread()
-            os._exit(0)
+        # the graphs that captured RCCL collectives pin the communicator: release them, or
+        # destroy_process_group() below never returns (scripts/dbg/teardown_probe.py)
+        h = None
+        f1.close()
+        f2.close()
     finally:
         dist.destroy_process_group()
 
@@ -552,9 +548,10 @@ def test_sharded_multi_step_graph_equals_per_step_launches(two_class):
         out, same, captured, s1, s2 = collect(q, [p], 1, 300)[0]
     finally:
         p.join(timeout=60)
-        if p.exitcode is None:  # the worker we started, stuck in teardown
+        if p.exitcode is None:  # the worker we started, stuck in teardown: fail, do not hang
             p.kill()
             p.join(10)
+    assert p.exitcode == 0, f"worker exit code {p.exitcode} (teardown)"
     assert captured and s1 == s2 == 14
     for l1, l2 in out:
         assert l1 == l2

@@ -112,37 +112,43 @@ def _script():
     return tb
 
 
-def _args(d, out, B):
+EPOCHS = 2
+
+
+def _args(d, out, B, shard):
     return ["--model", "graph_transformer_optimized", "--train-sessions", str(d / "train.csv"),
             "--val-sessions", str(d / "val.csv"), "--graph-edges", str(d / "graph_edges.csv"),
             "--embedding-dim", "32", "--hidden-dim", "32", "--num-layers", "2", "--num-heads", "2",
-            "--dropout", "0", "--batch-size", str(B), "--num-negatives", "5", "--max-epochs", "1",
-            "--num-workers", "0", "--output-dir", str(out)]
+            "--dropout", "0", "--batch-size", str(B), "--num-negatives", "5", "--max-epochs", str(EPOCHS),
+            "--num-workers", "0", "--output-dir", str(out), "--shard-table", "on" if shard else "off"]
 
 
-def _rank_main(rank, world, port, d, out, B, q):
+def _rank_main(rank, world, port, d, out, B, q, shard):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
                       LOCAL_RANK=str(rank), GTR_SHARE_DEVICE="1")
-    try:
-        tr = _script().main(_args(d, out, B))
-        sd = {k: v.detach().cpu().numpy() for k, v in tr.model.state_dict().items()}
-        q.put((rank, tr.history, sd))
-    finally:
-        import torch.distributed as dist
+    # main() releases the captured graphs and destroys the process group itself
+    tr = _script().main(_args(d, out, B, shard))
+    import torch.distributed as dist
 
-        if dist.is_initialized():
-            dist.destroy_process_group()
+    assert not dist.is_initialized()
+    sd = {k: v.detach().cpu().numpy() for k, v in tr.model.state_dict().items()}
+    q.put((rank, tr.history, sd, tr.shard_table, tr._fused.shard_state is not None))
 
 
-def test_train_baseline_two_ranks_match_oracle_on_the_global_batch(tmp_path):
+@pytest.mark.parametrize("shard", [False, True], ids=["replicated", "row_sharded"])
+def test_train_baseline_two_ranks_match_oracle_on_the_global_batch(tmp_path, shard):
     """Two ranks of the drop-in train_baseline.py (SyncBN data parallel, B = 8 per rank,
-    sharing the GPU over gloo) against the CPU ORACLE replaying the epoch on the global
-    batches of 16 sessions (one-GPU semantics): the same initial weights (set_seed(42) + the
-    factory), the same epoch order (the DataLoader iterator's _base_seed and RandomSampler
-    draws), the same per-session examples and position-keyed negatives (oracle/batch_ref.py
-    restates the device stream; rank r builds sessions [16 i + 8 r, +8) of global batch i).
-    Replicas are bit-identical; the epoch loss and every trained parameter match the
-    oracle ELEMENTWISE (gpu_helpers.close_trained), the running statistics too."""
+    sharing the GPU over gloo) for two epochs against the CPU ORACLE replaying them on the
+    global batches of 16 sessions (one-GPU semantics): the same initial weights
+    (set_seed(42) + the factory), the same epoch orders (per epoch the DataLoader
+    iterator's _base_seed and RandomSampler draws; the validation pass between the epochs
+    draws one _base_seed), the same per-session examples and position-keyed negatives
+    (oracle/batch_ref.py restates the device stream; rank r builds sessions [16 i + 8 r, +8)
+    of global batch i).  ``row_sharded``: ``--shard-table on``, the item table and its
+    moments row-sharded across the two ranks (SURVEY §8e ii).  Replicas are bit-identical;
+    each epoch's loss and every trained parameter match the oracle ELEMENTWISE
+    (gpu_helpers.close_trained), the running statistics too; the ranks leave through
+    ``destroy_process_group`` (exit code 0)."""
     import batch_ref as BR
     import etpgt_ref as R
 
@@ -159,13 +165,15 @@ def test_train_baseline_two_ranks_match_oracle_on_the_global_batch(tmp_path):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, d, tmp_path / "dp", B, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, d, tmp_path / "dp", B, q, shard))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = {}
     try:
         for item in collect(q, procs, world):
-            rank, hist, sd = item
+            rank, hist, sd, tr_shard, st_shard = item
+            assert tr_shard == st_shard == shard
             res[rank] = (hist, sd)
     finally:
         for p in procs:
@@ -182,11 +190,15 @@ def test_train_baseline_two_ranks_match_oracle_on_the_global_batch(tmp_path):
     set_seed(42)
     init = create_graph_transformer_optimized(T, embedding_dim=32, hidden_dim=32, num_layers=2, num_heads=2,
                                               dropout=0.0, use_laplacian_pe=True, use_ffn=False, ffn_expansion=2)
-    torch.empty((), dtype=torch.int64).random_()  # the epoch iterator's _base_seed draw
-    seed = int(torch.empty((), dtype=torch.int64).random_().item())  # the epoch's RandomSampler draw
-    g = torch.Generator()
-    g.manual_seed(seed)
-    order = torch.randperm(len(tr), generator=g).numpy()
+    orders = []
+    for e in range(EPOCHS):
+        if e > 0:
+            torch.empty((), dtype=torch.int64).random_()  # the validation pass's iterator (shuffle=False)
+        torch.empty((), dtype=torch.int64).random_()  # the epoch iterator's _base_seed draw
+        seed = int(torch.empty((), dtype=torch.int64).random_().item())  # the epoch's RandomSampler draw
+        g = torch.Generator()
+        g.manual_seed(seed)
+        orders.append(torch.randperm(len(tr), generator=g).numpy())
     ref = R.ref_create_graph_transformer_optimized(T, embedding_dim=32, hidden_dim=32, num_layers=2, num_heads=2,
                                                    dropout=0.0, use_laplacian_pe=True)
     isd = {k: v.clone() for k, v in init.state_dict().items()}
@@ -197,14 +209,16 @@ def test_train_baseline_two_ranks_match_oracle_on_the_global_batch(tmp_path):
     ei = tr.edge_index.numpy()
     keys = np.unique(ei[0].astype(np.int64) * tr.num_items + ei[1].astype(np.int64))
     S, GB = len(tr), world * B
-    losses = []
-    for i in range(-(-S // GB)):
-        b = min(GB, S - i * GB)
-        ex = BR.build_batch(tr._ptr, tr._items, keys, tr.num_items, order, i * GB, b, 50, n, 42)
-        rb = R.ref_batch_from(collate_sessions(ex))
-        losses.append(float(trio.step(lambda mod, o: R.ref_train_step(mod, rb, o, "bpr"))))
-    want = float(np.mean(losses))
-    assert abs(hist["train_loss"][0] - want) <= 1e-3 * abs(want), (hist["train_loss"][0], want)
+    assert len(hist["train_loss"]) == EPOCHS
+    for e, order in enumerate(orders):
+        losses = []
+        for i in range(-(-S // GB)):
+            b = min(GB, S - i * GB)
+            ex = BR.build_batch(tr._ptr, tr._items, keys, tr.num_items, order, e * S + i * GB, b, 50, n, 42)
+            rb = R.ref_batch_from(collate_sessions(ex))
+            losses.append(float(trio.step(lambda mod, o: R.ref_train_step(mod, rb, o, "bpr"))))
+        want = float(np.mean(losses))
+        assert abs(hist["train_loss"][e] - want) <= 1e-3 * abs(want), (e, hist["train_loss"][e], want)
     trio.compare({k: torch.from_numpy(sd[k]) for k, _ in ref.named_parameters()}, lr=1e-3)
     b64 = dict(trio.ref64.named_buffers())
     b1 = dict(trio.ref1.named_buffers())
