@@ -1165,6 +1165,15 @@ __global__ __launch_bounds__(AR_BLOCK) __attribute__((amdgpu_waves_per_eu(GTR_AR
 #ifndef GTR_AR4_WAVES_EU
 #define GTR_AR4_WAVES_EU 6
 #endif
+#ifndef AR4_FOLD      // 1: a round's edges folded with one rescale (U + 1 exps); 0: edge by edge (2 per edge)
+#define AR4_FOLD 1
+#endif
+#ifndef AR4_WBLDS     // 1: the gate's weights staged in LDS per workgroup; 0: loaded per wave after the edges
+#define AR4_WBLDS 0
+#endif
+#ifndef AR4_LANEDROP  // 1: the round's dropout hashes lane-parallel (one per lane) when they fit one wave
+#define AR4_LANEDROP 0
+#endif
 
 template <int O>
 __device__ __forceinline__ float xor_add(float x) {
@@ -1225,6 +1234,9 @@ __global__ __launch_bounds__(AR_BLOCK) __attribute__((amdgpu_waves_per_eu(GTR_AR
   constexpr int EPR = U * SPR;   // edges of a row per round
   static_assert(RPI >= 2, "a sub-group per row of the pair");
   __shared__ __attribute__((aligned(16))) float s_out[AR_ROWS][D];
+#if AR4_WBLDS
+  __shared__ __attribute__((aligned(16))) float s_wb[3 * D];  // the gate's weights
+#endif
   __shared__ float s_lg[AR_WAVES][AR_ECH][AR_HMAX];
   __shared__ float s_mz[AR_WAVES][2][AR_HMAX][2];
   __shared__ float s_red[2 * AR_BLOCK + D];
@@ -1238,37 +1250,56 @@ __global__ __launch_bounds__(AR_BLOCK) __attribute__((amdgpu_waves_per_eu(GTR_AR
   if (g >= Gn) return;  // block-uniform: only live workgroups write partials and arrive
   const int r0 = g * AR_ROWS, nrow = min(AR_ROWS, N - r0);
   GTR_PH(20 + a.layer, 0);
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int t0 = r0 + wave * AR_RPW;
+  const bool live = t0 < N;                 // wave-uniform
+  const bool two = t0 + 1 < N;
+  const int tc = live ? t0 : 0;             // clamped: the loads below are unconditional
+  const int e0 = a.bt.in_ptr[tc], em = a.bt.in_ptr[tc + 1];
+  const int e2r = a.bt.in_ptr[min(tc + 2, N)];
   const uint32_t ctr = a.rng_ctr ? load_step_ctr(a.rng_ctr) + a.ctr_add : 0u;
+  // the gate's weights are staged once per workgroup, their load issued behind the row
+  // pointers' (an LDS read after the edges instead of a dependent L2 round trip at the end
+  // of every wave)
+  static_assert(3 * D / 4 <= AR_BLOCK, "one float4 of the gate weights per thread");
+#if AR4_WBLDS
+  if (tid < 3 * D / 4)
+    *reinterpret_cast<float4*>(&s_wb[4 * tid]) = *reinterpret_cast<const float4*>(a.w_beta + 4 * tid);
+  __syncthreads();
+#endif
   const Drop dr{a.seed, a.thresh, a.scale, a.drop_on != 0};
   const uint32_t st_attn = drop_stream(0, (uint32_t)a.layer, ctr);
   const int sub = lane / LPR, c4 = lane - sub * LPR, col = 4 * c4;
   const int rr = sub / SPR, si = sub - rr * SPR;  // this lane's row of the pair, its slot in the row
   const int C = a.C, H = a.H;
+  const int hsh = __ffs(H) - 1;       // H is a power of two (D and C are)
   const int HL = C >= 4 ? C / 4 : 1;  // lanes of one head inside a sub-group
   const int head = col / C;
   const bool leader = (c4 & (HL - 1)) == 0;
-  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  const int t0 = r0 + wave * AR_RPW;
-  if (t0 < N) {  // wave-uniform
-    const bool two = t0 + 1 < N;
-    const int e0 = a.bt.in_ptr[t0], em = a.bt.in_ptr[t0 + 1];
-    const int e2 = two ? a.bt.in_ptr[t0 + 2] : em;
+  const float inv_sc = 1.0f / a.sqrt_c;
+  // dropout multipliers of a round's (row, slot, head) triples, one per lane, when they fit
+  // one wave (EPR * H <= 32): a lane hashes one triple instead of every lane hashing U
+  const bool lane_drop = AR4_LANEDROP && dr.on && 2 * EPR * H <= 64;
+  if (live) {  // wave-uniform
+    const int e2 = two ? e2r : em;
     const int ne0 = em - e0, ne = e2 - e0;
     const bool mine = rr == 0 || two;          // this lane's row exists
     const int eb = rr == 0 ? 0 : ne0;          // the row's first edge (pair-local)
     const int nr = rr == 0 ? ne0 : ne - ne0;   // the row's in-edges
     const int nmax = max(ne0, ne - ne0);
     GTR_PH(20 + a.layer, 8);
-    const float* qrow = a.qkvs + (size_t)(t0 + rr) * (4 * D) + col;
-    const float4 q = mine ? *reinterpret_cast<const float4*>(qrow) : z4;
-    const float4 sv = mine ? *reinterpret_cast<const float4*>(qrow + 3 * D) : z4;
+    const float* qrow = a.qkvs + (size_t)(t0 + (mine ? rr : 0)) * (4 * D) + col;
+    const float4 q = *reinterpret_cast<const float4*>(qrow);
+    const float4 sv = *reinterpret_cast<const float4*>(qrow + 3 * D);
     const bool lds_lg = ne <= AR_ECH;
     const float* K = a.qkvs + D + col;
     const float* V = a.qkvs + 2 * D + col;
     OnlineSm st{-INFINITY, 0.0f, z4};
     // the pair's source ids, one per lane (pairs of more than 64 in-edges: per round)
     const bool one_chunk = ne <= 64;
-    const int my_src = lane < ne ? a.bt.in_src[e0 + lane] : 0;
+    const int my_src = a.bt.in_src[ne > 0 ? e0 + min(lane, ne - 1) : 0];  // clamped, unconditional
+    // this lane's triple for the lane-parallel dropout hash: (row dr_r, slot dr_s, head dr_h)
+    const int dr_r = lane >> (hsh + __ffs(EPR) - 1), dr_s = (lane >> hsh) & (EPR - 1), dr_h = lane & (H - 1);
     for (int j = 0; j < nmax; j += EPR) {
       int ids = my_src, ib = eb;
       if (!one_chunk) {  // hub pair: this round's ids -- row 0's edges j.. in lanes 0-31, row 1's in 32-63
@@ -1286,48 +1317,107 @@ __global__ __launch_bounds__(AR_BLOCK) __attribute__((amdgpu_waves_per_eu(GTR_AR
         kc[u] = *reinterpret_cast<const float4*>(K + off);
         vc[u] = *reinterpret_cast<const float4*>(V + off);
       }
+      float mkl = 1.0f;
+      if (lane_drop) {
+        const int k = j + dr_s;
+        const int nrr = dr_r == 0 ? ne0 : ne - ne0;
+        const int eg = e0 + (dr_r == 0 ? 0 : ne0) + k;
+        mkl = (dr_r < 2 && k < nrr) ? dr.mul(st_attn, (uint32_t)(eg * H + dr_h)) : 0.0f;
+      }
+#if AR4_FOLD
+      float lg[U], mk[U];
+      float mx = -INFINITY;
+#endif
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int k = j + u * SPR + si;
-        float dt = q.x * kc[u].x + q.y * kc[u].y + q.z * kc[u].z + q.w * kc[u].w;
-        const float l = group_sum(dt, HL) / a.sqrt_c;
+        const float dt = q.x * kc[u].x + q.y * kc[u].y + q.z * kc[u].z + q.w * kc[u].w;
+        const float l = group_sum(dt, HL) * inv_sc;
+        const int e = eb + k;
+        float m1 = lane_drop ? __shfl(mkl, (((rr * EPR + u * SPR + si) << hsh) + head) & 63) : 0.0f;
+#if AR4_FOLD
+        lg[u] = -INFINITY;
+#endif
         if (mine && k < nr) {
-          const int e = eb + k;
-          const int eg = e0 + e;
+          if (!lane_drop) m1 = dr.mul(st_attn, (uint32_t)((e0 + e) * H + head));
           if (leader) {
             if (lds_lg) s_lg[wave][e][head] = l;
-            else a.alpha[(size_t)eg * H + head] = l;
+            else a.alpha[(size_t)(e0 + e) * H + head] = l;
           }
-          sm_push(st, l, dr.mul(st_attn, (uint32_t)(eg * H + head)), vc[u]);
+#if AR4_FOLD
+          lg[u] = l;
+          mx = fmaxf(mx, l);
+#else
+          sm_push(st, l, m1, vc[u]);
+#endif
         }
+#if AR4_FOLD
+        mk[u] = m1;
+#endif
       }
+#if AR4_FOLD
+      // fold the round's edges: one rescale of the running state, one exp per edge
+      if (mx != -INFINITY) {
+        const float mn = fmaxf(st.m, mx);
+        const float sc = st.m == -INFINITY ? 0.0f : expf(st.m - mn);
+        st.z *= sc;
+        st.acc.x *= sc; st.acc.y *= sc; st.acc.z *= sc; st.acc.w *= sc;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (lg[u] != -INFINITY) {
+            const float p = expf(lg[u] - mn);
+            st.z += p;
+            const float w = p * mk[u];
+            st.acc.x += w * vc[u].x;
+            st.acc.y += w * vc[u].y;
+            st.acc.z += w * vc[u].z;
+            st.acc.w += w * vc[u].w;
+          }
+        }
+        st.m = mn;
+      }
+#endif
     }
     GTR_PH(20 + a.layer, 9);
     sm_combine_upto<LPR, LPR * SPR>(st);  // the row's SPR sub-groups
     const float zd = st.z + 1e-16f;
+    const float rz = 1.0f / zd;
     if (si == 0 && leader) {
       s_mz[wave][rr][head][0] = st.m;
-      s_mz[wave][rr][head][1] = zd;
+      s_mz[wave][rr][head][1] = rz;
     }
     if (!lds_lg) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // raw logits in alpha
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     GTR_PH(20 + a.layer, 10);
-    const float4 w1 = *reinterpret_cast<const float4*>(a.w_beta + col);  // the gate's weights, late: registers
-    const float4 w2 = *reinterpret_cast<const float4*>(a.w_beta + D + col);
-    const float4 w3 = *reinterpret_cast<const float4*>(a.w_beta + 2 * D + col);
     // alpha of every (edge, head) pair of the row pair, lane-parallel (contiguous stores)
-    for (int idx = lane; idx < ne * H; idx += 64) {
-      const int e = idx / H, h = idx - e * H;
-      const int r = e >= ne0 ? 1 : 0;
-      const size_t at = (size_t)(e0 + e) * H + h;
-      const float l = lds_lg ? s_lg[wave][e][h] : a.alpha[at];
-      a.alpha[at] = expf(l - s_mz[wave][r][h][0]) / s_mz[wave][r][h][1];
+    if (lds_lg) {
+      for (int idx = lane; idx < ne * H; idx += 64) {
+        const int e = idx >> hsh, h = idx & (H - 1);
+        const int r = e >= ne0 ? 1 : 0;
+        a.alpha[(size_t)(e0 + e) * H + h] = expf(s_lg[wave][e][h] - s_mz[wave][r][h][0]) * s_mz[wave][r][h][1];
+      }
+    } else {
+      for (int idx = lane; idx < ne * H; idx += 64) {
+        const int e = idx >> hsh, h = idx & (H - 1);
+        const int r = e >= ne0 ? 1 : 0;
+        const size_t at = (size_t)(e0 + e) * H + h;
+        a.alpha[at] = expf(a.alpha[at] - s_mz[wave][r][h][0]) * s_mz[wave][r][h][1];
+      }
     }
     GTR_PH(20 + a.layer, 11);
     // aggregate, beta gate, outputs (slot 0 of each row's sub-groups stores the row)
-    const float4 ag = make_float4(st.acc.x / zd, st.acc.y / zd, st.acc.z / zd, st.acc.w / zd);
+#if AR4_WBLDS
+    const float4 w1 = *reinterpret_cast<const float4*>(&s_wb[col]);
+    const float4 w2 = *reinterpret_cast<const float4*>(&s_wb[D + col]);
+    const float4 w3 = *reinterpret_cast<const float4*>(&s_wb[2 * D + col]);
+#else
+    const float4 w1 = *reinterpret_cast<const float4*>(a.w_beta + col);  // late: registers
+    const float4 w2 = *reinterpret_cast<const float4*>(a.w_beta + D + col);
+    const float4 w3 = *reinterpret_cast<const float4*>(a.w_beta + 2 * D + col);
+#endif
+    const float4 ag = make_float4(st.acc.x * rz, st.acc.y * rz, st.acc.z * rz, st.acc.w * rz);
     float uu = w1.x * ag.x + w2.x * sv.x + w3.x * (ag.x - sv.x);
     uu += w1.y * ag.y + w2.y * sv.y + w3.y * (ag.y - sv.y);
     uu += w1.z * ag.z + w2.z * sv.z + w3.z * (ag.z - sv.z);

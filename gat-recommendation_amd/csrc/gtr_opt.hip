@@ -1136,11 +1136,18 @@ bool dim_ok(int D) { return D == 32 || D == 64 || D == 128 || D == 256; }
 // deterministic, equal to any stable sort of the (key, slot) pairs.
 #define RS_BITS 10
 #define RS_RADIX (1 << RS_BITS)
+#ifndef RS_THREADS
 #define RS_THREADS 256
+#endif
 #define RS_MAX_ROUNDS 16
+// digit totals are accumulated into RS_TOTC copies (tile mod RS_TOTC): one copy per address
+// saw every tile's atomic add (~240-way contention at C3 B = 8192); k_rs_offs sums the copies
+#ifndef RS_TOTC
+#define RS_TOTC 16
+#endif
 
-int rs_rounds(int n) {
-  const int r = (n + 65535) / 65536;
+int rs_rounds(int n) {  // tiles of ~n / 256 items (>= RS_THREADS)
+  const int r = (n + RS_THREADS * 256 - 1) / (RS_THREADS * 256);
   return r < 1 ? 1 : (r > RS_MAX_ROUNDS ? RS_MAX_ROUNDS : r);
 }
 
@@ -1194,7 +1201,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_hist(const int32_t* keys, int
   __syncthreads();
   for (int d = threadIdx.x; d < RADIX; d += RS_THREADS) {
     hist[(size_t)blockIdx.x * RADIX + d] = h[d];  // tile-major, coalesced
-    if (h[d]) atomicAdd(tot + d, h[d]);             // digit totals (integer: order-free)
+    if (h[d]) atomicAdd(tot + (blockIdx.x % RS_TOTC) * RADIX + d, h[d]);  // digit totals (integer: order-free)
   }
 }
 
@@ -1231,7 +1238,9 @@ __global__ __launch_bounds__(1024) void k_rs_offs(const int32_t* __restrict__ hi
   int v[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) v[q] = b0 + q < b1 ? hist[(size_t)(b0 + q) * RADIX + d] : 0;
-  const int tv = tot[tid];  // RADIX threads == RADIX digits
+  int tv = 0;  // RADIX threads == RADIX digits: the digit's total over the RS_TOTC copies
+#pragma unroll
+  for (int c = 0; c < RS_TOTC; ++c) tv += tot[c * RADIX + tid];
   const int incl = wave_incl_scan_i(tv, dl);
   if (dl == 63) s_ws[sl] = incl;
   int sum = 0;
@@ -1296,8 +1305,12 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const int32_t* kin, c
     if (ctr.rng_ctr) *ctr.rng_ctr += 1;
     if (ctr.consts) lazy_consts_for(ctr.opt, t, ctr.consts);
   }
-  if (blockIdx.x == 0)
-    for (int d = tid; d < RADIX; d += RS_THREADS) tot[d] = 0;
+  for (int c = blockIdx.x; c < RS_TOTC; c += gridDim.x)
+    for (int d = tid; d < RADIX; d += RS_THREADS) tot[c * RADIX + d] = 0;
+  const int base = blockIdx.x * RS_THREADS * rounds;
+  // the first round's (key, value) requested before the tables are staged
+  int key_n = base + tid < n ? kin[base + tid] : 0;
+  int val_n = base + tid < n ? vin[base + tid] : 0;
   for (int d = tid; d < RADIX; d += RS_THREADS) {
     run[d] = offs[(size_t)blockIdx.x * RADIX + d];
 #pragma unroll
@@ -1305,10 +1318,7 @@ __global__ __launch_bounds__(RS_THREADS) void k_rs_scatter(const int32_t* kin, c
   }
   __syncthreads();
   const unsigned long long lt = (1ull << lane) - 1ull;
-  const int base = blockIdx.x * RS_THREADS * rounds;
   // the next round's (key, value) are requested while this round is ranked and written
-  int key_n = base + tid < n ? kin[base + tid] : 0;
-  int val_n = base + tid < n ? vin[base + tid] : 0;
   for (int r = 0; r < rounds; ++r) {
     const int i = base + r * RS_THREADS + tid;
     const bool live = i < n;
@@ -1356,7 +1366,7 @@ size_t rs_bytes(int n) {
   const size_t tile = (size_t)RS_THREADS * rs_rounds(n);
   const size_t ntile = ((size_t)n + tile - 1) / tile;
   return 4 * (size_t)n * sizeof(int32_t) + 2 * (size_t)RS_RADIX * ntile * sizeof(int32_t) +
-         4 * RS_RADIX * sizeof(int32_t) + 256;
+         4 * RS_TOTC * RS_RADIX * sizeof(int32_t) + 256;
 }
 
 hipError_t rs_sort(void* tmp, const int32_t* keys, int32_t* skeys, const int32_t* vals, int32_t* svals, int n,
@@ -1369,7 +1379,7 @@ hipError_t rs_sort(void* tmp, const int32_t* keys, int32_t* skeys, const int32_t
   int32_t* v2 = k2 + n;
   int32_t* hist = v2 + n;
   int32_t* offs = hist + (size_t)RS_RADIX * ntile;
-  int32_t* tot = offs + (size_t)RS_RADIX * ntile;  // [passes][RS_RADIX] digit totals (kept zero between calls)
+  int32_t* tot = offs + (size_t)RS_RADIX * ntile;  // [passes][RS_TOTC][RS_RADIX] digit totals (kept zero between calls)
   // digit width: keys of <= 18 bits (T < 2^18: C3 / C4's 82k table) at >= 256k items in
   // two passes of 9-bit digits -- half the histogram / offset work and twice the run length
   // of a digit's scattered writes per tile (C3 B = 8192: 0.7710 -> 0.7686 ms per step; at
@@ -1385,7 +1395,7 @@ hipError_t rs_sort(void* tmp, const int32_t* keys, int32_t* skeys, const int32_t
     const bool last = p == passes - 1;
     int32_t* ko = last ? skeys : (p % 2 == 0 ? k1 : k2);
     int32_t* vo = last ? svals : (p % 2 == 0 ? v1 : v2);
-    int32_t* tp = tot + p * RS_RADIX;
+    int32_t* tp = tot + p * RS_TOTC * RS_RADIX;
     const RsCtr cc = (last && ctr) ? *ctr : RsCtr{};
     if (RB == 9) {
       if (p == 0 && prep)  // the first pass builds the contribution list as it counts

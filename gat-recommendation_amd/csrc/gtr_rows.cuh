@@ -175,7 +175,11 @@ __device__ __forceinline__ float4 piece_sum(const gtr_batch& bt, const int32_t* 
       for (int u = 0; u < QF; ++u) {
         const int cq = __shfl(code, gb + ((q0 + u) & (C4 - 1)));
         f[u] = __shfl(cf, gb + ((q0 + u) & (C4 - 1)));
+#ifdef GTR_DBG_TAIL_SE0  // timing probe only (wrong sums): every session-row read hits row 0
+        const float* src = cq < 0 ? se : dx0 + (size_t)cq * D;
+#else
         const float* src = cq < 0 ? se + (size_t)(cq & 0x7FFFFFFF) * D : dx0 + (size_t)cq * D;
+#endif
         v[u] = q0 + u < cnt ? reinterpret_cast<const float4*>(src)[gl] : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll

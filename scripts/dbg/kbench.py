@@ -69,6 +69,7 @@ def main():
             out[f"conv_bwd{l}"] = timeit(lambda: L.check(lib.gtr_conv_bwd(C.byref(cfg), C.byref(bs), ws.structs, l,
                                                                          ws.dx0.data_ptr(), st())), reps)
     out["wgrad"] = timeit(lambda: eng._wgrad(ws, cfg, bs, 0, eng.L, st()), reps)
+    out["begin"] = timeit(lambda: step._begin(bs, st()), reps)  # contribution sort (large batches)
     out["tail"] = timeit(lambda: step._launch_b(False), reps)
     print({k: (round(v, 1) if isinstance(v, float) else v) for k, v in out.items()}, flush=True)
 
