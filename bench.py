@@ -392,7 +392,7 @@ def main():
                              else "none (one process)"),
                 "dp_exchange": ("row-sharded table: all-to-all of row ids, rows and row gradients "
                                 f"({step.shard.volume()}; blocks "
-                                + ("fitted to the staged batches" if args.fit_blocks else "static bound") + ")")
+                                + ("fitted to the staged batches, +10 % headroom" if args.fit_blocks else "static bound") + ")")
                                if shard else step.dp is not None,
                 "hip_graph": not args.no_graph,
                 "batch_images": "resident, one graph per image" if resident else "copied per step (D2D)",

@@ -90,6 +90,20 @@ __device__ __forceinline__ float bfly_max(float x) {
   }
 }
 
+// Inclusive prefix sum of an integer over the wave's 64 lanes in DPP steps (VALU only, no
+// LDS round trip per step): row_shr 1 / 2 / 4 / 8 inside each row of 16 (out-of-row lanes
+// read 0), then row_bcast:15 (lane 15 of row r into rows 1 and 3) and row_bcast:31 (lane
+// 31 into rows 2 and 3).  Integer sums: exact in any order.
+__device__ __forceinline__ int wave_incl_scan_dpp(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xF, 0xF, true);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xF, 0xF, true);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xF, 0xF, true);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
 // Ascending butterfly sum over aligned groups of G lanes (G a compile-time power of two).
 template <int G>
 __device__ __forceinline__ float group_sum_c(float x) {

@@ -110,38 +110,45 @@ __global__ __launch_bounds__(RB_THREADS) void k_route_count(RouteK a) {
 }
 
 // Pass 2 (one workgroup): exclusive offsets of every block per owner, the owners' totals
-// into the count slots, overflow status.
+// into the count slots, overflow status.  Thread t owns a contiguous chunk of blocks; each
+// (class, owner) counter's 256 chunk sums are scanned across the threads by DPP wave scans
+// plus the 4 wave totals (a serial walk over the 256 chunk sums per counter was a chain of
+// 256 dependent LDS reads, ~10 us of k_route_count at 420 blocks).
 __device__ void route_scan_body(const RouteK& a) {
-  __shared__ int s_part[RB_THREADS][2 * SH_MAXP];
-  const int tid = threadIdx.x;
+  constexpr int NW = RB_THREADS / 64;
+  __shared__ int s_sum[2 * SH_MAXP][RB_THREADS];
+  __shared__ int s_wsum[2 * SH_MAXP][NW];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int NQ = a.ncls * a.P;  // (class, owner) counters, class-major
   if (tid == 0) a.status[0] = 0;  // this step's flag (a kernel write: no memset node in the captured step)
   const int per = (a.nblk + RB_THREADS - 1) / RB_THREADS;
   const int b0 = min(a.nblk, tid * per), b1 = min(a.nblk, b0 + per);
   for (int q = 0; q < NQ; ++q) {
-    int s = 0;
-    for (int b = b0; b < b1; ++b) s += a.bcnt[(size_t)b * NQ + q];
-    s_part[tid][q] = s;
+    int sq = 0;
+    for (int b = b0; b < b1; ++b) sq += a.bcnt[(size_t)b * NQ + q];
+    s_sum[q][tid] = sq;
+  }
+  for (int q = 0; q < NQ; ++q) {  // wave-uniform
+    const int x = s_sum[q][tid];
+    const int incl = wave_incl_scan_dpp(x);
+    s_sum[q][tid] = incl - x;
+    if (lane == 63) s_wsum[q][wave] = incl;
   }
   __syncthreads();
-  if (tid < NQ) {  // scan over the threads' chunks for (class, owner) tid
-    int run = 0;
-    for (int t = 0; t < RB_THREADS; ++t) {
-      const int v = s_part[t][tid];
-      s_part[t][tid] = run;
-      run += v;
-    }
+  if (tid < NQ) {  // counter tid's total: the owner block's count slot, overflow status
+    int tot = 0;
+    for (int w = 0; w < NW; ++w) tot += s_wsum[tid][w];
     const int c = tid / a.P, q = tid - c * a.P;
     const int lim = (c ? a.cap_s : a.cap) - 1;
-    a.send_ids[(size_t)q * a.blk + (c ? a.cap : 0)] = min(run, lim);
-    if (run > lim) {
+    a.send_ids[(size_t)q * a.blk + (c ? a.cap : 0)] = min(tot, lim);
+    if (tot > lim) {
       a.status[0] = 1;
       atomicOr(a.status + 1, 1);
     }
   }
-  __syncthreads();
   for (int q = 0; q < NQ; ++q) {
-    int run = s_part[tid][q];
+    int run = s_sum[q][tid];
+    for (int w = 0; w < wave; ++w) run += s_wsum[q][w];
     for (int b = b0; b < b1; ++b) {
       const int v = a.bcnt[(size_t)b * NQ + q];
       a.bcnt[(size_t)b * NQ + q] = run;

@@ -72,6 +72,7 @@ class FusedTrainStep:
         if self.sync_bn and not self.data_parallel:
             raise ValueError("sync_bn needs the data-parallel step")
         self.dp = None
+        self.sync_alias = False
         self.graph_b = None
         self._coll_capture_refused = False  # set once if the transport refuses stream capture
         eng = self.eng
@@ -168,19 +169,25 @@ class FusedTrainStep:
         n, b, e = (int(v) for v in t.tolist())
         return Caps(n, b, e, caps.n_neg)
 
-    def fit_shard_blocks(self, batches):
+    def fit_shard_blocks(self, batches, headroom: float = 1.1):
         """Row-sharded table: size the exchange blocks to the most distinct rows any rank
         asks one owner for over ``batches`` (each rank passes its own; the ranks agree on
-        the maximum -- a collective) instead of the static bound of ``shard_capacity``
-        (the all-to-alls move whole blocks, so smaller blocks are less xGMI
-        traffic per step).  A later batch that needs more rows overflows its block: the
-        step is flagged and applied as a zero-gradient step, and the host raises at the
-        next check.  Rebuilds the exchange buffers: captured graphs go stale."""
+        the maximum -- a collective) times ``headroom``, instead of the static bound of
+        ``shard_capacity`` (the all-to-alls move whole blocks, so smaller blocks
+        are less xGMI traffic per step).  A later batch that needs more rows overflows its
+        block: the step is flagged and applied as a zero-gradient step, and the host raises
+        at the next check.  Without headroom the maximum over the bench's 64 staged batches
+        per rank is exceeded by 0.9 % of later rank-batches (6.8 % of 8-rank steps) on the C4
+        data; 5 % headroom already leaves none of 2,048 (scripts/block_overflow.py,
+        profiles/r06/block_overflow_c4_n8_b1024.json), so the default takes 10 %.  Rebuilds
+        the exchange buffers: captured graphs go stale."""
         if self.shard is None:
             raise RuntimeError("fit_shard_blocks needs the row-sharded table (shard_table=True)")
+        import math
+
         from etpgt.train.sharded import ShardExchange, block_rows
 
-        r = block_rows(batches, self.world, self.shard.split)
+        r = tuple(int(math.ceil(v * float(headroom))) for v in block_rows(batches, self.world, self.shard.split))
         if self.world > 1:
             import torch.distributed as dist
 
@@ -461,14 +468,22 @@ class FusedTrainStep:
         g = ws.g_cap
         rg = readout_grid(self.caps.b_cap)
         self.sync_bufs = []
+        # one rank: the "gathered" partials ARE the producer's own rows, so the consumers read
+        # them in place and no gather (a copy per BatchNorm, four per step at L = 2) runs;
+        # GTR_SYNC_NOALIAS=1 keeps the copies (a one-rank rehearsal of the gathers)
+        self.sync_alias = W == 1 and os.environ.get("GTR_SYNC_NOALIAS") != "1"
         for l in range(Lc):
             # fused kernels: every row group's partial rows; split path: ONE merged forward row
             # (count, mean, M2) and the finalized backward sums per rank (gtr_config.split_sync)
             rows_f = 1 if self.split else g
             rows_b = 1 if self.split else (rg if l == Lc - 1 else g)
-            pa = torch.zeros(W, rows_f * (1 + 2 * D), dtype=torch.float32, device=self.dev)
-            ga = torch.zeros(W, rows_b * 2 * D, dtype=torch.float32, device=self.dev)
             st = ws.structs[l]
+            if self.sync_alias:
+                pa = ws.layers[l]["bn_part"]
+                ga = ws.layers[l]["bn_gsum" if self.split else "bn_gpart"]
+            else:
+                pa = torch.zeros(W, rows_f * (1 + 2 * D), dtype=torch.float32, device=self.dev)
+                ga = torch.zeros(W, rows_b * 2 * D, dtype=torch.float32, device=self.dev)
             st.bn_part_all, st.bn_gpart_all = pa.data_ptr(), ga.data_ptr()
             st.nparts_fwd, st.nparts_bwd = W * rows_f, W * rows_b
             self.sync_bufs.append((pa, ga, rows_f * (1 + 2 * D), rows_b * 2 * D))
@@ -479,12 +494,16 @@ class FusedTrainStep:
     def _gather_fwd(self, l):
         from etpgt.train.distributed import all_gather_packs
 
+        if self.sync_alias:
+            return
         pa, _, n, _ = self.sync_bufs[l]
         all_gather_packs(pa, self.ws.layers[l]["bn_part"].view(-1)[:n], self.group)
 
     def _gather_bwd(self, l):
         from etpgt.train.distributed import all_gather_packs
 
+        if self.sync_alias:
+            return
         _, ga, _, n = self.sync_bufs[l]
         src = self.ws.layers[l]["bn_gsum" if self.split else "bn_gpart"]
         all_gather_packs(ga, src.view(-1)[:n], self.group)
@@ -739,7 +758,7 @@ class FusedTrainStep:
         """True when no piece of the step runs a real collective: one rank with aliased
         exchange buffers (DpExchange.alias / ShardExchange.alias), no SyncBN gathers, no
         early union -- the pieces then run as ONE graph, with no host launch between them."""
-        if self.sync_bn or self.early_union:
+        if (self.sync_bn and not self.sync_alias) or self.early_union:
             return False
         if self.shard is not None:
             return self.shard.alias
