@@ -57,6 +57,11 @@ def main():
         else:
             out[f"conv_fwd{l}"] = timeit(lambda: L.check(lib.gtr_conv_fwd(C.byref(cfg), C.byref(bs), C.byref(emb),
                                                                          ws.structs, l, st())), reps)
+    if step.split and os.environ.get("KB_EVAL") == "1":  # the attention launch without BatchNorm partials
+        ce = type(cfg).from_buffer_copy(cfg)
+        ce.training = 0
+        out["attn_fwd1_eval"] = timeit(lambda: L.check(lib.gtr_attn_fwd(C.byref(ce), C.byref(bs), ws.structs, 1,
+                                                                       st())), reps)
     out["head"] = timeit(lambda: eng.run_head(ws, cfg, bs, L.RO_FWD | L.RO_LOSS | L.RO_BWD, step.loss_kind,
                                               step.temperature, step.alpha), reps)
     for l in range(eng.L - 1, -1, -1):
