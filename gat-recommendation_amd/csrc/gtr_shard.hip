@@ -33,9 +33,21 @@ namespace {
 using namespace gtr;
 
 #define RB_THREADS 256
-#define RB_ROUNDS 1
-#define RB_SLOTS (RB_THREADS * RB_ROUNDS)
+#define RB_MAX_BLOCKS 512  // route workgroups: rounds of RB_THREADS slots each, <= this many workgroups
 #define SH_MAXP 16
+
+// Rounds of RB_THREADS slots per route workgroup: one round up to RB_MAX_BLOCKS workgroups
+// (round 5: single-round blocks, C4 B = 1024 route 24.5 -> 18.5 us), more past that -- at
+// 855k slots (C4 B = 8192) single-round blocks were 3,340 workgroups whose arrival tickets
+// on ONE counter serialized (k_route_count 45.8 us).
+__host__ __device__ inline int route_rounds(int m_cap) {
+  const int r = (m_cap + RB_THREADS * RB_MAX_BLOCKS - 1) / (RB_THREADS * RB_MAX_BLOCKS);
+  return r < 1 ? 1 : r;
+}
+__host__ __device__ inline int route_blocks(int m_cap) {
+  const int slots = RB_THREADS * route_rounds(m_cap);
+  return (m_cap + slots - 1) / slots;
+}
 
 struct RouteK {
   gtr_batch bt;
@@ -49,10 +61,11 @@ struct RouteK {
   const float* pe_tab;
   float* node_pe;
   int32_t* bcnt;    // [nblk][2P] first-occurrence counts per (class, owner), then exclusive offsets
+  int32_t* rcnt;    // [nblk * rounds][2P] the same counts per 256-slot round (k_route_write's workgroups)
   int32_t* status;
   uint32_t* ticket; // arrival counter of k_route_count (scratch tail; zero between launches)
   int32_t* node_mark;  // [T] (cap_s > 0): rows a node reads, stamped with the step
-  int T, P, cap, pe_k, m_cap, nblk;
+  int T, P, cap, pe_k, m_cap, nblk, rounds, pad_r;
   int cap_s, blk, ncls, n_cap;  // class-1 slots per peer, id-block stride, classes (1 / 2)
   const int64_t* step_dev;      // this step (node_mark stamps): *step_dev + step_offset
   int step_offset, pad_t;
@@ -86,11 +99,13 @@ __device__ void route_scan_body(const RouteK& a);
 // written through and the arrival is a relaxed ticket: no release fence per block).
 __global__ __launch_bounds__(RB_THREADS) void k_route_count(RouteK a) {
   __shared__ int s_cnt[2 * SH_MAXP];
+  __shared__ int s_rc[2 * SH_MAXP];
   __shared__ int s_flag;
-  if (threadIdx.x < 2 * SH_MAXP) s_cnt[threadIdx.x] = 0;
+  const int NQ = a.ncls * a.P;
+  if (threadIdx.x < 2 * SH_MAXP) { s_cnt[threadIdx.x] = 0; s_rc[threadIdx.x] = 0; }
   __syncthreads();
-  for (int r = 0; r < RB_ROUNDS; ++r) {
-    const int i = blockIdx.x * RB_SLOTS + r * RB_THREADS + threadIdx.x;
+  for (int r = 0; r < a.rounds; ++r) {
+    const int i = (blockIdx.x * a.rounds + r) * RB_THREADS + threadIdx.x;
     int key, q;
     bool first;
     slot_info(a, i, key, q, first);
@@ -98,9 +113,15 @@ __global__ __launch_bounds__(RB_THREADS) void k_route_count(RouteK a) {
       const int c = slot_class(a, i, key, true);
       if (a.ncls == 2 && c == 0) a.node_mark[key] = route_step(a);  // read by k_route_write (next launch)
       atomicAdd(&s_cnt[c * a.P + q], 1);  // integer counts: order-independent
+      atomicAdd(&s_rc[c * a.P + q], 1);
     }
+    __syncthreads();
+    if (threadIdx.x < NQ) {  // the round's counts (read by the next launch)
+      a.rcnt[((size_t)blockIdx.x * a.rounds + r) * NQ + threadIdx.x] = s_rc[threadIdx.x];
+      s_rc[threadIdx.x] = 0;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   if (threadIdx.x < a.ncls * a.P)
     __hip_atomic_store(a.bcnt + (size_t)blockIdx.x * a.ncls * a.P + threadIdx.x, s_cnt[threadIdx.x], __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
@@ -158,17 +179,24 @@ __device__ void route_scan_body(const RouteK& a) {
 }
 
 // Pass 3: inclusive first-occurrence rank of each slot among its owner's rows (slot
-// order), compact row q*cap + rank, owner lists, remapped batch ids (+ PE rows).
+// order), compact row q*cap + rank, owner lists, remapped batch ids (+ PE rows).  One
+// workgroup per 256-slot round (the count's workgroups hold several rounds past 512 of
+// them): its offsets are its count block's plus the earlier rounds' counts of that block.
 __global__ __launch_bounds__(RB_THREADS) void k_route_write(RouteK a) {
   __shared__ int s_run[2 * SH_MAXP];
   __shared__ int s_wt[RB_THREADS / 64][2 * SH_MAXP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int NQ = a.ncls * a.P;
-  if (tid < NQ) s_run[tid] = a.bcnt[(size_t)blockIdx.x * NQ + tid];
+  const int cb = blockIdx.x / a.rounds, r0 = blockIdx.x - cb * a.rounds;
+  if (tid < NQ) {
+    int off = a.bcnt[(size_t)cb * NQ + tid];
+    for (int r = 0; r < r0; ++r) off += a.rcnt[((size_t)cb * a.rounds + r) * NQ + tid];
+    s_run[tid] = off;
+  }
   __syncthreads();
   const unsigned long long le = lane == 63 ? ~0ull : ((1ull << (lane + 1)) - 1ull);
-  for (int r = 0; r < RB_ROUNDS; ++r) {
-    const int i = blockIdx.x * RB_SLOTS + r * RB_THREADS + tid;
+  {
+    const int i = blockIdx.x * RB_THREADS + tid;
     int key, q;
     bool first;
     const bool valid = slot_info(a, i, key, q, first);
@@ -212,13 +240,6 @@ __global__ __launch_bounds__(RB_THREADS) void k_route_write(RouteK a) {
     } else if (i < a.m_cap) {
       a.ckeys[i] = -1;
     }
-    __syncthreads();
-    if (tid < NQ) {
-      int t = 0;
-      for (int w = 0; w < RB_THREADS / 64; ++w) t += s_wt[w][tid];
-      s_run[tid] += t;
-    }
-    __syncthreads();
   }
 }
 
@@ -531,8 +552,11 @@ int gtr_shard_route_scratch(int m_cap, int world, size_t* bytes) {
     set_error("gtr_shard_route_scratch: bad arguments");
     return GTR_E_ARG;
   }
-  // [nblk][P] block counts + the arrival ticket (64-byte aligned slot after them)
-  *bytes = (((size_t)((m_cap + RB_SLOTS - 1) / RB_SLOTS) * 2 * world * sizeof(int32_t) + 63) & ~(size_t)63) + 64;
+  // [nblk][2P] block counts, [nblk * rounds][2P] round counts, the arrival ticket (64-byte
+  // aligned slots)
+  const size_t nb = (size_t)route_blocks(m_cap), nr = nb * route_rounds(m_cap);
+  *bytes = ((nb * 2 * world * sizeof(int32_t) + 63) & ~(size_t)63) + ((nr * 2 * world * sizeof(int32_t) + 63) &
+                                                                      ~(size_t)63) + 64;
   return GTR_OK;
 }
 
@@ -557,18 +581,21 @@ int gtr_shard_route(const gtr_batch* bt, const int32_t* skeys, const int32_t* sv
   k.step_dev = sh->opt.step_dev;
   k.step_offset = (int)sh->opt.step_offset;
   k.m_cap = bt->n_cap + bt->b_cap * (1 + bt->n_neg);
-  k.nblk = (k.m_cap + RB_SLOTS - 1) / RB_SLOTS;
+  k.rounds = route_rounds(k.m_cap);
+  k.nblk = route_blocks(k.m_cap);
   const size_t cnt_bytes = ((size_t)k.nblk * k.ncls * k.P * sizeof(int32_t) + 63) & ~(size_t)63;
-  if (scratch_bytes < cnt_bytes + 64) {
-    set_error("gtr_shard_route: scratch of %zu bytes < %zu", scratch_bytes, cnt_bytes + 64);
+  const size_t rcnt_bytes = ((size_t)k.nblk * k.rounds * k.ncls * k.P * sizeof(int32_t) + 63) & ~(size_t)63;
+  if (scratch_bytes < cnt_bytes + rcnt_bytes + 64) {
+    set_error("gtr_shard_route: scratch of %zu bytes < %zu", scratch_bytes, cnt_bytes + rcnt_bytes + 64);
     return GTR_E_ARG;
   }
   k.bcnt = static_cast<int32_t*>(scratch);
-  k.ticket = reinterpret_cast<uint32_t*>(static_cast<char*>(scratch) + cnt_bytes);
+  k.rcnt = reinterpret_cast<int32_t*>(static_cast<char*>(scratch) + cnt_bytes);
+  k.ticket = reinterpret_cast<uint32_t*>(static_cast<char*>(scratch) + cnt_bytes + rcnt_bytes);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_route_count, dim3(k.nblk), dim3(RB_THREADS), 0, s, k);  // + the scan (last arriver)
   GTR_HIP_CHECK_LAUNCH();
-  hipLaunchKernelGGL(k_route_write, dim3(k.nblk), dim3(RB_THREADS), 0, s, k);
+  hipLaunchKernelGGL(k_route_write, dim3(k.nblk * k.rounds), dim3(RB_THREADS), 0, s, k);
   GTR_HIP_CHECK_LAUNCH();
   return GTR_OK;
 }
