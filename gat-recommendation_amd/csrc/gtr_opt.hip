@@ -538,8 +538,7 @@ struct TailK {
 // ---- large batches: windowed segmented sums (gtr_rows.cuh) ----------------------------
 template <int D>
 __global__ __launch_bounds__(GTR_BLOCK) void k_tail_carry(gtr_batch bt, int T, gtr_tail tl) {
-  tail_carry_body<D, GTR_BLOCK>(blockIdx.x + 1, bt, T, tl.skeys, tl.svals, tl.dx0, tl.se, tl.coef_tgt, tl.coef_neg,
-                                tl.carry);
+  tail_carry_block<D>(bt, T, tl.skeys, tl.svals, tl.dx0, tl.se, tl.coef_tgt, tl.coef_neg, tl.carry);
 }
 
 #ifndef GTR_TAIL_QF
@@ -1763,7 +1762,7 @@ int gtr_step_tail(const gtr_batch* bt, int num_items, int dim, const gtr_tail* t
     const int nwin = (m_cap + TW - 1) / TW;
     k.nb_rows = nwin;
     if (nwin > 1) {
-#define GTR_CARRY(DD) hipLaunchKernelGGL(k_tail_carry<DD>, dim3(nwin - 1), dim3(GTR_BLOCK), 0, s, *bt, num_items, t)
+#define GTR_CARRY(DD) hipLaunchKernelGGL(k_tail_carry<DD>, dim3(carry_blocks(m_cap)), dim3(GTR_BLOCK), 0, s, *bt, num_items, t)
       switch (dim) {
         case 32: GTR_CARRY(32); break;
         case 64: GTR_CARRY(64); break;
@@ -1915,10 +1914,10 @@ int gtr_dp_pack(const gtr_batch* bt, int num_items, int dim, const gtr_tail* tai
     k.nb_rows = nwin;
     if (nwin > 1) {
       switch (dim) {
-        case 32: hipLaunchKernelGGL(k_tail_carry<32>, dim3(nwin - 1), dim3(GTR_BLOCK), 0, s, *bt, num_items, *tail); break;
-        case 64: hipLaunchKernelGGL(k_tail_carry<64>, dim3(nwin - 1), dim3(GTR_BLOCK), 0, s, *bt, num_items, *tail); break;
-        case 128: hipLaunchKernelGGL(k_tail_carry<128>, dim3(nwin - 1), dim3(GTR_BLOCK), 0, s, *bt, num_items, *tail); break;
-        default: hipLaunchKernelGGL(k_tail_carry<256>, dim3(nwin - 1), dim3(GTR_BLOCK), 0, s, *bt, num_items, *tail); break;
+        case 32: hipLaunchKernelGGL(k_tail_carry<32>, dim3(carry_blocks(lay->m_cap)), dim3(GTR_BLOCK), 0, s, *bt, num_items, *tail); break;
+        case 64: hipLaunchKernelGGL(k_tail_carry<64>, dim3(carry_blocks(lay->m_cap)), dim3(GTR_BLOCK), 0, s, *bt, num_items, *tail); break;
+        case 128: hipLaunchKernelGGL(k_tail_carry<128>, dim3(carry_blocks(lay->m_cap)), dim3(GTR_BLOCK), 0, s, *bt, num_items, *tail); break;
+        default: hipLaunchKernelGGL(k_tail_carry<256>, dim3(carry_blocks(lay->m_cap)), dim3(GTR_BLOCK), 0, s, *bt, num_items, *tail); break;
       }
       GTR_HIP_CHECK_LAUNCH();
     }

@@ -197,14 +197,17 @@ __device__ __forceinline__ float4 piece_sum(const gtr_batch& bt, const int32_t* 
 // The sorted contribution list is cut into windows of TW slots.  A row's segment that
 // starts in window w is summed by window w's block over its in-window part; the part
 // lying in each following window w' (it can span many: hot Zipf items collect thousands
-// of node contributions) is a "carry" summed beforehand (tail_carry_body), so no thread
+// of node contributions) is a "carry" summed beforehand (tail_carry_wave), so no thread
 // walks a long segment serially.  Sums run in slot order inside a piece and pieces are
 // added in window order: deterministic.  The single-GPU tail, the data-parallel pack and
 // the row-sharded pack all sum this way, so their segment sums are bitwise equal.
 
 // Carry of window w (>= 1) whose first slot continues the previous window's segment:
 // the sum over [w*TW, first key change in w), split over the block's groups in fixed
-// contiguous pieces and combined in group order.  carry: [nwin][D].  Block-uniform exit.
+// contiguous pieces and combined in group order -- a whole block per window, used up to
+// GTR_CARRY_WAVE_WINDOWS windows (a hot row's full-window piece then runs in 8 parallel
+// pieces, the launch's critical path at a few hundred windows).  carry: [nwin][D].
+// Block-uniform exit.
 template <int D, int BLOCK>
 __device__ __forceinline__ void tail_carry_body(int w, const gtr_batch& bt, int T, const int32_t* skeys,
                                                 const int32_t* svals, const float* dx0, const float* se,
@@ -235,6 +238,79 @@ __device__ __forceinline__ void tail_carry_body(int w, const gtr_batch& bt, int 
     }
     reinterpret_cast<float4*>(carry)[(size_t)w * C4 + tid] = g;
   }
+}
+
+// Carry of window w (>= 1) whose first slot continues the previous window's segment: the
+// sum over [w*TW, first key change in w), by ONE wave (the window's few slots did not fill
+// a 256-thread block: round 5's block per window spent 23 us of launch at 6,680 windows).
+// The wave's 64 / C4 lane groups take contiguous pieces in order and are combined in group
+// order.  carry: [nwin][D].  Wave-uniform exit; s_part: this wave's [64 / C4][C4] scratch.
+template <int D>
+__device__ __forceinline__ void tail_carry_wave(int w, const gtr_batch& bt, int T, const int32_t* skeys,
+                                                const int32_t* svals, const float* dx0, const float* se,
+                                                const float* coef_tgt, const float* coef_neg, float* carry,
+                                                float4* s_part) {
+  constexpr int C4 = D / 4, NGW = 64 / C4;
+  const int lane = threadIdx.x & 63;
+  const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
+  const int w0 = w * TW, w1 = min(w0 + TW, m_cap);
+  if (w0 >= m_cap) return;
+  const int key = skeys[w0];
+  if (key <= 0 || key >= T || skeys[w0 - 1] != key) return;  // wave-uniform
+  int e = w1;  // the segment's end inside the window
+  for (int b = w0; b < w1; b += 64) {
+    const int k = b + lane;
+    const unsigned long long bal = __ballot(k < w1 && skeys[k] != key);
+    if (bal) {
+      e = b + __ffsll((long long)bal) - 1;
+      break;
+    }
+  }
+  const int grp = lane / C4, gl = lane % C4;
+  const int len = e - w0, per = (len + NGW - 1) / NGW;
+  const int ps = min(e, w0 + grp * per), pe = min(e, ps + per);
+  s_part[grp * C4 + gl] = piece_sum<D>(bt, svals, ps, pe, dx0, se, coef_tgt, coef_neg, gl, grp * C4);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (lane < C4) {
+    float4 g = s_part[lane];
+    for (int q = 1; q < NGW; ++q) {
+      const float4 t = s_part[q * C4 + lane];
+      g.x += t.x; g.y += t.y; g.z += t.z; g.w += t.w;
+    }
+    reinterpret_cast<float4*>(carry)[(size_t)w * C4 + lane] = g;
+  }
+}
+
+// Carries by wave (GTR_BLOCK / 64 windows per workgroup) from this many windows on, by
+// block below: C3 B = 8192 (6,680 windows) tail + carry 112 -> 105 us by wave; C3 B = 1024
+// (840 windows) 66 -> 71 us by wave, where a hot row's full-window piece in 2 instead of 8
+// parallel pieces sets the launch.  Both variants sum every tail kind (single GPU, data
+// parallel, row-sharded) the same way for a given m_cap.
+#define GTR_CARRY_WAVE_WINDOWS 2048
+__host__ __device__ inline bool carry_by_wave(int m_cap) { return (m_cap + TW - 1) / TW >= GTR_CARRY_WAVE_WINDOWS; }
+
+// Launch of the carries (windows 1 .. nwin - 1): workgroups of the launch.
+__host__ __device__ inline int carry_blocks(int m_cap) {
+  const int nwin = (m_cap + TW - 1) / TW;
+  if (nwin <= 1) return 0;
+  return carry_by_wave(m_cap) ? (nwin - 1 + GTR_BLOCK / 64 - 1) / (GTR_BLOCK / 64) : nwin - 1;
+}
+
+template <int D>
+__device__ __forceinline__ void tail_carry_block(const gtr_batch& bt, int T, const int32_t* skeys,
+                                                 const int32_t* svals, const float* dx0, const float* se,
+                                                 const float* coef_tgt, const float* coef_neg, float* carry) {
+  const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
+  if (!carry_by_wave(m_cap)) {
+    tail_carry_body<D, GTR_BLOCK>((int)blockIdx.x + 1, bt, T, skeys, svals, dx0, se, coef_tgt, coef_neg, carry);
+    return;
+  }
+  __shared__ __attribute__((aligned(16))) float4 s_part[GTR_BLOCK];  // 64 per wave: (64 / C4) groups x C4
+  const int wave = threadIdx.x >> 6;
+  tail_carry_wave<D>((int)blockIdx.x * (GTR_BLOCK / 64) + wave + 1, bt, T, skeys, svals, dx0, se, coef_tgt,
+                     coef_neg, carry, s_part + wave * 64);
 }
 
 // Segment starts (key changes) of window [w0, w1) in slot order -> s_bnd[0..nb), returns

@@ -315,8 +315,7 @@ struct PackK {
 // Large batches: carries of the windows (gtr_rows.cuh), summed before k_shard_pack.
 template <int D>
 __global__ __launch_bounds__(GTR_BLOCK) void k_shard_carry(gtr_batch bt, int T, gtr_tail tl) {
-  tail_carry_body<D, GTR_BLOCK>(blockIdx.x + 1, bt, T, tl.skeys, tl.svals, tl.dx0, tl.se, tl.coef_tgt, tl.coef_neg,
-                                tl.carry);
+  tail_carry_block<D>(bt, T, tl.skeys, tl.svals, tl.dx0, tl.se, tl.coef_tgt, tl.coef_neg, tl.carry);
 }
 
 // Windowed rows part (large batches): the segments starting in window w, each summed as
@@ -656,7 +655,7 @@ int gtr_shard_pack(const gtr_batch* bt, const gtr_shard* sh, const gtr_tail* tai
     const int nwin = (k.m_cap + TW - 1) / TW;
     k.nb_rows = nwin;
     if (nwin > 1) {
-      const dim3 cg(nwin - 1);
+      const dim3 cg(carry_blocks(k.m_cap));
       switch (sh->dim) {
         case 32: hipLaunchKernelGGL(k_shard_carry<32>, cg, dim3(GTR_BLOCK), 0, s, *bt, sh->num_items, *tail); break;
         case 64: hipLaunchKernelGGL(k_shard_carry<64>, cg, dim3(GTR_BLOCK), 0, s, *bt, sh->num_items, *tail); break;
