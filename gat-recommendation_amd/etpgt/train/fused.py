@@ -265,6 +265,9 @@ class FusedTrainStep:
         # slots: conv_fwd(l) -> l, readout -> L, conv_bwd(l) -> 2L - l; weighted by the
         # launches' measured slack (the readout is shorter than a layer kernel)
         wts = [1.0] * eng.L + [0.75] + [1.0] * eng.L
+        if eng.D <= 64:  # round 6 A/B at C2 (scripts/gpu/sweep_wts.sh): forward slices 0.75, the
+            # last layer's backward 1.25 -- 0.0745 -> 0.0741 ms per step (twice, alternating runs)
+            wts = [0.75] * eng.L + [0.75] + [1.25] + [1.0] * (eng.L - 1)
         if os.environ.get("GTR_SWEEP_WTS"):  # experiments: comma-separated slot weights
             wts = [float(x) for x in os.environ["GTR_SWEEP_WTS"].split(",")]
         # single-GPU small batches: gtr_step_begin's work runs as extra workgroups of
