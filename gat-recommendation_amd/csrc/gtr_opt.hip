@@ -555,11 +555,13 @@ __device__ __forceinline__ void window_rows(int w, const gtr_batch& bt, int T, c
   const int tid = threadIdx.x;
   const int m_cap = bt.n_cap + bt.b_cap * (1 + bt.n_neg);
   const int w0 = w * TW, w1 = min(w0 + TW, m_cap);
+  __shared__ WinSlots s_ws;
+  if (GTR_WIN_LDS) window_decode(bt, tl.skeys, tl.svals, tl.coef_tgt, tl.coef_neg, w0, w1, s_ws);
   const int nb = window_bounds<GTR_BLOCK>(tl.skeys, w0, w1, s_bnd);
   const int grp = tid / C4, gl = tid % C4, gb = grp * C4 % 64;
   for (int q = grp; q < nb; q += NG) {
     const int s0 = s_bnd[q];
-    const int key = tl.skeys[s0];
+    const int key = GTR_WIN_LDS ? s_ws.key[s0 - w0] : tl.skeys[s0];
     if (key <= 0 || key >= T) continue;
     const int e = q + 1 < nb ? s_bnd[q + 1] : w1;
     const size_t base = (size_t)key * C4 + gl;
@@ -570,7 +572,7 @@ __device__ __forceinline__ void window_rows(int w, const gtr_batch& bt, int T, c
     float4 vv = sw_ld(reinterpret_cast<const float4*>(tl.table_v) + base);
     const int32_t sw = lazy_stamp ? lazy_stamp[key] : 0;
     const float4 g = window_segment_sum<D, GTR_TAIL_QF>(bt, tl.skeys, tl.svals, tl.dx0, tl.se, tl.coef_tgt,
-                                                        tl.coef_neg, tl.carry, w, s0, e, w1, m_cap, key, gl, gb);
+                                                        tl.coef_neg, tl.carry, w, s0, e, w1, m_cap, key, gl, gb, &s_ws);
     if (lazy_stamp) lazy_mv_forward(mv, vv, sw, lazy_t, st);
     st.apply(pv.x, mv.x, vv.x, g.x);
     st.apply(pv.y, mv.y, vv.y, g.y);
@@ -887,16 +889,18 @@ __device__ __forceinline__ void dp_pack_window(int w, const DpPackK& a, int32_t*
     if (i > 0 && sk[i - 1] == sk[i])
       reinterpret_cast<float4*>(rows + (size_t)i * D)[idx % C4] = make_float4(0.f, 0.f, 0.f, 0.f);
   }
+  __shared__ WinSlots s_ws;
+  if (GTR_WIN_LDS) window_decode(a.bt, sk, a.tl.svals, a.tl.coef_tgt, a.tl.coef_neg, w0, w1, s_ws);
   const int nb = window_bounds<GTR_BLOCK>(sk, w0, w1, s_bnd);
   const int grp = tid / C4, gl = tid % C4, gb = grp * C4 % 64;
   for (int q = grp; q < nb; q += NG) {
     const int s0 = s_bnd[q];
-    const int key = sk[s0];
+    const int key = GTR_WIN_LDS ? s_ws.key[s0 - w0] : sk[s0];
     const int e = q + 1 < nb ? s_bnd[q + 1] : w1;
     float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
     if (key > 0 && key < a.T)
       g = window_segment_sum<D>(a.bt, sk, a.tl.svals, a.tl.dx0, a.tl.se, a.tl.coef_tgt, a.tl.coef_neg, a.tl.carry, w,
-                                s0, e, w1, m_cap, key, gl, gb);
+                                s0, e, w1, m_cap, key, gl, gb, &s_ws);
     reinterpret_cast<float4*>(rows + (size_t)s0 * D)[gl] = g;
   }
 }

@@ -193,6 +193,74 @@ __device__ __forceinline__ float4 piece_sum(const gtr_batch& bt, const int32_t* 
   return g;
 }
 
+// The slots of one window decoded once, one slot per thread and all at once, into LDS:
+// sort key, source code (dx0 node row, or session row with the top bit set) and
+// coefficient -- exactly what piece_sum decodes per chunk.  The window's segment sums then
+// start from LDS instead of two dependent global rounds (slot id, then its coefficient)
+// per chunk of every segment.  No barrier here: the callers' window_bounds barriers
+// publish the writes.
+#ifndef GTR_WIN_LDS
+#define GTR_WIN_LDS 1
+#endif
+struct WinSlots {
+  int key[TW];
+  int code[TW];
+  float cf[TW];
+};
+__device__ __forceinline__ void window_decode(const gtr_batch& bt, const int32_t* skeys, const int32_t* svals,
+                                              const float* coef_tgt, const float* coef_neg, int w0, int w1,
+                                              WinSlots& ws) {
+  const int tid = threadIdx.x;
+  if (tid < TW && w0 + tid < w1) {
+    const int j = svals[w0 + tid];
+    int code;
+    float cf;
+    if (j < bt.n_cap) {
+      code = j;
+      cf = 1.0f;
+    } else if (j < bt.n_cap + bt.b_cap) {
+      const int b = j - bt.n_cap;
+      code = (int)(0x80000000u | (uint32_t)b);
+      cf = coef_tgt[b];
+    } else {
+      const int q = j - bt.n_cap - bt.b_cap;
+      code = (int)(0x80000000u | (uint32_t)(q / bt.n_neg));
+      cf = coef_neg[q];
+    }
+    ws.key[tid] = skeys[w0 + tid];
+    ws.code[tid] = code;
+    ws.cf[tid] = cf;
+  }
+}
+
+// piece_sum over slots [s, e) of window w0 with the decoded slots in LDS: the same products
+// added in the same slot order (bitwise piece_sum's sum); QF rows in flight per lane.
+template <int D, int QF = 8>
+__device__ __forceinline__ float4 piece_sum_lds(const WinSlots& ws, int w0, int s, int e, const float* dx0,
+                                                const float* se, int gl) {
+  float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int q0 = s; q0 < e; q0 += QF) {
+    float4 v[QF];
+    float f[QF];
+#pragma unroll
+    for (int u = 0; u < QF; ++u) {
+      const bool in = q0 + u < e;
+      const int k = in ? q0 + u - w0 : 0;
+      const int cq = ws.code[k];
+      f[u] = ws.cf[k];
+      const float* src = cq < 0 ? se + (size_t)(cq & 0x7FFFFFFF) * D : dx0 + (size_t)cq * D;
+      v[u] = in ? reinterpret_cast<const float4*>(src)[gl] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < QF; ++u) {
+      if (q0 + u < e) {
+        g.x += f[u] * v[u].x; g.y += f[u] * v[u].y; g.z += f[u] * v[u].z; g.w += f[u] * v[u].w;
+      }
+    }
+  }
+  return g;
+}
+
 // ---- large batches (m_cap > GTR_BEGIN_MCAP): windowed segmented sums ------------------
 // The sorted contribution list is cut into windows of TW slots.  A row's segment that
 // starts in window w is summed by window w's block over its in-window part; the part
@@ -345,9 +413,15 @@ template <int D, int QF = 8>
 __device__ __forceinline__ float4 window_segment_sum(const gtr_batch& bt, const int32_t* skeys, const int32_t* svals,
                                                      const float* dx0, const float* se, const float* coef_tgt,
                                                      const float* coef_neg, const float* carry, int w, int s0, int e,
-                                                     int w1, int m_cap, int key, int gl, int gb) {
+                                                     int w1, int m_cap, int key, int gl, int gb,
+                                                     const WinSlots* wsl) {
   constexpr int C4 = D / 4;
+#if GTR_WIN_LDS
+  (void)bt; (void)svals; (void)coef_tgt; (void)coef_neg; (void)gb;
+  float4 g = piece_sum_lds<D, QF>(*wsl, w * TW, s0, e, dx0, se, gl);
+#else
   float4 g = piece_sum<D, QF>(bt, svals, s0, e, dx0, se, coef_tgt, coef_neg, gl, gb);
+#endif
   if (e == w1) {  // the segment may continue: add the carries in window order
     for (int w2 = w + 1; w2 * TW < m_cap && skeys[w2 * TW] == key; ++w2) {
       const float4 c = reinterpret_cast<const float4*>(carry)[(size_t)w2 * C4 + gl];

@@ -328,11 +328,13 @@ __device__ __forceinline__ void shard_pack_window(int w, const PackK& a) {
   const int tid = threadIdx.x;
   const int w0 = w * TW, w1 = min(w0 + TW, a.m_cap);
   const int32_t* sk = a.tl.skeys;
+  __shared__ WinSlots s_ws;
+  if (GTR_WIN_LDS) window_decode(a.bt, sk, a.tl.svals, a.tl.coef_tgt, a.tl.coef_neg, w0, w1, s_ws);
   const int nb = window_bounds<GTR_BLOCK>(sk, w0, w1, s_bnd);
   const int grp = tid / C4, gl = tid % C4, gb = grp * C4 % 64;
   for (int q = grp; q < nb; q += NG) {
     const int s0 = s_bnd[q];
-    const int key = sk[s0];
+    const int key = GTR_WIN_LDS ? s_ws.key[s0 - w0] : sk[s0];
     if (key < 0 || key >= a.T) continue;
     const int ck = a.ckeys[s0];
     if (ck < 0) continue;
@@ -340,7 +342,7 @@ __device__ __forceinline__ void shard_pack_window(int w, const PackK& a) {
     float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
     if (key > 0)  // padding_idx = 0: no gradient (the owner still applies g = 0)
       g = window_segment_sum<D>(a.bt, sk, a.tl.svals, a.tl.dx0, a.tl.se, a.tl.coef_tgt, a.tl.coef_neg, a.tl.carry, w,
-                                s0, e, w1, a.m_cap, key, gl, gb);
+                                s0, e, w1, a.m_cap, key, gl, gb, &s_ws);
     reinterpret_cast<float4*>(a.send_grads + grad_row_off(ck, a.blk, a.grad_stride, D))[gl] = g;
   }
 }
