@@ -984,6 +984,8 @@ extern "C" int gtr_qkvs_bwd(const gtr_config* cfg, const gtr_batch* bt, const gt
 namespace {
 
 // Shared argument checks of the FFN entry points; fills the dropout parameters.
+bool ffn_generic(const gtr_config* cfg, const gtr_ffn& f);
+
 int ffn_check(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layers, int l, const char* fn,
               bool need_train, uint32_t& thresh, float& scale, int& drop_on) {
   if (!cfg || !bt || !layers || l < 0 || l >= cfg->num_layers || !layers[l].ffn) {
@@ -1001,8 +1003,12 @@ int ffn_check(const gtr_config* cfg, const gtr_batch* bt, const gtr_layer* layer
   }
   if (!f.w1 || !f.b1 || !f.w2 || !f.b2 || !f.y || !f.a || !f.z) { set_error("%s: missing FFN buffers", fn); return GTR_E_ARG; }
   if (need_train && !cfg->training) { set_error("%s: backward requires training mode", fn); return GTR_E_ARG; }
-  if (cfg->training && (cfg->sync_bn || cfg->consumer_reduce)) {
-    set_error("%s: the FFN variant reads producer-finalized BatchNorm statistics (consumer_reduce 0, no sync_bn)", fn);
+  // BatchNorm statistics: producer-finalized, or (SyncBN, split_sync) folded by the FFN's
+  // first GEMM from every rank's merged row like the next layer's projection does
+  if (cfg->training && (cfg->sync_bn || cfg->consumer_reduce) &&
+      !(cfg->sync_bn && cfg->split_sync && !ffn_generic(cfg, f))) {
+    set_error("%s: the FFN variant takes producer-finalized BatchNorm statistics, or SyncBN's merged rows "
+              "(split_sync) at dim 64 / 128 with expansion 4", fn);
     return GTR_E_ARG;
   }
   drop_on = (cfg->training && cfg->dropout > 0.0f) ? 1 : 0;
@@ -1044,6 +1050,15 @@ extern "C" int gtr_ffn_fwd(const gtr_config* cfg, const gtr_batch* bt, const gtr
   k.p_out = L.out; k.p_xin = L.xin; k.p_stats = L.bn_stats; k.p_rmean = L.bn_rmean; k.p_rvar = L.bn_rvar;
   k.p_nbt = L.bn_nbt; k.p_gamma = L.bn_gamma; k.p_beta = L.bn_beta; k.bn_mom = cfg->bn_momentum;
   k.w_all = f.w1; k.b_all = f.b1; k.xin = f.y; k.qkvs = f.a;
+  if (cfg->sync_bn && cfg->training) {  // SyncBN: the ranks' merged rows of this layer (gtr_qkvs_fwd's fold)
+    if (!L.bn_part_all || L.nparts_fwd <= 0) {
+      set_error("gtr_ffn_fwd: sync_bn needs the gathered merged rows of layer %d", l);
+      return GTR_E_ARG;
+    }
+    k.sync = 1;
+    k.p_part_all = L.bn_part_all;
+    k.p_nparts = L.nparts_fwd;
+  }
   const int bm = D == 64 ? ProjGeom<64>::BM : ProjGeom<128>::BM;
   const int grid = gemm_grid((bt->n_cap + bm - 1) / bm, D == 64 ? 2 : 1);
   if (D == 64) hipLaunchKernelGGL((k_proj<64, PJ_FOLD>), dim3(grid), dim3(GM_BLOCK), 0, s, k);

@@ -278,12 +278,16 @@ class Workspace:
 
     def readout_args(self, cfg):
         """(config, layer structs) of the readout: with FFN blocks the identity view of the
-        last block's output (dropout 0, eps 0)."""
+        last block's output (dropout 0, eps 0, fixed statistics: no SyncBN fold -- the last
+        layer's BatchNorm was folded by its FFN's first GEMM)."""
         if self.ffns is None:
             return cfg, self.structs
         c = type(cfg).from_buffer_copy(cfg)
         c.dropout = 0.0
         c.bn_eps = 0.0
+        c.sync_bn = 0
+        c.consumer_reduce = 0
+        c.split_sync = 0
         return c, self.ro_structs
 
     def enable_wfold(self, eng) -> int:
@@ -477,6 +481,19 @@ class Engine:
         else:
             L.check(lib.gtr_conv_bwd(C.byref(cfg), C.byref(bs), ws.structs, l, ws.dx0.data_ptr(), st), "conv_bwd")
 
+    def ffn_fwd(self, ws: Workspace, cfg: L.GtrConfig, bs: L.GtrBatch, l: int, st: int):
+        """Layer l's feed-forward block (use_ffn=True): y, a, z (gtr_ffn_fwd)."""
+        L.check(L.lib().gtr_ffn_fwd(C.byref(cfg), C.byref(bs), ws.structs, l, st), "ffn_fwd")
+
+    def ffn_bwd(self, ws: Workspace, cfg: L.GtrConfig, bs: L.GtrBatch, l: int, st: int, wgrad: bool = True):
+        """Layer l's feed-forward backward (-> layers[l].dy + its BatchNorm sums) and, with
+        ``wgrad``, its weight-gradient slabs."""
+        lib = L.lib()
+        L.check(lib.gtr_ffn_bwd(C.byref(cfg), C.byref(bs), ws.structs, l, st), "ffn_bwd")
+        if wgrad:
+            L.check(lib.gtr_ffn_wgrad(C.byref(cfg), C.byref(bs), ws.structs, l, ws.ffn_slabs[l].data_ptr(),
+                                      ws.P, self.flat.layout.ffn_stride, st), "ffn_wgrad")
+
     def run_forward(self, ws: Workspace, cfg: L.GtrConfig, bs: L.GtrBatch, flags: int,
                     loss_kind: int = 0, temperature: float = 1.0, alpha: float = 0.7, split: bool | None = None):
         st = self.stream()
@@ -484,7 +501,7 @@ class Engine:
         for l in range(self.L):
             self.layer_fwd(ws, cfg, bs, l, emb, st, split)
             if ws.ffns is not None:
-                L.check(L.lib().gtr_ffn_fwd(C.byref(cfg), C.byref(bs), ws.structs, l, st), "ffn_fwd")
+                self.ffn_fwd(ws, cfg, bs, l, st)
         self.run_head(ws, cfg, bs, flags, loss_kind, temperature, alpha)
 
     def run_head(self, ws, cfg, bs, flags, loss_kind=0, temperature=1.0, alpha=0.7, dse_out=False, table=None):
@@ -534,10 +551,7 @@ class Engine:
             side = None  # FFN blocks: every gradient kernel on the main stream
         for l in range(self.L - 1, -1, -1):
             if ws.ffns is not None:
-                L.check(lib.gtr_ffn_bwd(C.byref(cfg), C.byref(bs), ws.structs, l, st), "ffn_bwd")
-                if wgrad:
-                    L.check(lib.gtr_ffn_wgrad(C.byref(cfg), C.byref(bs), ws.structs, l, ws.ffn_slabs[l].data_ptr(),
-                                              ws.P, self.flat.layout.ffn_stride, st), "ffn_wgrad")
+                self.ffn_bwd(ws, cfg, bs, l, st, wgrad)
             self.layer_bwd(ws, cfg, bs, l, st, split)
             if wgrad and side is not None and l >= 1:
                 side.wait_stream(main)

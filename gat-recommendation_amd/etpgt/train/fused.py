@@ -38,12 +38,13 @@ class FusedTrainStep:
         if loss not in ("bpr", "listwise", "dual", "sampled_softmax"):
             raise ValueError(f"Unknown loss type: {loss}")
         if getattr(model, "use_ffn", False):
-            from etpgt.train.distributed import world_info as _wi
-
-            multi = bool(data_parallel) if data_parallel is not None else _wi(process_group)[1] > 1
-            if multi or shard_table or sync_bn or os.environ.get("GTR_TAILW") == "1":
-                raise NotImplementedError("the FFN variant (use_ffn=True) trains on one GPU: no data-parallel / "
-                                          "row-sharded / SyncBN step, no GTR_TAILW")
+            # the FFN variant trains data parallel (replicated table), with or without SyncBN;
+            # SyncBN folds the gathered rows in the FFN's first GEMM (dim 64 / 128, expansion 4)
+            if shard_table or os.environ.get("GTR_TAILW") == "1":
+                raise NotImplementedError("the FFN variant (use_ffn=True) has no row-sharded-table step and no "
+                                          "GTR_TAILW")
+            if sync_bn and not (model.embedding_dim in (64, 128) and getattr(model, "ffn_expansion", 4) == 4):
+                raise NotImplementedError("SyncBN with the FFN variant covers dim 64 / 128 at ffn_expansion 4")
         self.model = model
         self.eng: Engine = model.hip_engine()
         self.dev = self.eng.device
@@ -590,19 +591,29 @@ class FusedTrainStep:
         def st():
             return torch.cuda.current_stream(self.dev).cuda_stream
 
+        ffn = ws.ffns is not None  # a layer's BatchNorm is then folded by its FFN's first GEMM
+
         def fwd(l):
             def f():
                 if l == 0:
                     self._begin(bs, st())
+                if ffn and l > 0:
+                    eng.ffn_fwd(ws, cfg, bs, l - 1, st())
                 eng.layer_fwd(ws, cfg, bs, l, eng.fill_embed(), st(), self.split)
             return f
 
         def head():
+            if ffn:
+                eng.ffn_fwd(ws, cfg, bs, Lc - 1, st())
             eng.run_head(ws, cfg, bs, L.RO_FWD | L.RO_LOSS | L.RO_BWD, self.loss_kind, self.temperature, self.alpha)
+            if ffn:  # layer Lc-1's dy and BatchNorm sums come from its FFN's backward
+                eng.ffn_bwd(ws, cfg, bs, Lc - 1, st())
 
         def bwd(l):
             def f():
                 eng.layer_bwd(ws, cfg, bs, l, st(), self.split)
+                if ffn and l > 0:
+                    eng.ffn_bwd(ws, cfg, bs, l - 1, st())
                 if l == 0:
                     eng._wgrad(ws, cfg, bs, 0, Lc, st())
                     self.dp.launch_pack(bs, st())

@@ -57,7 +57,13 @@ class Trainer:
         from etpgt.train.distributed import world_info
 
         self.rank, self.world = world_info()
-        self.sync_bn = (self.world > 1) if sync_bn is None else bool(sync_bn)
+        if sync_bn is None:
+            # SyncBN covers the FFN variant at dim 64 / 128 with expansion 4 (gtr_ffn_fwd folds
+            # the gathered rows); elsewhere its data-parallel step keeps per-rank statistics
+            ffn_sync = (not getattr(model, "use_ffn", False)
+                        or (getattr(model, "embedding_dim", 0) in (64, 128) and getattr(model, "ffn_expansion", 4) == 4))
+            sync_bn = self.world > 1 and ffn_sync
+        self.sync_bn = bool(sync_bn)
         if shard_table is None:
             shard_table = os.environ.get("GTR_SHARD_TABLE") == "1"
         self.shard_table = bool(shard_table) and self.world > 1
@@ -94,7 +100,6 @@ class Trainer:
         spec = _fused_loss_spec(self.loss_fn)
         opt = self.optimizer
         ok = (isinstance(self.model, GraphTransformer) and torch.device(self.device).type == "cuda"
-              and not (self.model.use_ffn and self.world > 1)
               and spec is not None and type(opt) in (torch.optim.AdamW, torch.optim.Adam)
               and len(opt.param_groups) == 1 and not opt.state
               and not opt.param_groups[0].get("amsgrad", False)

@@ -138,9 +138,6 @@ def main(argv=None):
     logger.info("Creating data loaders%s...", " (batches built on the GPU)" if dev_batches else "")
     kw = dict(graph_edges_path=args.graph_edges, batch_size=args.batch_size, num_negatives=args.num_negatives,
               max_session_length=args.max_session_length, num_workers=args.num_workers)
-    if world > 1 and args.model == "graph_transformer":
-        raise NotImplementedError("data-parallel training covers graph_transformer_optimized (the fused step); "
-                                  "the FFN variant trains on one GPU")
     if world > 1 and not dev_batches:
         raise NotImplementedError("data-parallel training builds its batches on the GPU (--device-batches on)")
     if dev_batches:

@@ -115,19 +115,19 @@ def _script():
 EPOCHS = 2
 
 
-def _args(d, out, B, shard):
-    return ["--model", "graph_transformer_optimized", "--train-sessions", str(d / "train.csv"),
+def _args(d, out, B, shard, model="graph_transformer_optimized", dim=32):
+    return ["--model", model, "--train-sessions", str(d / "train.csv"),
             "--val-sessions", str(d / "val.csv"), "--graph-edges", str(d / "graph_edges.csv"),
-            "--embedding-dim", "32", "--hidden-dim", "32", "--num-layers", "2", "--num-heads", "2",
+            "--embedding-dim", str(dim), "--hidden-dim", str(dim), "--num-layers", "2", "--num-heads", "2",
             "--dropout", "0", "--batch-size", str(B), "--num-negatives", "5", "--max-epochs", str(EPOCHS),
             "--num-workers", "0", "--output-dir", str(out), "--shard-table", "on" if shard else "off"]
 
 
-def _rank_main(rank, world, port, d, out, B, q, shard):
+def _rank_main(rank, world, port, d, out, B, q, shard, model="graph_transformer_optimized", dim=32):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
                       LOCAL_RANK=str(rank), GTR_SHARE_DEVICE="1")
     # main() releases the captured graphs and destroys the process group itself
-    tr = _script().main(_args(d, out, B, shard))
+    tr = _script().main(_args(d, out, B, shard, model, dim))
     import torch.distributed as dist
 
     assert not dist.is_initialized()
@@ -135,8 +135,10 @@ def _rank_main(rank, world, port, d, out, B, q, shard):
     q.put((rank, tr.history, sd, tr.shard_table, tr._fused.shard_state is not None))
 
 
-@pytest.mark.parametrize("shard", [False, True], ids=["replicated", "row_sharded"])
-def test_train_baseline_two_ranks_match_oracle_on_the_global_batch(tmp_path, shard):
+@pytest.mark.parametrize("shard,model", [(False, "graph_transformer_optimized"), (True, "graph_transformer_optimized"),
+                                         (False, "graph_transformer")],
+                         ids=["replicated", "row_sharded", "ffn_replicated"])
+def test_train_baseline_two_ranks_match_oracle_on_the_global_batch(tmp_path, shard, model):
     """Two ranks of the drop-in train_baseline.py (SyncBN data parallel, B = 8 per rank,
     sharing the GPU over gloo) for two epochs against the CPU ORACLE replaying them on the
     global batches of 16 sessions (one-GPU semantics): the same initial weights
@@ -145,7 +147,9 @@ def test_train_baseline_two_ranks_match_oracle_on_the_global_batch(tmp_path, sha
     draws one _base_seed), the same per-session examples and position-keyed negatives
     (oracle/batch_ref.py restates the device stream; rank r builds sessions [16 i + 8 r, +8)
     of global batch i).  ``row_sharded``: ``--shard-table on``, the item table and its
-    moments row-sharded across the two ranks (SURVEY §8e ii).  Replicas are bit-identical;
+    moments row-sharded across the two ranks (SURVEY §8e ii).  ``ffn_replicated``: the
+    reference's ``--model graph_transformer`` (use_ffn=True, FFN x 4) at d = 64, SyncBN
+    folded by each FFN's first GEMM.  Replicas are bit-identical;
     each epoch's loss and every trained parameter match the oracle ELEMENTWISE
     (gpu_helpers.close_trained), the running statistics too; the ranks leave through
     ``destroy_process_group`` (exit code 0)."""
@@ -156,7 +160,7 @@ def test_train_baseline_two_ranks_match_oracle_on_the_global_batch(tmp_path, sha
     from gpu_helpers import OracleTrio, close_trained
 
     from etpgt.data.batch import collate_sessions
-    from etpgt.model import create_graph_transformer_optimized
+    from etpgt.model import create_graph_transformer, create_graph_transformer_optimized
     from etpgt.train.dataloader import SessionDataset
     from etpgt.utils.seed import set_seed
 
@@ -165,7 +169,9 @@ def test_train_baseline_two_ranks_match_oracle_on_the_global_batch(tmp_path, sha
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, d, tmp_path / "dp", B, q, shard))
+    ffn = model == "graph_transformer"
+    dim = 64 if ffn else 32  # the FFN kernels cover d 64 / 128 / 256
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, d, tmp_path / "dp", B, q, shard, model, dim))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -181,15 +187,19 @@ def test_train_baseline_two_ranks_match_oracle_on_the_global_batch(tmp_path, sha
     assert all(p.exitcode == 0 for p in procs)
     for k, v in res[0][1].items():
         assert np.array_equal(v, res[1][1][k]), f"replicas diverged: {k}"
-    assert os.path.exists(tmp_path / "dp" / "graph_transformer_optimized" / "history.json")
+    assert os.path.exists(tmp_path / "dp" / model / "history.json")
     hist, sd = res[0]
     # ---- the oracle replays the epoch on the global batches
     tr = SessionDataset(d / "train.csv", d / "graph_edges.csv", n, 50)
     va = SessionDataset(d / "val.csv", d / "graph_edges.csv", n, 50)
     T = max(tr.num_items, va.num_items)
     set_seed(42)
-    init = create_graph_transformer_optimized(T, embedding_dim=32, hidden_dim=32, num_layers=2, num_heads=2,
-                                              dropout=0.0, use_laplacian_pe=True, use_ffn=False, ffn_expansion=2)
+    if ffn:
+        init = create_graph_transformer(T, embedding_dim=dim, hidden_dim=dim, num_layers=2, num_heads=2, dropout=0.0,
+                                        readout_type="mean", use_laplacian_pe=True)
+    else:
+        init = create_graph_transformer_optimized(T, embedding_dim=dim, hidden_dim=dim, num_layers=2, num_heads=2,
+                                                  dropout=0.0, use_laplacian_pe=True, use_ffn=False, ffn_expansion=2)
     orders = []
     for e in range(EPOCHS):
         if e > 0:
@@ -199,8 +209,12 @@ def test_train_baseline_two_ranks_match_oracle_on_the_global_batch(tmp_path, sha
         g = torch.Generator()
         g.manual_seed(seed)
         orders.append(torch.randperm(len(tr), generator=g).numpy())
-    ref = R.ref_create_graph_transformer_optimized(T, embedding_dim=32, hidden_dim=32, num_layers=2, num_heads=2,
-                                                   dropout=0.0, use_laplacian_pe=True)
+    if ffn:
+        ref = R.RefGraphTransformer(T, embedding_dim=dim, hidden_dim=dim, num_layers=2, num_heads=2, dropout=0.0,
+                                    use_laplacian_pe=True, use_ffn=True, ffn_expansion=4)
+    else:
+        ref = R.ref_create_graph_transformer_optimized(T, embedding_dim=dim, hidden_dim=dim, num_layers=2,
+                                                       num_heads=2, dropout=0.0, use_laplacian_pe=True)
     isd = {k: v.clone() for k, v in init.state_dict().items()}
     isd["laplacian_pe._cached_pe"] = torch.from_numpy(sd["laplacian_pe._cached_pe"]).clone()
     ref.laplacian_pe._cached_pe = isd["laplacian_pe._cached_pe"]
