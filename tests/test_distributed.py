@@ -319,3 +319,44 @@ def test_trainer_refuses_the_autograd_loop_under_data_parallel():
         assert p.exitcode == 0
     for r in range(world):
         assert "data-parallel training (2 ranks) needs the fused HIP step" in msgs[r], msgs[r]
+
+
+def _trainer_sync_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from etpgt.model import create_graph_transformer, create_graph_transformer_optimized
+        from etpgt.train.trainer import Trainer
+
+        out = {}
+        for name, m in (("opt64", create_graph_transformer_optimized(50, embedding_dim=64, hidden_dim=64)),
+                        ("ffn64", create_graph_transformer(50, embedding_dim=64, hidden_dim=64, num_layers=2)),
+                        ("ffn256", create_graph_transformer(50)),
+                        ("ffn64x2", create_graph_transformer(50, embedding_dim=64, hidden_dim=64, ffn_expansion=2))):
+            opt = torch.optim.AdamW(m.parameters(), lr=1e-3)
+            tr = Trainer(m, [], [], opt, device="cpu", output_dir=f"/tmp/_tr_sync_{port}_{rank}", max_epochs=1)
+            out[name] = tr.sync_bn
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_trainer_sync_bn_default_at_two_ranks():
+    """Trainer at world 2: SyncBN by default for the optimized model and for the FFN model
+    at d 64 / 128 with expansion 4 (gtr_ffn_fwd folds the gathered rows); per-rank
+    BatchNorm statistics for the FFN shapes the SyncBN fold does not cover."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_trainer_sync_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    for r in range(world):
+        assert res[r] == {"opt64": True, "ffn64": True, "ffn256": False, "ffn64x2": False}, res[r]
