@@ -447,7 +447,12 @@ def main():
         seq = None
         step.close()
         torch.distributed.barrier()
-        torch.distributed.destroy_process_group()
+        torn_down = _bounded(torch.distributed.destroy_process_group, 120.0)
+        if not torn_down:  # guard only: the released-graph teardown returns in < 1 s (profiles/r06)
+            print("bench: destroy_process_group did not return within 120 s; the line is printed and the "
+                  "process exits without it", file=sys.stderr, flush=True)
+    else:
+        torn_down = True
     if rank == 0:
         legs = [int(x) for x in args.strong_batches.split(",") if x.strip() and int(x) > 0]
         if legs and not cfg.get("shard") and os.environ.get("GTR_STRONG_CHILD") != "1":
@@ -456,6 +461,19 @@ def main():
             out["strong_scaling"] = strong_scaling_legs(world, legs, args.strong_steps)
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(out) + "\n").encode())
+    if not torn_down:
+        sys.stderr.flush()
+        os._exit(0)
+
+
+def _bounded(fn, seconds: float) -> bool:
+    """Run ``fn`` in a daemon thread; True when it returned within ``seconds``."""
+    import threading
+
+    t = threading.Thread(target=fn, daemon=True)
+    t.start()
+    t.join(seconds)
+    return not t.is_alive()
 
 
 def _child_line(cmd: list, env: dict, timeout: float) -> dict:
