@@ -1873,6 +1873,9 @@ __device__ __forceinline__ void st_row(float* p, const float (&x)[EPL]) {
 #ifndef GTR_RW_NRG128
 #define GTR_RW_NRG128 4
 #endif
+#ifndef GTR_RW_FOLD
+#define GTR_RW_FOLD 1
+#endif
 template <int D>
 struct RwGeom {
   static constexpr int NRG = D >= 128 ? GTR_RW_NRG128 : 4;
@@ -1943,6 +1946,9 @@ __device__ __forceinline__ void consume_round(ScoreAcc<RwGeom<D>::EPL>& A, const
                                               bool lead, bool use_bpr, bool use_lw, float inv_bn, float w_bpr,
                                               float inv_t, float* sc, float* coef_row) {
   constexpr int EPL = RwGeom<D>::EPL, NRG = RwGeom<D>::NRG, RND = NRG * KQ;
+#if GTR_RW_FOLD
+  float lq[KQ];  // the round's listwise logits (-inf past n), folded below with ONE rescale
+#endif
 #pragma unroll
   for (int q = 0; q < KQ; ++q) {
     const int k = r * RND + q * NRG + rg;
@@ -1950,6 +1956,9 @@ __device__ __forceinline__ void consume_round(ScoreAcc<RwGeom<D>::EPL>& A, const
 #pragma unroll
     for (int e = 0; e < EPL; ++e) d += se[e] * rv[q][e];
     d = group_sum(d, RwGeom<D>::RL);
+#if GTR_RW_FOLD
+    lq[q] = k < n ? d * inv_t : -INFINITY;
+#endif
     if (k < n) {
       if (use_bpr) {
         const float sg = 1.0f / (1.0f + expf(-(pos - d)));
@@ -1961,6 +1970,7 @@ __device__ __forceinline__ void consume_round(ScoreAcc<RwGeom<D>::EPL>& A, const
         if (!use_lw && lead) coef_row[k] = -dz;
       }
       if (use_lw) {
+#if !GTR_RW_FOLD
         const float l = d * inv_t;
         const float mn = fmaxf(A.mg, l);
         const float c = expf(A.mg - mn), p = expf(l - mn);
@@ -1968,12 +1978,41 @@ __device__ __forceinline__ void consume_round(ScoreAcc<RwGeom<D>::EPL>& A, const
 #pragma unroll
         for (int e = 0; e < EPL; ++e) A.accl[e] = A.accl[e] * c + p * rv[q][e];
         A.mg = mn;
+#endif
         if (lead) {
           if (sc) sc[k] = d; else coef_row[k] = d;  // raw score; coefficient once lse is known
         }
       }
     }
   }
+#if GTR_RW_FOLD
+  // the round's KQ rows into the online softmax with one max and one rescale (KQ + 1 expf
+  // instead of 2 KQ, EPL rescale multiplies instead of KQ * EPL); a round with no live row
+  // (past n) leaves the state as it is
+  if (use_lw) {
+    float mn = A.mg;
+#pragma unroll
+    for (int q = 0; q < KQ; ++q) mn = fmaxf(mn, lq[q]);
+    if (mn != -INFINITY) {
+      const float c = expf(A.mg - mn);
+      float pq[KQ];
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) pq[q] = expf(lq[q] - mn);
+      float z = A.zg * c;
+#pragma unroll
+      for (int q = 0; q < KQ; ++q) z += pq[q];
+      A.zg = z;
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {
+        float acc = A.accl[e] * c;
+#pragma unroll
+        for (int q = 0; q < KQ; ++q) acc = __builtin_fmaf(pq[q], rv[q][e], acc);
+        A.accl[e] = acc;
+      }
+      A.mg = mn;
+    }
+  }
+#endif
 }
 
 template <int D>
