@@ -38,11 +38,11 @@ class FusedTrainStep:
         if loss not in ("bpr", "listwise", "dual", "sampled_softmax"):
             raise ValueError(f"Unknown loss type: {loss}")
         if getattr(model, "use_ffn", False):
-            # the FFN variant trains data parallel (replicated table), with or without SyncBN;
-            # SyncBN folds the gathered rows in the FFN's first GEMM (dim 64 / 128, expansion 4)
-            if shard_table or os.environ.get("GTR_TAILW") == "1":
-                raise NotImplementedError("the FFN variant (use_ffn=True) has no row-sharded-table step and no "
-                                          "GTR_TAILW")
+            # the FFN variant trains data parallel (replicated or row-sharded table), with or
+            # without SyncBN; SyncBN folds the gathered rows in the FFN's first GEMM (dim 64 / 128,
+            # expansion 4)
+            if os.environ.get("GTR_TAILW") == "1":
+                raise NotImplementedError("the FFN variant (use_ffn=True) has no GTR_TAILW step")
             if sync_bn and not (model.embedding_dim in (64, 128) and getattr(model, "ffn_expansion", 4) == 4):
                 raise NotImplementedError("SyncBN with the FFN variant covers dim 64 / 128 at ffn_expansion 4")
         self.model = model
@@ -650,14 +650,22 @@ class FusedTrainStep:
                     "step_begin")
             sh.route(bs, st())
 
+        ffn = ws.ffns is not None  # FFN blocks: placed as in _pieces (a layer's BatchNorm folded by its FFN)
+
         def fwd(l):
             with sh.side():  # beside the class-1 (scoring) rows' exchange when forked
+                if ffn and l > 0:
+                    eng.ffn_fwd(ws, cfg, bc, l - 1, st())
                 eng.layer_fwd(ws, cfg, bc, l, eng.fill_embed(tab), st(), self.split)
 
         def head():
             sh.join()
+            if ffn:
+                eng.ffn_fwd(ws, cfg, bc, Lc - 1, st())
             eng.run_head(ws, cfg, bc, L.RO_FWD | L.RO_LOSS | L.RO_BWD, self.loss_kind, self.temperature, self.alpha,
                          table=tab)
+            if ffn:  # layer Lc-1's dy and BatchNorm sums come from its FFN's backward
+                eng.ffn_bwd(ws, cfg, bc, Lc - 1, st())
 
         # the scoring rows beside the forward and the gradient rows beside the weight
         # gradients: RCCL, the step captured whole (or eager) -- never across the
@@ -666,6 +674,8 @@ class FusedTrainStep:
 
         def bwd(l):
             eng.layer_bwd(ws, cfg, bc, l, st(), self.split)
+            if ffn and l > 0:
+                eng.ffn_bwd(ws, cfg, bc, l - 1, st())
             if l == 0:
                 if overlap:  # gradient rows packed first; they travel beside the weight gradients
                     sh.pack(bs, st(), parts=1)

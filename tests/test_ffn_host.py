@@ -65,14 +65,17 @@ def test_oracle_ffn_masks_shapes_and_rate():
     assert "ffn_h" not in R.hip_dropout_masks(987654321, 3, p, 2, ei, N, D, H)
 
 
-def test_ffn_models_refuse_sharded_fused_steps_and_unsupported_shapes():
+def test_ffn_models_refuse_unsupported_fused_steps_and_shapes(monkeypatch):
     from etpgt.train.fused import FusedTrainStep
 
-    # data parallel (with or without SyncBN) is supported (tests/test_gpu_ffn_dp.py); the
-    # row-sharded table and SyncBN outside dim 64 / 128 at expansion 4 refuse up front
+    # data parallel on the replicated or row-sharded table, with or without SyncBN, is
+    # supported (tests/test_gpu_ffn_dp.py); GTR_TAILW and SyncBN outside dim 64 / 128 at
+    # expansion 4 refuse up front
     m = create_graph_transformer(50, embedding_dim=64, hidden_dim=64, num_layers=2, num_heads=2, use_ffn=True)
+    monkeypatch.setenv("GTR_TAILW", "1")
     with pytest.raises(NotImplementedError, match="use_ffn"):
-        FusedTrainStep(m, shard_table=True)
+        FusedTrainStep(m)
+    monkeypatch.delenv("GTR_TAILW")
     m2 = create_graph_transformer(50, embedding_dim=64, hidden_dim=64, num_layers=2, num_heads=2, use_ffn=True,
                                   ffn_expansion=2)
     with pytest.raises(NotImplementedError, match="ffn_expansion 4"):

@@ -49,7 +49,7 @@ def _concat(b0, b1):
     return cat(b0, b1)
 
 
-def _worker(rank, world, port, q, sync):
+def _worker(rank, world, port, q, sync, shard=False):
     # exact f32-input MFMA (the averaging protocol is pinned at lr 1e-2, as test_gpu_distributed)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GTR_GEMM="f32")
     import torch.distributed as dist
@@ -61,11 +61,14 @@ def _worker(rank, world, port, q, sync):
         T = data.table_rows
         m, _ = _pair(T, 31)
         m.train()
-        f = FusedTrainStep(m, lr=1e-2, weight_decay=1e-2, loss="listwise" if sync else "bpr", sync_bn=sync)
+        f = FusedTrainStep(m, lr=1e-2, weight_decay=1e-2, loss="listwise" if sync else "bpr", sync_bn=sync,
+                           shard_table=shard)
         assert f.data_parallel and f.world == world and f.sync_bn == sync
         bl = batches(data, B, NNEG, STEPS * world, seed=32)
         losses = [float(f(bl[s * world + rank].to("cuda"))) for s in range(STEPS)]
         assert f.split  # the FFN blocks run on the split layer path
+        assert (f.shard_state is not None) == shard
+        f.sync_table()  # row-sharded: the shards back into the model's table (collective)
         bufs = {n: b.detach().cpu().numpy().copy() for n, b in m.named_buffers() if "running" in n}
         q.put((rank, losses, {n: p.detach().cpu().numpy().copy() for n, p in m.named_parameters()}, bufs))
     finally:
@@ -74,12 +77,12 @@ def _worker(rank, world, port, q, sync):
         dist.destroy_process_group()
 
 
-def _run(sync):
+def _run(sync, shard=False):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, sync)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, sync, shard)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -96,12 +99,14 @@ def _run(sync):
     return res
 
 
-def test_ffn_sync_bn_two_ranks_equal_oracle_on_the_global_batch():
+@pytest.mark.parametrize("shard", [False, True], ids=["replicated", "row_sharded"])
+def test_ffn_sync_bn_two_ranks_equal_oracle_on_the_global_batch(shard):
     """SyncBN: two ranks train the FFN model like one GPU on the concatenated global batch
     (BatchNorm over all 2 x B sessions, the FFN weights among the averaged small
-    parameters): losses, every parameter and the running statistics against the oracle."""
+    parameters): losses, every parameter and the running statistics against the oracle.
+    ``row_sharded``: the item table and its moments row-sharded across the ranks."""
     world = 2
-    res = _run(True)
+    res = _run(True, shard)
     data = small_data()
     T = data.table_rows
     _, ref = _pair(T, 31)

@@ -136,8 +136,8 @@ def _rank_main(rank, world, port, d, out, B, q, shard, model="graph_transformer_
 
 
 @pytest.mark.parametrize("shard,model", [(False, "graph_transformer_optimized"), (True, "graph_transformer_optimized"),
-                                         (False, "graph_transformer")],
-                         ids=["replicated", "row_sharded", "ffn_replicated"])
+                                         (False, "graph_transformer"), (True, "graph_transformer")],
+                         ids=["replicated", "row_sharded", "ffn_replicated", "ffn_row_sharded"])
 def test_train_baseline_two_ranks_match_oracle_on_the_global_batch(tmp_path, shard, model):
     """Two ranks of the drop-in train_baseline.py (SyncBN data parallel, B = 8 per rank,
     sharing the GPU over gloo) for two epochs against the CPU ORACLE replaying them on the
